@@ -1,0 +1,96 @@
+// raster_common.h — device-side data layout shared by the HIP kernels and the C-ABI host code.
+// HBM layout:
+//   VsIn      48 B/vertex  {pos.xyz, normal.xyz, color.xyz, uv.xy, pad} (the 44 B of the 100-byte
+//                          Trident Vertex that reach the output; Vertex.h:9-78), SoA-of-records
+//   VsSkin    32 B/vertex  {bone indices, bone weights}, only when any draw has BoneCount > 0
+//   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation
+//   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
+//   TriRec    64 B/record  snapped screen vertices, NDC z, 1/w, (prim<<3|sub), 3 vary slots
+//   binrange   8 B/record  (bx0, by0, bx1, by1) in 64x64-pixel bins
+//   bin_list   4 B/entry   record ids per bin (order-free: visibility is resolved by a 64-bit key)
+//   colour     4 B/pixel   B8G8R8A8_UNORM;  depth 4 B/pixel D32_SFLOAT bits
+#pragma once
+
+#include <stdint.h>
+#include "../../include/tri_raster.h"
+
+#define TRI_BIN_LOG2 6
+#define TRI_BIN (1 << TRI_BIN_LOG2)
+#define TRI_BLOCK 256
+#define TRI_PRIM_MAX ((1u << 29) - 1u)
+#define TRI_REC_CULLED 0xFFFFFFFFu
+#define TRI_REC_CLIPPED 0xFFFFFFFEu
+#define TRI_MAX_CLIP_VERTS 12
+#define TRI_WMIN 1e-5f
+#define TRI_GUARD_BAND_PX 16000.0f
+
+// overflow flag bits (tri_ctx counters.flags)
+#define TRI_OVF_CLIP_RECORDS 0x1u
+#define TRI_OVF_CLIP_VERTS 0x2u
+#define TRI_OVF_BIN_LIST 0x4u
+
+struct __attribute__((aligned(16))) TriVsIn {
+    float px, py, pz, nx;
+    float ny, nz, cr, cg;
+    float cb, u, v, pad;
+};
+
+struct __attribute__((aligned(16))) TriVsSkin {
+    int32_t idx[4];
+    float w[4];
+};
+
+struct __attribute__((aligned(16))) TriRec {
+    int32_t X[3];
+    int32_t Y[3];
+    float z[3];
+    float iw[3];
+    uint32_t prim_sub;  // prim << 3 | sub; TRI_REC_CULLED; TRI_REC_CLIPPED (v[0] = first sub-record)
+    uint32_t v[3];      // vary slots (post orientation swap)
+};
+static_assert(sizeof(TriRec) == 64, "TriRec must be one 64-byte line");
+
+struct __attribute__((aligned(16))) TriDrawDev {
+    float model[16];
+    float tint[4];
+    float tex_scale[2];
+    float tex_offset[2];
+    float tiling;
+    int32_t tex_id;      // resolved texture table index (unused slots alias slot 0)
+    int32_t bone_offset;
+    int32_t bone_count;
+    int32_t first_index;
+    int32_t base_vertex;
+    uint32_t min_index;
+    uint32_t vert_count; // VS invocations for this draw (max-min+1), 0 = inactive
+};
+
+struct TriTexDesc {
+    const uint32_t* texels;  // RGBA8 sRGB, row-major
+    uint32_t w, h;
+};
+
+struct TriCounters {  // per-frame fields are zeroed before every frame; `flags` is sticky
+    uint32_t ovf_records;
+    uint32_t ovf_verts;
+    uint32_t tris_setup;
+    uint32_t tris_clipped;
+    uint32_t bin_entries;
+    uint32_t pad[2];
+    uint32_t flags;
+};
+#define TRI_COUNTERS_RESET_BYTES 28
+
+struct TriFrameParams {
+    int32_t W, H, y0, y1;
+    int32_t nbx, nby, nbins, ppt;
+    float hw, hh, gx, gy;
+    uint32_t nprims, nslots, ndraws, nchunks;
+    uint32_t ovf_rec_cap, ovf_vert_cap, bin_cap, bone_count;
+    uint32_t clear_bgra;
+    uint32_t write_depth;
+    uint32_t pad0, pad1;
+    float pv[16];
+    tri_global_ubo ubo;
+    tri_material_record mat0;
+};

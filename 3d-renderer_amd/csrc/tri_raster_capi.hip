@@ -1,0 +1,652 @@
+// tri_raster_capi.hip — the C-ABI (include/tri_raster.h) over the gfx950 kernels.
+// Owns device memory, the stream and timing events; mirrors Trident::Renderer's upload / frame
+// semantics (Renderer.cpp:1784-2116 geometry, :3404-3656 texture slots, :5822-6051 uniforms,
+// :5110-5151 draws, :5297-5338 readback).
+#include "raster_launch.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_last_error = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                        \
+    do {                                                                                     \
+        hipError_t _e = (expr);                                                              \
+        if (_e != hipSuccess)                                                                \
+            return fail(_e == hipErrorOutOfMemory ? TRI_E_OOM : TRI_E_HIP, "%s: %s (%s:%d)", \
+                        #expr, hipGetErrorString(_e), __FILE__, __LINE__);                   \
+    } while (0)
+
+template <typename T>
+int grow(T*& p, size_t& cap, size_t need) {
+    if (need <= cap && p) return TRI_OK;
+    if (p) HIP_TRY(hipFree(p));
+    p = nullptr;
+    cap = std::max<size_t>(need, 1);
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&p), cap * sizeof(T)));
+    return TRI_OK;
+}
+
+uint32_t unorm8_host(float c) {
+    const float cc = std::fmin(std::fmax(c, 0.0f), 1.0f);
+    return (uint32_t)(int)(cc * 255.0f + 0.5f);
+}
+
+struct TimingSet {
+    hipEvent_t ev[6];
+};
+
+}  // namespace
+
+struct tri_ctx {
+    tri_config cfg{};
+    int device = 0;
+    int32_t W = 0, H = 0, y0 = 0, y1 = 0, nbx = 0, nby = 0, nbins = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+
+    // geometry (UploadMeshFromCache)
+    TriVsIn* d_vin = nullptr; size_t cap_vin = 0;
+    TriVsSkin* d_skin = nullptr; size_t cap_skin = 0;
+    bool has_skin_data = false;
+    uint64_t nverts = 0;
+    uint32_t* d_idx = nullptr; size_t cap_idx = 0;
+    uint64_t nidx = 0;
+    std::vector<tri_mesh_range> meshes;
+    std::vector<uint32_t> mesh_min, mesh_max;
+    bool geometry_set = false;
+
+    tri_material_record mat0{{1, 1, 1, 1}, {1, 1, 1, 0}};
+
+    // texture slots; slot 0 = default 1x1 white
+    uint32_t* d_tex[TRI_MAX_TEXTURE_SLOTS] = {};
+    uint32_t tex_w[TRI_MAX_TEXTURE_SLOTS] = {}, tex_h[TRI_MAX_TEXTURE_SLOTS] = {};
+    TriTexDesc* d_texdesc = nullptr;
+    bool tex_dirty = true;
+    float* d_lut = nullptr;
+
+    float* d_bones = nullptr; size_t cap_bones = 0;
+    uint32_t nbones = 0;
+
+    // per frame
+    tri_global_ubo ubo{};
+    float pv[16] = {};
+    uint32_t clear_bgra = 0;
+    bool frame_set = false;
+    std::vector<tri_draw> draws;
+    bool draws_dirty = true;
+
+    // resolved draws
+    TriDrawDev* d_draws = nullptr; size_t cap_draws = 0;
+    uint32_t* d_vbase = nullptr; size_t cap_vbase = 0;
+    uint32_t* d_pbase = nullptr; size_t cap_pbase = 0;
+    void* h_stage = nullptr; size_t cap_stage = 0;  // pinned upload staging
+    hipEvent_t stage_free = nullptr;
+    uint32_t ndraws = 0, nslots = 0, nprims = 0;
+    bool any_skin = false;
+
+    // work buffers
+    float4* d_clip = nullptr; size_t cap_clip = 0;
+    float4* d_vary = nullptr; size_t cap_vary = 0;
+    TriRec* d_recs = nullptr; size_t cap_recs = 0;
+    uint2* d_brange = nullptr; size_t cap_brange = 0;
+    uint32_t* d_bin_total = nullptr; size_t cap_bin_total = 0;
+    uint32_t* d_bin_start = nullptr; size_t cap_bin_start = 0;
+    uint32_t* d_bin_cursor = nullptr; size_t cap_bin_cursor = 0;
+    uint32_t* d_bin_list = nullptr; size_t cap_bin_list = 0;
+    TriCounters* d_ctr = nullptr;
+    uint32_t ovf_rec_cap = 1u << 16, ovf_vert_cap = 1u << 17;
+    uint32_t bin_cap = 0;
+
+    uint32_t* d_color_own = nullptr;
+    float* d_depth_own = nullptr;
+    uint32_t* d_color = nullptr;
+    float* d_depth = nullptr;
+
+    bool timing = false;
+    std::vector<TimingSet> pending;
+    std::vector<TimingSet> free_sets;
+    tri_timing acc{};
+};
+
+namespace {
+
+int make_current(tri_ctx* c) {
+    HIP_TRY(hipSetDevice(c->device));
+    return TRI_OK;
+}
+
+// glm mat4 * mat4 (column j = ((A0*B[j][0] + A1*B[j][1]) + A2*B[j][2]) + A3*B[j][3])
+void mat4_mul(const float* a, const float* b, float* r) {
+    for (int j = 0; j < 4; ++j)
+        for (int i = 0; i < 4; ++i) {
+            float s = a[0 * 4 + i] * b[j * 4 + 0];
+            s = s + a[1 * 4 + i] * b[j * 4 + 1];
+            s = s + a[2 * 4 + i] * b[j * 4 + 2];
+            s = s + a[3 * 4 + i] * b[j * 4 + 3];
+            r[j * 4 + i] = s;
+        }
+}
+
+int upload_texture_table(tri_ctx* c) {
+    if (!c->tex_dirty) return TRI_OK;
+    TriTexDesc h[TRI_MAX_TEXTURE_SLOTS];
+    for (int s = 0; s < TRI_MAX_TEXTURE_SLOTS; ++s) {
+        const int src = c->d_tex[s] ? s : 0;  // unused slots alias slot 0 (Renderer.cpp:3645-3656)
+        h[s].texels = c->d_tex[src];
+        h[s].w = c->tex_w[src];
+        h[s].h = c->tex_h[src];
+    }
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(c->d_texdesc, h, sizeof h, hipMemcpyHostToDevice));
+    c->tex_dirty = false;
+    return TRI_OK;
+}
+
+// Resolve the draw list against the uploaded meshes (GatherMeshDraws + the draw loop's skips).
+int resolve_draws(tri_ctx* c) {
+    if (!c->draws_dirty) return TRI_OK;
+    const uint32_t n = (uint32_t)c->draws.size();
+    std::vector<TriDrawDev> dd(n);
+    std::vector<uint32_t> vb(n + 1), pb(n + 1);
+    uint64_t vslots = 0, prims = 0;
+    bool skin = false;
+    for (uint32_t d = 0; d < n; ++d) {
+        const tri_draw& src = c->draws[d];
+        TriDrawDev& o = dd[d];
+        std::memset(&o, 0, sizeof o);
+        std::memcpy(o.model, src.pc.model, 64);
+        std::memcpy(o.tint, src.pc.tint, 16);
+        o.tex_scale[0] = src.pc.texture_scale[0];
+        o.tex_scale[1] = src.pc.texture_scale[1];
+        o.tex_offset[0] = src.pc.texture_offset[0];
+        o.tex_offset[1] = src.pc.texture_offset[1];
+        o.tiling = src.pc.tiling_factor;
+        const int32_t slot = src.pc.texture_slot;
+        o.tex_id = (slot >= 0 && slot < TRI_MAX_TEXTURE_SLOTS) ? slot : 0;
+        o.bone_offset = src.pc.bone_offset;
+        o.bone_count = src.pc.bone_count;
+        vb[d] = (uint32_t)vslots;
+        pb[d] = (uint32_t)prims;
+        if (src.mesh_index >= c->meshes.size()) continue;  // Renderer.cpp:5118-5127 skip
+        const tri_mesh_range& mr = c->meshes[src.mesh_index];
+        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > c->nidx) continue;
+        o.first_index = (int32_t)mr.first_index;
+        o.base_vertex = mr.base_vertex;
+        o.min_index = c->mesh_min[src.mesh_index];
+        o.vert_count = c->mesh_max[src.mesh_index] - o.min_index + 1;
+        vslots += o.vert_count;
+        prims += mr.index_count / 3;
+        skin = skin || (o.bone_count > 0);
+    }
+    vb[n] = (uint32_t)vslots;
+    pb[n] = (uint32_t)prims;
+    if (vslots > 0xFFFFFFF0ull) return fail(TRI_E_INVALID, "too many vertex-shader invocations (%llu)", (unsigned long long)vslots);
+    if (prims > TRI_PRIM_MAX) return fail(TRI_E_INVALID, "too many primitives (%llu > %u)", (unsigned long long)prims, TRI_PRIM_MAX);
+    int rc;
+    if ((rc = grow(c->d_draws, c->cap_draws, std::max<size_t>(n, 1)))) return rc;
+    if ((rc = grow(c->d_vbase, c->cap_vbase, n + 1))) return rc;
+    if ((rc = grow(c->d_pbase, c->cap_pbase, n + 1))) return rc;
+    const size_t bytes = n * sizeof(TriDrawDev) + 2 * (n + 1) * sizeof(uint32_t);
+    if (c->stage_free) HIP_TRY(hipEventSynchronize(c->stage_free));
+    if (bytes > c->cap_stage) {
+        if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
+        c->h_stage = nullptr;
+        c->cap_stage = bytes * 2;
+        HIP_TRY(hipHostMalloc(&c->h_stage, c->cap_stage, hipHostMallocDefault));
+    }
+    char* st = static_cast<char*>(c->h_stage);
+    std::memcpy(st, dd.data(), n * sizeof(TriDrawDev));
+    std::memcpy(st + n * sizeof(TriDrawDev), vb.data(), (n + 1) * 4);
+    std::memcpy(st + n * sizeof(TriDrawDev) + (n + 1) * 4, pb.data(), (n + 1) * 4);
+    if (n) HIP_TRY(hipMemcpyAsync(c->d_draws, st, n * sizeof(TriDrawDev), hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_vbase, st + n * sizeof(TriDrawDev), (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_pbase, st + n * sizeof(TriDrawDev) + (n + 1) * 4, (n + 1) * 4,
+                           hipMemcpyHostToDevice, c->stream));
+    if (!c->stage_free) HIP_TRY(hipEventCreateWithFlags(&c->stage_free, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(c->stage_free, c->stream));
+    c->ndraws = n;
+    c->nslots = (uint32_t)vslots;
+    c->nprims = (uint32_t)prims;
+    c->any_skin = skin;
+    c->draws_dirty = false;
+    return TRI_OK;
+}
+
+int ensure_work_buffers(tri_ctx* c) {
+    int rc;
+    const size_t nrec = (size_t)c->nprims + c->ovf_rec_cap;
+    const size_t nvary = 3ull * ((size_t)c->nslots + c->ovf_vert_cap);
+    if (c->bin_cap == 0) c->bin_cap = 2u * c->nprims + 4u * (uint32_t)c->nbins + 65536u;
+    bool realloc = c->cap_clip < std::max<size_t>(c->nslots, 1) || c->cap_vary < nvary || c->cap_recs < nrec ||
+                   c->cap_bin_list < c->bin_cap;
+    if (realloc) HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((rc = grow(c->d_clip, c->cap_clip, std::max<size_t>(c->nslots, 1)))) return rc;
+    if ((rc = grow(c->d_vary, c->cap_vary, nvary))) return rc;
+    if ((rc = grow(c->d_recs, c->cap_recs, nrec))) return rc;
+    if ((rc = grow(c->d_brange, c->cap_brange, nrec))) return rc;
+    if ((rc = grow(c->d_bin_list, c->cap_bin_list, c->bin_cap))) return rc;
+    return TRI_OK;
+}
+
+int collect_timing(tri_ctx* c) {
+    if (c->pending.empty()) return TRI_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    for (TimingSet& t : c->pending) {
+        float ms[5], tot;
+        for (int i = 0; i < 5; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], t.ev[i], t.ev[i + 1]));
+        HIP_TRY(hipEventElapsedTime(&tot, t.ev[0], t.ev[5]));
+        c->acc.ms_vertex += ms[0];
+        c->acc.ms_setup += ms[1];
+        c->acc.ms_binscan += ms[2];
+        c->acc.ms_scatter += ms[3];
+        c->acc.ms_raster += ms[4];
+        c->acc.ms_frame += tot;
+        c->acc.frames += 1;
+        c->free_sets.push_back(t);
+    }
+    c->pending.clear();
+    return TRI_OK;
+}
+
+int check_overflow(tri_ctx* c) {
+    TriCounters h;
+    HIP_TRY(hipMemcpy(&h, c->d_ctr, sizeof h, hipMemcpyDeviceToHost));
+    if (!h.flags) return TRI_OK;
+    const uint32_t zero = 0;
+    HIP_TRY(hipMemcpy(&c->d_ctr->flags, &zero, 4, hipMemcpyHostToDevice));
+    if (h.flags & TRI_OVF_CLIP_RECORDS) c->ovf_rec_cap *= 4;
+    if (h.flags & TRI_OVF_CLIP_VERTS) c->ovf_vert_cap *= 4;
+    if (h.flags & TRI_OVF_BIN_LIST) c->bin_cap = std::max<uint32_t>(c->bin_cap * 2, h.bin_entries + h.bin_entries / 4);
+    int rc = ensure_work_buffers(c);
+    if (rc) return rc;
+    return fail(TRI_E_OVERFLOW, "frame overflowed an internal buffer (flags 0x%x); capacities grown, re-render",
+                h.flags);
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* tri_last_error(void) { return g_last_error.c_str(); }
+int tri_abi_version(void) { return TRI_RASTER_ABI_VERSION; }
+
+int tri_create(const tri_config* cfg, tri_ctx** out) {
+    if (!cfg || !out) return fail(TRI_E_INVALID, "tri_create: null argument");
+    *out = nullptr;
+    if (cfg->width == 0 || cfg->height == 0 || cfg->width > TRI_MAX_DIM || cfg->height > TRI_MAX_DIM)
+        return fail(TRI_E_INVALID, "tri_create: framebuffer %ux%u outside 1..%d", cfg->width, cfg->height, TRI_MAX_DIM);
+    uint32_t y0 = cfg->band_y0, y1 = cfg->band_y1;
+    if (y0 == 0 && y1 == 0) y1 = cfg->height;
+    if (y0 >= y1 || y1 > cfg->height) return fail(TRI_E_INVALID, "tri_create: bad row band [%u,%u)", y0, y1);
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0)
+        return fail(TRI_E_HIP, "tri_create: no HIP device available");
+    tri_ctx* c = new tri_ctx();
+    c->cfg = *cfg;
+    if (cfg->device >= 0) {
+        if (cfg->device >= ndev) { delete c; return fail(TRI_E_INVALID, "tri_create: device %d of %d", cfg->device, ndev); }
+        c->device = cfg->device;
+    } else if (hipGetDevice(&c->device) != hipSuccess) {
+        delete c;
+        return fail(TRI_E_HIP, "tri_create: hipGetDevice failed");
+    }
+    c->W = (int32_t)cfg->width;
+    c->H = (int32_t)cfg->height;
+    c->y0 = (int32_t)y0;
+    c->y1 = (int32_t)y1;
+    c->nbx = (c->W + TRI_BIN - 1) / TRI_BIN;
+    c->nby = (c->y1 - c->y0 + TRI_BIN - 1) / TRI_BIN;
+    c->nbins = c->nbx * c->nby;
+    auto bail = [&](int rc) { tri_destroy(c); return rc; };
+    int rc = make_current(c);
+    if (rc) return bail(rc);
+    if (tri_kernels_init() != hipSuccess) return bail(fail(TRI_E_HIP, "tri_create: kernel attribute setup failed"));
+    if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
+        return bail(fail(TRI_E_HIP, "tri_create: stream creation failed"));
+    c->stream = c->own_stream;
+    const size_t px = (size_t)c->W * (size_t)(c->y1 - c->y0);
+    if (hipMalloc(&c->d_color_own, px * 4) != hipSuccess || hipMalloc(&c->d_depth_own, px * 4) != hipSuccess ||
+        hipMalloc(&c->d_ctr, sizeof(TriCounters)) != hipSuccess ||
+        hipMalloc(&c->d_texdesc, sizeof(TriTexDesc) * TRI_MAX_TEXTURE_SLOTS) != hipSuccess ||
+        hipMalloc(&c->d_lut, 256 * sizeof(float)) != hipSuccess)
+        return bail(fail(TRI_E_OOM, "tri_create: target allocation failed"));
+    c->d_color = c->d_color_own;
+    c->d_depth = c->d_depth_own;
+    size_t cap = 0;
+    if ((rc = grow(c->d_bin_total, cap, (size_t)c->nbins))) return bail(rc);
+    c->cap_bin_total = cap; cap = 0;
+    if ((rc = grow(c->d_bin_start, cap, (size_t)c->nbins + 1))) return bail(rc);
+    c->cap_bin_start = cap; cap = 0;
+    if ((rc = grow(c->d_bin_cursor, cap, (size_t)c->nbins))) return bail(rc);
+    c->cap_bin_cursor = cap;
+    if (hipMemset(c->d_bin_total, 0, c->nbins * 4) != hipSuccess || hipMemset(c->d_ctr, 0, sizeof(TriCounters)) != hipSuccess)
+        return bail(fail(TRI_E_HIP, "tri_create: memset failed"));
+    float lut[256];
+    for (int i = 0; i < 256; ++i) {  // R8G8B8A8_SRGB decode (sRGB EOTF), evaluated in double
+        const double v = i / 255.0;
+        lut[i] = (float)(v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4));
+    }
+    if (hipMemcpy(c->d_lut, lut, sizeof lut, hipMemcpyHostToDevice) != hipSuccess)
+        return bail(fail(TRI_E_HIP, "tri_create: LUT upload failed"));
+    const uint8_t white[4] = {0xFF, 0xFF, 0xFF, 0xFF};  // CreateDefaultTexture (Renderer.cpp:3404-3436)
+    if ((rc = tri_upload_texture(c, 0, white, 1, 1))) return bail(rc);
+    const float clear[4] = {0.005f, 0.005f, 0.005f, 1.0f};  // m_ClearColor default (Renderer.h:469)
+    c->clear_bgra = unorm8_host(clear[2]) | (unorm8_host(clear[1]) << 8) | (unorm8_host(clear[0]) << 16) |
+                    (unorm8_host(clear[3]) << 24);
+    *out = c;
+    return TRI_OK;
+}
+
+int tri_destroy(tri_ctx* c) {
+    if (!c) return TRI_OK;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    auto f = [](void* p) { if (p) (void)hipFree(p); };
+    f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones);
+    for (auto& t : c->d_tex) f(t);
+    f(c->d_draws); f(c->d_vbase); f(c->d_pbase);
+    f(c->d_clip); f(c->d_vary); f(c->d_recs); f(c->d_brange);
+    f(c->d_bin_total); f(c->d_bin_start); f(c->d_bin_cursor); f(c->d_bin_list); f(c->d_ctr);
+    f(c->d_color_own); f(c->d_depth_own);
+    if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->stage_free) (void)hipEventDestroy(c->stage_free);
+    for (auto& v : {std::cref(c->pending), std::cref(c->free_sets)})
+        for (const TimingSet& t : v.get())
+            for (auto e : t.ev) (void)hipEventDestroy(e);
+    if (c->own_stream) (void)hipStreamDestroy(c->own_stream);
+    delete c;
+    return TRI_OK;
+}
+
+int tri_set_stream(tri_ctx* c, void* s) {
+    if (!c) return fail(TRI_E_INVALID, "tri_set_stream: null context");
+    c->stream = s ? static_cast<hipStream_t>(s) : c->own_stream;
+    return TRI_OK;
+}
+
+int tri_upload_geometry(tri_ctx* c, const tri_vertex* v, uint64_t nv, const uint32_t* idx, uint64_t ni,
+                        const tri_mesh_range* meshes, uint32_t nm) {
+    if (!c) return fail(TRI_E_INVALID, "tri_upload_geometry: null context");
+    if ((nv && !v) || (ni && !idx) || (nm && !meshes)) return fail(TRI_E_INVALID, "tri_upload_geometry: null array");
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    // AoS 100-byte Vertex -> 48-byte shading records (+ 32-byte skin records when weights exist)
+    std::vector<TriVsIn> vin(nv);
+    std::vector<TriVsSkin> skin;
+    bool has_skin = false;
+    for (uint64_t i = 0; i < nv; ++i) {
+        const tri_vertex& s = v[i];
+        TriVsIn& o = vin[i];
+        o.px = s.position[0]; o.py = s.position[1]; o.pz = s.position[2];
+        o.nx = s.normal[0]; o.ny = s.normal[1]; o.nz = s.normal[2];
+        o.cr = s.color[0]; o.cg = s.color[1]; o.cb = s.color[2];
+        o.u = s.texcoord[0]; o.v = s.texcoord[1]; o.pad = 0.0f;
+        has_skin = has_skin || s.bone_weights[0] > 0.f || s.bone_weights[1] > 0.f || s.bone_weights[2] > 0.f ||
+                   s.bone_weights[3] > 0.f;
+    }
+    if (has_skin) {
+        skin.resize(nv);
+        for (uint64_t i = 0; i < nv; ++i) {
+            std::memcpy(skin[i].idx, v[i].bone_indices, 16);
+            std::memcpy(skin[i].w, v[i].bone_weights, 16);
+        }
+        if ((rc = grow(c->d_skin, c->cap_skin, nv))) return rc;
+        HIP_TRY(hipMemcpy(c->d_skin, skin.data(), nv * sizeof(TriVsSkin), hipMemcpyHostToDevice));
+    }
+    c->has_skin_data = has_skin;
+    if ((rc = grow(c->d_vin, c->cap_vin, std::max<uint64_t>(nv, 1)))) return rc;
+    if (nv) HIP_TRY(hipMemcpy(c->d_vin, vin.data(), nv * sizeof(TriVsIn), hipMemcpyHostToDevice));
+    if ((rc = grow(c->d_idx, c->cap_idx, std::max<uint64_t>(ni, 1)))) return rc;
+    if (ni) HIP_TRY(hipMemcpy(c->d_idx, idx, ni * 4, hipMemcpyHostToDevice));
+    c->nverts = nv;
+    c->nidx = ni;
+    c->meshes.assign(meshes, meshes + nm);
+    c->mesh_min.assign(nm, 0);
+    c->mesh_max.assign(nm, 0);
+    for (uint32_t m = 0; m < nm; ++m) {  // referenced vertex range per mesh (VS invocation range)
+        const tri_mesh_range& mr = meshes[m];
+        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > ni) continue;
+        const uint32_t cnt = (mr.index_count / 3) * 3;
+        uint32_t mn = 0xFFFFFFFFu, mx = 0;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            mn = std::min(mn, idx[mr.first_index + i]);
+            mx = std::max(mx, idx[mr.first_index + i]);
+        }
+        if (mx - mn >= 0x7FFFFFFFu) return fail(TRI_E_INVALID, "mesh %u: index range too large", m);
+        c->mesh_min[m] = mn;
+        c->mesh_max[m] = mx;
+    }
+    c->geometry_set = true;
+    c->draws_dirty = true;
+    return TRI_OK;
+}
+
+int tri_upload_materials(tri_ctx* c, const tri_material_record* r, uint32_t n) {
+    if (!c) return fail(TRI_E_INVALID, "tri_upload_materials: null context");
+    if (n && !r) return fail(TRI_E_INVALID, "tri_upload_materials: null records");
+    c->mat0 = n ? r[0] : tri_material_record{{1, 1, 1, 1}, {1, 1, 1, 0}};
+    return TRI_OK;
+}
+
+int tri_upload_texture(tri_ctx* c, uint32_t slot, const uint8_t* rgba, uint32_t w, uint32_t h) {
+    if (!c) return fail(TRI_E_INVALID, "tri_upload_texture: null context");
+    if (slot >= TRI_MAX_TEXTURE_SLOTS) return fail(TRI_E_INVALID, "tri_upload_texture: slot %u >= %d", slot, TRI_MAX_TEXTURE_SLOTS);
+    if (!rgba || w == 0 || h == 0 || (uint64_t)w * h > (1ull << 28))
+        return fail(TRI_E_INVALID, "tri_upload_texture: bad texture %ux%u", w, h);
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if (c->d_tex[slot]) HIP_TRY(hipFree(c->d_tex[slot]));
+    c->d_tex[slot] = nullptr;
+    HIP_TRY(hipMalloc(&c->d_tex[slot], (size_t)w * h * 4));
+    HIP_TRY(hipMemcpy(c->d_tex[slot], rgba, (size_t)w * h * 4, hipMemcpyHostToDevice));
+    c->tex_w[slot] = w;
+    c->tex_h[slot] = h;
+    c->tex_dirty = true;
+    return TRI_OK;
+}
+
+int tri_upload_bone_palette(tri_ctx* c, const float* m, uint32_t n) {
+    if (!c) return fail(TRI_E_INVALID, "tri_upload_bone_palette: null context");
+    if (n && !m) return fail(TRI_E_INVALID, "tri_upload_bone_palette: null matrices");
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    if ((rc = grow(c->d_bones, c->cap_bones, std::max<size_t>(16ull * n, 16)))) return rc;
+    if (n) HIP_TRY(hipMemcpy(c->d_bones, m, 64ull * n, hipMemcpyHostToDevice));
+    c->nbones = n;
+    return TRI_OK;
+}
+
+int tri_set_frame(tri_ctx* c, const tri_global_ubo* ubo, const float clear[4]) {
+    if (!c || !ubo) return fail(TRI_E_INVALID, "tri_set_frame: null argument");
+    if (ubo->ai_blend_config[3] > 0.0f && ubo->ai_blend_config[0] > 0.0f)
+        return fail(TRI_E_UNSUPPORTED, "tri_set_frame: AI frame blend (AiBlendConfig.w > 0) is outside the hot path");
+    c->ubo = *ubo;
+    mat4_mul(ubo->projection, ubo->view, c->pv);  // (P*V), Default.vert:104
+    if (clear)
+        c->clear_bgra = unorm8_host(clear[2]) | (unorm8_host(clear[1]) << 8) | (unorm8_host(clear[0]) << 16) |
+                        (unorm8_host(clear[3]) << 24);
+    c->frame_set = true;
+    return TRI_OK;
+}
+
+int tri_set_draws(tri_ctx* c, const tri_draw* d, uint32_t n) {
+    if (!c) return fail(TRI_E_INVALID, "tri_set_draws: null context");
+    if (n && !d) return fail(TRI_E_INVALID, "tri_set_draws: null draws");
+    c->draws.assign(d, d + n);
+    c->draws_dirty = true;
+    return TRI_OK;
+}
+
+int tri_bind_output(tri_ctx* c, void* color, void* depth) {
+    if (!c) return fail(TRI_E_INVALID, "tri_bind_output: null context");
+    c->d_color = color ? static_cast<uint32_t*>(color) : c->d_color_own;
+    c->d_depth = depth ? static_cast<float*>(depth) : c->d_depth_own;
+    return TRI_OK;
+}
+
+int tri_render(tri_ctx* c) {
+    if (!c) return fail(TRI_E_INVALID, "tri_render: null context");
+    if (!c->frame_set) return fail(TRI_E_STATE, "tri_render: tri_set_frame was not called");
+    if (!c->draws.empty() && !c->geometry_set) return fail(TRI_E_STATE, "tri_render: draws without geometry");
+    int rc = make_current(c);
+    if (rc) return rc;
+    if ((rc = upload_texture_table(c))) return rc;
+    if ((rc = resolve_draws(c))) return rc;
+    if (c->any_skin && !c->has_skin_data) {
+        // a skinned draw over vertices without weights: skin matrix = 0 -> everything collapses
+        // to the origin, exactly like the shader with all-zero weights; give the kernel zeros.
+        if ((rc = grow(c->d_skin, c->cap_skin, std::max<uint64_t>(c->nverts, 1)))) return rc;
+        HIP_TRY(hipMemsetAsync(c->d_skin, 0, std::max<uint64_t>(c->nverts, 1) * sizeof(TriVsSkin), c->stream));
+        c->has_skin_data = true;
+    }
+    if ((rc = ensure_work_buffers(c))) return rc;
+    HIP_TRY(hipMemsetAsync(c->d_ctr, 0, TRI_COUNTERS_RESET_BYTES, c->stream));
+
+    TriFrameParams fp;
+    std::memset(&fp, 0, sizeof fp);
+    fp.W = c->W; fp.H = c->H; fp.y0 = c->y0; fp.y1 = c->y1;
+    fp.nbx = c->nbx; fp.nby = c->nby; fp.nbins = c->nbins;
+    const uint32_t target_chunks = 512;
+    uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
+    ppt = std::min<uint32_t>(std::max<uint32_t>(ppt, 1), 32);
+    fp.ppt = (int32_t)ppt;
+    fp.nchunks = (c->nprims + ppt * TRI_BLOCK - 1) / (ppt * TRI_BLOCK);
+    fp.hw = (float)c->W * 0.5f;
+    fp.hh = (float)c->H * 0.5f;
+    fp.gx = (2.0f * TRI_GUARD_BAND_PX) / (float)c->W - 1.0f;
+    fp.gy = (2.0f * TRI_GUARD_BAND_PX) / (float)c->H - 1.0f;
+    fp.nprims = c->nprims;
+    fp.nslots = c->nslots;
+    fp.ndraws = c->ndraws;
+    fp.ovf_rec_cap = c->ovf_rec_cap;
+    fp.ovf_vert_cap = c->ovf_vert_cap;
+    fp.bin_cap = c->bin_cap;
+    fp.bone_count = c->nbones;
+    fp.clear_bgra = c->clear_bgra;
+    fp.write_depth = (c->cfg.flags & TRI_FLAG_NO_DEPTH_OUTPUT) ? 0u : 1u;
+    std::memcpy(fp.pv, c->pv, 64);
+    fp.ubo = c->ubo;
+    fp.mat0 = c->mat0;
+
+    TriDeviceBuffers b;
+    b.vin = c->d_vin;
+    b.vskin = c->any_skin ? c->d_skin : nullptr;
+    b.bones = c->d_bones;
+    b.vertex_count = c->nverts;
+    b.indices = c->d_idx;
+    b.draws = c->d_draws;
+    b.draw_vbase = c->d_vbase;
+    b.draw_pbase = c->d_pbase;
+    b.textures = c->d_texdesc;
+    b.srgb_lut = c->d_lut;
+    b.clip = c->d_clip;
+    b.vary = c->d_vary;
+    b.recs = c->d_recs;
+    b.brange = c->d_brange;
+    b.bin_total = c->d_bin_total;
+    b.bin_start = c->d_bin_start;
+    b.bin_cursor = c->d_bin_cursor;
+    b.bin_list = c->d_bin_list;
+    b.counters = c->d_ctr;
+    b.color = c->d_color;
+    b.depth = c->d_depth;
+
+    hipEvent_t* ev = nullptr;
+    TimingSet ts{};
+    if (c->timing) {
+        if (!c->free_sets.empty()) {
+            ts = c->free_sets.back();
+            c->free_sets.pop_back();
+        } else {
+            for (auto& e : ts.ev) HIP_TRY(hipEventCreate(&e));
+        }
+        ev = ts.ev;
+    }
+    HIP_TRY(tri_launch_frame(fp, b, c->stream, ev));
+    if (c->timing) c->pending.push_back(ts);
+    return TRI_OK;
+}
+
+int tri_synchronize(tri_ctx* c) {
+    if (!c) return fail(TRI_E_INVALID, "tri_synchronize: null context");
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    return check_overflow(c);
+}
+
+int tri_readback(tri_ctx* c, uint8_t* bgra, uint32_t* depth) {
+    if (!c) return fail(TRI_E_INVALID, "tri_readback: null context");
+    int rc = tri_synchronize(c);
+    if (rc) return rc;
+    const size_t px = (size_t)c->W * (size_t)(c->y1 - c->y0);
+    if (bgra) HIP_TRY(hipMemcpy(bgra, c->d_color, px * 4, hipMemcpyDeviceToHost));
+    if (depth) {
+        if (c->cfg.flags & TRI_FLAG_NO_DEPTH_OUTPUT)
+            return fail(TRI_E_STATE, "tri_readback: depth output disabled by TRI_FLAG_NO_DEPTH_OUTPUT");
+        HIP_TRY(hipMemcpy(depth, c->d_depth, px * 4, hipMemcpyDeviceToHost));
+    }
+    return TRI_OK;
+}
+
+int tri_set_timing(tri_ctx* c, int enable) {
+    if (!c) return fail(TRI_E_INVALID, "tri_set_timing: null context");
+    int rc = collect_timing(c);
+    if (rc) return rc;
+    c->timing = enable != 0;
+    c->acc = tri_timing{};
+    return TRI_OK;
+}
+
+int tri_get_timing(tri_ctx* c, tri_timing* out) {
+    if (!c || !out) return fail(TRI_E_INVALID, "tri_get_timing: null argument");
+    int rc = collect_timing(c);
+    if (rc) return rc;
+    *out = c->acc;
+    return TRI_OK;
+}
+
+int tri_get_frame_stats(tri_ctx* c, tri_frame_stats* out) {
+    if (!c || !out) return fail(TRI_E_INVALID, "tri_get_frame_stats: null argument");
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    TriCounters h;
+    HIP_TRY(hipMemcpy(&h, c->d_ctr, sizeof h, hipMemcpyDeviceToHost));
+    std::memset(out, 0, sizeof *out);
+    out->triangles_in = c->nprims;
+    out->triangles_setup = h.tris_setup;
+    out->triangles_clipped = h.tris_clipped;
+    out->bin_entries = h.bin_entries;
+    out->vertices_shaded = c->nslots;
+    out->bins_x = (uint32_t)c->nbx;
+    out->bins_y = (uint32_t)c->nby;
+    out->bin_size = TRI_BIN;
+    return TRI_OK;
+}
+
+}  // extern "C"

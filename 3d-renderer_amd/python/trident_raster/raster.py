@@ -1,0 +1,163 @@
+"""Python binding of the product C-ABI (libtri_raster.so, include/tri_raster.h).
+
+This is plumbing for tests and bench.py: every call goes straight to the HIP library. There is no
+CPU fallback — if the in-tree library is missing, import fails loudly.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.normpath(os.path.join(_HERE, "..", ".."))
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libtri_raster.so")
+
+_lib = None
+
+
+class TriError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"tri_raster error {code}: {msg}")
+        self.code = code
+
+
+def load_library(path=LIB_PATH):
+    """Load the HIP rasterizer library (built by `make -C 3d-renderer_amd`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"HIP rasterizer library not built: {path} (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, res, args in abi.CABI_FUNCTIONS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.tri_abi_version() != 1:
+        raise ImportError("tri_raster ABI version mismatch")
+    _lib = lib
+    return lib
+
+
+def _check(rc):
+    if rc != abi.TRI_OK:
+        msg = _lib.tri_last_error().decode(errors="replace")
+        raise TriError(rc, msg)
+
+
+def _ptr(a):
+    return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
+
+
+class TriRaster:
+    """One tri_ctx: a W x H framebuffer (optionally a row band) on one HIP device."""
+
+    def __init__(self, width, height, band=None, device=-1, flags=0):
+        lib = load_library()
+        cfg = abi.TriConfig()
+        cfg.width, cfg.height = width, height
+        cfg.band_y0, cfg.band_y1 = band if band is not None else (0, 0)
+        cfg.device = device
+        cfg.flags = flags
+        ctx = C.c_void_p()
+        _check(lib.tri_create(C.byref(cfg), C.byref(ctx)))
+        self._ctx = ctx
+        self.width, self.height = width, height
+        self.band = band if band is not None else (0, height)
+        self.rows = self.band[1] - self.band[0]
+
+    def close(self):
+        if self._ctx:
+            _lib.tri_destroy(self._ctx)
+            self._ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    # ---- uploads ----
+    def upload_geometry(self, vertices, indices, meshes):
+        v = np.ascontiguousarray(vertices, dtype=abi.VERTEX_DTYPE)
+        i = np.ascontiguousarray(indices, dtype=np.uint32)
+        m = np.ascontiguousarray(meshes, dtype=abi.MESH_RANGE_DTYPE)
+        _check(_lib.tri_upload_geometry(self._ctx, _ptr(v), v.size, _ptr(i), i.size, _ptr(m), m.size))
+
+    def upload_materials(self, records):
+        n = len(records)
+        arr = (abi.TriMaterialRecord * max(n, 1))()
+        for k, (base, factors) in enumerate(records):
+            arr[k].base_color_factor = (C.c_float * 4)(*base)
+            arr[k].material_factors = (C.c_float * 4)(*factors)
+        _check(_lib.tri_upload_materials(self._ctx, arr, n))
+
+    def upload_texture(self, slot, rgba8):
+        t = np.ascontiguousarray(rgba8, dtype=np.uint8)
+        assert t.ndim == 3 and t.shape[2] == 4
+        _check(_lib.tri_upload_texture(self._ctx, slot, _ptr(t), t.shape[1], t.shape[0]))
+
+    def upload_bone_palette(self, mats):
+        m = np.ascontiguousarray(mats, dtype=np.float32).reshape(-1, 16)
+        _check(_lib.tri_upload_bone_palette(self._ctx, _ptr(m), m.shape[0]))
+
+    # ---- frame ----
+    def set_frame(self, ubo, clear=(0.005, 0.005, 0.005, 1.0)):
+        cl = (C.c_float * 4)(*clear)
+        _check(_lib.tri_set_frame(self._ctx, C.byref(ubo), C.byref(cl)))
+
+    def set_draws(self, draws):
+        arr, n = abi.draws_array(draws)
+        _check(_lib.tri_set_draws(self._ctx, arr, n))
+
+    def set_stream(self, stream_ptr):
+        _check(_lib.tri_set_stream(self._ctx, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def bind_output(self, color_ptr, depth_ptr):
+        _check(_lib.tri_bind_output(self._ctx, C.c_void_p(color_ptr) if color_ptr else None,
+                                    C.c_void_p(depth_ptr) if depth_ptr else None))
+
+    def render(self):
+        _check(_lib.tri_render(self._ctx))
+
+    def synchronize(self):
+        _check(_lib.tri_synchronize(self._ctx))
+
+    def readback(self, depth=True):
+        """Returns (bgra uint8 [rows, W, 4], depth uint32 bits [rows, W] or None)."""
+        col = np.empty((self.rows, self.width, 4), dtype=np.uint8)
+        dep = np.empty((self.rows, self.width), dtype=np.uint32) if depth else None
+        _check(_lib.tri_readback(self._ctx, _ptr(col), _ptr(dep) if depth else None))
+        return col, dep
+
+    def render_frame(self, retries=2):
+        """render + synchronize, re-rendering once after an internal-buffer overflow (buffers grow)."""
+        for attempt in range(retries + 1):
+            self.render()
+            try:
+                self.synchronize()
+                return
+            except TriError as e:
+                if e.code != abi.TRI_E_OVERFLOW or attempt == retries:
+                    raise
+
+    def set_timing(self, enable):
+        _check(_lib.tri_set_timing(self._ctx, 1 if enable else 0))
+
+    def timing(self):
+        t = abi.TriTiming()
+        _check(_lib.tri_get_timing(self._ctx, C.byref(t)))
+        return {k: getattr(t, k) for k, _ in abi.TriTiming._fields_}
+
+    def frame_stats(self):
+        s = abi.TriFrameStats()
+        _check(_lib.tri_get_frame_stats(self._ctx, C.byref(s)))
+        return {k: getattr(s, k) for k, _ in abi.TriFrameStats._fields_}

@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Hot-path benchmark: frames/s of the HIP software rasterizer on BASELINE.json's configs.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--config c3|c2|c1]
+  python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 ... bench.py --gpus N
+
+One step = one frame of Trident's graphics-pipeline stage: the per-frame UBO + draw-list update
+(UpdateUniformBuffer / push constants, Renderer.cpp:5822-6051, :5110-5151) and the five gfx950
+kernels (vs_transform, tri_setup_bin, bin scan, scatter, tile_raster_shade) over geometry resident
+in HBM; N > 1 = sort-first row bands (geometry replicated) + an RCCL all-gather of the BGRA8 bands
+into the full frame on every rank. value = whole frames per second (strong scaling: a frame's work
+is fixed, N GPUs share it). Rank 0 prints ONE JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "3d-renderer_amd", "python"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md)
+METRIC = "frames/sec + Mpixels/sec at 1080p & 4K; achieved HBM GB/s vs roofline"
+
+
+def build_scene(name):
+    from trident_raster import scenes
+
+    if name == "c3":
+        return scenes.scene_c3_grid(3840, 2160, 708)
+    if name == "c2":
+        return scenes.scene_c2_sphere(1920, 1080)
+    if name == "c1":
+        return scenes.scene_c1_cube(0, 640, 480)
+    raise SystemExit(f"unknown config {name}")
+
+
+class BandRenderer:
+    """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers."""
+
+    def __init__(self, scene, rank, world, device_index):
+        import torch
+        from trident_raster import raster, scenes
+
+        H, W = scene.height, scene.width
+        assert H % world == 0, "row bands must be equal for all_gather_into_tensor"
+        rows = H // world
+        self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
+        self.band = (rank * rows, (rank + 1) * rows)
+        self.dev = torch.device("cuda", device_index)
+        self.color = torch.empty(rows * W, dtype=torch.int32, device=self.dev)
+        self.depth = torch.empty(rows * W, dtype=torch.float32, device=self.dev)
+        self.frame = torch.empty(H * W, dtype=torch.int32, device=self.dev) if world > 1 else self.color
+        self.r = raster.TriRaster(W, H, band=self.band, device=device_index)
+        self.r.bind_output(self.color.data_ptr(), self.depth.data_ptr())
+        self.r.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+        scenes.load_scene(self.r, scene)
+
+    def step(self):
+        s = self.scene
+        self.r.set_frame(s.ubo, s.clear)  # per-frame uniform update
+        self.r.set_draws(s.draws)         # per-frame draw list (push constants)
+        self.r.render()
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.all_gather_into_tensor(self.frame, self.color)
+
+
+def timed_run(br, steps, warmup, dist_on):
+    import torch
+
+    for _ in range(warmup):
+        br.step()
+    br.r.synchronize()
+    torch.cuda.synchronize(br.dev)
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.barrier()
+    br.r.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        br.step()
+    torch.cuda.synchronize(br.dev)
+    if dist_on:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    br.r.synchronize()  # surfaces TRI_E_OVERFLOW if any timed frame overflowed
+    timing = br.r.timing()
+    br.r.set_timing(False)
+    if dist_on:
+        t = torch.tensor([dt], dtype=torch.float64, device=br.dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, timing
+
+
+def cpu_baseline(scene, seconds):
+    """The CPU oracle (a multithreaded C++ port of the same pipeline) on this host's cores, over a
+    bounded sample of whole frames of the same workload (lavapipe is absent on this image)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import oracle_py
+
+    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    oracle_py.render(scene, threads=threads)  # warm-up frame (page-in, allocator)
+    n, t0 = 0, time.perf_counter()
+    while True:
+        oracle_py.render(scene, threads=threads)
+        n += 1
+        if time.perf_counter() - t0 >= seconds:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{n} full {scene.width}x{scene.height} frame(s) of {scene.name} "
+                      f"({scene.triangles} tris) rendered by oracle/tri_oracle.cpp, {dt:.1f} s"}
+
+
+def pmc_traffic(workload, rows_frac):
+    """HBM bytes per k_raster launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(workload, {}).get("k_raster")
+        return None if e is None else float(e["hbm_bytes_per_launch"]) * rows_frac
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--config", default="c3")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-secondary", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus and world > 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    import torch
+
+    torch.cuda.set_device(local)
+    dist_on = world > 1
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    scene = build_scene(args.config)
+    br = BandRenderer(scene, rank, world, local)
+    dt, timing = timed_run(br, args.steps, args.warmup, dist_on)
+    fps = args.steps / dt
+    W, H = scene.width, scene.height
+    stats = br.r.frame_stats()
+
+    # roofline of the dominant kernel (k_raster = tile_raster_shade): its algorithmic bytes per
+    # launch are the colour + depth it must store for its band (4 + 4 B per pixel).
+    frames_timed = max(int(timing["frames"]), 1)
+    raster_ms = timing["ms_raster"] / frames_timed
+    frame_ms = timing["ms_frame"] / frames_timed
+    raster_bytes = 8.0 * W * br.rows
+    achieved = raster_bytes / (raster_ms * 1e-3) / 1e9
+    frame_bytes = scene.algorithmic_bytes(rows=br.rows)
+    traffic = pmc_traffic(scene.name, br.rows / H)
+
+    secondary = {}
+    if not args.no_secondary and args.config == "c3":
+        s2 = build_scene("c2")
+        br2 = BandRenderer(s2, rank, world, local)
+        dt2, t2 = timed_run(br2, max(args.steps, 50), args.warmup, dist_on)
+        fps2 = max(args.steps, 50) / dt2
+        secondary = {"c2_sphere50k_1920x1080": {"frames_per_s": fps2, "mpix_per_s": fps2 * s2.width * s2.height / 1e6,
+                                                "ms_per_frame": 1e3 / fps2,
+                                                "raster_kernel_ms": t2["ms_raster"] / max(t2["frames"], 1)}}
+        br2.r.close()
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(scene, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": fps,
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": dt / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (procedural PCG32-seeded scene; reference Assimp assets absent)",
+            "config": {"workload": scene.name, "width": W, "height": H, "triangles": scene.triangles,
+                       "vertices": int(scene.vertices.shape[0]), "bin": stats["bin_size"],
+                       "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+            "mpix_per_s": fps * W * H / 1e6,
+            "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_raster",
+                         "kernel_ms": raster_ms, "algorithmic_bytes": raster_bytes},
+            "frame_roofline": {"algorithmic_bytes": frame_bytes, "gpu_ms": frame_ms,
+                               "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9,
+                               "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+            "stage_ms": {k: timing[k] / frames_timed for k in
+                         ("ms_vertex", "ms_setup", "ms_binscan", "ms_scatter", "ms_raster", "ms_frame")},
+            "frame_stats": stats,
+            "secondary": secondary,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    br.r.close()
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

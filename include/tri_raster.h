@@ -1,0 +1,221 @@
+/*
+ * tri_raster.h — C-ABI drop-in boundary for the MI355X (gfx950) HIP software rasterizer that
+ * replaces Trident's Vulkan graphics-pipeline stage (the work recorded by
+ * Renderer::RecordCommandBuffer, Trident/src/Renderer/Renderer.cpp:4890-5636, and executed by the
+ * driver with Default.vert / Default.frag).
+ *
+ * Plain C: no torch, no HIP types in the signatures. Device memory, streams and events are owned by
+ * the context; callers pass host pointers (copied) except in tri_bind_output / tri_set_stream, which
+ * take opaque device pointers / a hipStream_t as void*.
+ *
+ * Every entry point returns an int status (TRI_OK == 0, negative on error) and records a message
+ * readable through tri_last_error() — mirroring the reference's "bool + TR_CORE_* log, no exceptions
+ * on the frame path" convention (Renderer.cpp:779-824). One host thread per context; not thread-safe
+ * (Application.cpp:82-134 is a single render thread).
+ *
+ * Which reference interface each entry point replaces is noted next to it. The C++
+ * Trident::Renderer-compatible shim (3d-renderer_amd/host/) calls these; INTEGRATION.md shows the
+ * binding a Trident maintainer would add.
+ */
+#ifndef TRI_RASTER_H
+#define TRI_RASTER_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TRI_RASTER_ABI_VERSION 1
+
+/* ---- status codes ---------------------------------------------------------------------- */
+#define TRI_OK 0
+#define TRI_E_INVALID (-1)     /* bad argument (null, out of range, size mismatch)              */
+#define TRI_E_HIP (-2)         /* HIP runtime error (no device, launch failure, ...)            */
+#define TRI_E_OOM (-3)         /* device allocation failed                                      */
+#define TRI_E_OVERFLOW (-4)    /* a frame overflowed an internal bin/clip buffer; buffers were   *
+                                * grown, re-render the frame                                    */
+#define TRI_E_UNSUPPORTED (-5) /* feature outside the hot path (AI frame blend)                 */
+#define TRI_E_STATE (-6)       /* call order violated (e.g. render before geometry upload)      */
+
+/* ---- limits mirrored from the reference ----------------------------------------------- */
+#define TRI_MAX_POINT_LIGHTS 8   /* kMaxPointLights, UniformBuffer.h:7                           */
+#define TRI_MAX_TEXTURE_SLOTS 256 /* Pipeline.h:18 (sampler2D BaseColorSamplers[256])            */
+#define TRI_MAX_BONE_INFLUENCES 4 /* Vertex::MaxBoneInfluences, Vertex.h:11                      */
+#define TRI_MAX_DIM 8192          /* framebuffer width/height limit (guard-band fixed point)    */
+
+/* ---- GPU ABI structs: byte-identical to the reference's --------------------------------- */
+
+/* Vertex (Trident/src/Renderer/Vertex.h:9-78): glm without SIMD alignment => 100-byte stride.
+ * Offsets: Position 0, Normal 12, Tangent 24, Bitangent 36, Color 48, TexCoord 60,
+ * BoneIndices 68, BoneWeights 84. */
+typedef struct tri_vertex {
+    float position[3];
+    float normal[3];
+    float tangent[3];
+    float bitangent[3];
+    float color[3];
+    float texcoord[2];
+    int32_t bone_indices[4];
+    float bone_weights[4];
+} tri_vertex;
+
+/* MeshDrawInfo (Renderer.h:293-299): one per uploaded mesh; indices are mesh-local and
+ * base_vertex is added at draw time (Renderer.cpp:2032-2038, :2062-2077). */
+typedef struct tri_mesh_range {
+    uint32_t first_index;
+    uint32_t index_count;
+    int32_t base_vertex;
+    int32_t material_index;
+} tri_mesh_range;
+
+/* RenderablePushConstant (Trident/src/Renderer/RenderData.h:14-30), 128 bytes. */
+typedef struct tri_push_constant {
+    float model[16]; /* column-major glm::mat4 */
+    float tint[4];
+    float texture_scale[2];
+    float texture_offset[2];
+    float tiling_factor;
+    int32_t texture_slot;
+    int32_t use_material_override;
+    float sort_bias;
+    int32_t material_index;
+    int32_t padding0;
+    int32_t bone_offset;
+    int32_t bone_count;
+} tri_push_constant;
+
+/* One vkCmdDrawIndexed(IndexCount, 1, FirstIndex, BaseVertex, 0) + its push constant
+ * (Renderer.cpp:5110-5151). mesh_index selects a tri_mesh_range. */
+typedef struct tri_draw {
+    uint32_t mesh_index;
+    uint32_t reserved[3];
+    tri_push_constant pc;
+} tri_draw;
+
+/* PointLightUniform (UniformBuffer.h:10-14). */
+typedef struct tri_point_light {
+    float position_range[4];  /* xyz = world position, w = radius */
+    float color_intensity[4]; /* rgb = colour, w = intensity      */
+} tri_point_light;
+
+/* GlobalUniformBuffer (UniformBuffer.h:17-28), 480 bytes std140, as written by
+ * Renderer::UpdateUniformBuffer (Renderer.cpp:5822-6051). */
+typedef struct tri_global_ubo {
+    float view[16];
+    float projection[16];
+    float camera_position[4];
+    float ambient_color_intensity[4];
+    float directional_light_direction[4];
+    float directional_light_color[4];
+    uint32_t light_counts[4];
+    float ai_blend_config[4];
+    tri_point_light point_lights[TRI_MAX_POINT_LIGHTS];
+} tri_global_ubo;
+
+/* MaterialUniformBuffer (UniformBuffer.h:31-35). Only record 0 is read by Default.frag:58-62. */
+typedef struct tri_material_record {
+    float base_color_factor[4];
+    float material_factors[4]; /* x metallic, y roughness, z ambient strength, w reserved */
+} tri_material_record;
+
+/* Context configuration. The viewport is always the full width x height framebuffer
+ * (Renderer.cpp:5062-5069: x=y=0, minDepth 0, maxDepth 1). band_y0/band_y1 select the row band
+ * this context rasterizes (multi-GPU screen partition); 0/0 means all rows. */
+typedef struct tri_config {
+    uint32_t width;
+    uint32_t height;
+    uint32_t band_y0;
+    uint32_t band_y1;
+    int32_t device; /* HIP device ordinal; -1 = current device */
+    uint32_t flags; /* TRI_FLAG_* */
+} tri_config;
+
+#define TRI_FLAG_NO_DEPTH_OUTPUT 0x1u /* skip the depth write (reference storeOp DONT_CARE) */
+
+/* Per-stage accumulated device time (HIP events on the context stream) and last-frame counters. */
+typedef struct tri_timing {
+    uint64_t frames;        /* frames timed since the last reset                  */
+    double ms_vertex;       /* vs_transform                                        */
+    double ms_setup;        /* tri_setup_bin (setup + clip + per-bin counts)       */
+    double ms_binscan;      /* bin prefix scan                                     */
+    double ms_scatter;      /* bin list scatter                                    */
+    double ms_raster;       /* tile_raster_shade (coverage + early-Z + PBR + store) */
+    double ms_frame;        /* first kernel start to last kernel end              */
+} tri_timing;
+
+typedef struct tri_frame_stats {
+    uint64_t triangles_in;      /* primitives submitted                            */
+    uint64_t triangles_setup;   /* primitives surviving clip/cull/snap             */
+    uint64_t triangles_clipped; /* primitives that went through geometric clipping */
+    uint64_t bin_entries;       /* (triangle, bin) pairs                           */
+    uint64_t vertices_shaded;   /* vertex-shader invocations                       */
+    uint32_t bins_x, bins_y, bin_size, reserved;
+} tri_frame_stats;
+
+typedef struct tri_ctx tri_ctx;
+
+/* ---- lifetime ---------------------------------------------------------------------------- */
+/* Renderer::Init (Renderer.h:115, Renderer.cpp:587-648): allocates the colour/depth targets and
+ * the default 1x1 white texture in slot 0 (Renderer.cpp:3404-3436). */
+int tri_create(const tri_config* config, tri_ctx** out_ctx);
+/* Renderer::Shutdown (Renderer.h:116). Null is accepted. */
+int tri_destroy(tri_ctx* ctx);
+/* Use an external hipStream_t (passed as void*) for every launch/copy; NULL = the context's own. */
+int tri_set_stream(tri_ctx* ctx, void* hip_stream);
+const char* tri_last_error(void);
+int tri_abi_version(void);
+
+/* ---- data upload (copies) ---------------------------------------------------------------- */
+/* Renderer::UploadMesh / AppendMeshes -> UploadMeshFromCache (Renderer.h:120-121,
+ * Renderer.cpp:1965-2116): one concatenated vertex buffer, one uint32 mesh-local index buffer and
+ * one MeshDrawInfo per mesh. Replaces the whole geometry set. */
+int tri_upload_geometry(tri_ctx* ctx, const tri_vertex* vertices, uint64_t vertex_count,
+                        const uint32_t* indices, uint64_t index_count,
+                        const tri_mesh_range* meshes, uint32_t mesh_count);
+/* Material buffer payload (BuildMaterialPayload, Renderer.cpp:5927-5951). count 0 => the default
+ * record {1,1,1,1},{1,1,1,0} (Renderer.cpp:5941-5943). */
+int tri_upload_materials(tri_ctx* ctx, const tri_material_record* records, uint32_t count);
+/* Texture slot upload (PopulateTextureSlot, Renderer.cpp:3469-3620): R8G8B8A8_SRGB texels,
+ * row-major, rows already flipped by the loader (TextureLoader.cpp:290-304). slot < 256. */
+int tri_upload_texture(tri_ctx* ctx, uint32_t slot, const uint8_t* rgba8_srgb, uint32_t width,
+                       uint32_t height);
+/* Bone palette SSBO (binding 4, PrepareBonePaletteBuffer Renderer.cpp:3168-3245):
+ * column-major mat4s. */
+int tri_upload_bone_palette(tri_ctx* ctx, const float* matrices, uint32_t matrix_count);
+
+/* ---- per frame --------------------------------------------------------------------------- */
+/* UpdateUniformBuffer's vkCmdUpdateBuffer (Renderer.cpp:5958) + the colour clear value
+ * (Renderer.cpp:5037-5050, SetClearColor Renderer.h:187). */
+int tri_set_frame(tri_ctx* ctx, const tri_global_ubo* ubo, const float clear_rgba[4]);
+/* The per-draw loop of RecordCommandBuffer (Renderer.cpp:5110-5151): draws in submission order. */
+int tri_set_draws(tri_ctx* ctx, const tri_draw* draws, uint32_t draw_count);
+/* Render into caller-owned device buffers (e.g. torch tensors for an RCCL all-gather):
+ * colour = band_rows * width uint32 BGRA8 texels, depth = band_rows * width float32. NULL resets
+ * to the context's own buffers. */
+int tri_bind_output(tri_ctx* ctx, void* device_bgra8, void* device_depth);
+/* Enqueue one frame on the context stream (asynchronous: vkQueueSubmit, Renderer.cpp:5679). */
+int tri_render(tri_ctx* ctx);
+/* Wait for the stream; reports TRI_E_OVERFLOW if a queued frame overflowed an internal buffer. */
+int tri_synchronize(tri_ctx* ctx);
+/* Frame readback (Renderer.cpp:5297-5338, :1299-1389): synchronous copy of the band, tightly packed
+ * BGRA8 (width*4 bytes per row) and float32 depth bits. Either pointer may be NULL. */
+int tri_readback(tri_ctx* ctx, uint8_t* bgra8, uint32_t* depth_bits);
+
+/* ---- measurement -------------------------------------------------------------------------- */
+int tri_set_timing(tri_ctx* ctx, int enable);      /* also resets the accumulators       */
+int tri_get_timing(tri_ctx* ctx, tri_timing* out); /* synchronizes                      */
+int tri_get_frame_stats(tri_ctx* ctx, tri_frame_stats* out); /* synchronizes           */
+
+#ifdef __cplusplus
+} /* extern "C" */
+
+static_assert(sizeof(tri_vertex) == 100, "Vertex stride must match Trident's 100-byte Vertex");
+static_assert(sizeof(tri_push_constant) == 128, "RenderablePushConstant is 128 bytes");
+static_assert(sizeof(tri_draw) == 144, "tri_draw layout");
+static_assert(sizeof(tri_global_ubo) == 480, "GlobalUniformBuffer is 480 bytes");
+static_assert(sizeof(tri_material_record) == 32, "MaterialUniformBuffer is 32 bytes");
+#endif
+
+#endif /* TRI_RASTER_H */

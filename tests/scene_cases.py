@@ -1,0 +1,137 @@
+"""Parity scenes shared by the CPU golden tests and the GPU parity tests.
+
+Each builder returns a trident_raster.scenes.Scene whose inputs are fully determined (Forge-style
+camera/entities, reference primitive meshes restated by the oracle, procedural meshes)."""
+import numpy as np
+
+from trident_raster import abi, scenes
+
+F = np.float32
+
+
+def c1_cube(frame=0, w=640, h=480):
+    return scenes.scene_c1_cube(frame, w, h)
+
+
+def primitives_row(oracle, w=320, h=240):
+    """Cube, sphere and quad primitives side by side (CreatePrimitiveEntity), editor camera (0,3,8)."""
+    cam = (0.0, 3.0, 8.0)
+    view, proj, fwd = oracle.editor_camera(cam, (0, 0, 0), 60.0, (w, h))
+    verts, idxs, meshes = [], [], []
+    vbase = ibase = 0
+    for kind in (1, 2, 3):
+        v, i = oracle.build_primitive(kind)
+        meshes.append((ibase, i.size, vbase, len(meshes)))
+        verts.append(v)
+        idxs.append(i)
+        vbase += v.size
+        ibase += i.size
+    m = np.array(meshes, dtype=abi.MESH_RANGE_DTYPE)
+    draws = []
+    for k, x in enumerate((-1.6, 0.0, 1.6)):
+        model = oracle.compose_transform((x, 3.0, 3.0), (20.0 * k, 35.0 + 10 * k, 5.0 * k), (1.0, 1.0, 1.0))
+        draws.append(abi.make_draw(k, model, texture_slot=0, material_index=k))
+    ubo = oracle.pack_ubo(view, proj, cam, [])
+    return scenes.Scene("primitives", w, h, np.concatenate(verts), np.concatenate(idxs), m, draws, ubo,
+                        materials=[((1, 1, 1, 1), (0.0, 1.0, 1.0, 0.0))] * 3)
+
+
+def sphere_c2(w=1920, h=1080, rings=125, segments=200, oracle=None):
+    s = scenes.scene_c2_sphere(w, h, rings, segments)
+    if oracle is not None:  # reference sphere builder restated by the oracle (glibc sin/cos)
+        v, i = oracle.build_uv_sphere(rings, segments, 3.0)
+        s.vertices, s.indices = v, i
+        s.meshes = np.array([(0, i.size, 0, 0)], dtype=abi.MESH_RANGE_DTYPE)
+    return s
+
+
+def grid_c3(w=1280, h=720, n=200):
+    return scenes.scene_c3_grid(w, h, n)
+
+
+def checker_texture(wt=16, ht=8, seed=7):
+    rng = np.random.default_rng(seed)
+    t = rng.integers(0, 256, size=(ht, wt, 4), dtype=np.uint8)
+    t[..., 3] = rng.integers(128, 256, size=(ht, wt), dtype=np.uint8)
+    return t
+
+
+def textured_grid(w=640, h=360, n=40):
+    s = scenes.scene_c3_grid(w, h, n)
+    s.textures = [(3, checker_texture())]
+    s.draws = [abi.make_draw(0, np.eye(4, dtype=F), texture_slot=3, material_index=0, tint=(1.0, 0.9, 0.8, 0.75),
+                             texture_scale=(1.5, 0.75), texture_offset=(0.1, -0.2), tiling=1.25)]
+    return s
+
+
+def near_clip_grid(w=640, h=480, n=60):
+    """Camera pitched down over a ground plane that passes through the near plane and behind the
+    eye: exercises homogeneous clipping (w <= 0, z < 0) and the guard band."""
+    cam = (0.0, 0.35, 0.0)
+    view, proj = scenes.editor_camera(cam, (-28.0, 12.0, 0.0), 70.0, (w, h), 0.1, 40.0)
+    v, idx = scenes.displaced_grid_mesh(n, extent=(30.0, 30.0), depth=0.0, amplitude=0.15)
+    # grid lies in x-y; rotate it to the x-z ground plane facing +y
+    model = scenes.compose_transform((0.0, 0.0, -5.0), (-90.0, 0.0, 0.0), (1.0, 1.0, 1.0))
+    lights = [{"type": "point", "position": (0.5, 1.0, -2.0), "range": 6.0, "intensity": 8.0}]
+    return scenes.Scene("near_clip", w, h, v, idx, np.array([(0, idx.size, 0, 0)], abi.MESH_RANGE_DTYPE),
+                        [abi.make_draw(0, model, material_index=0)], scenes.pack_ubo(view, proj, cam, lights),
+                        materials=[((0.8, 0.8, 0.8, 1.0), (0.5, 0.3, 1.0, 0.0))])
+
+
+def depth_ties(w=256, h=256):
+    """Two coplanar quads: the later draw must win every tie (LESS_OR_EQUAL), plus a far-plane
+    straddling quad (per-pixel far clip)."""
+    quad_v, quad_i = scenes.cube_mesh()  # reuse vertex layout; build a quad by hand below
+    v = np.zeros(4, abi.VERTEX_DTYPE)
+    v["position"] = [(-1, -1, 0), (1, -1, 0), (1, 1, 0), (-1, 1, 0)]
+    v["normal"] = (0, 0, 1)
+    v["color"] = 1.0
+    v["texcoord"] = [(0, 0), (1, 0), (1, 1), (0, 1)]
+    idx = np.array([0, 1, 2, 0, 2, 3], np.uint32)
+    meshes = np.array([(0, 6, 0, 0)], abi.MESH_RANGE_DTYPE)
+    cam = (0.0, 0.0, 4.0)
+    view, proj = scenes.editor_camera(cam, (0, 0, 0), 60.0, (w, h), 0.1, 6.0)
+    m1 = scenes.compose_transform((0, 0, 0), (0, 0, 0), (1, 1, 1))
+    m2 = scenes.compose_transform((0.3, 0.2, 0), (0, 0, 0), (1, 1, 1))
+    m3 = scenes.compose_transform((0.0, -0.5, -1.0), (70.0, 0, 0), (3, 3, 3))  # pokes past far = 6
+    draws = [abi.make_draw(0, m1, tint=(1, 0.2, 0.2, 1)), abi.make_draw(0, m2, tint=(0.2, 1, 0.2, 1)),
+             abi.make_draw(0, m1, tint=(0.2, 0.2, 1, 1)), abi.make_draw(0, m3, tint=(1, 1, 0.3, 1))]
+    return scenes.Scene("depth_ties", w, h, v, idx, meshes, draws, scenes.pack_ubo(view, proj, cam, []),
+                        materials=[((1, 1, 1, 1), (0.2, 0.5, 1.0, 0.0))])
+
+
+def skinned_quad(oracle, w=256, h=256):
+    """GPU skinning branch (Default.vert:64-85): 2-bone palette at an offset, weights per vertex,
+    one out-of-range bone index (skipped)."""
+    v, i = oracle.build_primitive(3)
+    v["bone_indices"] = [(0, 1, 0, 0), (1, 0, 0, 0), (0, 5, 0, 0), (1, 1, 0, 0)]
+    v["bone_weights"] = [(0.75, 0.25, 0, 0), (1.0, 0, 0, 0), (0.6, 0.4, 0, 0), (0.5, 0.5, 0, 0)]
+    bones = np.stack([np.eye(4, dtype=F).reshape(16),
+                      np.eye(4, dtype=F).reshape(16),
+                      oracle.compose_transform((0.2, 0.1, 0.0), (0, 0, 25.0), (1.2, 0.9, 1.0)).reshape(16)])
+    cam = (0.0, 0.0, 2.0)
+    view, proj, _ = oracle.editor_camera(cam, (0, 0, 0), 60.0, (w, h))
+    model = oracle.compose_transform((0.0, 0.0, 0.0), (0.0, 0.0, 0.0), (1, 1, 1))
+    d = abi.make_draw(0, model, bone_offset=1, bone_count=2)
+    return scenes.Scene("skinned", w, h, v, i, np.array([(0, i.size, 0, 0)], abi.MESH_RANGE_DTYPE), [d],
+                        oracle.pack_ubo(view, proj, cam, []), materials=[], bones=bones)
+
+
+def invalid_inputs(oracle, w=200, h=150):
+    """Bad mesh index, out-of-range vertex index, empty mesh: silently skipped (Renderer.cpp:2946-2956,
+    :5118-5127); the valid cube still renders."""
+    v, i = oracle.build_primitive(1)
+    bad = np.concatenate([i, np.array([0, 1, 999], np.uint32)])
+    meshes = np.array([(0, i.size, 0, 0), (i.size, 3, 0, 0), (0, 0, 0, 0)], abi.MESH_RANGE_DTYPE)
+    cam = (0.0, 0.0, 3.0)
+    view, proj, _ = oracle.editor_camera(cam, (0, 0, 0), 60.0, (w, h))
+    model = oracle.compose_transform((0.0, 0.0, 0.0), (30.0, 40.0, 0.0), (1, 1, 1))
+    draws = [abi.make_draw(7, model), abi.make_draw(1, model), abi.make_draw(2, model), abi.make_draw(0, model)]
+    return scenes.Scene("invalid", w, h, v, bad, meshes, draws, oracle.pack_ubo(view, proj, cam, []))
+
+
+def empty_scene(w=128, h=96):
+    view, proj = scenes.editor_camera((0, 0, 5), (0, 0, 0), 60.0, (w, h))
+    return scenes.Scene("empty", w, h, np.zeros(0, abi.VERTEX_DTYPE), np.zeros(0, np.uint32),
+                        np.zeros(0, abi.MESH_RANGE_DTYPE), [], scenes.pack_ubo(view, proj, (0, 0, 5)),
+                        clear=(0.1, 0.2, 0.3, 1.0))
