@@ -1,12 +1,12 @@
 // raster_common.h — device-side data layout shared by the HIP kernels and the C-ABI host code.
 // HBM layout:
 //   VsIn      48 B/vertex  {pos.xyz, normal.xyz, color.xyz, uv.xy, pad} (the 44 B of the 100-byte
-//                          Trident Vertex that reach the output; Vertex.h:9-78), SoA-of-records
+//                          Trident Vertex that reach the output; Vertex.h:9-78)
 //   VsSkin    32 B/vertex  {bone indices, bone weights}, only when any draw has BoneCount > 0
 //   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation
 //   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
 //   TriRec    64 B/record  snapped screen vertices, NDC z, 1/w, (prim<<3|sub), 3 vary slots
-//   binrange   8 B/record  (bx0, by0, bx1, by1) in 64x64-pixel bins
+//   brange     8 B/record  (bx0|by0<<16, bx1|by1<<16) in 64x64-pixel bins
 //   bin_list   4 B/entry   record ids per bin (order-free: visibility is resolved by a 64-bit key)
 //   colour     4 B/pixel   B8G8R8A8_UNORM;  depth 4 B/pixel D32_SFLOAT bits
 #pragma once
@@ -20,14 +20,18 @@
 #define TRI_PRIM_MAX ((1u << 29) - 1u)
 #define TRI_REC_CULLED 0xFFFFFFFFu
 #define TRI_REC_CLIPPED 0xFFFFFFFEu
+#define TRI_BR_CULLED 0xFFFFFFFFu
+#define TRI_BR_CLIPPED 0xFFFFFFFEu
 #define TRI_MAX_CLIP_VERTS 12
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f
+#define TRI_CLIP_GRID 64
 
-// overflow flag bits (tri_ctx counters.flags)
+// overflow flag bits (TriCounters.flags)
 #define TRI_OVF_CLIP_RECORDS 0x1u
 #define TRI_OVF_CLIP_VERTS 0x2u
 #define TRI_OVF_BIN_LIST 0x4u
+#define TRI_OVF_CLIP_QUEUE 0x8u
 
 struct __attribute__((aligned(16))) TriVsIn {
     float px, py, pz, nx;
@@ -50,19 +54,27 @@ struct __attribute__((aligned(16))) TriRec {
 };
 static_assert(sizeof(TriRec) == 64, "TriRec must be one 64-byte line");
 
+// Per-draw vertex-stage constants (push constant + hoisted normal matrix).
 struct __attribute__((aligned(16))) TriDrawDev {
     float model[16];
-    float tint[4];
+    float nm[9];         // transpose(inverse(mat3(model))), glm cofactor form, computed on the host
     float tex_scale[2];
     float tex_offset[2];
     float tiling;
-    int32_t tex_id;      // resolved texture table index (unused slots alias slot 0)
     int32_t bone_offset;
     int32_t bone_count;
     int32_t first_index;
     int32_t base_vertex;
     uint32_t min_index;
     uint32_t vert_count; // VS invocations for this draw (max-min+1), 0 = inactive
+    uint32_t pad[3];
+};
+
+// Per-draw fragment-stage constants.
+struct __attribute__((aligned(16))) TriDrawShade {
+    float tint[4];
+    int32_t tex_id;  // texture table index (unused slots alias slot 0)
+    int32_t pad[3];
 };
 
 struct TriTexDesc {
@@ -76,10 +88,24 @@ struct TriCounters {  // per-frame fields are zeroed before every frame; `flags`
     uint32_t tris_setup;
     uint32_t tris_clipped;
     uint32_t bin_entries;
-    uint32_t pad[2];
+    uint32_t clip_queue;
+    uint32_t pad;
     uint32_t flags;
 };
 #define TRI_COUNTERS_RESET_BYTES 28
+
+// Frame constants of Default.frag hoisted on the host (fast shading path).
+struct TriShadeConst {
+    float cam[4];
+    float base[4];        // MaterialUniformBuffer[0].BaseColorFactor
+    float metallic, roughness, amb_strength, pad0;
+    float amb[4];         // AmbientColorIntensity.rgb * .w
+    uint32_t has_sun, npt, pad1, pad2;
+    float sun_l[4];       // normalize(-DirectionalLightDirection)
+    float sun_rad[4];     // DirectionalLightColor.rgb * .w
+    float pl_pos[TRI_MAX_POINT_LIGHTS][4];  // xyz, 1/max(radius, 1e-4)
+    float pl_rad[TRI_MAX_POINT_LIGHTS][4];  // ColorIntensity.rgb * .w
+};
 
 struct TriFrameParams {
     int32_t W, H, y0, y1;
@@ -89,8 +115,10 @@ struct TriFrameParams {
     uint32_t ovf_rec_cap, ovf_vert_cap, bin_cap, bone_count;
     uint32_t clear_bgra;
     uint32_t write_depth;
-    uint32_t pad0, pad1;
+    uint32_t exact_shading;
+    uint32_t pad0;
     float pv[16];
     tri_global_ubo ubo;
     tri_material_record mat0;
+    TriShadeConst sc;
 };

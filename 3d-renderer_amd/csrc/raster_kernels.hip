@@ -1,17 +1,22 @@
 // raster_kernels.hip — hand-written gfx950 (CDNA4) kernels for Trident's graphics-pipeline stage.
 //
 //   k_vertex   vs_transform   Default.vert:60-105, one lane per (draw, referenced vertex)
-//   k_setup    tri_setup_bin  primitive assembly + homogeneous clip + cull + 8-bit snap + bbox,
-//                             per-chunk LDS bin histogram (Pipeline.cpp:611-643)
+//   k_setup    tri_setup_bin  primitive assembly + trivial reject + cull + 8-bit snap + bbox,
+//                             per-chunk LDS bin histogram (Pipeline.cpp:611-643); triangles that need
+//                             homogeneous clipping are queued for k_clip
+//   k_clip     rare path: Sutherland-Hodgman against w>=WMIN, z>=0 and the guard band + fan
 //   k_binscan  bin prefix scan (one workgroup)
 //   k_scatter  bin list scatter (LDS-privatised cursors, one global atomic per (chunk, bin))
 //   k_raster   tile_raster_shade: one workgroup per 64x64 bin; coverage + early-Z resolved in LDS
 //              with 64-bit (depth, primitive-order) keys (== in-order LESS_OR_EQUAL,
-//              Pipeline.cpp:655-658), then Default.frag:123-192 once per pixel, coalesced
+//              Pipeline.cpp:655-658), then Default.frag:123-192 once per visible pixel, coalesced
 //              B8G8R8A8 + D32 stores.
 //
 // Raster rules (shared with oracle/tri_oracle.cpp) are reproduced with the same
-// float evaluation order; the file is compiled with -ffp-contract=off so depth is bit-exact.
+// float evaluation order; the file is compiled with -ffp-contract=off so depth is bit-exact. The
+// fragment stage has two builds: EXACT (IEEE div/sqrt/powf, the oracle's operation order) and the
+// default fast build (v_rcp/v_rsq/v_exp/v_log, hoisted frame constants), both within 1 LSB of the
+// oracle's UNORM8 output.
 #include "raster_launch.h"
 
 #include <hip/hip_runtime.h>
@@ -20,6 +25,7 @@
 namespace {
 
 constexpr uint64_t kBgKey = (0x3F800000ull << 32) | 0xFFFFFFFFull;  // depth 1.0, lowest priority
+constexpr float kPi = 3.14159265359f;                                  // Default.frag:65
 
 struct VsOut {
     float4 clip;
@@ -87,27 +93,11 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
         const float nz = (s[2] * snx + s[6] * sny) + s[10] * snz;
         snx = nx; sny = ny; snz = nz;
     }
-    const float* m = dr.model;
-    const float4 world = mat_vec_seq(m, sp);
-    // transpose(inverse(mat3(M))), glm cofactor form; m[c*4+r]
-    const float m00 = m[0], m01 = m[1], m02 = m[2];
-    const float m10 = m[4], m11 = m[5], m12 = m[6];
-    const float m20 = m[8], m21 = m[9], m22 = m[10];
-    const float det = (m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02)) +
-                      m20 * (m01 * m12 - m11 * m02);
-    const float od = 1.0f / det;
-    const float i00 = +(m11 * m22 - m21 * m12) * od;
-    const float i10 = -(m10 * m22 - m20 * m12) * od;
-    const float i20 = +(m10 * m21 - m20 * m11) * od;
-    const float i01 = -(m01 * m22 - m21 * m02) * od;
-    const float i11 = +(m00 * m22 - m20 * m02) * od;
-    const float i21 = -(m00 * m21 - m20 * m01) * od;
-    const float i02 = +(m01 * m12 - m11 * m02) * od;
-    const float i12 = -(m00 * m12 - m10 * m02) * od;
-    const float i22 = +(m00 * m11 - m10 * m01) * od;
-    float nnx = (i00 * snx + i01 * sny) + i02 * snz;
-    float nny = (i10 * snx + i11 * sny) + i12 * snz;
-    float nnz = (i20 * snx + i21 * sny) + i22 * snz;
+    const float4 world = mat_vec_seq(dr.model, sp);
+    const float* nm = dr.nm;  // NM[c*3+r]; N' = NM * n
+    float nnx = (nm[0] * snx + nm[3] * sny) + nm[6] * snz;
+    float nny = (nm[1] * snx + nm[4] * sny) + nm[7] * snz;
+    float nnz = (nm[2] * snx + nm[5] * sny) + nm[8] * snz;
     const float inv = 1.0f / sqrtf((nnx * nnx + nny * nny) + nnz * nnz);
     nnx = nnx * inv; nny = nny * inv; nnz = nnz * inv;
     const float u = (in.u * dr.tex_scale[0]) * dr.tiling + dr.tex_offset[0];
@@ -130,7 +120,6 @@ __device__ __forceinline__ bool setup_direct(const TriFrameParams& fp, float4 c0
                                              uint32_t s0, uint32_t s1, uint32_t s2, uint32_t prim_sub,
                                              TriRec& r, uint2& br) {
     const float4 c[3] = {c0, c1, c2};
-    const uint32_t sl[3] = {s0, s1, s2};
     int32_t X[3], Y[3];
     float z[3], iw[3];
 #pragma unroll
@@ -146,13 +135,6 @@ __device__ __forceinline__ bool setup_direct(const TriFrameParams& fp, float4 c0
     const int64_t S = (int64_t)(X[1] - X[0]) * (int64_t)(Y[2] - Y[0]) -
                       (int64_t)(Y[1] - Y[0]) * (int64_t)(X[2] - X[0]);
     if (S >= 0) return false;  // zero area or back-facing (cull BACK, front CCW)
-    // swap v1 <-> v2
-    r.X[0] = X[0]; r.X[1] = X[2]; r.X[2] = X[1];
-    r.Y[0] = Y[0]; r.Y[1] = Y[2]; r.Y[2] = Y[1];
-    r.z[0] = z[0]; r.z[1] = z[2]; r.z[2] = z[1];
-    r.iw[0] = iw[0]; r.iw[1] = iw[2]; r.iw[2] = iw[1];
-    r.v[0] = sl[0]; r.v[1] = sl[2]; r.v[2] = sl[1];
-    r.prim_sub = prim_sub;
     const int32_t xmin = min(X[0], min(X[1], X[2])), xmax = max(X[0], max(X[1], X[2]));
     const int32_t ymin = min(Y[0], min(Y[1], Y[2])), ymax = max(Y[0], max(Y[1], Y[2]));
     int32_t px0 = -floor_shift8(128 - xmin), px1 = floor_shift8(xmax - 128);
@@ -162,23 +144,108 @@ __device__ __forceinline__ bool setup_direct(const TriFrameParams& fp, float4 c0
     py0 = max(py0, fp.y0);
     py1 = min(py1, fp.y1 - 1);
     if (px0 > px1 || py0 > py1) return false;
+    // swap v1 <-> v2 so the edge functions see S' = -S > 0
+    r.X[0] = X[0]; r.X[1] = X[2]; r.X[2] = X[1];
+    r.Y[0] = Y[0]; r.Y[1] = Y[2]; r.Y[2] = Y[1];
+    r.z[0] = z[0]; r.z[1] = z[2]; r.z[2] = z[1];
+    r.iw[0] = iw[0]; r.iw[1] = iw[2]; r.iw[2] = iw[1];
+    r.v[0] = s0; r.v[1] = s2; r.v[2] = s1;
+    r.prim_sub = prim_sub;
     const uint32_t bx0 = (uint32_t)px0 >> TRI_BIN_LOG2, bx1 = (uint32_t)px1 >> TRI_BIN_LOG2;
     const uint32_t by0 = (uint32_t)(py0 - fp.y0) >> TRI_BIN_LOG2, by1 = (uint32_t)(py1 - fp.y0) >> TRI_BIN_LOG2;
     br = make_uint2(bx0 | (by0 << 16), bx1 | (by1 << 16));
     return true;
 }
 
-__device__ __forceinline__ void hist_add(uint32_t* hist, int nbx, uint2 br) {
+template <typename F>
+__device__ __forceinline__ void for_bins(uint2 br, int nbx, F&& f) {
     const uint32_t bx0 = br.x & 0xFFFFu, by0 = br.x >> 16, bx1 = br.y & 0xFFFFu, by1 = br.y >> 16;
     for (uint32_t by = by0; by <= by1; ++by)
-        for (uint32_t bx = bx0; bx <= bx1; ++bx) atomicAdd(&hist[by * nbx + bx], 1u);
+        for (uint32_t bx = bx0; bx <= bx1; ++bx) f(by * (uint32_t)nbx + bx);
 }
 
-__device__ __forceinline__ void lerp_vs(const VsOut& a, const VsOut& b, float t, VsOut& o) {
+__global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
+    extern __shared__ uint32_t hist[];
+    __shared__ uint32_t red[2];
+    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) hist[i] = 0;
+    if (threadIdx.x == 0) { red[0] = 0; red[1] = 0; }
+    __syncthreads();
+    uint32_t nsetup = 0, nclip = 0;
+    const uint32_t chunk0 = blockIdx.x * (uint32_t)(TRI_BLOCK * fp.ppt);
+    for (int k = 0; k < fp.ppt; ++k) {
+        const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
+        if (p >= fp.nprims) break;
+        const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
+        const TriDrawDev& dr = b.draws[d];
+        const uint32_t t = p - b.draw_pbase[d];
+        const uint32_t* ip = b.indices + dr.first_index + 3ull * t;
+        const uint32_t vb = b.draw_vbase[d] - dr.min_index;
+        const uint32_t sl0 = vb + ip[0], sl1 = vb + ip[1], sl2 = vb + ip[2];
+        const float4 c0 = b.clip[sl0], c1 = b.clip[sl1], c2 = b.clip[sl2];
+        TriRec r;
+        uint2 br = make_uint2(TRI_BR_CULLED, 0u);
+        bool ok = false;
+        if (!(isnan(c0.w) || isnan(c1.w) || isnan(c2.w))) {
+            // trivial reject: all three vertices outside one clip half-space
+#define ALLNEG(e0, e1, e2) ((e0) < 0.0f && (e1) < 0.0f && (e2) < 0.0f)
+            const bool rej = ALLNEG(c0.z, c1.z, c2.z) || ALLNEG(c0.w - c0.z, c1.w - c1.z, c2.w - c2.z) ||
+                             ALLNEG(c0.x + c0.w, c1.x + c1.w, c2.x + c2.w) ||
+                             ALLNEG(c0.w - c0.x, c1.w - c1.x, c2.w - c2.x) ||
+                             ALLNEG(c0.y + c0.w, c1.y + c1.w, c2.y + c2.w) ||
+                             ALLNEG(c0.w - c0.y, c1.w - c1.y, c2.w - c2.y);
+#undef ALLNEG
+            if (!rej) {
+                auto outside = [&](float4 c) {
+                    return (c.w < TRI_WMIN) || (c.z < 0.0f) || (c.x < -fp.gx * c.w) || (c.x > fp.gx * c.w) ||
+                           (c.y < -fp.gy * c.w) || (c.y > fp.gy * c.w);
+                };
+                if (outside(c0) || outside(c1) || outside(c2)) {
+                    ++nclip;
+                    const uint32_t q = atomicAdd(&b.counters->clip_queue, 1u);
+                    if (q < fp.ovf_rec_cap) b.clip_queue[q] = p;
+                    else atomicOr(&b.counters->flags, TRI_OVF_CLIP_QUEUE);
+                } else {
+                    ok = setup_direct(fp, c0, c1, c2, sl0, sl1, sl2, p << 3, r, br);
+                }
+            }
+        }
+        if (ok) {
+            ++nsetup;
+            for_bins(br, fp.nbx, [&](uint32_t bi) { atomicAdd(&hist[bi], 1u); });
+        } else {
+            r.prim_sub = TRI_REC_CULLED;
+            br = make_uint2(TRI_BR_CULLED, 0u);
+        }
+        b.recs[p] = r;
+        b.brange[p] = br;
+    }
+    if (nsetup) atomicAdd(&red[0], nsetup);
+    if (nclip) atomicAdd(&red[1], nclip);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        if (red[0]) atomicAdd(&b.counters->tris_setup, red[0]);
+        if (red[1]) atomicAdd(&b.counters->tris_clipped, red[1]);
+    }
+    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) {
+        const uint32_t h = hist[i];
+        if (h) atomicAdd(&b.bin_total[i], h);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// k_clip: homogeneous Sutherland-Hodgman + fan (oracle clip_polygon), rare path
+// ------------------------------------------------------------------------------------------
+struct ClipVert {
+    float4 c;
+    float b0, b1, b2;
+};
+
+__device__ __forceinline__ ClipVert lerp_cv(const ClipVert& a, const ClipVert& b, float t) {
+    ClipVert o;
 #define L(f) o.f = a.f + t * (b.f - a.f)
-    L(clip.x); L(clip.y); L(clip.z); L(clip.w);
-    L(wx); L(wy); L(wz); L(nx); L(ny); L(nz); L(u); L(v); L(cr); L(cg); L(cb);
+    L(c.x); L(c.y); L(c.z); L(c.w); L(b0); L(b1); L(b2);
 #undef L
+    return o;
 }
 
 __device__ __forceinline__ float plane_dist(const TriFrameParams& fp, int plane, float4 c) {
@@ -192,157 +259,94 @@ __device__ __forceinline__ float plane_dist(const TriFrameParams& fp, int plane,
     }
 }
 
-// Rare path: homogeneous Sutherland-Hodgman + fan (oracle clip_polygon). Sub-records and the
-// clipped vertices' varyings go to the overflow regions.
-__device__ __noinline__ void clip_path(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t prim,
-                                       const uint32_t* slots, uint32_t* hist, uint32_t* nsetup) {
-    VsOut bufA[TRI_MAX_CLIP_VERTS], bufB[TRI_MAX_CLIP_VERTS];
-    for (int k = 0; k < 3; ++k) {
-        const float4 c = b.clip[slots[k]];
-        const float4* vv = b.vary + 3ull * slots[k];
-        const float4 a0 = vv[0], a1 = vv[1], a2 = vv[2];
-        VsOut& o = bufA[k];
-        o.clip = c;
-        o.wx = a0.x; o.wy = a0.y; o.wz = a0.z; o.u = a0.w;
-        o.nx = a1.x; o.ny = a1.y; o.nz = a1.z; o.v = a1.w;
-        o.cr = a2.x; o.cg = a2.y; o.cb = a2.z;
-    }
-    int n = 3;
-    VsOut* src = bufA;
-    VsOut* dst = bufB;
-    for (int plane = 0; plane < 6 && n > 0; ++plane) {
-        int m = 0;
-        for (int i = 0; i < n; ++i) {
-            const VsOut& a = src[i];
-            const VsOut& bb = src[(i + 1) % n];
-            const float da = plane_dist(fp, plane, a.clip), db = plane_dist(fp, plane, bb.clip);
-            if (da >= 0.0f) dst[m++] = a;
-            if ((da >= 0.0f) != (db >= 0.0f)) {
-                const float t = da / (da - db);
-                lerp_vs(a, bb, t, dst[m++]);
-            }
-        }
-        n = m;
-        VsOut* tmp = src; src = dst; dst = tmp;
-    }
-    TriRec main{};
-    main.prim_sub = TRI_REC_CULLED;
-    uint2 main_br = make_uint2(0xFFFFFFFFu, 0u);
-    if (n >= 3) {
-        const uint32_t nsub = (uint32_t)(n - 2);
-        const uint32_t rbase = atomicAdd(&b.counters->ovf_records, nsub);
-        const uint32_t vbase = atomicAdd(&b.counters->ovf_verts, (uint32_t)n);
-        if (rbase + nsub > fp.ovf_rec_cap || vbase + (uint32_t)n > fp.ovf_vert_cap) {
-            atomicOr(&b.counters->flags, (rbase + nsub > fp.ovf_rec_cap) ? TRI_OVF_CLIP_RECORDS : TRI_OVF_CLIP_VERTS);
-        } else {
-            const uint32_t sbase = fp.nslots + vbase;
-            for (int k = 0; k < n; ++k) {
-                float4* vo = b.vary + 3ull * (sbase + k);
-                const VsOut& s = src[k];
-                vo[0] = make_float4(s.wx, s.wy, s.wz, s.u);
-                vo[1] = make_float4(s.nx, s.ny, s.nz, s.v);
-                vo[2] = make_float4(s.cr, s.cg, s.cb, 0.0f);
-            }
-            const uint32_t first = fp.nprims + rbase;
-            for (int k = 1; k + 1 < n; ++k) {
-                TriRec r;
-                uint2 br = make_uint2(0xFFFFFFFFu, 0u);
-                const uint32_t ps = (prim << 3) | (uint32_t)(k - 1);
-                const bool ok = setup_direct(fp, src[0].clip, src[k].clip, src[k + 1].clip, sbase, sbase + k,
-                                             sbase + k + 1, ps, r, br);
-                if (!ok) { r.prim_sub = TRI_REC_CULLED; br = make_uint2(0xFFFFFFFFu, 0u); }
-                else { hist_add(hist, fp.nbx, br); ++*nsetup; }
-                b.recs[first + k - 1] = r;
-                b.brange[first + k - 1] = br;
-            }
-            main.prim_sub = TRI_REC_CLIPPED;
-            main.v[0] = first;
-            main.v[1] = nsub;
-            main_br = make_uint2(0xFFFFFFFEu, 0u);
-        }
-    }
-    b.recs[prim] = main;
-    b.brange[prim] = main_br;
-}
-
-__global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
-    extern __shared__ uint32_t hist[];
-    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) hist[i] = 0;
-    __syncthreads();
-    uint32_t nsetup = 0, nclip = 0;
-    const uint32_t chunk0 = blockIdx.x * (uint32_t)(TRI_BLOCK * fp.ppt);
-    for (int k = 0; k < fp.ppt; ++k) {
-        const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
-        if (p >= fp.nprims) break;
-        const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
+__global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDeviceBuffers b) {
+    const uint32_t nq = min(b.counters->clip_queue, fp.ovf_rec_cap);
+    uint32_t nsetup = 0;
+    for (uint32_t q = blockIdx.x * TRI_BLOCK + threadIdx.x; q < nq; q += gridDim.x * TRI_BLOCK) {
+        const uint32_t prim = b.clip_queue[q];
+        const int d = find_range(b.draw_pbase, (int)fp.ndraws, prim);
         const TriDrawDev& dr = b.draws[d];
-        const uint32_t t = p - b.draw_pbase[d];
-        const uint32_t* ip = b.indices + dr.first_index + 3ull * t;
-        const uint32_t vb = b.draw_vbase[d];
-        uint32_t sl[3];
-        float4 c[3];
-        bool bad = false;
-#pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            sl[j] = vb + (ip[j] - dr.min_index);
-            c[j] = b.clip[sl[j]];
-            bad = bad || isnan(c[j].w);
+        const uint32_t* ip = b.indices + dr.first_index + 3ull * (prim - b.draw_pbase[d]);
+        const uint32_t vb = b.draw_vbase[d] - dr.min_index;
+        uint32_t srcv[3];
+        // polygon vertex = clip position (lerped exactly like the oracle: depth stays bit-exact) +
+        // barycentric weights on the source triangle (for the varyings: colour-only effect)
+        ClipVert buf[2][TRI_MAX_CLIP_VERTS];
+        for (int k = 0; k < 3; ++k) {
+            srcv[k] = vb + ip[k];
+            buf[0][k].c = b.clip[srcv[k]];
+            buf[0][k].b0 = k == 0 ? 1.0f : 0.0f;
+            buf[0][k].b1 = k == 1 ? 1.0f : 0.0f;
+            buf[0][k].b2 = k == 2 ? 1.0f : 0.0f;
         }
-        TriRec r;
-        uint2 br = make_uint2(0xFFFFFFFFu, 0u);
-        bool ok = false;
-        if (!bad) {
-            // trivial reject: all three vertices outside one clip half-space
-            bool rej = false;
-#define ALLNEG(expr0, expr1, expr2) ((expr0) < 0.0f && (expr1) < 0.0f && (expr2) < 0.0f)
-            rej = rej || ALLNEG(c[0].z, c[1].z, c[2].z);
-            rej = rej || ALLNEG(c[0].w - c[0].z, c[1].w - c[1].z, c[2].w - c[2].z);
-            rej = rej || ALLNEG(c[0].x + c[0].w, c[1].x + c[1].w, c[2].x + c[2].w);
-            rej = rej || ALLNEG(c[0].w - c[0].x, c[1].w - c[1].x, c[2].w - c[2].x);
-            rej = rej || ALLNEG(c[0].y + c[0].w, c[1].y + c[1].w, c[2].y + c[2].w);
-            rej = rej || ALLNEG(c[0].w - c[0].y, c[1].w - c[1].y, c[2].w - c[2].y);
-#undef ALLNEG
-            if (!rej) {
-                bool need_clip = false;
+        int n = 3, cur = 0;
+        for (int plane = 0; plane < 6 && n > 0; ++plane) {
+            int m = 0;
+            for (int i = 0; i < n; ++i) {
+                const ClipVert a = buf[cur][i];
+                const ClipVert bb = buf[cur][i + 1 < n ? i + 1 : 0];
+                const float da = plane_dist(fp, plane, a.c), db = plane_dist(fp, plane, bb.c);
+                if (da >= 0.0f && m < TRI_MAX_CLIP_VERTS) buf[cur ^ 1][m++] = a;
+                if ((da >= 0.0f) != (db >= 0.0f) && m < TRI_MAX_CLIP_VERTS) {
+                    const float t = da / (da - db);
+                    buf[cur ^ 1][m++] = lerp_cv(a, bb, t);
+                }
+            }
+            n = m;
+            cur ^= 1;
+        }
+        const ClipVert* src = buf[cur];
+        TriRec main{};
+        main.prim_sub = TRI_REC_CULLED;
+        uint2 main_br = make_uint2(TRI_BR_CULLED, 0u);
+        if (n >= 3) {
+            const uint32_t nsub = (uint32_t)(n - 2);
+            const uint32_t rbase = atomicAdd(&b.counters->ovf_records, nsub);
+            const uint32_t vbase = atomicAdd(&b.counters->ovf_verts, (uint32_t)n);
+            if (rbase + nsub > fp.ovf_rec_cap || vbase + (uint32_t)n > fp.ovf_vert_cap) {
+                atomicOr(&b.counters->flags,
+                         (rbase + nsub > fp.ovf_rec_cap) ? TRI_OVF_CLIP_RECORDS : TRI_OVF_CLIP_VERTS);
+            } else {
+                const uint32_t sbase = fp.nslots + vbase;
+                const float4* v0 = b.vary + 3ull * srcv[0];
+                const float4* v1 = b.vary + 3ull * srcv[1];
+                const float4* v2 = b.vary + 3ull * srcv[2];
+                for (int k = 0; k < n; ++k) {
+                    float4* vo = b.vary + 3ull * (sbase + k);
+                    const ClipVert& s = src[k];
 #pragma unroll
-                for (int j = 0; j < 3; ++j) {
-                    need_clip = need_clip || (c[j].w < TRI_WMIN) || (c[j].z < 0.0f) ||
-                                (c[j].x < -fp.gx * c[j].w) || (c[j].x > fp.gx * c[j].w) ||
-                                (c[j].y < -fp.gy * c[j].w) || (c[j].y > fp.gy * c[j].w);
+                    for (int j = 0; j < 3; ++j) {
+                        const float4 x = v0[j], y = v1[j], z = v2[j];
+                        vo[j] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
+                                            (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, (s.b0 * x.w + s.b1 * y.w) + s.b2 * z.w);
+                    }
                 }
-                if (need_clip) {
-                    ++nclip;
-                    clip_path(fp, b, p, sl, hist, &nsetup);
-                    continue;
+                const uint32_t first = fp.nprims + rbase;
+                for (int k = 1; k + 1 < n; ++k) {
+                    TriRec r;
+                    uint2 br = make_uint2(TRI_BR_CULLED, 0u);
+                    const uint32_t ps = (prim << 3) | (uint32_t)(k - 1);
+                    if (setup_direct(fp, src[0].c, src[k].c, src[k + 1].c, sbase, sbase + k, sbase + k + 1, ps, r,
+                                     br)) {
+                        ++nsetup;
+                        for_bins(br, fp.nbx, [&](uint32_t bi) { atomicAdd(&b.bin_total[bi], 1u); });
+                    } else {
+                        r.prim_sub = TRI_REC_CULLED;
+                        br = make_uint2(TRI_BR_CULLED, 0u);
+                    }
+                    b.recs[first + k - 1] = r;
+                    b.brange[first + k - 1] = br;
                 }
-                ok = setup_direct(fp, c[0], c[1], c[2], sl[0], sl[1], sl[2], p << 3, r, br);
+                main.prim_sub = TRI_REC_CLIPPED;
+                main.v[0] = first;
+                main.v[1] = nsub;
+                main_br = make_uint2(TRI_BR_CLIPPED, 0u);
             }
         }
-        if (ok) {
-            ++nsetup;
-            hist_add(hist, fp.nbx, br);
-        } else {
-            r.prim_sub = TRI_REC_CULLED;
-            br = make_uint2(0xFFFFFFFFu, 0u);
-        }
-        b.recs[p] = r;
-        b.brange[p] = br;
+        b.recs[prim] = main;
+        b.brange[prim] = main_br;
     }
-    // block-reduce the counters (one atomic per workgroup)
-    __shared__ uint32_t red[2];
-    if (threadIdx.x == 0) { red[0] = 0; red[1] = 0; }
-    __syncthreads();
-    if (nsetup) atomicAdd(&red[0], nsetup);
-    if (nclip) atomicAdd(&red[1], nclip);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        if (red[0]) atomicAdd(&b.counters->tris_setup, red[0]);
-        if (red[1]) atomicAdd(&b.counters->tris_clipped, red[1]);
-    }
-    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) {
-        const uint32_t h = hist[i];
-        if (h) atomicAdd(&b.bin_total[i], h);
-    }
+    if (nsetup) atomicAdd(&b.counters->tris_setup, nsetup);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -388,13 +392,12 @@ __device__ __forceinline__ void for_each_binned(const TriFrameParams& fp, const 
         const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
         if (p >= fp.nprims) break;
         const uint2 br = b.brange[p];
-        if (br.x == 0xFFFFFFFFu) continue;
-        if (br.x == 0xFFFFFFFEu) {
-            const TriRec& mr = b.recs[p];
-            const uint32_t first = mr.v[0], cnt = mr.v[1];
+        if (br.x == TRI_BR_CULLED) continue;
+        if (br.x == TRI_BR_CLIPPED) {
+            const uint32_t first = b.recs[p].v[0], cnt = b.recs[p].v[1];
             for (uint32_t s = 0; s < cnt; ++s) {
                 const uint2 sb = b.brange[first + s];
-                if (sb.x != 0xFFFFFFFFu) f(first + s, sb);
+                if (sb.x != TRI_BR_CULLED) f(first + s, sb);
             }
             continue;
         }
@@ -408,7 +411,9 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_scatter(TriFrameParams fp, TriDev
     uint32_t* base = lds + fp.nbins;
     for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) hist[i] = 0;
     __syncthreads();
-    for_each_binned(fp, b, [&](uint32_t, uint2 br) { hist_add(hist, fp.nbx, br); });
+    for_each_binned(fp, b, [&](uint32_t, uint2 br) {
+        for_bins(br, fp.nbx, [&](uint32_t bi) { atomicAdd(&hist[bi], 1u); });
+    });
     __syncthreads();
     for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) {
         const uint32_t h = hist[i];
@@ -418,36 +423,35 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_scatter(TriFrameParams fp, TriDev
     __syncthreads();
     const uint32_t cap = fp.bin_cap;
     for_each_binned(fp, b, [&](uint32_t rec, uint2 br) {
-        const uint32_t bx0 = br.x & 0xFFFFu, by0 = br.x >> 16, bx1 = br.y & 0xFFFFu, by1 = br.y >> 16;
-        for (uint32_t by = by0; by <= by1; ++by)
-            for (uint32_t bx = bx0; bx <= bx1; ++bx) {
-                const uint32_t bi = by * fp.nbx + bx;
-                const uint32_t pos = base[bi] + atomicAdd(&hist[bi], 1u);
-                if (pos < cap) b.bin_list[pos] = rec;
-            }
+        for_bins(br, fp.nbx, [&](uint32_t bi) {
+            const uint32_t pos = base[bi] + atomicAdd(&hist[bi], 1u);
+            if (pos < cap) b.bin_list[pos] = rec;
+        });
     });
 }
 
 // ------------------------------------------------------------------------------------------
-// tile_raster_shade
+// tile_raster_shade: coverage
 // ------------------------------------------------------------------------------------------
 struct EdgeSetup {
-    int64_t a[3], b[3], c[3];
+    int32_t A[3], B[3];
+    int64_t D[3];
     float dzdX, dzdY;
 };
 
 // Mirrors oracle setup_triangle()'s edge / depth-plane derivation.
-__device__ __forceinline__ void edge_setup(const TriRec& r, EdgeSetup& e, int64_t D[3]) {
+__device__ __forceinline__ void edge_setup(const TriRec& r, EdgeSetup& e) {
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const int i = k, j = (k + 1) % 3;
-        const int64_t a = (int64_t)r.Y[i] - r.Y[j];
-        const int64_t bb = (int64_t)r.X[j] - r.X[i];
-        const int64_t c = -(a * r.X[i] + bb * r.Y[i]);
+        const int32_t a = r.Y[i] - r.Y[j];
+        const int32_t bb = r.X[j] - r.X[i];
+        const int64_t c = -((int64_t)a * r.X[i] + (int64_t)bb * r.Y[i]);
         const bool tl = (a > 0) || (a == 0 && bb > 0);
-        const int64_t cp = c + 128 * a + 128 * bb - (tl ? 0 : 1);
-        e.a[k] = a; e.b[k] = bb; e.c[k] = c;
-        D[k] = cp >> 8;
+        const int64_t cp = c + 128 * (int64_t)a + 128 * (int64_t)bb - (tl ? 0 : 1);
+        e.A[k] = a;
+        e.B[k] = bb;
+        e.D[k] = cp >> 8;
     }
     const int64_t S = (int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
                       (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]);
@@ -474,7 +478,7 @@ __device__ __forceinline__ TriRec load_rec(const TriRec* recs, uint32_t i) {
     return r;
 }
 
-// Fragment depth at pixel centre (Xp, Yp): plane through the snapped vertices, fixed order.
+// Fragment depth at pixel centre: plane through the snapped vertices, fixed evaluation order.
 __device__ __forceinline__ float frag_depth(const TriRec& r, const EdgeSetup& e, int32_t px, int32_t py) {
     const float fdx = (float)(256 * px + 128 - r.X[0]);
     const float fdy = (float)(256 * py + 128 - r.Y[0]);
@@ -484,82 +488,106 @@ __device__ __forceinline__ float frag_depth(const TriRec& r, const EdgeSetup& e,
 }
 
 __device__ __forceinline__ bool depth_key(float z, bool far_clip, uint32_t lowbits, uint64_t& key) {
-    if (far_clip && z > 1.0f) return false;
+    if (far_clip && z > 1.0f) return false;  // per-pixel far-plane (z <= w) clip
     if (!(z > 0.0f)) z = 0.0f;
     if (z > 1.0f) z = 1.0f;
     key = ((uint64_t)__float_as_uint(z) << 32) | lowbits;
     return true;
 }
 
-// ---- Default.frag ----------------------------------------------------------------------------
+__device__ __forceinline__ void rec_bbox(const TriRec& r, int32_t ox, int32_t oy, int32_t bw, int32_t bh, int32_t& cx0,
+                                         int32_t& cx1, int32_t& cy0, int32_t& cy1) {
+    const int32_t xmin = min(r.X[0], min(r.X[1], r.X[2])), xmax = max(r.X[0], max(r.X[1], r.X[2]));
+    const int32_t ymin = min(r.Y[0], min(r.Y[1], r.Y[2])), ymax = max(r.Y[0], max(r.Y[1], r.Y[2]));
+    cx0 = max(-floor_shift8(128 - xmin), ox);
+    cx1 = min(floor_shift8(xmax - 128), ox + bw - 1);
+    cy0 = max(-floor_shift8(128 - ymin), oy);
+    cy1 = min(floor_shift8(ymax - 128), oy + bh - 1);
+}
+
+__device__ __forceinline__ uint32_t key_low(uint32_t prim_sub) {
+    return ((TRI_PRIM_MAX - (prim_sub >> 3)) << 3) | (prim_sub & 7u);
+}
+
+__device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int32_t cx1, int32_t cy0, int32_t cy1,
+                                              int32_t ox, int32_t oy, uint64_t* keys) {
+    EdgeSetup e;
+    edge_setup(r, e);
+    bool rej = false;
+    int32_t F[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) F[k] = clamp_edge((int64_t)e.A[k] * cx0 + (int64_t)e.B[k] * cy0 + e.D[k], rej);
+    if (rej) return;
+    const bool far_clip = (r.z[0] > 1.0f) || (r.z[1] > 1.0f) || (r.z[2] > 1.0f);
+    const uint32_t low = key_low(r.prim_sub);
+    for (int32_t py = cy0; py <= cy1; ++py) {
+        int32_t f0 = F[0], f1 = F[1], f2 = F[2];
+        for (int32_t px = cx0; px <= cx1; ++px) {
+            if ((f0 | f1 | f2) >= 0) {
+                uint64_t key;
+                if (depth_key(frag_depth(r, e, px, py), far_clip, low, key))
+                    atomicMin(&keys[(py - oy) * TRI_BIN + (px - ox)], key);
+            }
+            f0 += e.A[0]; f1 += e.A[1]; f2 += e.A[2];
+        }
+        F[0] += e.B[0]; F[1] += e.B[1]; F[2] += e.B[2];
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// tile_raster_shade: Default.frag
+// ------------------------------------------------------------------------------------------
 struct f3 { float x, y, z; };
 __device__ __forceinline__ f3 mk(float x, float y, float z) { return {x, y, z}; }
 __device__ __forceinline__ f3 add(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
-__device__ __forceinline__ f3 sub(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 sub3(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 __device__ __forceinline__ f3 mul(f3 a, f3 b) { return {a.x * b.x, a.y * b.y, a.z * b.z}; }
 __device__ __forceinline__ f3 muls(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
 __device__ __forceinline__ float dot3(f3 a, f3 b) { return (a.x * b.x + a.y * b.y) + a.z * b.z; }
 __device__ __forceinline__ f3 norm3(f3 v) { return muls(v, 1.0f / sqrtf(dot3(v, v))); }
 
-constexpr float kPi = 3.14159265359f;
+// fast-path primitives (hardware v_rcp / v_rsq / v_exp / v_log, explicit FMA)
+__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
+__device__ __forceinline__ float frsq(float x) { return __builtin_amdgcn_rsqf(x); }
+__device__ __forceinline__ float fdot(f3 a, f3 b) {
+    return __builtin_fmaf(a.z, b.z, __builtin_fmaf(a.y, b.y, a.x * b.x));
+}
+__device__ __forceinline__ f3 fnorm(f3 v) { return muls(v, frsq(fdot(v, v))); }
+__device__ __forceinline__ float fpow(float x, float y) {  // x >= 0
+    return __builtin_amdgcn_exp2f(y * __builtin_amdgcn_logf(x));
+}
+__device__ __forceinline__ float sat(float x) { return fminf(fmaxf(x, 0.0f), 1.0f); }
 
-__device__ __forceinline__ float schlick_ggx(float NdotV, float roughness) {
-    const float r = roughness + 1.0f;
-    const float k = (r * r) / 8.0f;
-    const float denom = NdotV * (1.0f - k) + k;
-    return NdotV / fmaxf(denom, 1e-4f);
+__device__ __forceinline__ uint32_t wrap_repeat(float f, uint32_t n) {  // REPEAT addressing of floor(f)
+    const int32_t i = (int32_t)fminf(fmaxf(f, -1.0e9f), 1.0e9f);
+    int32_t r = i % (int32_t)n;
+    if (r < 0) r += (int32_t)n;
+    return (uint32_t)r;
 }
 
-__device__ __forceinline__ f3 eval_pbr(f3 L, f3 rad, f3 N, f3 V, f3 albedo, float metallic, float roughness,
-                                       f3 F0) {
-    const f3 H = norm3(add(V, L));
-    // DistributionGGX
-    const float a = roughness * roughness;
-    const float a2 = a * a;
-    const float NdotH = fmaxf(dot3(N, H), 0.0f);
-    const float NdotH2 = NdotH * NdotH;
-    const float dd = (NdotH2 * (a2 - 1.0f) + 1.0f);
-    const float NDF = a2 / ((kPi * dd) * dd);
-    // GeometrySmith
-    const float NdotV = fmaxf(dot3(N, V), 0.0f);
-    const float NdotL = fmaxf(dot3(N, L), 0.0f);
-    const float G = schlick_ggx(NdotL, roughness) * schlick_ggx(NdotV, roughness);
-    // FresnelSchlick
-    const float p = powf(fminf(fmaxf(1.0f - fmaxf(dot3(H, V), 0.0f), 0.0f), 1.0f), 5.0f);
-    const f3 F = mk(F0.x + (1.0f - F0.x) * p, F0.y + (1.0f - F0.y) * p, F0.z + (1.0f - F0.z) * p);
-    const float ng = NDF * G;
-    const f3 num = muls(F, ng);
-    const float den = fmaxf((4.0f * NdotV) * NdotL, 1e-4f);
-    const f3 spec = mk(num.x / den, num.y / den, num.z / den);
-    const f3 kD = muls(mk(1.0f - F.x, 1.0f - F.y, 1.0f - F.z), 1.0f - metallic);
-    const f3 diff = mk((kD.x * albedo.x) / kPi, (kD.y * albedo.y) / kPi, (kD.z * albedo.z) / kPi);
-    return muls(mul(add(diff, spec), rad), NdotL);
-}
-
+// texture(): R8G8B8A8_SRGB decode before LINEAR filtering, REPEAT, level 0 (Renderer.cpp:3592-3607)
 __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, float v0, const float* lut) {
+    if (t.w == 1 && t.h == 1) {  // 1x1 (the default white slot): all four taps are texel (0,0)
+        const uint32_t p = t.texels[0];
+        return make_float4(lut[p & 0xFFu], lut[(p >> 8) & 0xFFu], lut[(p >> 16) & 0xFFu], (float)(p >> 24) / 255.0f);
+    }
     const float u = u0 * (float)t.w - 0.5f;
     const float v = v0 * (float)t.h - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
     const float a = u - fu, bb = v - fv;
-    const int64_t i0 = (int64_t)fu, j0 = (int64_t)fv;
-    auto wrap = [](int64_t i, uint32_t n) -> uint32_t {
-        int64_t r = i % (int64_t)n;
-        if (r < 0) r += n;
-        return (uint32_t)r;
-    };
-    const uint32_t x0 = wrap(i0, t.w), x1 = wrap(i0 + 1, t.w);
-    const uint32_t y0 = wrap(j0, t.h), y1 = wrap(j0 + 1, t.h);
+    const uint32_t x0 = wrap_repeat(fu, t.w), y0 = wrap_repeat(fv, t.h);
+    const uint32_t x1 = (x0 + 1 == t.w) ? 0u : x0 + 1, y1 = (y0 + 1 == t.h) ? 0u : y0 + 1;
     const uint32_t p00 = t.texels[(uint64_t)y0 * t.w + x0], p10 = t.texels[(uint64_t)y0 * t.w + x1];
     const uint32_t p01 = t.texels[(uint64_t)y1 * t.w + x0], p11 = t.texels[(uint64_t)y1 * t.w + x1];
-    auto ch = [&](uint32_t px, int c) -> float {
-        const uint32_t by = (px >> (8 * c)) & 0xFFu;
-        return c == 3 ? (float)by / 255.0f : lut[by];
-    };
     float4 r;
     float* rp = &r.x;
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const float t00 = ch(p00, c), t10 = ch(p10, c), t01 = ch(p01, c), t11 = ch(p11, c);
+        auto ch = [&](uint32_t px) -> float {
+            const uint32_t by = (px >> (8 * c)) & 0xFFu;
+            return c == 3 ? (float)by / 255.0f : lut[by];
+        };
+        const float t00 = ch(p00), t10 = ch(p10), t01 = ch(p01), t11 = ch(p11);
         const float l0 = t00 + a * (t10 - t00);
         const float l1 = t01 + a * (t11 - t01);
         rp[c] = l0 + bb * (l1 - l0);
@@ -572,58 +600,55 @@ __device__ __forceinline__ uint32_t unorm8(float c) {
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
 }
 
-__device__ __forceinline__ uint32_t shade_pixel(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                                int32_t px, int32_t py, const float* lut) {
-    const uint32_t low = (uint32_t)key;
-    const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
-    const uint32_t subi = low & 7u;
-    TriRec r = load_rec(b.recs, prim);
-    if (r.prim_sub == TRI_REC_CLIPPED) r = load_rec(b.recs, r.v[0] + subi);
-    // exact edge functions at the pixel centre -> screen barycentrics -> perspective-correct
-    const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
-    int64_t e[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int i = k, j = (k + 1) % 3;
-        const int64_t a = (int64_t)r.Y[i] - r.Y[j];
-        const int64_t bb = (int64_t)r.X[j] - r.X[i];
-        const int64_t c = -(a * r.X[i] + bb * r.Y[i]);
-        e[k] = a * Xp + bb * Yp + c;
-    }
-    const int64_t S = (int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
-                      (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]);
-    const float fS = (float)S;
-    const float l0 = (float)e[1] / fS, l1 = (float)e[2] / fS, l2 = (float)e[0] / fS;
-    const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
-    const float qs = (q0 + q1) + q2;
-    const float w0 = q0 / qs, w1 = q1 / qs, w2 = q2 / qs;
-    const float4* va = b.vary + 3ull * r.v[0];
-    const float4* vb = b.vary + 3ull * r.v[1];
-    const float4* vc = b.vary + 3ull * r.v[2];
-    auto ip = [&](float x0, float x1, float x2) { return (w0 * x0 + w1 * x1) + w2 * x2; };
-    const float4 a0 = va[0], a1 = va[1], a2 = va[2];
-    const float4 b0 = vb[0], b1 = vb[1], b2 = vb[2];
-    const float4 c0 = vc[0], c1 = vc[1], c2 = vc[2];
-    const f3 world = mk(ip(a0.x, b0.x, c0.x), ip(a0.y, b0.y, c0.y), ip(a0.z, b0.z, c0.z));
-    const f3 nrm = mk(ip(a1.x, b1.x, c1.x), ip(a1.y, b1.y, c1.y), ip(a1.z, b1.z, c1.z));
-    const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
-    const f3 vcol = mk(ip(a2.x, b2.x, c2.x), ip(a2.y, b2.y, c2.y), ip(a2.z, b2.z, c2.z));
+struct Frag {
+    f3 world, nrm, vcol;
+    float u, v;
+    float4 s;     // sampled texel (linear)
+    float4 tint;
+};
 
-    const int d = find_range(b.draw_pbase, (int)fp.ndraws, prim);
-    const TriDrawDev& dr = b.draws[d];
+// ---- EXACT build: Default.frag with IEEE div/sqrt/powf in the oracle's operation order ----------
+__device__ __forceinline__ float schlick_ggx(float NdotV, float roughness) {
+    const float r = roughness + 1.0f;
+    const float k = (r * r) / 8.0f;
+    const float denom = NdotV * (1.0f - k) + k;
+    return NdotV / fmaxf(denom, 1e-4f);
+}
+
+__device__ __forceinline__ f3 eval_pbr_exact(f3 L, f3 rad, f3 N, f3 V, f3 albedo, float metallic, float roughness,
+                                             f3 F0) {
+    const f3 H = norm3(add(V, L));
+    const float a = roughness * roughness;
+    const float a2 = a * a;
+    const float NdotH = fmaxf(dot3(N, H), 0.0f);
+    const float NdotH2 = NdotH * NdotH;
+    const float dd = (NdotH2 * (a2 - 1.0f) + 1.0f);
+    const float NDF = a2 / ((kPi * dd) * dd);
+    const float NdotV = fmaxf(dot3(N, V), 0.0f);
+    const float NdotL = fmaxf(dot3(N, L), 0.0f);
+    const float G = schlick_ggx(NdotL, roughness) * schlick_ggx(NdotV, roughness);
+    const float p = powf(sat(1.0f - fmaxf(dot3(H, V), 0.0f)), 5.0f);
+    const f3 F = mk(F0.x + (1.0f - F0.x) * p, F0.y + (1.0f - F0.y) * p, F0.z + (1.0f - F0.z) * p);
+    const f3 num = muls(F, NDF * G);
+    const float den = fmaxf((4.0f * NdotV) * NdotL, 1e-4f);
+    const f3 spec = mk(num.x / den, num.y / den, num.z / den);
+    const f3 kD = muls(mk(1.0f - F.x, 1.0f - F.y, 1.0f - F.z), 1.0f - metallic);
+    const f3 diff = mk((kD.x * albedo.x) / kPi, (kD.y * albedo.y) / kPi, (kD.z * albedo.z) / kPi);
+    return muls(mul(add(diff, spec), rad), NdotL);
+}
+
+__device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag& f) {
     const tri_global_ubo& g = fp.ubo;
     const tri_material_record& mat = fp.mat0;
-
-    const f3 N = norm3(norm3(nrm));
-    const f3 V = norm3(sub(mk(g.camera_position[0], g.camera_position[1], g.camera_position[2]), world));
-    const float4 s = sample_tex(b.textures[dr.tex_id], u, v, lut);
-    const f3 albedo = mul(mul(mul(mk(s.x, s.y, s.z), mk(mat.base_color_factor[0], mat.base_color_factor[1],
-                                                           mat.base_color_factor[2])),
-                              mk(dr.tint[0], dr.tint[1], dr.tint[2])),
-                          vcol);
-    const float metallic = fminf(fmaxf(mat.material_factors[0], 0.0f), 1.0f);
+    const f3 N = norm3(norm3(f.nrm));
+    const f3 V = norm3(sub3(mk(g.camera_position[0], g.camera_position[1], g.camera_position[2]), f.world));
+    const f3 albedo = mul(mul(mul(mk(f.s.x, f.s.y, f.s.z), mk(mat.base_color_factor[0], mat.base_color_factor[1],
+                                                               mat.base_color_factor[2])),
+                              mk(f.tint.x, f.tint.y, f.tint.z)),
+                          f.vcol);
+    const float metallic = sat(mat.material_factors[0]);
     const float roughness = fminf(fmaxf(mat.material_factors[1], 0.045f), 1.0f);
-    const float amb_s = fminf(fmaxf(mat.material_factors[2], 0.0f), 1.0f);
+    const float amb_s = sat(mat.material_factors[2]);
     const float om = 0.04f * (1.0f - metallic);
     const f3 F0 = mk(om + albedo.x * metallic, om + albedo.y * metallic, om + albedo.z * metallic);
     f3 direct = mk(0.f, 0.f, 0.f);
@@ -632,23 +657,23 @@ __device__ __forceinline__ uint32_t shade_pixel(const TriFrameParams& fp, const 
                               -g.directional_light_direction[2]));
         const f3 rad = muls(mk(g.directional_light_color[0], g.directional_light_color[1], g.directional_light_color[2]),
                             g.directional_light_color[3]);
-        direct = add(direct, eval_pbr(L, rad, N, V, albedo, metallic, roughness, F0));
+        direct = add(direct, eval_pbr_exact(L, rad, N, V, albedo, metallic, roughness, F0));
     }
     const uint32_t np = min(g.light_counts[1], 8u);
     for (uint32_t i = 0; i < np; ++i) {
         const tri_point_light& pl = g.point_lights[i];
-        const f3 to = sub(mk(pl.position_range[0], pl.position_range[1], pl.position_range[2]), world);
+        const f3 to = sub3(mk(pl.position_range[0], pl.position_range[1], pl.position_range[2]), f.world);
         const float dist = sqrtf(dot3(to, to));
         if (dist <= 1e-4f) continue;
         const f3 L = mk(to.x / dist, to.y / dist, to.z / dist);
         const float radius = fmaxf(pl.position_range[3], 1e-4f);
-        const float nd = fminf(fmaxf(dist / radius, 0.0f), 1.0f);
+        const float nd = sat(dist / radius);
         float att = 1.0f - nd;
         att = att * att;
         const f3 rad = muls(muls(mk(pl.color_intensity[0], pl.color_intensity[1], pl.color_intensity[2]),
                                  pl.color_intensity[3]),
                             att);
-        direct = add(direct, eval_pbr(L, rad, N, V, albedo, metallic, roughness, F0));
+        direct = add(direct, eval_pbr_exact(L, rad, N, V, albedo, metallic, roughness, F0));
     }
     const f3 amb = muls(mul(muls(mk(g.ambient_color_intensity[0], g.ambient_color_intensity[1],
                                     g.ambient_color_intensity[2]),
@@ -659,43 +684,140 @@ __device__ __forceinline__ uint32_t shade_pixel(const TriFrameParams& fp, const 
     col = mk(col.x / (col.x + 1.0f), col.y / (col.y + 1.0f), col.z / (col.z + 1.0f));
     const float gamma = 1.0f / 2.2f;
     col = mk(powf(col.x, gamma), powf(col.y, gamma), powf(col.z, gamma));
-    const float alpha = (mat.base_color_factor[3] * dr.tint[3]) * s.w;
-    return unorm8(col.z) | (unorm8(col.y) << 8) | (unorm8(col.x) << 16) | (unorm8(alpha) << 24);
+    const float alpha = (mat.base_color_factor[3] * f.tint.w) * f.s.w;
+    return make_float4(col.x, col.y, col.z, alpha);
+}
+
+// ---- fast build: same algebra, frame constants hoisted, hardware transcendental approximations ---
+struct PbrPix {
+    f3 N, V, F0, diffK;
+    float NdotV, gV;
+};
+
+__device__ __forceinline__ f3 eval_pbr_fast(const TriShadeConst& sc, const PbrPix& px, f3 L, f3 rad) {
+    const float rough = sc.roughness;
+    const float a = rough * rough;
+    const float a2 = a * a;
+    const float rr = rough + 1.0f;
+    const float k = rr * rr * 0.125f;
+    const f3 H = fnorm(add(px.V, L));
+    const float NdotH = fmaxf(fdot(px.N, H), 0.0f);
+    const float HdotV = fmaxf(fdot(H, px.V), 0.0f);
+    const float NdotL = fmaxf(fdot(px.N, L), 0.0f);
+    const float dd = __builtin_fmaf(NdotH * NdotH, a2 - 1.0f, 1.0f);
+    const float NDF = a2 * frcp(kPi * dd * dd);
+    const float gL = NdotL * frcp(fmaxf(__builtin_fmaf(NdotL, 1.0f - k, k), 1e-4f));
+    const float q = sat(1.0f - HdotV);
+    const float q2 = q * q;
+    const float p5 = q2 * q2 * q;
+    const f3 F = mk(__builtin_fmaf(1.0f - px.F0.x, p5, px.F0.x), __builtin_fmaf(1.0f - px.F0.y, p5, px.F0.y),
+                    __builtin_fmaf(1.0f - px.F0.z, p5, px.F0.z));
+    const float s = NDF * gL * px.gV * frcp(fmaxf(4.0f * px.NdotV * NdotL, 1e-4f));
+    const float w = NdotL;
+    return mk(__builtin_fmaf(1.0f - F.x, px.diffK.x, F.x * s) * rad.x * w,
+              __builtin_fmaf(1.0f - F.y, px.diffK.y, F.y * s) * rad.y * w,
+              __builtin_fmaf(1.0f - F.z, px.diffK.z, F.z * s) * rad.z * w);
+}
+
+__device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f) {
+    PbrPix px;
+    px.N = fnorm(f.nrm);
+    px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), f.world));
+    const f3 albedo = mul(mul(mul(mk(f.s.x, f.s.y, f.s.z), mk(sc.base[0], sc.base[1], sc.base[2])),
+                              mk(f.tint.x, f.tint.y, f.tint.z)),
+                          f.vcol);
+    const float m = sc.metallic;
+    const float om = 0.04f * (1.0f - m);
+    px.F0 = mk(__builtin_fmaf(albedo.x, m, om), __builtin_fmaf(albedo.y, m, om), __builtin_fmaf(albedo.z, m, om));
+    px.diffK = muls(albedo, (1.0f - m) * (1.0f / kPi));
+    px.NdotV = fmaxf(fdot(px.N, px.V), 0.0f);
+    const float rr = sc.roughness + 1.0f;
+    const float k = rr * rr * 0.125f;
+    px.gV = px.NdotV * frcp(fmaxf(__builtin_fmaf(px.NdotV, 1.0f - k, k), 1e-4f));
+    f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
+              sc.amb[2] * albedo.z * sc.amb_strength);
+    if (sc.has_sun)
+        c = add(c, eval_pbr_fast(sc, px, mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]),
+                                 mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2])));
+    for (uint32_t i = 0; i < sc.npt; ++i) {
+        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), f.world);
+        const float d2 = fdot(to, to);
+        if (d2 <= 1e-8f) continue;  // dist <= 1e-4
+        const float inv = frsq(d2);
+        const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
+        const float att = att0 * att0;
+        c = add(c, eval_pbr_fast(sc, px, muls(to, inv),
+                                 mk(sc.pl_rad[i][0] * att, sc.pl_rad[i][1] * att, sc.pl_rad[i][2] * att)));
+    }
+    const float g = 1.0f / 2.2f;
+    const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
+    return make_float4(fpow(t.x, g), fpow(t.y, g), fpow(t.z, g), (sc.base[3] * f.tint.w) * f.s.w);
+}
+
+// Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
+template <bool EXACT>
+__device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
+                                               int32_t px, int32_t py, const float* lut, Frag& f) {
+    const uint32_t low = (uint32_t)key;
+    const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
+    TriRec r = load_rec(b.recs, prim);
+    if (r.prim_sub == TRI_REC_CLIPPED) r = load_rec(b.recs, r.v[0] + (low & 7u));
+    float l0, l1, l2;
+    if (EXACT) {  // exact int64 edge functions (oracle order)
+        const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
+        int64_t e[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int i = k, j = (k + 1) % 3;
+            const int64_t a = (int64_t)r.Y[i] - r.Y[j];
+            const int64_t bb = (int64_t)r.X[j] - r.X[i];
+            const int64_t c = -(a * r.X[i] + bb * r.Y[i]);
+            e[k] = a * Xp + bb * Yp + c;
+        }
+        const int64_t S = (int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
+                          (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]);
+        const float fS = (float)S;
+        l0 = (float)e[1] / fS; l1 = (float)e[2] / fS; l2 = (float)e[0] / fS;
+    } else {  // float edge functions relative to vertex 0 (operands < 2^24: exact conversions)
+        const float dx = (float)(256 * px + 128 - r.X[0]), dy = (float)(256 * py + 128 - r.Y[0]);
+        const float fX1 = (float)(r.X[1] - r.X[0]), fY1 = (float)(r.Y[1] - r.Y[0]);
+        const float fX2 = (float)(r.X[2] - r.X[0]), fY2 = (float)(r.Y[2] - r.Y[0]);
+        const float iS = frcp(fX1 * fY2 - fY1 * fX2);
+        l2 = (fX1 * dy - fY1 * dx) * iS;
+        l1 = (fY2 * dx - fX2 * dy) * iS;
+        l0 = 1.0f - l1 - l2;
+    }
+    const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
+    const float qs = (q0 + q1) + q2;
+    float w0, w1, w2;
+    if (EXACT) {
+        w0 = q0 / qs; w1 = q1 / qs; w2 = q2 / qs;
+    } else {
+        const float iq = frcp(qs);
+        w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
+    }
+    const float4* va = b.vary + 3ull * r.v[0];
+    const float4* vb = b.vary + 3ull * r.v[1];
+    const float4* vc = b.vary + 3ull * r.v[2];
+    auto ip = [&](float x0, float x1, float x2) { return (w0 * x0 + w1 * x1) + w2 * x2; };
+    const float4 a0 = va[0], a1 = va[1], a2 = va[2];
+    const float4 b0 = vb[0], b1 = vb[1], b2 = vb[2];
+    const float4 c0 = vc[0], c1 = vc[1], c2 = vc[2];
+    f.world = mk(ip(a0.x, b0.x, c0.x), ip(a0.y, b0.y, c0.y), ip(a0.z, b0.z, c0.z));
+    f.nrm = mk(ip(a1.x, b1.x, c1.x), ip(a1.y, b1.y, c1.y), ip(a1.z, b1.z, c1.z));
+    f.u = ip(a0.w, b0.w, c0.w);
+    f.v = ip(a1.w, b1.w, c1.w);
+    f.vcol = mk(ip(a2.x, b2.x, c2.x), ip(a2.y, b2.y, c2.y), ip(a2.z, b2.z, c2.z));
+    const int d = find_range(b.draw_pbase, (int)fp.ndraws, prim);
+    const TriDrawShade ds = b.draw_shade[d];
+    f.tint = make_float4(ds.tint[0], ds.tint[1], ds.tint[2], ds.tint[3]);
+    f.s = sample_tex(b.textures[ds.tex_id], f.u, f.v, lut);
 }
 
 constexpr int kBigArea = 96;  // bbox∩bin pixels above which a triangle is rasterized cooperatively
 constexpr int kBigQueue = 1024;
 
-__device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int32_t cx1, int32_t cy0, int32_t cy1,
-                                              int32_t ox, int32_t oy, uint64_t* keys) {
-    EdgeSetup e;
-    int64_t D[3];
-    edge_setup(r, e, D);
-    bool rej = false;
-    int32_t F[3], A[3], B[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        F[k] = clamp_edge(e.a[k] * cx0 + e.b[k] * cy0 + D[k], rej);
-        A[k] = (int32_t)e.a[k];
-        B[k] = (int32_t)e.b[k];
-    }
-    if (rej) return;
-    const bool far_clip = (r.z[0] > 1.0f) || (r.z[1] > 1.0f) || (r.z[2] > 1.0f);
-    const uint32_t low = ((TRI_PRIM_MAX - (r.prim_sub >> 3)) << 3) | (r.prim_sub & 7u);
-    for (int32_t py = cy0; py <= cy1; ++py) {
-        int32_t f0 = F[0], f1 = F[1], f2 = F[2];
-        for (int32_t px = cx0; px <= cx1; ++px) {
-            if ((f0 | f1 | f2) >= 0) {
-                uint64_t key;
-                if (depth_key(frag_depth(r, e, px, py), far_clip, low, key))
-                    atomicMin(&keys[(py - oy) * TRI_BIN + (px - ox)], key);
-            }
-            f0 += A[0]; f1 += A[1]; f2 += A[2];
-        }
-        F[0] += B[0]; F[1] += B[1]; F[2] += B[2];
-    }
-}
-
+template <bool EXACT>
 __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint64_t keys[TRI_BIN * TRI_BIN];
     __shared__ uint32_t bigq[kBigQueue];
@@ -711,15 +833,12 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
     if (tid == 0) nbig = 0;
     __syncthreads();
     const uint32_t s0 = b.bin_start[bin];
-    uint32_t s1 = b.bin_start[bin + 1];
-    s1 = min(s1, fp.bin_cap);
+    const uint32_t s1 = min(b.bin_start[bin + 1], fp.bin_cap);
     for (uint32_t i = s0 + tid; i < s1; i += TRI_BLOCK) {
         const uint32_t ri = b.bin_list[i];
         const TriRec r = load_rec(b.recs, ri);
-        const int32_t xmin = min(r.X[0], min(r.X[1], r.X[2])), xmax = max(r.X[0], max(r.X[1], r.X[2]));
-        const int32_t ymin = min(r.Y[0], min(r.Y[1], r.Y[2])), ymax = max(r.Y[0], max(r.Y[1], r.Y[2]));
-        const int32_t cx0 = max(-floor_shift8(128 - xmin), ox), cx1 = min(floor_shift8(xmax - 128), ox + bw - 1);
-        const int32_t cy0 = max(-floor_shift8(128 - ymin), oy), cy1 = min(floor_shift8(ymax - 128), oy + bh - 1);
+        int32_t cx0, cx1, cy0, cy1;
+        rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
         if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > kBigArea) {
             const uint32_t q = atomicAdd(&nbig, 1u);
@@ -729,28 +848,25 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
     }
     __syncthreads();
     const uint32_t nb = min(nbig, (uint32_t)kBigQueue);
-    for (uint32_t q = 0; q < nb; ++q) {
+    for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
         const TriRec r = load_rec(b.recs, bigq[q]);
-        const int32_t xmin = min(r.X[0], min(r.X[1], r.X[2])), xmax = max(r.X[0], max(r.X[1], r.X[2]));
-        const int32_t ymin = min(r.Y[0], min(r.Y[1], r.Y[2])), ymax = max(r.Y[0], max(r.Y[1], r.Y[2]));
-        const int32_t cx0 = max(-floor_shift8(128 - xmin), ox), cx1 = min(floor_shift8(xmax - 128), ox + bw - 1);
-        const int32_t cy0 = max(-floor_shift8(128 - ymin), oy), cy1 = min(floor_shift8(ymax - 128), oy + bh - 1);
+        int32_t cx0, cx1, cy0, cy1;
+        rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         EdgeSetup e;
-        int64_t D[3];
-        edge_setup(r, e, D);
+        edge_setup(r, e);
         bool rej = false;
         int32_t F[3];
 #pragma unroll
-        for (int k = 0; k < 3; ++k) F[k] = clamp_edge(e.a[k] * cx0 + e.b[k] * cy0 + D[k], rej);
+        for (int k = 0; k < 3; ++k) F[k] = clamp_edge((int64_t)e.A[k] * cx0 + (int64_t)e.B[k] * cy0 + e.D[k], rej);
         if (rej) continue;  // uniform across the workgroup
         const bool far_clip = (r.z[0] > 1.0f) || (r.z[1] > 1.0f) || (r.z[2] > 1.0f);
-        const uint32_t low = ((TRI_PRIM_MAX - (r.prim_sub >> 3)) << 3) | (r.prim_sub & 7u);
+        const uint32_t low = key_low(r.prim_sub);
         const int32_t rw = cx1 - cx0 + 1, rh = cy1 - cy0 + 1;
         for (int j = tid; j < rw * rh; j += TRI_BLOCK) {
             const int32_t dy = j / rw, dx = j - dy * rw;
-            const int32_t f0 = F[0] + (int32_t)e.a[0] * dx + (int32_t)e.b[0] * dy;
-            const int32_t f1 = F[1] + (int32_t)e.a[1] * dx + (int32_t)e.b[1] * dy;
-            const int32_t f2 = F[2] + (int32_t)e.a[2] * dx + (int32_t)e.b[2] * dy;
+            const int32_t f0 = F[0] + e.A[0] * dx + e.B[0] * dy;
+            const int32_t f1 = F[1] + e.A[1] * dx + e.B[1] * dy;
+            const int32_t f2 = F[2] + e.A[2] * dx + e.B[2] * dy;
             if ((f0 | f1 | f2) >= 0) {
                 const int32_t px = cx0 + dx, py = cy0 + dy;
                 uint64_t key;
@@ -773,7 +889,10 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
             z = 1.0f;
         } else {
             z = __uint_as_float((uint32_t)(key >> 32));
-            out = shade_pixel(fp, b, key, px, py, lut);
+            Frag f;
+            fetch_fragment<EXACT>(fp, b, key, px, py, lut, f);
+            const float4 c = EXACT ? fs_exact(fp, f) : fs_fast(fp.sc, f);
+            out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
         }
         const size_t o = (size_t)(py - fp.y0) * fp.W + px;
         b.color[o] = out;
@@ -783,29 +902,6 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
 
 }  // namespace
 
-hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
-                            hipEvent_t* ev) {
-    auto rec = [&](int i) {
-        if (ev) (void)hipEventRecord(ev[i], stream);
-    };
-    rec(0);
-    if (fp.nslots > 0)
-        hipLaunchKernelGGL(k_vertex, dim3((fp.nslots + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
-    rec(1);
-    const size_t hist_bytes = (size_t)fp.nbins * sizeof(uint32_t);
-    if (fp.nchunks > 0)
-        hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), hist_bytes, stream, fp, b);
-    rec(2);
-    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, stream, fp, b);
-    rec(3);
-    if (fp.nchunks > 0)
-        hipLaunchKernelGGL(k_scatter, dim3(fp.nchunks), dim3(TRI_BLOCK), 2 * hist_bytes, stream, fp, b);
-    rec(4);
-    hipLaunchKernelGGL(k_raster, dim3(fp.nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
-    rec(5);
-    return hipGetLastError();
-}
-
 hipError_t tri_kernels_init() {
     const int lds_max = 2 * 16384 * (int)sizeof(uint32_t);
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scatter),
@@ -813,4 +909,38 @@ hipError_t tri_kernels_init() {
     if (e != hipSuccess) return e;
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_setup),
                                hipFuncAttributeMaxDynamicSharedMemorySize, lds_max / 2);
+}
+
+hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
+                            hipEvent_t* ev) {
+    static const bool debug_sync = getenv("TRI_DEBUG_SYNC") != nullptr;
+    static const char* names[] = {"vertex", "setup+clip", "binscan", "scatter", "raster", "end"};
+    auto rec = [&](int i) {
+        if (ev) (void)hipEventRecord(ev[i], stream);
+        if (debug_sync) {
+            const hipError_t e = hipStreamSynchronize(stream);
+            fprintf(stderr, "[tri_raster] before %s: %s\n", names[i], hipGetErrorString(e));
+        }
+    };
+    rec(kStageVertex);
+    if (fp.nslots > 0)
+        hipLaunchKernelGGL(k_vertex, dim3((fp.nslots + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
+    rec(kStageSetup);
+    const size_t hist_bytes = (size_t)fp.nbins * sizeof(uint32_t);
+    if (fp.nchunks > 0) {
+        hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), hist_bytes, stream, fp, b);
+        hipLaunchKernelGGL(k_clip, dim3(TRI_CLIP_GRID), dim3(TRI_BLOCK), 0, stream, fp, b);
+    }
+    rec(kStageBinscan);
+    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, stream, fp, b);
+    rec(kStageScatter);
+    if (fp.nchunks > 0)
+        hipLaunchKernelGGL(k_scatter, dim3(fp.nchunks), dim3(TRI_BLOCK), 2 * hist_bytes, stream, fp, b);
+    rec(kStageRaster);
+    if (fp.exact_shading)
+        hipLaunchKernelGGL(k_raster<true>, dim3(fp.nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
+    else
+        hipLaunchKernelGGL(k_raster<false>, dim3(fp.nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
+    rec(kStageCount);
+    return hipGetLastError();
 }

@@ -6,19 +6,21 @@
 
 struct TriDeviceBuffers {
     const TriVsIn* vin;
-    const TriVsSkin* vskin;     // may be null when no draw skins
+    const TriVsSkin* vskin;      // may be null when no draw skins
     const float* bones;
     uint64_t vertex_count;
     const uint32_t* indices;
     const TriDrawDev* draws;
+    const TriDrawShade* draw_shade;
     const uint32_t* draw_vbase;  // ndraws+1
     const uint32_t* draw_pbase;  // ndraws+1
     const TriTexDesc* textures;  // TRI_MAX_TEXTURE_SLOTS entries, aliases resolved
     const float* srgb_lut;       // 256 entries, sRGB -> linear (computed on the host in double)
-    float4* clip;                // nslots + ovf verts (clip only for nslots)
+    float4* clip;                // nslots
     float4* vary;                // 3 * (nslots + ovf_vert_cap)
     TriRec* recs;                // nprims + ovf_rec_cap
     uint2* brange;               // nprims + ovf_rec_cap
+    uint32_t* clip_queue;        // ovf_rec_cap primitive ids needing geometric clipping
     uint32_t* bin_total;         // nbins (zero at frame start; re-zeroed by the scan)
     uint32_t* bin_start;         // nbins + 1
     uint32_t* bin_cursor;        // nbins
@@ -28,9 +30,12 @@ struct TriDeviceBuffers {
     float* depth;                // band rows * W (may be null)
 };
 
-// One frame = 5 dependent launches on `stream`; `events` (may be null) gets 6 timestamps.
+enum TriStage { kStageVertex = 0, kStageSetup, kStageBinscan, kStageScatter, kStageRaster, kStageCount };
+
 // Raise the dynamic-LDS limit of the histogram kernels (up to 2 x 16384 bins x 4 B).
 hipError_t tri_kernels_init();
 
+// One frame = 6 dependent launches on `stream`; `events` (may be null) gets kStageCount+1 stamps:
+// [vertex | setup+clip | binscan | scatter | raster].
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* events);

@@ -98,6 +98,8 @@ struct tri_ctx {
 
     // resolved draws
     TriDrawDev* d_draws = nullptr; size_t cap_draws = 0;
+    TriDrawShade* d_draw_shade = nullptr; size_t cap_draw_shade = 0;
+    uint32_t* d_clip_queue = nullptr; size_t cap_clip_queue = 0;
     uint32_t* d_vbase = nullptr; size_t cap_vbase = 0;
     uint32_t* d_pbase = nullptr; size_t cap_pbase = 0;
     void* h_stage = nullptr; size_t cap_stage = 0;  // pinned upload staging
@@ -136,6 +138,56 @@ int make_current(tri_ctx* c) {
     return TRI_OK;
 }
 
+// transpose(inverse(mat3(M))) exactly as Default.vert:95 evaluates it per vertex (glm cofactor
+// form, same float operation order as the oracle); out[c*3+r] = NM[c][r] = inverse[r][c].
+void normal_matrix(const float* M, float* out) {
+    auto m = [M](int c, int r) { return M[c * 4 + r]; };
+    const float det = (m(0, 0) * (m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) -
+                       m(1, 0) * (m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2))) +
+                      m(2, 0) * (m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2));
+    const float od = 1.0f / det;
+    float inv[3][3];
+    inv[0][0] = +(m(1, 1) * m(2, 2) - m(2, 1) * m(1, 2)) * od;
+    inv[1][0] = -(m(1, 0) * m(2, 2) - m(2, 0) * m(1, 2)) * od;
+    inv[2][0] = +(m(1, 0) * m(2, 1) - m(2, 0) * m(1, 1)) * od;
+    inv[0][1] = -(m(0, 1) * m(2, 2) - m(2, 1) * m(0, 2)) * od;
+    inv[1][1] = +(m(0, 0) * m(2, 2) - m(2, 0) * m(0, 2)) * od;
+    inv[2][1] = -(m(0, 0) * m(2, 1) - m(2, 0) * m(0, 1)) * od;
+    inv[0][2] = +(m(0, 1) * m(1, 2) - m(1, 1) * m(0, 2)) * od;
+    inv[1][2] = -(m(0, 0) * m(1, 2) - m(1, 0) * m(0, 2)) * od;
+    inv[2][2] = +(m(0, 0) * m(1, 1) - m(1, 0) * m(0, 1)) * od;
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) out[c * 3 + r] = inv[r][c];
+}
+
+float clamp01(float x) { return std::fmin(std::fmax(x, 0.0f), 1.0f); }
+
+// Default.frag frame constants hoisted for the fast shading build (Default.frag:131-174).
+void shade_constants(const tri_global_ubo& g, const tri_material_record& m, TriShadeConst& sc) {
+    std::memset(&sc, 0, sizeof sc);
+    std::memcpy(sc.cam, g.camera_position, 16);
+    std::memcpy(sc.base, m.base_color_factor, 16);
+    sc.metallic = clamp01(m.material_factors[0]);
+    sc.roughness = std::fmin(std::fmax(m.material_factors[1], 0.045f), 1.0f);
+    sc.amb_strength = clamp01(m.material_factors[2]);
+    for (int i = 0; i < 3; ++i) sc.amb[i] = g.ambient_color_intensity[i] * g.ambient_color_intensity[3];
+    sc.has_sun = g.light_counts[0] > 0u ? 1u : 0u;
+    const float lx = -g.directional_light_direction[0], ly = -g.directional_light_direction[1],
+                lz = -g.directional_light_direction[2];
+    const float il = 1.0f / std::sqrt((lx * lx + ly * ly) + lz * lz);
+    sc.sun_l[0] = lx * il; sc.sun_l[1] = ly * il; sc.sun_l[2] = lz * il;
+    for (int i = 0; i < 3; ++i) sc.sun_rad[i] = g.directional_light_color[i] * g.directional_light_color[3];
+    sc.npt = std::min<uint32_t>(g.light_counts[1], TRI_MAX_POINT_LIGHTS);
+    for (uint32_t i = 0; i < sc.npt; ++i) {
+        const tri_point_light& pl = g.point_lights[i];
+        for (int k = 0; k < 3; ++k) {
+            sc.pl_pos[i][k] = pl.position_range[k];
+            sc.pl_rad[i][k] = pl.color_intensity[k] * pl.color_intensity[3];
+        }
+        sc.pl_pos[i][3] = 1.0f / std::fmax(pl.position_range[3], 1e-4f);
+    }
+}
+
 // glm mat4 * mat4 (column j = ((A0*B[j][0] + A1*B[j][1]) + A2*B[j][2]) + A3*B[j][3])
 void mat4_mul(const float* a, const float* b, float* r) {
     for (int j = 0; j < 4; ++j)
@@ -168,6 +220,7 @@ int resolve_draws(tri_ctx* c) {
     if (!c->draws_dirty) return TRI_OK;
     const uint32_t n = (uint32_t)c->draws.size();
     std::vector<TriDrawDev> dd(n);
+    std::vector<TriDrawShade> ds(n);
     std::vector<uint32_t> vb(n + 1), pb(n + 1);
     uint64_t vslots = 0, prims = 0;
     bool skin = false;
@@ -176,14 +229,17 @@ int resolve_draws(tri_ctx* c) {
         TriDrawDev& o = dd[d];
         std::memset(&o, 0, sizeof o);
         std::memcpy(o.model, src.pc.model, 64);
-        std::memcpy(o.tint, src.pc.tint, 16);
+        normal_matrix(src.pc.model, o.nm);
+        TriDrawShade& sh = ds[d];
+        std::memset(&sh, 0, sizeof sh);
+        std::memcpy(sh.tint, src.pc.tint, 16);
+        const int32_t slot = src.pc.texture_slot;
+        sh.tex_id = (slot >= 0 && slot < TRI_MAX_TEXTURE_SLOTS) ? slot : 0;
         o.tex_scale[0] = src.pc.texture_scale[0];
         o.tex_scale[1] = src.pc.texture_scale[1];
         o.tex_offset[0] = src.pc.texture_offset[0];
         o.tex_offset[1] = src.pc.texture_offset[1];
         o.tiling = src.pc.tiling_factor;
-        const int32_t slot = src.pc.texture_slot;
-        o.tex_id = (slot >= 0 && slot < TRI_MAX_TEXTURE_SLOTS) ? slot : 0;
         o.bone_offset = src.pc.bone_offset;
         o.bone_count = src.pc.bone_count;
         vb[d] = (uint32_t)vslots;
@@ -205,9 +261,13 @@ int resolve_draws(tri_ctx* c) {
     if (prims > TRI_PRIM_MAX) return fail(TRI_E_INVALID, "too many primitives (%llu > %u)", (unsigned long long)prims, TRI_PRIM_MAX);
     int rc;
     if ((rc = grow(c->d_draws, c->cap_draws, std::max<size_t>(n, 1)))) return rc;
+    if ((rc = grow(c->d_draw_shade, c->cap_draw_shade, std::max<size_t>(n, 1)))) return rc;
     if ((rc = grow(c->d_vbase, c->cap_vbase, n + 1))) return rc;
     if ((rc = grow(c->d_pbase, c->cap_pbase, n + 1))) return rc;
-    const size_t bytes = n * sizeof(TriDrawDev) + 2 * (n + 1) * sizeof(uint32_t);
+    const size_t o_shade = n * sizeof(TriDrawDev);
+    const size_t o_vb = o_shade + n * sizeof(TriDrawShade);
+    const size_t o_pb = o_vb + (n + 1) * 4;
+    const size_t bytes = o_pb + (n + 1) * 4;
     if (c->stage_free) HIP_TRY(hipEventSynchronize(c->stage_free));
     if (bytes > c->cap_stage) {
         if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
@@ -217,12 +277,16 @@ int resolve_draws(tri_ctx* c) {
     }
     char* st = static_cast<char*>(c->h_stage);
     std::memcpy(st, dd.data(), n * sizeof(TriDrawDev));
-    std::memcpy(st + n * sizeof(TriDrawDev), vb.data(), (n + 1) * 4);
-    std::memcpy(st + n * sizeof(TriDrawDev) + (n + 1) * 4, pb.data(), (n + 1) * 4);
-    if (n) HIP_TRY(hipMemcpyAsync(c->d_draws, st, n * sizeof(TriDrawDev), hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_vbase, st + n * sizeof(TriDrawDev), (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
-    HIP_TRY(hipMemcpyAsync(c->d_pbase, st + n * sizeof(TriDrawDev) + (n + 1) * 4, (n + 1) * 4,
-                           hipMemcpyHostToDevice, c->stream));
+    std::memcpy(st + o_shade, ds.data(), n * sizeof(TriDrawShade));
+    std::memcpy(st + o_vb, vb.data(), (n + 1) * 4);
+    std::memcpy(st + o_pb, pb.data(), (n + 1) * 4);
+    if (n) {
+        HIP_TRY(hipMemcpyAsync(c->d_draws, st, n * sizeof(TriDrawDev), hipMemcpyHostToDevice, c->stream));
+        HIP_TRY(hipMemcpyAsync(c->d_draw_shade, st + o_shade, n * sizeof(TriDrawShade), hipMemcpyHostToDevice,
+                               c->stream));
+    }
+    HIP_TRY(hipMemcpyAsync(c->d_vbase, st + o_vb, (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_pbase, st + o_pb, (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
     if (!c->stage_free) HIP_TRY(hipEventCreateWithFlags(&c->stage_free, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(c->stage_free, c->stream));
     c->ndraws = n;
@@ -245,6 +309,7 @@ int ensure_work_buffers(tri_ctx* c) {
     if ((rc = grow(c->d_vary, c->cap_vary, nvary))) return rc;
     if ((rc = grow(c->d_recs, c->cap_recs, nrec))) return rc;
     if ((rc = grow(c->d_brange, c->cap_brange, nrec))) return rc;
+    if ((rc = grow(c->d_clip_queue, c->cap_clip_queue, c->ovf_rec_cap))) return rc;
     if ((rc = grow(c->d_bin_list, c->cap_bin_list, c->bin_cap))) return rc;
     return TRI_OK;
 }
@@ -275,7 +340,7 @@ int check_overflow(tri_ctx* c) {
     if (!h.flags) return TRI_OK;
     const uint32_t zero = 0;
     HIP_TRY(hipMemcpy(&c->d_ctr->flags, &zero, 4, hipMemcpyHostToDevice));
-    if (h.flags & TRI_OVF_CLIP_RECORDS) c->ovf_rec_cap *= 4;
+    if (h.flags & (TRI_OVF_CLIP_RECORDS | TRI_OVF_CLIP_QUEUE)) c->ovf_rec_cap *= 4;
     if (h.flags & TRI_OVF_CLIP_VERTS) c->ovf_vert_cap *= 4;
     if (h.flags & TRI_OVF_BIN_LIST) c->bin_cap = std::max<uint32_t>(c->bin_cap * 2, h.bin_entries + h.bin_entries / 4);
     int rc = ensure_work_buffers(c);
@@ -365,7 +430,7 @@ int tri_destroy(tri_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones);
     for (auto& t : c->d_tex) f(t);
-    f(c->d_draws); f(c->d_vbase); f(c->d_pbase);
+    f(c->d_draws); f(c->d_draw_shade); f(c->d_clip_queue); f(c->d_vbase); f(c->d_pbase);
     f(c->d_clip); f(c->d_vary); f(c->d_recs); f(c->d_brange);
     f(c->d_bin_total); f(c->d_bin_start); f(c->d_bin_cursor); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own);
@@ -548,9 +613,11 @@ int tri_render(tri_ctx* c) {
     fp.bone_count = c->nbones;
     fp.clear_bgra = c->clear_bgra;
     fp.write_depth = (c->cfg.flags & TRI_FLAG_NO_DEPTH_OUTPUT) ? 0u : 1u;
+    fp.exact_shading = (c->cfg.flags & TRI_FLAG_EXACT_SHADING) ? 1u : 0u;
     std::memcpy(fp.pv, c->pv, 64);
     fp.ubo = c->ubo;
     fp.mat0 = c->mat0;
+    shade_constants(c->ubo, c->mat0, fp.sc);
 
     TriDeviceBuffers b;
     b.vin = c->d_vin;
@@ -559,6 +626,8 @@ int tri_render(tri_ctx* c) {
     b.vertex_count = c->nverts;
     b.indices = c->d_idx;
     b.draws = c->d_draws;
+    b.draw_shade = c->d_draw_shade;
+    b.clip_queue = c->d_clip_queue;
     b.draw_vbase = c->d_vbase;
     b.draw_pbase = c->d_pbase;
     b.textures = c->d_texdesc;

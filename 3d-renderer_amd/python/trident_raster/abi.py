@@ -20,6 +20,7 @@ TRI_E_STATE = -6
 TRI_MAX_POINT_LIGHTS = 8
 TRI_MAX_TEXTURE_SLOTS = 256
 TRI_FLAG_NO_DEPTH_OUTPUT = 0x1
+TRI_FLAG_EXACT_SHADING = 0x2
 
 VERTEX_DTYPE = np.dtype(
     [

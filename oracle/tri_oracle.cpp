@@ -242,8 +242,8 @@ int clip_polygon(const Setup& su, const VsOut in[3], VsOut* out /* >= 9 */) {
             const VsOut& a = src[i];
             const VsOut& b = src[(i + 1) % n];
             const float da = dist(a), db = dist(b);
-            if (da >= 0.0f) dst[m++] = a;
-            if ((da >= 0.0f) != (db >= 0.0f)) {
+            if (da >= 0.0f && m < 12) dst[m++] = a;
+            if ((da >= 0.0f) != (db >= 0.0f) && m < 12) {
                 const float t = da / (da - db);
                 dst[m++] = lerp_vs(a, b, t);
             }
