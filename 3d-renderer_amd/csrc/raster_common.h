@@ -25,7 +25,8 @@
 #define TRI_MAX_CLIP_VERTS 12
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f
-#define TRI_CLIP_GRID 64
+#define TRI_CLIP_GRID 16
+#define TRI_MAX_PPT 8  // primitives per k_setup thread
 
 // overflow flag bits (TriCounters.flags)
 #define TRI_OVF_CLIP_RECORDS 0x1u
@@ -43,6 +44,25 @@ struct __attribute__((aligned(16))) TriVsSkin {
     int32_t idx[4];
     float w[4];
 };
+
+// Per-vertex window-space record written by k_vertex (the perspective divide + viewport transform
+// + 8-bit snap are done once per vertex): X (signed 24 bits) | outcode << 24, Y, z_ndc, 1/w.
+struct __attribute__((aligned(16))) TriSnap {
+    int32_t xo;
+    int32_t y;
+    float z;
+    float iw;
+};
+// outcode bits: one per Vulkan clip half-space a vertex is outside of, + "needs geometric clip"
+#define TRI_OC_ZNEG 0x01u   /* z < 0     */
+#define TRI_OC_ZFAR 0x02u   /* z > w     */
+#define TRI_OC_XNEG 0x04u   /* x < -w    */
+#define TRI_OC_XPOS 0x08u   /* x > w     */
+#define TRI_OC_YNEG 0x10u   /* y < -w    */
+#define TRI_OC_YPOS 0x20u   /* y > w     */
+#define TRI_OC_CLIP 0x40u   /* w < WMIN, z < 0 or outside the guard band */
+#define TRI_OC_BAD 0x80u    /* vertex index out of range */
+#define TRI_OC_REJECT 0x3Fu
 
 struct __attribute__((aligned(16))) TriRec {
     int32_t X[3];
@@ -82,17 +102,16 @@ struct TriTexDesc {
     uint32_t w, h;
 };
 
-struct TriCounters {  // per-frame fields are zeroed before every frame; `flags` is sticky
+struct TriCounters {  // per-frame fields are zeroed before every frame; `flags`/`bin_max` are sticky
     uint32_t ovf_records;
     uint32_t ovf_verts;
     uint32_t tris_setup;
     uint32_t tris_clipped;
     uint32_t bin_entries;
     uint32_t clip_queue;
-    uint32_t pad;
+    uint32_t bin_max;  // largest per-bin entry count seen (sizes the bin queues after an overflow)
     uint32_t flags;
 };
-#define TRI_COUNTERS_RESET_BYTES 28
 
 // Frame constants of Default.frag hoisted on the host (fast shading path).
 struct TriShadeConst {
@@ -110,6 +129,9 @@ struct TriShadeConst {
 struct TriFrameParams {
     int32_t W, H, y0, y1;
     int32_t nbx, nby, nbins, ppt;
+    int32_t bin_log2;
+    uint32_t ablate;  // diagnostics only (TRI_ABLATE env): 1 = skip shading, 2 = skip coverage
+    int32_t pad_b1, pad_b2;
     float hw, hh, gx, gy;
     uint32_t nprims, nslots, ndraws, nchunks;
     uint32_t ovf_rec_cap, ovf_vert_cap, bin_cap, bone_count;

@@ -1,13 +1,12 @@
 // raster_kernels.hip — hand-written gfx950 (CDNA4) kernels for Trident's graphics-pipeline stage.
 //
 //   k_vertex   vs_transform   Default.vert:60-105, one lane per (draw, referenced vertex)
-//   k_setup    tri_setup_bin  primitive assembly + trivial reject + cull + 8-bit snap + bbox,
-//                             per-chunk LDS bin histogram (Pipeline.cpp:611-643); triangles that need
-//                             homogeneous clipping are queued for k_clip
+//   k_setup    tri_setup_bin  primitive assembly + trivial reject + cull + bbox on the per-vertex
+//                             snapped coordinates (Pipeline.cpp:611-643), binned into per-bin queues
+//                             (LDS histogram, one global atomic per touched (chunk, bin)); triangles
+//                             that need homogeneous clipping are queued for k_clip
 //   k_clip     rare path: Sutherland-Hodgman against w>=WMIN, z>=0 and the guard band + fan
-//   k_binscan  bin prefix scan (one workgroup)
-//   k_scatter  bin list scatter (LDS-privatised cursors, one global atomic per (chunk, bin))
-//   k_raster   tile_raster_shade: one workgroup per 64x64 bin; coverage + early-Z resolved in LDS
+//   k_raster   tile_raster_shade: one workgroup per 32x32 (or 64x64) bin; coverage + early-Z in LDS
 //              with 64-bit (depth, primitive-order) keys (== in-order LESS_OR_EQUAL,
 //              Pipeline.cpp:655-658), then Default.frag:123-192 once per visible pixel, coalesced
 //              B8G8R8A8 + D32 stores.
@@ -57,14 +56,26 @@ __device__ __forceinline__ float4 mat_vec_seq(const float* m, float4 v) {
 // ------------------------------------------------------------------------------------------
 // vs_transform
 // ------------------------------------------------------------------------------------------
+__device__ __forceinline__ void snap_compute(const TriFrameParams& fp, float4 c, int32_t& X, int32_t& Y, float& z,
+                                             float& iw);
+__device__ __forceinline__ uint32_t outcode(const TriFrameParams& fp, float4 c);
+
+__device__ __forceinline__ void reset_counters(TriCounters* c) {
+    c->ovf_records = 0; c->ovf_verts = 0; c->tris_setup = 0; c->tris_clipped = 0;
+    c->bin_entries = 0; c->clip_queue = 0;  // `flags` / `bin_max` are sticky (cleared by the host)
+}
+
+__global__ void k_reset(TriDeviceBuffers b) { reset_counters(b.counters); }
+
 __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
     const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
+    if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
     if (slot >= fp.nslots) return;
     const int d = find_range(b.draw_vbase, (int)fp.ndraws, slot);
     const TriDrawDev& dr = b.draws[d];
     const int64_t gi = (int64_t)dr.base_vertex + (int64_t)(dr.min_index + (slot - b.draw_vbase[d]));
     if (gi < 0 || (uint64_t)gi >= b.vertex_count) {
-        b.clip[slot] = make_float4(0.f, 0.f, 0.f, __builtin_nanf(""));
+        b.snap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
         return;
     }
     const TriVsIn in = b.vin[gi];
@@ -102,7 +113,17 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
     nnx = nnx * inv; nny = nny * inv; nnz = nnz * inv;
     const float u = (in.u * dr.tex_scale[0]) * dr.tiling + dr.tex_offset[0];
     const float v = (in.v * dr.tex_scale[1]) * dr.tiling + dr.tex_offset[1];
-    b.clip[slot] = mat_vec_seq(fp.pv, world);
+    const float4 clip = mat_vec_seq(fp.pv, world);
+    b.clip[slot] = clip;
+    const uint32_t oc = outcode(fp, clip);
+    TriSnap sn{(int32_t)(oc << 24), 0, 0.0f, 0.0f};
+    if (!(oc & TRI_OC_CLIP)) {
+        int32_t X, Y;
+        snap_compute(fp, clip, X, Y, sn.z, sn.iw);
+        sn.xo = (X & 0x00FFFFFF) | (int32_t)(oc << 24);  // |X| < 2^22 inside the guard band
+        sn.y = Y;
+    }
+    b.snap[slot] = sn;
     float4* vo = b.vary + 3ull * slot;
     vo[0] = make_float4(world.x, world.y, world.z, u);
     vo[1] = make_float4(nnx, nny, nnz, v);
@@ -114,24 +135,38 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ int32_t floor_shift8(int32_t v) { return v >> 8; }
 
-// Direct setup of a triangle whose vertices are all inside w>=WMIN, z>=0 and the guard band.
+// Perspective divide (x * (1/w), one correctly rounded divide), viewport transform
+// (Renderer.cpp:5062-5069) and 8-bit sub-pixel snap of one vertex. Mirrors oracle setup_triangle().
+__device__ __forceinline__ void snap_compute(const TriFrameParams& fp, float4 c, int32_t& X, int32_t& Y, float& z,
+                                             float& iw) {
+    iw = 1.0f / c.w;
+    const float xd = c.x * iw, yd = c.y * iw;
+    z = c.z * iw;
+    const float xf = xd * fp.hw + fp.hw;
+    const float yf = yd * fp.hh + fp.hh;
+    X = (int32_t)rintf(xf * 256.0f);
+    Y = (int32_t)rintf(yf * 256.0f);
+}
+
+__device__ __forceinline__ uint32_t outcode(const TriFrameParams& fp, float4 c) {
+    uint32_t oc = 0;
+    if (c.z < 0.0f) oc |= TRI_OC_ZNEG;
+    if (c.w - c.z < 0.0f) oc |= TRI_OC_ZFAR;
+    if (c.x + c.w < 0.0f) oc |= TRI_OC_XNEG;
+    if (c.w - c.x < 0.0f) oc |= TRI_OC_XPOS;
+    if (c.y + c.w < 0.0f) oc |= TRI_OC_YNEG;
+    if (c.w - c.y < 0.0f) oc |= TRI_OC_YPOS;
+    if ((c.w < TRI_WMIN) || (c.z < 0.0f) || (c.x < -fp.gx * c.w) || (c.x > fp.gx * c.w) ||
+        (c.y < -fp.gy * c.w) || (c.y > fp.gy * c.w))
+        oc |= TRI_OC_CLIP;
+    return oc;
+}
+
+// Setup of a triangle from snapped vertices (all inside w>=WMIN, z>=0 and the guard band).
 // Mirrors oracle setup_triangle(). Returns false when culled or when its bbox is empty.
-__device__ __forceinline__ bool setup_direct(const TriFrameParams& fp, float4 c0, float4 c1, float4 c2,
-                                             uint32_t s0, uint32_t s1, uint32_t s2, uint32_t prim_sub,
-                                             TriRec& r, uint2& br) {
-    const float4 c[3] = {c0, c1, c2};
-    int32_t X[3], Y[3];
-    float z[3], iw[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const float xd = c[k].x / c[k].w, yd = c[k].y / c[k].w, zd = c[k].z / c[k].w;
-        iw[k] = 1.0f / c[k].w;
-        const float xf = xd * fp.hw + fp.hw;
-        const float yf = yd * fp.hh + fp.hh;
-        X[k] = (int32_t)rintf(xf * 256.0f);
-        Y[k] = (int32_t)rintf(yf * 256.0f);
-        z[k] = zd;
-    }
+__device__ __forceinline__ bool setup_snapped(const TriFrameParams& fp, const int32_t X[3], const int32_t Y[3],
+                                              const float z[3], const float iw[3], uint32_t s0, uint32_t s1,
+                                              uint32_t s2, uint32_t prim_sub, TriRec& r, uint2& br) {
     const int64_t S = (int64_t)(X[1] - X[0]) * (int64_t)(Y[2] - Y[0]) -
                       (int64_t)(Y[1] - Y[0]) * (int64_t)(X[2] - X[0]);
     if (S >= 0) return false;  // zero area or back-facing (cull BACK, front CCW)
@@ -151,10 +186,22 @@ __device__ __forceinline__ bool setup_direct(const TriFrameParams& fp, float4 c0
     r.iw[0] = iw[0]; r.iw[1] = iw[2]; r.iw[2] = iw[1];
     r.v[0] = s0; r.v[1] = s2; r.v[2] = s1;
     r.prim_sub = prim_sub;
-    const uint32_t bx0 = (uint32_t)px0 >> TRI_BIN_LOG2, bx1 = (uint32_t)px1 >> TRI_BIN_LOG2;
-    const uint32_t by0 = (uint32_t)(py0 - fp.y0) >> TRI_BIN_LOG2, by1 = (uint32_t)(py1 - fp.y0) >> TRI_BIN_LOG2;
+    const uint32_t bl = (uint32_t)fp.bin_log2;
+    const uint32_t bx0 = (uint32_t)px0 >> bl, bx1 = (uint32_t)px1 >> bl;
+    const uint32_t by0 = (uint32_t)(py0 - fp.y0) >> bl, by1 = (uint32_t)(py1 - fp.y0) >> bl;
     br = make_uint2(bx0 | (by0 << 16), bx1 | (by1 << 16));
     return true;
+}
+
+__device__ __forceinline__ bool setup_from_clip(const TriFrameParams& fp, float4 c0, float4 c1, float4 c2,
+                                                uint32_t s0, uint32_t s1, uint32_t s2, uint32_t prim_sub, TriRec& r,
+                                                uint2& br) {
+    int32_t X[3], Y[3];
+    float z[3], iw[3];
+    snap_compute(fp, c0, X[0], Y[0], z[0], iw[0]);
+    snap_compute(fp, c1, X[1], Y[1], z[1], iw[1]);
+    snap_compute(fp, c2, X[2], Y[2], z[2], iw[2]);
+    return setup_snapped(fp, X, Y, z, iw, s0, s1, s2, prim_sub, r, br);
 }
 
 template <typename F>
@@ -164,71 +211,97 @@ __device__ __forceinline__ void for_bins(uint2 br, int nbx, F&& f) {
         for (uint32_t bx = bx0; bx <= bx1; ++bx) f(by * (uint32_t)nbx + bx);
 }
 
+__device__ __forceinline__ void note_bin_overflow(const TriDeviceBuffers& b, uint32_t needed) {
+    atomicOr(&b.counters->flags, TRI_OVF_BIN_LIST);
+    atomicMax(&b.counters->bin_max, needed);
+}
+
+// One workgroup bins a chunk of TRI_BLOCK * ppt consecutive primitives: setup per primitive, an LDS
+// histogram over the bins they touch (plus a list of touched bins), ONE global atomicAdd per touched
+// bin to reserve a contiguous range of that bin's queue, then the queue writes. Entry order inside a
+// bin is free: k_raster resolves visibility with (depth, primitive order) keys.
 __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
-    extern __shared__ uint32_t hist[];
-    __shared__ uint32_t red[2];
+    extern __shared__ uint32_t lds[];
+    uint32_t* hist = lds;                                           // nbins counters -> queue cursors
+    uint16_t* touched = reinterpret_cast<uint16_t*>(lds + fp.nbins);  // bins touched by this chunk
+    __shared__ uint32_t red[4];
     for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) hist[i] = 0;
-    if (threadIdx.x == 0) { red[0] = 0; red[1] = 0; }
+    if (threadIdx.x == 0) { red[0] = 0; red[1] = 0; red[2] = 0; red[3] = 0; }
     __syncthreads();
     uint32_t nsetup = 0, nclip = 0;
     const uint32_t chunk0 = blockIdx.x * (uint32_t)(TRI_BLOCK * fp.ppt);
-    for (int k = 0; k < fp.ppt; ++k) {
+    uint2 brk[TRI_MAX_PPT];
+#pragma unroll
+    for (int k = 0; k < TRI_MAX_PPT; ++k) {
+        brk[k] = make_uint2(TRI_BR_CULLED, 0u);
         const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
-        if (p >= fp.nprims) break;
+        if (k >= fp.ppt || p >= fp.nprims) continue;
         const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
         const TriDrawDev& dr = b.draws[d];
         const uint32_t t = p - b.draw_pbase[d];
         const uint32_t* ip = b.indices + dr.first_index + 3ull * t;
         const uint32_t vb = b.draw_vbase[d] - dr.min_index;
         const uint32_t sl0 = vb + ip[0], sl1 = vb + ip[1], sl2 = vb + ip[2];
-        const float4 c0 = b.clip[sl0], c1 = b.clip[sl1], c2 = b.clip[sl2];
+        const TriSnap a0 = b.snap[sl0], a1 = b.snap[sl1], a2 = b.snap[sl2];
+        const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
         TriRec r;
         uint2 br = make_uint2(TRI_BR_CULLED, 0u);
         bool ok = false;
-        if (!(isnan(c0.w) || isnan(c1.w) || isnan(c2.w))) {
-            // trivial reject: all three vertices outside one clip half-space
-#define ALLNEG(e0, e1, e2) ((e0) < 0.0f && (e1) < 0.0f && (e2) < 0.0f)
-            const bool rej = ALLNEG(c0.z, c1.z, c2.z) || ALLNEG(c0.w - c0.z, c1.w - c1.z, c2.w - c2.z) ||
-                             ALLNEG(c0.x + c0.w, c1.x + c1.w, c2.x + c2.w) ||
-                             ALLNEG(c0.w - c0.x, c1.w - c1.x, c2.w - c2.x) ||
-                             ALLNEG(c0.y + c0.w, c1.y + c1.w, c2.y + c2.w) ||
-                             ALLNEG(c0.w - c0.y, c1.w - c1.y, c2.w - c2.y);
-#undef ALLNEG
-            if (!rej) {
-                auto outside = [&](float4 c) {
-                    return (c.w < TRI_WMIN) || (c.z < 0.0f) || (c.x < -fp.gx * c.w) || (c.x > fp.gx * c.w) ||
-                           (c.y < -fp.gy * c.w) || (c.y > fp.gy * c.w);
-                };
-                if (outside(c0) || outside(c1) || outside(c2)) {
-                    ++nclip;
-                    const uint32_t q = atomicAdd(&b.counters->clip_queue, 1u);
-                    if (q < fp.ovf_rec_cap) b.clip_queue[q] = p;
-                    else atomicOr(&b.counters->flags, TRI_OVF_CLIP_QUEUE);
-                } else {
-                    ok = setup_direct(fp, c0, c1, c2, sl0, sl1, sl2, p << 3, r, br);
-                }
+        // invalid vertex, or trivial reject: all three vertices outside one clip half-space
+        if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
+            if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
+                ++nclip;
+                const uint32_t q = atomicAdd(&b.counters->clip_queue, 1u);
+                if (q < fp.ovf_rec_cap) b.clip_queue[q] = p;
+                else atomicOr(&b.counters->flags, TRI_OVF_CLIP_QUEUE);
+            } else {
+                const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
+                const int32_t Y[3] = {a0.y, a1.y, a2.y};
+                const float z[3] = {a0.z, a1.z, a2.z};
+                const float iw[3] = {a0.iw, a1.iw, a2.iw};
+                ok = setup_snapped(fp, X, Y, z, iw, sl0, sl1, sl2, p << 3, r, br);
             }
         }
         if (ok) {
             ++nsetup;
-            for_bins(br, fp.nbx, [&](uint32_t bi) { atomicAdd(&hist[bi], 1u); });
+            brk[k] = br;
+            for_bins(br, fp.nbx, [&](uint32_t bi) {
+                if (atomicAdd(&hist[bi], 1u) == 0u) touched[atomicAdd(&red[2], 1u)] = (uint16_t)bi;
+            });
         } else {
             r.prim_sub = TRI_REC_CULLED;
-            br = make_uint2(TRI_BR_CULLED, 0u);
         }
         b.recs[p] = r;
-        b.brange[p] = br;
     }
     if (nsetup) atomicAdd(&red[0], nsetup);
     if (nclip) atomicAdd(&red[1], nclip);
     __syncthreads();
+    const uint32_t ntouched = red[2];
+    const uint32_t cap = fp.bin_cap;
+    uint32_t entries = 0;
+    for (uint32_t i = threadIdx.x; i < ntouched; i += TRI_BLOCK) {  // reserve queue ranges
+        const uint32_t bi = touched[i];
+        const uint32_t cnt = hist[bi];
+        const uint32_t base = atomicAdd(&b.bin_count[bi], cnt);
+        if (base + cnt > cap) note_bin_overflow(b, base + cnt);
+        hist[bi] = base;
+        entries += cnt;
+    }
+    if (entries) atomicAdd(&red[3], entries);
+    __syncthreads();
     if (threadIdx.x == 0) {
         if (red[0]) atomicAdd(&b.counters->tris_setup, red[0]);
         if (red[1]) atomicAdd(&b.counters->tris_clipped, red[1]);
+        if (red[3]) atomicAdd(&b.counters->bin_entries, red[3]);
     }
-    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) {
-        const uint32_t h = hist[i];
-        if (h) atomicAdd(&b.bin_total[i], h);
+#pragma unroll
+    for (int k = 0; k < TRI_MAX_PPT; ++k) {  // fill the reserved ranges
+        if (brk[k].x == TRI_BR_CULLED) continue;
+        const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
+        for_bins(brk[k], fp.nbx, [&](uint32_t bi) {
+            const uint32_t pos = atomicAdd(&hist[bi], 1u);
+            if (pos < cap) b.bin_list[(size_t)bi * cap + pos] = p;
+        });
     }
 }
 
@@ -261,7 +334,7 @@ __device__ __forceinline__ float plane_dist(const TriFrameParams& fp, int plane,
 
 __global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDeviceBuffers b) {
     const uint32_t nq = min(b.counters->clip_queue, fp.ovf_rec_cap);
-    uint32_t nsetup = 0;
+    uint32_t nsetup = 0, nentries = 0;
     for (uint32_t q = blockIdx.x * TRI_BLOCK + threadIdx.x; q < nq; q += gridDim.x * TRI_BLOCK) {
         const uint32_t prim = b.clip_queue[q];
         const int d = find_range(b.draw_pbase, (int)fp.ndraws, prim);
@@ -298,7 +371,6 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDevice
         const ClipVert* src = buf[cur];
         TriRec main{};
         main.prim_sub = TRI_REC_CULLED;
-        uint2 main_br = make_uint2(TRI_BR_CULLED, 0u);
         if (n >= 3) {
             const uint32_t nsub = (uint32_t)(n - 2);
             const uint32_t rbase = atomicAdd(&b.counters->ovf_records, nsub);
@@ -326,108 +398,30 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDevice
                     TriRec r;
                     uint2 br = make_uint2(TRI_BR_CULLED, 0u);
                     const uint32_t ps = (prim << 3) | (uint32_t)(k - 1);
-                    if (setup_direct(fp, src[0].c, src[k].c, src[k + 1].c, sbase, sbase + k, sbase + k + 1, ps, r,
-                                     br)) {
+                    if (setup_from_clip(fp, src[0].c, src[k].c, src[k + 1].c, sbase, sbase + k, sbase + k + 1, ps, r,
+                                        br)) {
                         ++nsetup;
-                        for_bins(br, fp.nbx, [&](uint32_t bi) { atomicAdd(&b.bin_total[bi], 1u); });
+                        const uint32_t rid = first + k - 1;
+                        for_bins(br, fp.nbx, [&](uint32_t bi) {  // rare path: one global atomic per entry
+                            const uint32_t pos = atomicAdd(&b.bin_count[bi], 1u);
+                            if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = rid;
+                            else note_bin_overflow(b, pos + 1);
+                            ++nentries;
+                        });
                     } else {
                         r.prim_sub = TRI_REC_CULLED;
-                        br = make_uint2(TRI_BR_CULLED, 0u);
                     }
                     b.recs[first + k - 1] = r;
-                    b.brange[first + k - 1] = br;
                 }
                 main.prim_sub = TRI_REC_CLIPPED;
                 main.v[0] = first;
                 main.v[1] = nsub;
-                main_br = make_uint2(TRI_BR_CLIPPED, 0u);
             }
         }
         b.recs[prim] = main;
-        b.brange[prim] = main_br;
     }
     if (nsetup) atomicAdd(&b.counters->tris_setup, nsetup);
-}
-
-// ------------------------------------------------------------------------------------------
-// bin prefix scan: one 1024-thread workgroup; nbins <= 16384
-// ------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_binscan(TriFrameParams fp, TriDeviceBuffers b) {
-    __shared__ uint32_t part[1024];
-    const int per = (fp.nbins + 1023) / 1024;
-    const int i0 = threadIdx.x * per;
-    uint32_t s = 0;
-    for (int i = i0; i < min(i0 + per, fp.nbins); ++i) s += b.bin_total[i];
-    part[threadIdx.x] = s;
-    __syncthreads();
-    for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
-        const uint32_t v = (threadIdx.x >= (unsigned)off) ? part[threadIdx.x - off] : 0u;
-        __syncthreads();
-        part[threadIdx.x] += v;
-        __syncthreads();
-    }
-    uint32_t run = threadIdx.x ? part[threadIdx.x - 1] : 0u;
-    for (int i = i0; i < min(i0 + per, fp.nbins); ++i) {
-        const uint32_t c = b.bin_total[i];
-        b.bin_start[i] = run;
-        b.bin_cursor[i] = run;
-        b.bin_total[i] = 0;  // ready for the next frame
-        run += c;
-    }
-    if (threadIdx.x == 1023) {
-        const uint32_t total = part[1023];
-        b.bin_start[fp.nbins] = total;
-        b.counters->bin_entries = total;
-        if (total > fp.bin_cap) atomicOr(&b.counters->flags, TRI_OVF_BIN_LIST);
-    }
-}
-
-// ------------------------------------------------------------------------------------------
-// bin list scatter
-// ------------------------------------------------------------------------------------------
-template <typename F>
-__device__ __forceinline__ void for_each_binned(const TriFrameParams& fp, const TriDeviceBuffers& b, F&& f) {
-    const uint32_t chunk0 = blockIdx.x * (uint32_t)(TRI_BLOCK * fp.ppt);
-    for (int k = 0; k < fp.ppt; ++k) {
-        const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
-        if (p >= fp.nprims) break;
-        const uint2 br = b.brange[p];
-        if (br.x == TRI_BR_CULLED) continue;
-        if (br.x == TRI_BR_CLIPPED) {
-            const uint32_t first = b.recs[p].v[0], cnt = b.recs[p].v[1];
-            for (uint32_t s = 0; s < cnt; ++s) {
-                const uint2 sb = b.brange[first + s];
-                if (sb.x != TRI_BR_CULLED) f(first + s, sb);
-            }
-            continue;
-        }
-        f(p, br);
-    }
-}
-
-__global__ __launch_bounds__(TRI_BLOCK) void k_scatter(TriFrameParams fp, TriDeviceBuffers b) {
-    extern __shared__ uint32_t lds[];
-    uint32_t* hist = lds;
-    uint32_t* base = lds + fp.nbins;
-    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) hist[i] = 0;
-    __syncthreads();
-    for_each_binned(fp, b, [&](uint32_t, uint2 br) {
-        for_bins(br, fp.nbx, [&](uint32_t bi) { atomicAdd(&hist[bi], 1u); });
-    });
-    __syncthreads();
-    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) {
-        const uint32_t h = hist[i];
-        if (h) base[i] = atomicAdd(&b.bin_cursor[i], h);
-        hist[i] = 0;
-    }
-    __syncthreads();
-    const uint32_t cap = fp.bin_cap;
-    for_each_binned(fp, b, [&](uint32_t rec, uint2 br) {
-        for_bins(br, fp.nbx, [&](uint32_t bi) {
-            const uint32_t pos = base[bi] + atomicAdd(&hist[bi], 1u);
-            if (pos < cap) b.bin_list[pos] = rec;
-        });
-    });
+    if (nentries) atomicAdd(&b.counters->bin_entries, nentries);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -509,6 +503,7 @@ __device__ __forceinline__ uint32_t key_low(uint32_t prim_sub) {
     return ((TRI_PRIM_MAX - (prim_sub >> 3)) << 3) | (prim_sub & 7u);
 }
 
+template <int BL>
 __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int32_t cx1, int32_t cy0, int32_t cy1,
                                               int32_t ox, int32_t oy, uint64_t* keys) {
     EdgeSetup e;
@@ -526,7 +521,7 @@ __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int3
             if ((f0 | f1 | f2) >= 0) {
                 uint64_t key;
                 if (depth_key(frag_depth(r, e, px, py), far_clip, low, key))
-                    atomicMin(&keys[(py - oy) * TRI_BIN + (px - ox)], key);
+                    atomicMin(&keys[((py - oy) << BL) + (px - ox)], key);
             }
             f0 += e.A[0]; f1 += e.A[1]; f2 += e.A[2];
         }
@@ -817,25 +812,48 @@ __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const T
 constexpr int kBigArea = 96;  // bbox∩bin pixels above which a triangle is rasterized cooperatively
 constexpr int kBigQueue = 1024;
 
-template <bool EXACT>
+// Bijective XCD-aware block -> bin remap (cdna_hip_programming.md §5 "XCD swizzle must be
+// bijective"): workgroups b, b+8, b+16 ... share an XCD's L2, so give them consecutive bins — each
+// XCD then rasterizes one contiguous band of the screen and re-reads neighbours' records from L2.
+__device__ __forceinline__ int xcd_bin(int b, int nb) {
+    const int xcd = b & 7, q = nb >> 3, r = nb & 7;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+}
+
+template <bool EXACT, int BL>
 __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
-    __shared__ uint64_t keys[TRI_BIN * TRI_BIN];
+    constexpr int BIN = 1 << BL;
+    __shared__ uint64_t keys[BIN * BIN];
     __shared__ uint32_t bigq[kBigQueue];
     __shared__ float lut[256];
-    __shared__ uint32_t nbig;
+    __shared__ uint32_t nbig, nentries;
     const int tid = threadIdx.x;
-    const int bin = blockIdx.x;
+    const int bin = xcd_bin(blockIdx.x, fp.nbins);
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
-    const int32_t ox = bx * TRI_BIN, oy = fp.y0 + by * TRI_BIN;
-    const int32_t bw = min(TRI_BIN, fp.W - ox), bh = min(TRI_BIN, fp.y1 - oy);
-    for (int i = tid; i < TRI_BIN * TRI_BIN; i += TRI_BLOCK) keys[i] = kBgKey;
+    const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
+    const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);
+    for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = kBgKey;
     if (tid < 256) lut[tid] = b.srgb_lut[tid];
-    if (tid == 0) nbig = 0;
+    if (tid == 0) {
+        nbig = 0;
+        const uint32_t cnt = b.bin_count[bin];
+        b.bin_count[bin] = 0;  // queue consumed: ready for the next frame
+        if (cnt > fp.bin_cap) note_bin_overflow(b, cnt);
+        nentries = min(cnt, fp.bin_cap);
+    }
     __syncthreads();
-    const uint32_t s0 = b.bin_start[bin];
-    const uint32_t s1 = min(b.bin_start[bin + 1], fp.bin_cap);
+    const uint32_t* queue = b.bin_list + (size_t)bin * fp.bin_cap;
+    uint32_t s0 = 0, s1 = nentries;
+    if (fp.ablate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
+        if (s1 > s0) {
+            const TriRec r = load_rec(b.recs, queue[0]);
+            const uint64_t key = (0x3F000000ull << 32) | key_low(r.prim_sub);
+            for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = key;
+        }
+        s1 = s0;
+    }
     for (uint32_t i = s0 + tid; i < s1; i += TRI_BLOCK) {
-        const uint32_t ri = b.bin_list[i];
+        const uint32_t ri = queue[i];
         const TriRec r = load_rec(b.recs, ri);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
@@ -844,7 +862,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
             const uint32_t q = atomicAdd(&nbig, 1u);
             if (q < kBigQueue) { bigq[q] = ri; continue; }
         }
-        raster_serial(r, cx0, cx1, cy0, cy1, ox, oy, keys);
+        raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);
     }
     __syncthreads();
     const uint32_t nb = min(nbig, (uint32_t)kBigQueue);
@@ -871,22 +889,25 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
                 const int32_t px = cx0 + dx, py = cy0 + dy;
                 uint64_t key;
                 if (depth_key(frag_depth(r, e, px, py), far_clip, low, key))
-                    atomicMin(&keys[(py - oy) * TRI_BIN + (px - ox)], key);
+                    atomicMin(&keys[((py - oy) << BL) + (px - ox)], key);
             }
         }
     }
     __syncthreads();
-    // shade + store: one wave per 64-pixel row -> 256-byte coalesced colour/depth stores
-    const int lx = tid & (TRI_BIN - 1);
-    for (int ly = tid >> TRI_BIN_LOG2; ly < bh; ly += TRI_BLOCK / TRI_BIN) {
+    // shade + store: each wave covers whole BIN-pixel row pieces -> coalesced colour/depth stores
+    const int lx = tid & (BIN - 1);
+    for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
         if (lx >= bw) continue;
-        const uint64_t key = keys[ly * TRI_BIN + lx];
+        const uint64_t key = keys[(ly << BL) + lx];
         const int32_t px = ox + lx, py = oy + ly;
         uint32_t out;
         float z;
         if (key == kBgKey) {
             out = fp.clear_bgra;
             z = 1.0f;
+        } else if (fp.ablate & 1) {  // diagnostics: coverage only
+            z = __uint_as_float((uint32_t)(key >> 32));
+            out = (uint32_t)key;
         } else {
             z = __uint_as_float((uint32_t)(key >> 32));
             Frag f;
@@ -903,18 +924,15 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
 }  // namespace
 
 hipError_t tri_kernels_init() {
-    const int lds_max = 2 * 16384 * (int)sizeof(uint32_t);
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_scatter),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-    if (e != hipSuccess) return e;
+    const int lds_max = 16384 * (int)(sizeof(uint32_t) + sizeof(uint16_t));
     return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_setup),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_max / 2);
+                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
 }
 
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* ev) {
     static const bool debug_sync = getenv("TRI_DEBUG_SYNC") != nullptr;
-    static const char* names[] = {"vertex", "setup+clip", "binscan", "scatter", "raster", "end"};
+    static const char* names[] = {"vertex", "setup", "clip", "raster", "end"};
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], stream);
         if (debug_sync) {
@@ -925,22 +943,24 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
     rec(kStageVertex);
     if (fp.nslots > 0)
         hipLaunchKernelGGL(k_vertex, dim3((fp.nslots + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
-    rec(kStageSetup);
-    const size_t hist_bytes = (size_t)fp.nbins * sizeof(uint32_t);
-    if (fp.nchunks > 0) {
-        hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), hist_bytes, stream, fp, b);
-        hipLaunchKernelGGL(k_clip, dim3(TRI_CLIP_GRID), dim3(TRI_BLOCK), 0, stream, fp, b);
-    }
-    rec(kStageBinscan);
-    hipLaunchKernelGGL(k_binscan, dim3(1), dim3(1024), 0, stream, fp, b);
-    rec(kStageScatter);
-    if (fp.nchunks > 0)
-        hipLaunchKernelGGL(k_scatter, dim3(fp.nchunks), dim3(TRI_BLOCK), 2 * hist_bytes, stream, fp, b);
-    rec(kStageRaster);
-    if (fp.exact_shading)
-        hipLaunchKernelGGL(k_raster<true>, dim3(fp.nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
     else
-        hipLaunchKernelGGL(k_raster<false>, dim3(fp.nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
+        hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
+    rec(kStageSetup);
+    const size_t lds_bytes = (size_t)fp.nbins * (sizeof(uint32_t) + sizeof(uint16_t));
+    if (fp.nchunks > 0)
+        hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), (lds_bytes + 15) & ~(size_t)15, stream, fp,
+                           b);
+    rec(kStageClip);
+    if (fp.nchunks > 0) hipLaunchKernelGGL(k_clip, dim3(TRI_CLIP_GRID), dim3(TRI_BLOCK), 0, stream, fp, b);
+    rec(kStageRaster);
+    const dim3 g(fp.nbins), t(TRI_BLOCK);
+    if (fp.bin_log2 == 5) {
+        if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 5>), g, t, 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_raster<false, 5>), g, t, 0, stream, fp, b);
+    } else {
+        if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 6>), g, t, 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_raster<false, 6>), g, t, 0, stream, fp, b);
+    }
     rec(kStageCount);
     return hipGetLastError();
 }

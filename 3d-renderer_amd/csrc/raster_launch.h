@@ -16,26 +16,25 @@ struct TriDeviceBuffers {
     const uint32_t* draw_pbase;  // ndraws+1
     const TriTexDesc* textures;  // TRI_MAX_TEXTURE_SLOTS entries, aliases resolved
     const float* srgb_lut;       // 256 entries, sRGB -> linear (computed on the host in double)
-    float4* clip;                // nslots
+    float4* clip;                // nslots (read only by k_clip)
+    TriSnap* snap;               // nslots
     float4* vary;                // 3 * (nslots + ovf_vert_cap)
     TriRec* recs;                // nprims + ovf_rec_cap
     uint2* brange;               // nprims + ovf_rec_cap
     uint32_t* clip_queue;        // ovf_rec_cap primitive ids needing geometric clipping
-    uint32_t* bin_total;         // nbins (zero at frame start; re-zeroed by the scan)
-    uint32_t* bin_start;         // nbins + 1
-    uint32_t* bin_cursor;        // nbins
-    uint32_t* bin_list;          // bin_cap
+    uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
+    uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)
     TriCounters* counters;
     uint32_t* color;             // band rows * W
     float* depth;                // band rows * W (may be null)
 };
 
-enum TriStage { kStageVertex = 0, kStageSetup, kStageBinscan, kStageScatter, kStageRaster, kStageCount };
+enum TriStage { kStageVertex = 0, kStageSetup, kStageClip, kStageRaster, kStageCount };
 
-// Raise the dynamic-LDS limit of the histogram kernels (up to 2 x 16384 bins x 4 B).
+// Raise the dynamic-LDS limit of the binning kernel (up to 16384 bins x 6 B).
 hipError_t tri_kernels_init();
 
-// One frame = 6 dependent launches on `stream`; `events` (may be null) gets kStageCount+1 stamps:
-// [vertex | setup+clip | binscan | scatter | raster].
+// One frame = 4 dependent launches on `stream`; `events` (may be null) gets kStageCount+1 stamps:
+// [vertex | setup+binning | clip | raster].
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* events);

@@ -53,7 +53,7 @@ uint32_t unorm8_host(float c) {
 }
 
 struct TimingSet {
-    hipEvent_t ev[6];
+    hipEvent_t ev[kStageCount + 1];
 };
 
 }  // namespace
@@ -109,12 +109,11 @@ struct tri_ctx {
 
     // work buffers
     float4* d_clip = nullptr; size_t cap_clip = 0;
+    TriSnap* d_snap = nullptr; size_t cap_snap = 0;
+    int32_t bin_log2 = 6;
     float4* d_vary = nullptr; size_t cap_vary = 0;
     TriRec* d_recs = nullptr; size_t cap_recs = 0;
-    uint2* d_brange = nullptr; size_t cap_brange = 0;
-    uint32_t* d_bin_total = nullptr; size_t cap_bin_total = 0;
-    uint32_t* d_bin_start = nullptr; size_t cap_bin_start = 0;
-    uint32_t* d_bin_cursor = nullptr; size_t cap_bin_cursor = 0;
+    uint32_t* d_bin_count = nullptr; size_t cap_bin_count = 0;
     uint32_t* d_bin_list = nullptr; size_t cap_bin_list = 0;
     TriCounters* d_ctr = nullptr;
     uint32_t ovf_rec_cap = 1u << 16, ovf_vert_cap = 1u << 17;
@@ -301,16 +300,22 @@ int ensure_work_buffers(tri_ctx* c) {
     int rc;
     const size_t nrec = (size_t)c->nprims + c->ovf_rec_cap;
     const size_t nvary = 3ull * ((size_t)c->nslots + c->ovf_vert_cap);
-    if (c->bin_cap == 0) c->bin_cap = 2u * c->nprims + 4u * (uint32_t)c->nbins + 65536u;
+    // per-bin queue capacity: ~8x the mean entries per bin (1.3 bins per triangle), >= 256,
+    // grown from the observed maximum after an overflow (check_overflow)
+    const uint64_t mean = ((uint64_t)c->nprims * 13 / 10) / (uint64_t)std::max(c->nbins, 1);
+    c->bin_cap = std::max<uint32_t>(c->bin_cap, (uint32_t)std::min<uint64_t>(((8 * mean + 64 + 63) / 64) * 64, 1u << 30));
+    c->bin_cap = std::max<uint32_t>(c->bin_cap, 256u);
+    const size_t nlist = (size_t)c->nbins * c->bin_cap;
+    if (nlist * 4 > (8ull << 30)) return fail(TRI_E_OOM, "bin queues would need %zu MB", nlist * 4 >> 20);
     bool realloc = c->cap_clip < std::max<size_t>(c->nslots, 1) || c->cap_vary < nvary || c->cap_recs < nrec ||
-                   c->cap_bin_list < c->bin_cap;
+                   c->cap_bin_list < nlist;
     if (realloc) HIP_TRY(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_clip, c->cap_clip, std::max<size_t>(c->nslots, 1)))) return rc;
+    if ((rc = grow(c->d_snap, c->cap_snap, std::max<size_t>(c->nslots, 1)))) return rc;
     if ((rc = grow(c->d_vary, c->cap_vary, nvary))) return rc;
     if ((rc = grow(c->d_recs, c->cap_recs, nrec))) return rc;
-    if ((rc = grow(c->d_brange, c->cap_brange, nrec))) return rc;
     if ((rc = grow(c->d_clip_queue, c->cap_clip_queue, c->ovf_rec_cap))) return rc;
-    if ((rc = grow(c->d_bin_list, c->cap_bin_list, c->bin_cap))) return rc;
+    if ((rc = grow(c->d_bin_list, c->cap_bin_list, nlist))) return rc;
     return TRI_OK;
 }
 
@@ -318,14 +323,13 @@ int collect_timing(tri_ctx* c) {
     if (c->pending.empty()) return TRI_OK;
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (TimingSet& t : c->pending) {
-        float ms[5], tot;
-        for (int i = 0; i < 5; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], t.ev[i], t.ev[i + 1]));
-        HIP_TRY(hipEventElapsedTime(&tot, t.ev[0], t.ev[5]));
-        c->acc.ms_vertex += ms[0];
-        c->acc.ms_setup += ms[1];
-        c->acc.ms_binscan += ms[2];
-        c->acc.ms_scatter += ms[3];
-        c->acc.ms_raster += ms[4];
+        float ms[kStageCount], tot;
+        for (int i = 0; i < kStageCount; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], t.ev[i], t.ev[i + 1]));
+        HIP_TRY(hipEventElapsedTime(&tot, t.ev[0], t.ev[kStageCount]));
+        c->acc.ms_vertex += ms[kStageVertex];
+        c->acc.ms_setup += ms[kStageSetup];
+        c->acc.ms_clip += ms[kStageClip];
+        c->acc.ms_raster += ms[kStageRaster];
         c->acc.ms_frame += tot;
         c->acc.frames += 1;
         c->free_sets.push_back(t);
@@ -342,7 +346,12 @@ int check_overflow(tri_ctx* c) {
     HIP_TRY(hipMemcpy(&c->d_ctr->flags, &zero, 4, hipMemcpyHostToDevice));
     if (h.flags & (TRI_OVF_CLIP_RECORDS | TRI_OVF_CLIP_QUEUE)) c->ovf_rec_cap *= 4;
     if (h.flags & TRI_OVF_CLIP_VERTS) c->ovf_vert_cap *= 4;
-    if (h.flags & TRI_OVF_BIN_LIST) c->bin_cap = std::max<uint32_t>(c->bin_cap * 2, h.bin_entries + h.bin_entries / 4);
+    if (h.flags & TRI_OVF_BIN_LIST) {
+        c->bin_cap = std::max<uint32_t>(c->bin_cap * 2, h.bin_max + h.bin_max / 4);
+        c->bin_cap = (c->bin_cap + 63) & ~63u;
+        const uint32_t zmax = 0;
+        HIP_TRY(hipMemcpy(&c->d_ctr->bin_max, &zmax, 4, hipMemcpyHostToDevice));
+    }
     int rc = ensure_work_buffers(c);
     if (rc) return rc;
     return fail(TRI_E_OVERFLOW, "frame overflowed an internal buffer (flags 0x%x); capacities grown, re-render",
@@ -380,8 +389,13 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
     c->H = (int32_t)cfg->height;
     c->y0 = (int32_t)y0;
     c->y1 = (int32_t)y1;
-    c->nbx = (c->W + TRI_BIN - 1) / TRI_BIN;
-    c->nby = (c->y1 - c->y0 + TRI_BIN - 1) / TRI_BIN;
+    // 32x32-pixel bins while the bin grid fits the 16384-entry LDS histograms, else 64x64
+    for (c->bin_log2 = 5; c->bin_log2 <= 6; ++c->bin_log2) {
+        const int32_t bs = 1 << c->bin_log2;
+        c->nbx = (c->W + bs - 1) / bs;
+        c->nby = (c->y1 - c->y0 + bs - 1) / bs;
+        if (c->nbx * c->nby <= 16384) break;
+    }
     c->nbins = c->nbx * c->nby;
     auto bail = [&](int rc) { tri_destroy(c); return rc; };
     int rc = make_current(c);
@@ -398,14 +412,8 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
         return bail(fail(TRI_E_OOM, "tri_create: target allocation failed"));
     c->d_color = c->d_color_own;
     c->d_depth = c->d_depth_own;
-    size_t cap = 0;
-    if ((rc = grow(c->d_bin_total, cap, (size_t)c->nbins))) return bail(rc);
-    c->cap_bin_total = cap; cap = 0;
-    if ((rc = grow(c->d_bin_start, cap, (size_t)c->nbins + 1))) return bail(rc);
-    c->cap_bin_start = cap; cap = 0;
-    if ((rc = grow(c->d_bin_cursor, cap, (size_t)c->nbins))) return bail(rc);
-    c->cap_bin_cursor = cap;
-    if (hipMemset(c->d_bin_total, 0, c->nbins * 4) != hipSuccess || hipMemset(c->d_ctr, 0, sizeof(TriCounters)) != hipSuccess)
+    if ((rc = grow(c->d_bin_count, c->cap_bin_count, (size_t)c->nbins))) return bail(rc);
+    if (hipMemset(c->d_bin_count, 0, c->nbins * 4) != hipSuccess || hipMemset(c->d_ctr, 0, sizeof(TriCounters)) != hipSuccess)
         return bail(fail(TRI_E_HIP, "tri_create: memset failed"));
     float lut[256];
     for (int i = 0; i < 256; ++i) {  // R8G8B8A8_SRGB decode (sRGB EOTF), evaluated in double
@@ -431,8 +439,8 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_clip_queue); f(c->d_vbase); f(c->d_pbase);
-    f(c->d_clip); f(c->d_vary); f(c->d_recs); f(c->d_brange);
-    f(c->d_bin_total); f(c->d_bin_start); f(c->d_bin_cursor); f(c->d_bin_list); f(c->d_ctr);
+    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs);
+    f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stage_free) (void)hipEventDestroy(c->stage_free);
@@ -561,6 +569,8 @@ int tri_set_frame(tri_ctx* c, const tri_global_ubo* ubo, const float clear[4]) {
 int tri_set_draws(tri_ctx* c, const tri_draw* d, uint32_t n) {
     if (!c) return fail(TRI_E_INVALID, "tri_set_draws: null context");
     if (n && !d) return fail(TRI_E_INVALID, "tri_set_draws: null draws");
+    if (n == c->draws.size() && (n == 0 || std::memcmp(c->draws.data(), d, n * sizeof(tri_draw)) == 0))
+        return TRI_OK;  // unchanged draw list: keep the device copy (no per-frame upload)
     c->draws.assign(d, d + n);
     c->draws_dirty = true;
     return TRI_OK;
@@ -589,15 +599,15 @@ int tri_render(tri_ctx* c) {
         c->has_skin_data = true;
     }
     if ((rc = ensure_work_buffers(c))) return rc;
-    HIP_TRY(hipMemsetAsync(c->d_ctr, 0, TRI_COUNTERS_RESET_BYTES, c->stream));
 
     TriFrameParams fp;
     std::memset(&fp, 0, sizeof fp);
     fp.W = c->W; fp.H = c->H; fp.y0 = c->y0; fp.y1 = c->y1;
     fp.nbx = c->nbx; fp.nby = c->nby; fp.nbins = c->nbins;
-    const uint32_t target_chunks = 512;
+    fp.bin_log2 = c->bin_log2;
+    const uint32_t target_chunks = 1024;  // >= 4 binning workgroups per CU
     uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
-    ppt = std::min<uint32_t>(std::max<uint32_t>(ppt, 1), 32);
+    ppt = std::min<uint32_t>(std::max<uint32_t>(ppt, 1), TRI_MAX_PPT);
     fp.ppt = (int32_t)ppt;
     fp.nchunks = (c->nprims + ppt * TRI_BLOCK - 1) / (ppt * TRI_BLOCK);
     fp.hw = (float)c->W * 0.5f;
@@ -614,6 +624,11 @@ int tri_render(tri_ctx* c) {
     fp.clear_bgra = c->clear_bgra;
     fp.write_depth = (c->cfg.flags & TRI_FLAG_NO_DEPTH_OUTPUT) ? 0u : 1u;
     fp.exact_shading = (c->cfg.flags & TRI_FLAG_EXACT_SHADING) ? 1u : 0u;
+    static const uint32_t ablate = [] {  // diagnostics only: TRI_ABLATE=1 no shading, 2 no coverage
+        const char* e = getenv("TRI_ABLATE");
+        return e ? (uint32_t)atoi(e) : 0u;
+    }();
+    fp.ablate = ablate;
     std::memcpy(fp.pv, c->pv, 64);
     fp.ubo = c->ubo;
     fp.mat0 = c->mat0;
@@ -633,12 +648,10 @@ int tri_render(tri_ctx* c) {
     b.textures = c->d_texdesc;
     b.srgb_lut = c->d_lut;
     b.clip = c->d_clip;
+    b.snap = c->d_snap;
     b.vary = c->d_vary;
     b.recs = c->d_recs;
-    b.brange = c->d_brange;
-    b.bin_total = c->d_bin_total;
-    b.bin_start = c->d_bin_start;
-    b.bin_cursor = c->d_bin_cursor;
+    b.bin_count = c->d_bin_count;
     b.bin_list = c->d_bin_list;
     b.counters = c->d_ctr;
     b.color = c->d_color;
@@ -714,7 +727,7 @@ int tri_get_frame_stats(tri_ctx* c, tri_frame_stats* out) {
     out->vertices_shaded = c->nslots;
     out->bins_x = (uint32_t)c->nbx;
     out->bins_y = (uint32_t)c->nby;
-    out->bin_size = TRI_BIN;
+    out->bin_size = 1u << c->bin_log2;
     return TRI_OK;
 }
 

@@ -122,10 +122,10 @@ class TriTiming(C.Structure):
         ("frames", C.c_uint64),
         ("ms_vertex", C.c_double),
         ("ms_setup", C.c_double),
-        ("ms_binscan", C.c_double),
-        ("ms_scatter", C.c_double),
+        ("ms_clip", C.c_double),
         ("ms_raster", C.c_double),
         ("ms_frame", C.c_double),
+        ("reserved", C.c_double),
     ]
 
 

@@ -139,12 +139,12 @@ typedef struct tri_config {
 /* Per-stage accumulated device time (HIP events on the context stream) and last-frame counters. */
 typedef struct tri_timing {
     uint64_t frames;        /* frames timed since the last reset                  */
-    double ms_vertex;       /* vs_transform                                        */
-    double ms_setup;        /* tri_setup_bin (setup + clip + per-bin counts)       */
-    double ms_binscan;      /* bin prefix scan                                     */
-    double ms_scatter;      /* bin list scatter                                    */
+    double ms_vertex;       /* vs_transform (+ per-vertex divide / viewport / snap) */
+    double ms_setup;        /* tri_setup_bin (setup + cull + per-bin queues)       */
+    double ms_clip;         /* homogeneous clipping of the (rare) straddling tris  */
     double ms_raster;       /* tile_raster_shade (coverage + early-Z + PBR + store) */
     double ms_frame;        /* first kernel start to last kernel end              */
+    double reserved;
 } tri_timing;
 
 typedef struct tri_frame_stats {

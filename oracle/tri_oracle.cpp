@@ -161,9 +161,10 @@ bool setup_triangle(const Setup& su, const VsOut* const vs[3], const uint32_t vi
     float z[3], iw[3];
     bool far = false;
     for (int k = 0; k < 3; ++k) {
+        // perspective divide as x * (1/w) with a correctly rounded 1/w (one divide per vertex)
         const vec4 c = vs[k]->clip;
-        const float xd = c.x / c.w, yd = c.y / c.w, zd = c.z / c.w;
         iw[k] = 1.0f / c.w;
+        const float xd = c.x * iw[k], yd = c.y * iw[k], zd = c.z * iw[k];
         const float xf = xd * su.hw + su.hw;
         const float yf = yd * su.hh + su.hh;
         X[k] = (int32_t)std::rint(xf * 256.0f);

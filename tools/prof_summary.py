@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Summarise rocprofv3 CSVs (tools/profile.sh) per kernel: mean duration and mean PMC counters per
+dispatch. gfx950 correction (MI355X_MICROARCH.md §HBM): FETCH_SIZE counts half the bytes of wide
+streaming reads, so hbm_read_bytes = 2 * FETCH_SIZE * 1024 (an upper bound for narrower reads);
+WRITE_SIZE is taken at face value (exact for 16-B/lane stores; ours are 4-B/lane dword stores)."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+
+def short(name):
+    for k in ("k_raster<false>", "k_raster<true>", "k_setup", "k_scatter", "k_vertex", "k_clip", "k_binscan",
+              "copyBuffer", "fillBuffer"):
+        if k in name:
+            return k.replace("<false>", "").replace("<true>", "_exact")
+    return name[:40]
+
+
+def main(root, workload, out_json):
+    res = defaultdict(lambda: defaultdict(list))
+    for f in glob.glob(os.path.join(root, "*", "*_counter_collection.csv")):
+        for row in csv.DictReader(open(f)):
+            res[short(row["Kernel_Name"])][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    stats = {}
+    for f in glob.glob(os.path.join(root, "*", "*_kernel_stats.csv")):
+        for row in csv.DictReader(open(f)):
+            stats[short(row["Name"])] = {"calls": int(row["Calls"]), "avg_ns": float(row["AverageNs"]),
+                                         "min_ns": float(row["MinNs"]), "max_ns": float(row["MaxNs"])}
+    summary = {}
+    for k in sorted(set(res) | set(stats)):
+        e = {"trace": stats.get(k)}
+        for c, v in res[k].items():
+            e[c] = sum(v) / len(v)
+        if "FETCH_SIZE" in e and "WRITE_SIZE" in e:
+            e["hbm_read_bytes_corrected"] = 2 * e["FETCH_SIZE"] * 1024
+            e["hbm_write_bytes"] = e["WRITE_SIZE"] * 1024
+            e["hbm_bytes_per_launch"] = e["hbm_read_bytes_corrected"] + e["hbm_write_bytes"]
+        summary[k] = e
+    doc = {}
+    if os.path.exists(out_json):
+        doc = json.load(open(out_json))
+    doc[workload] = summary
+    json.dump(doc, open(out_json, "w"), indent=1, sort_keys=True)
+    for k, e in summary.items():
+        t = e.get("trace") or {}
+        print(f"{k:16s} avg {t.get('avg_ns', 0)/1e3:8.1f} us  " +
+              "  ".join(f"{c}={v:.4g}" for c, v in sorted(e.items()) if c != "trace"))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1], sys.argv[2], sys.argv[3])
