@@ -1,0 +1,172 @@
+// Renderer.h — Trident::Renderer, the reference's renderer API (Trident/src/Renderer/Renderer.h:77-598)
+// for the draw path, backed by the HIP software rasterizer through the C-ABI (include/tri_raster.h)
+// instead of Vulkan. Same names, argument meaning and error behaviour (no exceptions on the frame
+// path; failures are logged and the frame is skipped, Renderer.cpp:779-824). Vulkan-typed getters
+// become opaque device pointers (GetViewportTexture).
+#pragma once
+
+#include <chrono>
+#include <cstdint>
+#include <map>
+#include <memory>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "../../../../include/tri_raster.h"
+#include "Camera.h"
+#include "Scene.h"
+
+namespace Trident {
+
+struct ViewportInfo {
+    uint32_t ViewportID = 0;
+    glm::vec2 Position{0.0f};
+    glm::vec2 Size{0.0f};
+};
+
+struct FrameTimingSample {
+    double FrameMilliseconds = 0.0;
+    double FramesPerSecond = 0.0;
+    std::chrono::system_clock::time_point CaptureTime{};
+};
+
+struct FrameTimingStats {  // Renderer.h:472-479
+    double MinimumMilliseconds = 0.0;
+    double MaximumMilliseconds = 0.0;
+    double AverageMilliseconds = 0.0;
+    double MinimumFPS = 0.0;
+    double MaximumFPS = 0.0;
+    double AverageFPS = 0.0;  // mean of per-frame 1000/ms (Renderer.cpp:6335-6342)
+};
+
+class Renderer {
+public:
+    Renderer();
+    ~Renderer();
+
+    void Init();
+    void Shutdown();
+    void DrawFrame();
+
+    void UploadMesh(const std::vector<Geometry::Mesh>& meshes, const std::vector<Geometry::Material>& materials,
+                    const std::vector<std::string>& textures);
+    void AppendMeshes(std::vector<Geometry::Mesh> meshes, std::vector<Geometry::Material> materials,
+                      std::vector<std::string> textures);
+    void UploadTexture(const std::string& texturePath, const Loader::TextureData& texture);
+    void SetEditorCamera(Camera* camera) { m_EditorCamera = camera; }
+    void SetRuntimeCamera(Camera* camera) { m_RuntimeCamera = camera; }
+    void SetRuntimeCameraReady(bool ready) { m_RuntimeCameraReady = ready; }
+    void SetActiveRegistry(ECS::Registry* registry) { m_Registry = registry; }
+    bool HasRuntimeCamera() const { return m_RuntimeCamera != nullptr && m_RuntimeCameraReady; }
+
+    int32_t ResolveTextureSlot(const std::string& texturePath);
+    size_t GetOrCreatePrimitiveMeshIndex(MeshComponent::PrimitiveType primitiveType);
+
+    void SetClearColor(const glm::vec4& color) { m_ClearColor = color; }
+    glm::vec4 GetClearColor() const { return m_ClearColor; }
+
+    size_t GetModelCount() const { return m_ModelCount; }
+    size_t GetTriangleCount() const { return m_TriangleCount; }
+    const FrameTimingStats& GetFrameTimingStats() const { return m_PerformanceStats; }
+    size_t GetFrameTimingHistoryCount() const { return m_PerformanceSampleCount; }
+
+    void SetViewport(uint32_t viewportId, const ViewportInfo& info);
+    ViewportInfo GetViewport() const;
+    // Vulkan returned a VkDescriptorSet for ImGui; here: the viewport's device B8G8R8A8 buffer.
+    void* GetViewportTexture(uint32_t viewportId) const;
+    const Camera* GetActiveCamera() const;
+    glm::mat4 GetViewportViewMatrix(uint32_t viewportId) const;
+    glm::mat4 GetViewportProjectionMatrix(uint32_t viewportId) const;
+
+    std::vector<Geometry::Material>& GetMaterials() { return m_Materials; }
+    const std::vector<Geometry::Material>& GetMaterials() const { return m_Materials; }
+
+    // Frame readback (ResolvePendingReadback, Renderer.cpp:1299-1389): RGBA8 rows of the viewport
+    // (BGRA reordered to RGBA), optionally the D32 depth.
+    bool ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgba, std::vector<float>* depth = nullptr);
+    // The exact uniform block + draw list DrawFrame submits for a viewport (GatherMeshDraws +
+    // UpdateUniformBuffer + the push-constant loop): host-only, used to test frame preparation.
+    bool BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::vector<tri_draw>& draws);
+    // Rasterizer flags (TRI_FLAG_*) used for viewports created from now on.
+    void SetRasterFlags(uint32_t flags) { m_RasterFlags = flags; }
+    bool IsShutdown() const { return m_Shutdown; }
+    // The concatenated buffers UploadMeshFromCache builds (the device copy of these is what
+    // tri_upload_geometry receives).
+    const std::vector<tri_vertex>& GetVertexBuffer() const { return m_VertexBuffer; }
+    const std::vector<uint32_t>& GetIndexBuffer() const { return m_IndexBuffer; }
+    std::vector<tri_mesh_range> GetMeshRanges() const;
+
+private:
+    struct MeshDrawInfo {  // Renderer.h:293-299
+        uint32_t m_FirstIndex = 0;
+        uint32_t m_IndexCount = 0;
+        int32_t m_BaseVertex = 0;
+        int32_t m_MaterialIndex = -1;
+    };
+    struct MeshDrawCommand {
+        glm::mat4 m_ModelMatrix{1.0f};
+        const MeshComponent* m_Component = nullptr;
+        const TextureComponent* m_TextureComponent = nullptr;
+        ECS::Entity m_Entity = 0;
+    };
+    struct ViewportContext {
+        ViewportInfo m_Info{};
+        tri_ctx* m_Ctx = nullptr;
+        uint32_t m_Width = 0, m_Height = 0;
+        uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0;
+    };
+
+    void UploadMeshFromCache();
+    void EnsurePrimitiveMeshesInCache();
+    size_t CreatePrimitiveMeshInCache(MeshComponent::PrimitiveType primitiveType);
+    void ResolveMaterialTextureSlots(const std::vector<std::string>& textures, size_t offset, size_t count);
+    void GatherMeshDraws();
+    void UpdateUniformBuffer(const Camera* camera, tri_global_ubo& out) const;
+    void BuildDrawList(std::vector<tri_draw>& out) const;
+    const Camera* GetActiveCamera(const ViewportContext& context) const;
+    bool PrepareViewport(ViewportContext& context);
+    void RecordFrameTiming(double milliseconds);
+
+    Camera* m_EditorCamera = nullptr;
+    Camera* m_RuntimeCamera = nullptr;
+    bool m_RuntimeCameraReady = false;
+    ECS::Registry* m_Registry = nullptr;
+
+    std::vector<Geometry::Mesh> m_GeometryCache;
+    std::vector<Geometry::Material> m_Materials;
+    std::vector<MeshDrawInfo> m_MeshDrawInfo;
+    std::vector<MeshDrawCommand> m_MeshDrawCommands;
+    size_t m_PrimitiveMeshIndices[3] = {SIZE_MAX, SIZE_MAX, SIZE_MAX};
+    bool m_IsUploadingMeshes = false;
+    std::vector<tri_vertex> m_VertexBuffer;
+    std::vector<uint32_t> m_IndexBuffer;
+    uint64_t m_GeometryGeneration = 1, m_TextureGeneration = 1, m_MaterialGeneration = 1;
+
+    struct TextureSlot {
+        std::string m_SourcePath;
+        Loader::TextureData m_Data;
+    };
+    std::vector<TextureSlot> m_TextureSlots;
+    std::unordered_map<std::string, uint32_t> m_TextureSlotLookup;
+
+    std::map<uint32_t, ViewportContext> m_Viewports;
+    ViewportInfo m_LastViewport{};
+    uint32_t m_RasterFlags = 0;
+
+    glm::vec3 m_AmbientColor{0.03f};
+    float m_AmbientIntensity = 1.0f;
+    glm::vec4 m_ClearColor{0.005f, 0.005f, 0.005f, 1.0f};
+    size_t m_ModelCount = 0;
+    size_t m_TriangleCount = 0;
+
+    static constexpr size_t s_PerformanceHistorySize = 240;
+    std::vector<FrameTimingSample> m_PerformanceHistory;
+    size_t m_PerformanceHistoryNextIndex = 0;
+    size_t m_PerformanceSampleCount = 0;
+    FrameTimingStats m_PerformanceStats{};
+    bool m_Initialised = false;
+    bool m_Shutdown = false;
+};
+
+}  // namespace Trident

@@ -1,0 +1,70 @@
+/* trident_app.h — a flat C driver over the C++ Trident::Renderer shim (host/include/trident/ headers).
+ *
+ * It plays the part of Trident-Forge's ApplicationLayer (Trident-Forge/src/Layer/ApplicationLayer.cpp)
+ * for tests and tools that are not C++: it owns one ECS::Registry, an EditorCamera and a
+ * RuntimeCamera, and forwards to RenderCommand. Everything below the shim is the drop-in C-ABI in
+ * include/tri_raster.h. All functions return TRI_OK or a negative TRI_E_* code.
+ */
+#ifndef TRIDENT_APP_H
+#define TRIDENT_APP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "../../../include/tri_raster.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct trident_app trident_app;
+
+/* primitive: 0 none, 1 cube, 2 sphere, 3 quad (MeshComponent::PrimitiveType) */
+enum { TRIDENT_PRIMITIVE_NONE = 0, TRIDENT_PRIMITIVE_CUBE = 1, TRIDENT_PRIMITIVE_SPHERE = 2, TRIDENT_PRIMITIVE_QUAD = 3 };
+enum { TRIDENT_LIGHT_DIRECTIONAL = 0, TRIDENT_LIGHT_POINT = 1 };
+
+int trident_app_create(uint32_t raster_flags, trident_app** out);
+void trident_app_destroy(trident_app* app);
+
+/* Renderer::AppendMeshes with one mesh + one material; returns the mesh index in *mesh_index. */
+int trident_app_append_mesh(trident_app* app, const tri_vertex* vertices, uint32_t vertex_count,
+                            const uint32_t* indices, uint32_t index_count, const float base_color[4],
+                            float metallic, float roughness, const char* texture_path, uint32_t* mesh_index);
+int trident_app_upload_texture(trident_app* app, const char* path, const uint8_t* rgba, uint32_t width,
+                               uint32_t height);
+
+/* Entity with Transform + MeshComponent (primitive, or mesh_index when primitive == 0). */
+int trident_app_add_mesh_entity(trident_app* app, int primitive, uint32_t mesh_index, const float position[3],
+                                const float rotation_deg[3], const float scale[3], uint32_t* entity);
+int trident_app_set_entity_texture(trident_app* app, uint32_t entity, const char* texture_path);
+int trident_app_set_entity_transform(trident_app* app, uint32_t entity, const float position[3],
+                                     const float rotation_deg[3], const float scale[3]);
+int trident_app_set_entity_visible(trident_app* app, uint32_t entity, int visible);
+int trident_app_add_light(trident_app* app, int type, const float position[3], const float direction[3],
+                          const float color[3], float intensity, float range, int enabled, uint32_t* entity);
+
+/* which: 0 editor, 1 runtime. Runtime camera readiness follows `ready`. */
+int trident_app_set_camera(trident_app* app, int which, const float position[3], const float rotation_deg[3],
+                           float fov_deg, float near_clip, float far_clip, int ready);
+int trident_app_set_viewport(trident_app* app, uint32_t viewport_id, uint32_t width, uint32_t height);
+int trident_app_set_clear_color(trident_app* app, const float rgba[4]);
+
+int trident_app_draw_frame(trident_app* app);
+int trident_app_read_pixels(trident_app* app, uint32_t viewport_id, uint8_t* rgba, float* depth /* nullable */);
+
+/* Frame inputs DrawFrame would submit for a viewport (host-only). */
+int trident_app_frame_inputs(trident_app* app, uint32_t viewport_id, tri_global_ubo* ubo, tri_draw* draws,
+                             uint32_t capacity, uint32_t* draw_count);
+/* The concatenated geometry (pointers stay valid until the next mesh change). */
+int trident_app_geometry(trident_app* app, const tri_vertex** vertices, size_t* vertex_count,
+                         const uint32_t** indices, size_t* index_count, tri_mesh_range* ranges, uint32_t capacity,
+                         uint32_t* range_count);
+int trident_app_materials(trident_app* app, tri_material_record* out, uint32_t capacity, uint32_t* count);
+/* Renderer::GetFrameTimingStats: min/max/avg ms, min/max/avg fps, sample count. */
+int trident_app_frame_timing(trident_app* app, double out[7]);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TRIDENT_APP_H */

@@ -1,0 +1,639 @@
+// Renderer.cpp — Trident::Renderer's draw path over the HIP rasterizer C-ABI.
+//
+// Mirrors the reference's CPU side of the hot path: primitive meshes (Renderer.cpp:72-246),
+// ComposeTransform (:417-427), UploadMesh/AppendMeshes/UploadMeshFromCache (:1784-2116), texture
+// slots (:3404-3804), GatherMeshDraws (:2910-2994), UpdateUniformBuffer (:5822-6051), the per-draw
+// push-constant loop (:5110-5151), per-viewport camera routing (:4545-4574), readback (:1299-1389)
+// and frame timing (:6286-6343). Vulkan command recording is replaced by tri_set_frame /
+// tri_set_draws / tri_render on one tri_ctx per viewport.
+#include "trident/Renderer.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <limits>
+
+namespace Trident {
+
+namespace {
+
+constexpr const char* kDefaultTextureKey = "renderer://default-white";
+constexpr size_t kInvalidMeshIndex = std::numeric_limits<size_t>::max();
+
+void LogError(const char* what, const char* detail) { std::fprintf(stderr, "[Trident] %s: %s\n", what, detail); }
+
+Geometry::Mesh BuildPrimitiveQuadMesh() {
+    Geometry::Mesh mesh;
+    Vertex v[4]{};
+    v[0].Position = {-0.5f, -0.5f, 0.0f};
+    v[1].Position = {0.5f, -0.5f, 0.0f};
+    v[2].Position = {0.5f, 0.5f, 0.0f};
+    v[3].Position = {-0.5f, 0.5f, 0.0f};
+    for (Vertex& it : v) {
+        it.Normal = {0.0f, 0.0f, 1.0f};
+        it.Tangent = {1.0f, 0.0f, 0.0f};
+        it.Bitangent = {0.0f, 1.0f, 0.0f};
+        it.Color = {1.0f, 1.0f, 1.0f};
+    }
+    v[0].TexCoord = {0.0f, 0.0f};
+    v[1].TexCoord = {1.0f, 0.0f};
+    v[2].TexCoord = {1.0f, 1.0f};
+    v[3].TexCoord = {0.0f, 1.0f};
+    mesh.Vertices.assign(v, v + 4);
+    mesh.Indices = {0, 1, 2, 0, 2, 3};  // counter clockwise with the projection Y flip
+    return mesh;
+}
+
+Geometry::Mesh BuildPrimitiveCubeMesh() {
+    struct Face {
+        glm::vec3 n, t, b;
+        glm::vec3 p[4];
+    };
+    const Face faces[6] = {
+        {{0, 0, 1}, {1, 0, 0}, {0, 1, 0}, {{-0.5f, -0.5f, 0.5f}, {0.5f, -0.5f, 0.5f}, {0.5f, 0.5f, 0.5f}, {-0.5f, 0.5f, 0.5f}}},
+        {{0, 0, -1}, {-1, 0, 0}, {0, 1, 0}, {{0.5f, -0.5f, -0.5f}, {-0.5f, -0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f}, {0.5f, 0.5f, -0.5f}}},
+        {{1, 0, 0}, {0, 0, -1}, {0, 1, 0}, {{0.5f, -0.5f, 0.5f}, {0.5f, -0.5f, -0.5f}, {0.5f, 0.5f, -0.5f}, {0.5f, 0.5f, 0.5f}}},
+        {{-1, 0, 0}, {0, 0, 1}, {0, 1, 0}, {{-0.5f, -0.5f, -0.5f}, {-0.5f, -0.5f, 0.5f}, {-0.5f, 0.5f, 0.5f}, {-0.5f, 0.5f, -0.5f}}},
+        {{0, 1, 0}, {1, 0, 0}, {0, 0, -1}, {{-0.5f, 0.5f, 0.5f}, {0.5f, 0.5f, 0.5f}, {0.5f, 0.5f, -0.5f}, {-0.5f, 0.5f, -0.5f}}},
+        {{0, -1, 0}, {1, 0, 0}, {0, 0, 1}, {{-0.5f, -0.5f, -0.5f}, {0.5f, -0.5f, -0.5f}, {0.5f, -0.5f, 0.5f}, {-0.5f, -0.5f, 0.5f}}},
+    };
+    const glm::vec2 uv[4] = {{0, 0}, {1, 0}, {1, 1}, {0, 1}};
+    Geometry::Mesh mesh;
+    uint32_t off = 0;
+    for (const Face& f : faces) {
+        for (int k = 0; k < 4; ++k) {
+            Vertex v{};
+            v.Position = f.p[k];
+            v.Normal = f.n;
+            v.Tangent = f.t;
+            v.Bitangent = f.b;
+            v.Color = {1.0f, 1.0f, 1.0f};
+            v.TexCoord = uv[k];
+            mesh.Vertices.push_back(v);
+        }
+        for (uint32_t i : {0u, 2u, 1u, 0u, 3u, 2u}) mesh.Indices.push_back(off + i);  // CW from outside
+        off += 4;
+    }
+    return mesh;
+}
+
+Geometry::Mesh BuildPrimitiveSphereMesh() {
+    const uint32_t rings = 16, segments = 24;
+    const float radius = 0.5f;
+    Geometry::Mesh mesh;
+    for (uint32_t r = 0; r <= rings; ++r) {
+        const float V = (float)r / (float)rings;
+        const float phi = V * glm::pi<float>();
+        for (uint32_t s = 0; s <= segments; ++s) {
+            const float U = (float)s / (float)segments;
+            const float theta = U * glm::two_pi<float>();
+            const float sp = std::sin(phi), cp = std::cos(phi), st = std::sin(theta), ct = std::cos(theta);
+            const glm::vec3 p{radius * sp * ct, radius * cp, radius * sp * st};
+            const glm::vec3 n = glm::normalize(p);
+            glm::vec3 t{-st, 0.0f, ct};
+            if (glm::length(t) < 0.0001f) t = {1.0f, 0.0f, 0.0f};
+            t = glm::normalize(t);
+            glm::vec3 b = glm::normalize(glm::cross(n, t));
+            if (glm::length(b) < 0.0001f) b = {0.0f, 1.0f, 0.0f};
+            Vertex v{};
+            v.Position = p;
+            v.Normal = n;
+            v.Tangent = t;
+            v.Bitangent = b;
+            v.Color = {1.0f, 1.0f, 1.0f};
+            v.TexCoord = {U, 1.0f - V};
+            mesh.Vertices.push_back(v);
+        }
+    }
+    const uint32_t row = segments + 1;
+    for (uint32_t r = 0; r < rings; ++r)
+        for (uint32_t s = 0; s < segments; ++s) {
+            const uint32_t i0 = r * row + s, i1 = (r + 1) * row + s, i2 = (r + 1) * row + s + 1, i3 = r * row + s + 1;
+            for (uint32_t i : {i0, i2, i1, i0, i3, i2}) mesh.Indices.push_back(i);
+        }
+    return mesh;
+}
+
+glm::mat4 ComposeTransform(const Transform& t) {  // T * Rx * Ry * Rz * S, degrees
+    glm::mat4 m{1.0f};
+    m = glm::translate(m, t.Position);
+    m = glm::rotate(m, glm::radians(t.Rotation.x), glm::vec3{1.0f, 0.0f, 0.0f});
+    m = glm::rotate(m, glm::radians(t.Rotation.y), glm::vec3{0.0f, 1.0f, 0.0f});
+    m = glm::rotate(m, glm::radians(t.Rotation.z), glm::vec3{0.0f, 0.0f, 1.0f});
+    return glm::scale(m, t.Scale);
+}
+
+std::string NormalizeTexturePath(const std::string& path) {
+    std::string s = path;
+    std::replace(s.begin(), s.end(), '\\', '/');
+    return s;
+}
+
+void CopyMat(const glm::mat4& m, float* out) {
+    for (int c = 0; c < 4; ++c)
+        for (int r = 0; r < 4; ++r) out[c * 4 + r] = m[c][r];
+}
+
+}  // namespace
+
+Renderer::Renderer() = default;
+Renderer::~Renderer() { Shutdown(); }
+
+void Renderer::Init() {
+    if (m_Initialised) return;
+    m_TextureSlots.clear();
+    m_TextureSlotLookup.clear();
+    TextureSlot white;  // CreateDefaultTexture (Renderer.cpp:3404-3436)
+    white.m_SourcePath = kDefaultTextureKey;
+    white.m_Data.Width = white.m_Data.Height = 1;
+    white.m_Data.Pixels = {0xFF, 0xFF, 0xFF, 0xFF};
+    m_TextureSlots.push_back(white);
+    m_TextureSlotLookup.emplace(kDefaultTextureKey, 0u);
+    m_PerformanceHistory.assign(s_PerformanceHistorySize, FrameTimingSample{});
+    m_Initialised = true;
+    m_Shutdown = false;
+}
+
+void Renderer::Shutdown() {
+    for (auto& it : m_Viewports) {
+        tri_destroy(it.second.m_Ctx);
+        it.second.m_Ctx = nullptr;
+    }
+    m_Viewports.clear();
+    if (m_Initialised) m_Shutdown = true;
+    m_Initialised = false;
+}
+
+// ---- geometry ---------------------------------------------------------------------------------
+void Renderer::UploadMesh(const std::vector<Geometry::Mesh>& meshes, const std::vector<Geometry::Material>& materials,
+                          const std::vector<std::string>& textures) {
+    m_GeometryCache = meshes;
+    m_Materials = materials;
+    for (size_t& p : m_PrimitiveMeshIndices) p = kInvalidMeshIndex;
+    ResolveMaterialTextureSlots(textures, 0, m_Materials.size());
+    UploadMeshFromCache();
+}
+
+void Renderer::AppendMeshes(std::vector<Geometry::Mesh> meshes, std::vector<Geometry::Material> materials,
+                            std::vector<std::string> textures) {
+    if (meshes.empty()) return;
+    const size_t oldMaterials = m_Materials.size();
+    for (Geometry::Mesh& m : meshes) {
+        if (m.MaterialIndex >= 0) m.MaterialIndex += static_cast<int32_t>(oldMaterials);
+        m_GeometryCache.emplace_back(std::move(m));
+    }
+    const size_t offset = m_Materials.size();
+    for (Geometry::Material& m : materials) m_Materials.emplace_back(std::move(m));
+    ResolveMaterialTextureSlots(textures, offset, materials.size());
+    UploadMeshFromCache();
+}
+
+size_t Renderer::GetOrCreatePrimitiveMeshIndex(MeshComponent::PrimitiveType type) {
+    if (type == MeshComponent::PrimitiveType::None) return kInvalidMeshIndex;
+    const size_t slot = static_cast<size_t>(type) - 1;
+    if (slot >= 3) return kInvalidMeshIndex;
+    const size_t existing = m_PrimitiveMeshIndices[slot];
+    if (existing != kInvalidMeshIndex && existing < m_GeometryCache.size()) return existing;
+    const size_t index = CreatePrimitiveMeshInCache(type);
+    if (index == kInvalidMeshIndex) return index;
+    if (!m_IsUploadingMeshes) UploadMeshFromCache();
+    return index;
+}
+
+size_t Renderer::CreatePrimitiveMeshInCache(MeshComponent::PrimitiveType type) {
+    const size_t slot = static_cast<size_t>(type) - 1;
+    if (type == MeshComponent::PrimitiveType::None || slot >= 3) return kInvalidMeshIndex;
+    const size_t existing = m_PrimitiveMeshIndices[slot];
+    if (existing != kInvalidMeshIndex && existing < m_GeometryCache.size()) return existing;
+    Geometry::Mesh mesh = type == MeshComponent::PrimitiveType::Cube     ? BuildPrimitiveCubeMesh()
+                          : type == MeshComponent::PrimitiveType::Sphere ? BuildPrimitiveSphereMesh()
+                                                                         : BuildPrimitiveQuadMesh();
+    Geometry::Material material{};  // primitives: metallic 0, roughness 1 (Renderer.cpp:1900-1906)
+    material.BaseColorFactor = {1.0f, 1.0f, 1.0f, 1.0f};
+    material.MetallicFactor = 0.0f;
+    material.RoughnessFactor = 1.0f;
+    material.BaseColorTextureSlot = 0;
+    mesh.MaterialIndex = static_cast<int32_t>(m_Materials.size());
+    m_Materials.push_back(material);
+    m_GeometryCache.push_back(std::move(mesh));
+    m_PrimitiveMeshIndices[slot] = m_GeometryCache.size() - 1;
+    ++m_MaterialGeneration;
+    return m_GeometryCache.size() - 1;
+}
+
+void Renderer::EnsurePrimitiveMeshesInCache() {
+    if (!m_Registry) return;
+    for (ECS::Entity e : m_Registry->GetEntities()) {
+        if (!m_Registry->HasComponent<MeshComponent>(e)) continue;
+        MeshComponent& c = m_Registry->GetComponent<MeshComponent>(e);
+        if (c.m_Primitive == MeshComponent::PrimitiveType::None) continue;
+        if (c.m_MeshIndex != kInvalidMeshIndex && c.m_MeshIndex < m_GeometryCache.size()) continue;
+        const size_t index = CreatePrimitiveMeshInCache(c.m_Primitive);
+        if (index != kInvalidMeshIndex) c.m_MeshIndex = index;
+    }
+}
+
+void Renderer::UploadMeshFromCache() {  // Renderer.cpp:1965-2116
+    m_IsUploadingMeshes = true;
+    EnsurePrimitiveMeshesInCache();
+    m_VertexBuffer.clear();
+    m_IndexBuffer.clear();
+    m_MeshDrawInfo.clear();
+    uint32_t firstIndex = 0;
+    int32_t baseVertex = 0;
+    for (const Geometry::Mesh& mesh : m_GeometryCache) {
+        const size_t v0 = m_VertexBuffer.size();
+        m_VertexBuffer.resize(v0 + mesh.Vertices.size());
+        std::memcpy(m_VertexBuffer.data() + v0, mesh.Vertices.data(), mesh.Vertices.size() * sizeof(Vertex));
+        m_IndexBuffer.insert(m_IndexBuffer.end(), mesh.Indices.begin(), mesh.Indices.end());  // mesh-local
+        MeshDrawInfo info;
+        info.m_FirstIndex = firstIndex;
+        info.m_IndexCount = static_cast<uint32_t>(mesh.Indices.size());
+        info.m_BaseVertex = baseVertex;
+        info.m_MaterialIndex = mesh.MaterialIndex;
+        m_MeshDrawInfo.push_back(info);
+        firstIndex += info.m_IndexCount;
+        baseVertex += static_cast<int32_t>(mesh.Vertices.size());
+    }
+    m_MeshDrawCommands.clear();
+    if (m_Registry) {
+        for (ECS::Entity e : m_Registry->GetEntities()) {
+            if (!m_Registry->HasComponent<MeshComponent>(e)) continue;
+            MeshComponent& c = m_Registry->GetComponent<MeshComponent>(e);
+            if (c.m_MeshIndex >= m_MeshDrawInfo.size()) continue;
+            const MeshDrawInfo& d = m_MeshDrawInfo[c.m_MeshIndex];
+            c.m_FirstIndex = d.m_FirstIndex;
+            c.m_IndexCount = d.m_IndexCount;
+            c.m_BaseVertex = d.m_BaseVertex;
+            c.m_MaterialIndex = d.m_MaterialIndex;
+        }
+    }
+    m_ModelCount = m_GeometryCache.size();
+    m_TriangleCount = m_IndexBuffer.size() / 3;
+    ++m_GeometryGeneration;
+    ++m_MaterialGeneration;
+    m_IsUploadingMeshes = false;
+}
+
+// ---- textures ---------------------------------------------------------------------------------
+void Renderer::UploadTexture(const std::string& texturePath, const Loader::TextureData& texture) {
+    const std::string key = NormalizeTexturePath(texturePath);
+    if (texture.Width <= 0 || texture.Height <= 0 ||
+        texture.Pixels.size() < (size_t)texture.Width * texture.Height * 4) {
+        LogError("UploadTexture", "texture has no RGBA8 pixel data; using the default slot");
+        m_TextureSlotLookup[key] = 0u;
+        return;
+    }
+    auto it = m_TextureSlotLookup.find(key);
+    uint32_t slot;
+    if (it != m_TextureSlotLookup.end() && it->second != 0) {
+        slot = it->second;
+    } else {
+        if (m_TextureSlots.size() >= TRI_MAX_TEXTURE_SLOTS) {
+            LogError("UploadTexture", "all 256 texture slots are in use; using the default slot");
+            m_TextureSlotLookup[key] = 0u;
+            return;
+        }
+        slot = static_cast<uint32_t>(m_TextureSlots.size());
+        m_TextureSlots.emplace_back();
+        m_TextureSlotLookup[key] = slot;
+    }
+    m_TextureSlots[slot].m_SourcePath = key;
+    m_TextureSlots[slot].m_Data = texture;
+    ++m_TextureGeneration;
+}
+
+int32_t Renderer::ResolveTextureSlot(const std::string& texturePath) {
+    const std::string key = NormalizeTexturePath(texturePath);
+    if (key.empty()) return 0;
+    auto it = m_TextureSlotLookup.find(key);
+    if (it != m_TextureSlotLookup.end()) return static_cast<int32_t>(it->second);
+    // No image decoder is linked on this path (stb is not vendored): unknown paths fall back to the
+    // default slot, exactly like a failed load in the reference (Renderer.cpp:3740-3745).
+    LogError("ResolveTextureSlot", (key + " not uploaded; using the default slot").c_str());
+    m_TextureSlotLookup.emplace(key, 0u);
+    return 0;
+}
+
+void Renderer::ResolveMaterialTextureSlots(const std::vector<std::string>& textures, size_t offset, size_t count) {
+    if (m_Materials.empty()) return;
+    const size_t safeOffset = std::min(offset, m_Materials.size());
+    const size_t n = std::min(count, m_Materials.size() - safeOffset);
+    for (size_t i = 0; i < n; ++i) {
+        Geometry::Material& m = m_Materials[safeOffset + i];
+        m.BaseColorTextureSlot = 0;
+        if (m.BaseColorTextureIndex < 0 || (size_t)m.BaseColorTextureIndex >= textures.size()) continue;
+        const std::string key = NormalizeTexturePath(textures[m.BaseColorTextureIndex]);
+        if (key.empty()) continue;
+        m.BaseColorTextureSlot = ResolveTextureSlot(key);
+    }
+    ++m_MaterialGeneration;
+}
+
+// ---- frame preparation --------------------------------------------------------------------------
+void Renderer::GatherMeshDraws() {  // Renderer.cpp:2910-2994
+    m_MeshDrawCommands.clear();
+    if (!m_Registry) return;
+    for (ECS::Entity e : m_Registry->GetEntities()) {
+        if (!m_Registry->HasComponent<MeshComponent>(e)) continue;
+        MeshComponent& c = m_Registry->GetComponent<MeshComponent>(e);
+        if (!c.m_Visible) continue;
+        if (c.m_Primitive != MeshComponent::PrimitiveType::None && c.m_MeshIndex == kInvalidMeshIndex) {
+            c.m_MeshIndex = GetOrCreatePrimitiveMeshIndex(c.m_Primitive);
+            if (c.m_MeshIndex == kInvalidMeshIndex) continue;
+        }
+        if (c.m_MeshIndex >= m_MeshDrawInfo.size()) continue;
+        if (m_MeshDrawInfo[c.m_MeshIndex].m_IndexCount == 0) continue;
+        MeshDrawCommand cmd;
+        if (m_Registry->HasComponent<Transform>(e)) cmd.m_ModelMatrix = ComposeTransform(m_Registry->GetComponent<Transform>(e));
+        if (m_Registry->HasComponent<TextureComponent>(e)) {
+            TextureComponent& t = m_Registry->GetComponent<TextureComponent>(e);
+            if (t.m_IsDirty || t.m_TextureSlot < 0) {
+                t.m_TextureSlot = ResolveTextureSlot(t.m_TexturePath);
+                t.m_IsDirty = false;
+            }
+            cmd.m_TextureComponent = &t;
+        }
+        cmd.m_Component = &c;
+        cmd.m_Entity = e;
+        m_MeshDrawCommands.push_back(cmd);
+    }
+}
+
+void Renderer::BuildDrawList(std::vector<tri_draw>& out) const {  // Renderer.cpp:5110-5151
+    out.clear();
+    for (const MeshDrawCommand& cmd : m_MeshDrawCommands) {
+        if (!cmd.m_Component || cmd.m_Component->m_MeshIndex >= m_MeshDrawInfo.size()) continue;
+        const MeshDrawInfo& info = m_MeshDrawInfo[cmd.m_Component->m_MeshIndex];
+        if (info.m_IndexCount == 0) continue;
+        tri_draw d;
+        std::memset(&d, 0, sizeof d);
+        d.mesh_index = static_cast<uint32_t>(cmd.m_Component->m_MeshIndex);
+        tri_push_constant& pc = d.pc;  // RenderablePushConstant defaults (RenderData.h:16-29)
+        CopyMat(cmd.m_ModelMatrix, pc.model);
+        pc.tint[0] = pc.tint[1] = pc.tint[2] = pc.tint[3] = 1.0f;
+        pc.texture_scale[0] = pc.texture_scale[1] = 1.0f;
+        pc.tiling_factor = 1.0f;
+        int32_t slot = 0;
+        if (cmd.m_TextureComponent && cmd.m_TextureComponent->m_TextureSlot >= 0)
+            slot = cmd.m_TextureComponent->m_TextureSlot;
+        else if (info.m_MaterialIndex >= 0 && (size_t)info.m_MaterialIndex < m_Materials.size())
+            slot = m_Materials[info.m_MaterialIndex].BaseColorTextureSlot;
+        pc.texture_slot = slot;
+        pc.material_index = info.m_MaterialIndex;
+        out.push_back(d);
+    }
+}
+
+void Renderer::UpdateUniformBuffer(const Camera* camera, tri_global_ubo& g) const {  // Renderer.cpp:5822-5925
+    std::memset(&g, 0, sizeof g);
+    if (camera) {
+        CopyMat(camera->GetViewMatrix(), g.view);
+        CopyMat(camera->GetProjectionMatrix(), g.projection);
+        const glm::vec3 p = camera->GetPosition();
+        g.camera_position[0] = p.x; g.camera_position[1] = p.y; g.camera_position[2] = p.z;
+    } else {
+        CopyMat(glm::mat4(1.0f), g.view);
+        CopyMat(glm::mat4(1.0f), g.projection);
+    }
+    g.camera_position[3] = 1.0f;
+    g.ambient_color_intensity[0] = m_AmbientColor.x;
+    g.ambient_color_intensity[1] = m_AmbientColor.y;
+    g.ambient_color_intensity[2] = m_AmbientColor.z;
+    g.ambient_color_intensity[3] = m_AmbientIntensity;
+    glm::vec3 dir = glm::normalize(glm::vec3{-0.5f, -1.0f, -0.3f});  // s_DefaultDirectional* (Renderer.h:464-466)
+    glm::vec3 color{1.0f, 0.98f, 0.92f};
+    float intensity = 5.0f;
+    uint32_t ndir = 0, npt = 0;
+    if (m_Registry) {
+        for (ECS::Entity e : m_Registry->GetEntities()) {
+            if (!m_Registry->HasComponent<LightComponent>(e)) continue;
+            const LightComponent& L = m_Registry->GetComponent<LightComponent>(e);
+            if (!L.m_Enabled) continue;
+            if (L.m_Type == LightComponent::Type::Directional) {
+                if (ndir == 0) {
+                    if (glm::dot(L.m_Direction, L.m_Direction) > 0.0001f) dir = glm::normalize(L.m_Direction);
+                    color = L.m_Color;
+                    intensity = std::max(L.m_Intensity, 0.0f);
+                }
+                ++ndir;
+                continue;
+            }
+            if (L.m_Type == LightComponent::Type::Point) {
+                if (npt >= TRI_MAX_POINT_LIGHTS) continue;
+                glm::vec3 pos{0.0f};
+                if (m_Registry->HasComponent<Transform>(e)) pos = m_Registry->GetComponent<Transform>(e).Position;
+                tri_point_light& pl = g.point_lights[npt++];
+                pl.position_range[0] = pos.x; pl.position_range[1] = pos.y; pl.position_range[2] = pos.z;
+                pl.position_range[3] = std::max(L.m_Range, 0.0f);
+                pl.color_intensity[0] = L.m_Color.x; pl.color_intensity[1] = L.m_Color.y;
+                pl.color_intensity[2] = L.m_Color.z; pl.color_intensity[3] = std::max(L.m_Intensity, 0.0f);
+            }
+        }
+    }
+    const bool fallback = (ndir == 0 && npt == 0);
+    g.directional_light_direction[0] = dir.x; g.directional_light_direction[1] = dir.y;
+    g.directional_light_direction[2] = dir.z; g.directional_light_direction[3] = 0.0f;
+    g.directional_light_color[0] = color.x; g.directional_light_color[1] = color.y;
+    g.directional_light_color[2] = color.z; g.directional_light_color[3] = intensity;
+    g.light_counts[0] = (ndir > 0 || fallback) ? 1u : 0u;
+    g.light_counts[1] = npt;
+    // AiBlendConfig stays 0: the AI frame blend is outside the hot path (Renderer.cpp:5916-5925)
+}
+
+const Camera* Renderer::GetActiveCamera(const ViewportContext& context) const {  // Renderer.cpp:4545-4574
+    const uint32_t id = context.m_Info.ViewportID;
+    if (id == 1u) return m_EditorCamera;
+    if (id == 2u) return (m_RuntimeCameraReady && m_RuntimeCamera) ? m_RuntimeCamera : m_EditorCamera;
+    if (m_EditorCamera) return m_EditorCamera;
+    return (m_RuntimeCameraReady && m_RuntimeCamera) ? m_RuntimeCamera : nullptr;
+}
+
+const Camera* Renderer::GetActiveCamera() const {
+    if (m_EditorCamera) return m_EditorCamera;
+    return (m_RuntimeCameraReady && m_RuntimeCamera) ? m_RuntimeCamera : nullptr;
+}
+
+void Renderer::SetViewport(uint32_t viewportId, const ViewportInfo& info) {
+    ViewportContext& ctx = m_Viewports[viewportId];
+    ctx.m_Info = info;
+    ctx.m_Info.ViewportID = viewportId;
+    m_LastViewport = ctx.m_Info;
+}
+
+ViewportInfo Renderer::GetViewport() const { return m_LastViewport; }
+
+glm::mat4 Renderer::GetViewportViewMatrix(uint32_t id) const {
+    auto it = m_Viewports.find(id);
+    const Camera* cam = it != m_Viewports.end() ? GetActiveCamera(it->second) : GetActiveCamera();
+    return cam ? cam->GetViewMatrix() : glm::mat4(1.0f);
+}
+
+glm::mat4 Renderer::GetViewportProjectionMatrix(uint32_t id) const {
+    auto it = m_Viewports.find(id);
+    const Camera* cam = it != m_Viewports.end() ? GetActiveCamera(it->second) : GetActiveCamera();
+    return cam ? cam->GetProjectionMatrix() : glm::mat4(1.0f);
+}
+
+std::vector<tri_mesh_range> Renderer::GetMeshRanges() const {
+    std::vector<tri_mesh_range> ranges(m_MeshDrawInfo.size());
+    for (size_t i = 0; i < ranges.size(); ++i)
+        ranges[i] = {m_MeshDrawInfo[i].m_FirstIndex, m_MeshDrawInfo[i].m_IndexCount, m_MeshDrawInfo[i].m_BaseVertex,
+                     m_MeshDrawInfo[i].m_MaterialIndex};
+    return ranges;
+}
+
+bool Renderer::PrepareViewport(ViewportContext& vc) {
+    const uint32_t w = (uint32_t)std::max(vc.m_Info.Size.x, 0.0f), h = (uint32_t)std::max(vc.m_Info.Size.y, 0.0f);
+    if (w == 0 || h == 0) return false;
+    if (vc.m_Ctx && (vc.m_Width != w || vc.m_Height != h)) {  // CreateOrResizeOffscreenResources
+        tri_destroy(vc.m_Ctx);
+        vc.m_Ctx = nullptr;
+    }
+    if (!vc.m_Ctx) {
+        tri_config cfg{w, h, 0, 0, -1, m_RasterFlags};
+        if (tri_create(&cfg, &vc.m_Ctx) != TRI_OK) {
+            LogError("viewport target", tri_last_error());
+            vc.m_Ctx = nullptr;
+            return false;
+        }
+        vc.m_Width = w;
+        vc.m_Height = h;
+        vc.m_GeometryGeneration = vc.m_TextureGeneration = vc.m_MaterialGeneration = 0;
+    }
+    if (vc.m_GeometryGeneration != m_GeometryGeneration) {
+        const std::vector<tri_mesh_range> ranges = GetMeshRanges();
+        if (tri_upload_geometry(vc.m_Ctx, m_VertexBuffer.data(), m_VertexBuffer.size(), m_IndexBuffer.data(),
+                                m_IndexBuffer.size(), ranges.data(), (uint32_t)ranges.size()) != TRI_OK) {
+            LogError("UploadMeshFromCache", tri_last_error());
+            return false;
+        }
+        vc.m_GeometryGeneration = m_GeometryGeneration;
+    }
+    if (vc.m_MaterialGeneration != m_MaterialGeneration) {  // BuildMaterialPayload (Renderer.cpp:5927-5951)
+        std::vector<tri_material_record> recs;
+        for (const Geometry::Material& m : m_Materials)
+            recs.push_back({{m.BaseColorFactor.x, m.BaseColorFactor.y, m.BaseColorFactor.z, m.BaseColorFactor.w},
+                            {m.MetallicFactor, m.RoughnessFactor, 1.0f, 0.0f}});
+        if (tri_upload_materials(vc.m_Ctx, recs.data(), (uint32_t)recs.size()) != TRI_OK) {
+            LogError("material buffer", tri_last_error());
+            return false;
+        }
+        vc.m_MaterialGeneration = m_MaterialGeneration;
+    }
+    if (vc.m_TextureGeneration != m_TextureGeneration) {
+        for (size_t s = 0; s < m_TextureSlots.size(); ++s) {
+            const Loader::TextureData& t = m_TextureSlots[s].m_Data;
+            if (tri_upload_texture(vc.m_Ctx, (uint32_t)s, t.Pixels.data(), (uint32_t)t.Width, (uint32_t)t.Height) !=
+                TRI_OK) {
+                LogError("texture slot", tri_last_error());
+                return false;
+            }
+        }
+        vc.m_TextureGeneration = m_TextureGeneration;
+    }
+    return true;
+}
+
+bool Renderer::BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::vector<tri_draw>& draws) {
+    auto it = m_Viewports.find(viewportId);
+    if (it == m_Viewports.end()) return false;
+    GatherMeshDraws();
+    UpdateUniformBuffer(GetActiveCamera(it->second), ubo);
+    BuildDrawList(draws);
+    return true;
+}
+
+void Renderer::DrawFrame() {  // Renderer.cpp:733-837
+    const auto t0 = std::chrono::steady_clock::now();
+    if (!m_Initialised || m_Shutdown) return;
+    GatherMeshDraws();
+    std::vector<tri_draw> draws;
+    BuildDrawList(draws);
+    const float clear[4] = {m_ClearColor.x, m_ClearColor.y, m_ClearColor.z, m_ClearColor.w};
+    std::vector<ViewportContext*> submitted;
+    for (auto& it : m_Viewports) {  // RecordCommandBuffer's per-viewport render passes
+        ViewportContext& vc = it.second;
+        if (!PrepareViewport(vc)) continue;
+        tri_global_ubo ubo;
+        UpdateUniformBuffer(GetActiveCamera(vc), ubo);
+        if (tri_set_frame(vc.m_Ctx, &ubo, clear) != TRI_OK ||
+            tri_set_draws(vc.m_Ctx, draws.data(), (uint32_t)draws.size()) != TRI_OK || tri_render(vc.m_Ctx) != TRI_OK) {
+            LogError("DrawFrame", tri_last_error());
+            continue;
+        }
+        submitted.push_back(&vc);
+    }
+    // Frame fence (Renderer.cpp:744-760). A frame that outgrew the bin/clip queues has grown them
+    // inside tri_synchronize and is re-rendered, so a presented frame is always complete.
+    for (ViewportContext* vc : submitted) {
+        int rc = tri_synchronize(vc->m_Ctx);
+        for (int retry = 0; rc == TRI_E_OVERFLOW && retry < 3; ++retry) {
+            rc = tri_render(vc->m_Ctx);
+            if (rc == TRI_OK) rc = tri_synchronize(vc->m_Ctx);
+        }
+        if (rc != TRI_OK) LogError("frame fence", tri_last_error());
+    }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    RecordFrameTiming(ms);
+}
+
+void Renderer::RecordFrameTiming(double ms) {  // Renderer.cpp:6286-6343
+    if (m_PerformanceHistory.empty()) return;
+    FrameTimingSample s;
+    s.FrameMilliseconds = ms;
+    s.FramesPerSecond = ms > 0.0 ? 1000.0 / ms : 0.0;
+    s.CaptureTime = std::chrono::system_clock::now();
+    m_PerformanceHistory[m_PerformanceHistoryNextIndex] = s;
+    m_PerformanceHistoryNextIndex = (m_PerformanceHistoryNextIndex + 1) % m_PerformanceHistory.size();
+    m_PerformanceSampleCount = std::min(m_PerformanceSampleCount + 1, m_PerformanceHistory.size());
+    FrameTimingStats st;
+    st.MinimumMilliseconds = std::numeric_limits<double>::max();
+    st.MinimumFPS = std::numeric_limits<double>::max();
+    double sumMs = 0.0, sumFps = 0.0;
+    for (size_t i = 0; i < m_PerformanceSampleCount; ++i) {
+        const FrameTimingSample& x = m_PerformanceHistory[i];
+        st.MinimumMilliseconds = std::min(st.MinimumMilliseconds, x.FrameMilliseconds);
+        st.MaximumMilliseconds = std::max(st.MaximumMilliseconds, x.FrameMilliseconds);
+        st.MinimumFPS = std::min(st.MinimumFPS, x.FramesPerSecond);
+        st.MaximumFPS = std::max(st.MaximumFPS, x.FramesPerSecond);
+        sumMs += x.FrameMilliseconds;
+        sumFps += x.FramesPerSecond;
+    }
+    st.AverageMilliseconds = sumMs / (double)m_PerformanceSampleCount;
+    st.AverageFPS = sumFps / (double)m_PerformanceSampleCount;
+    m_PerformanceStats = st;
+}
+
+void* Renderer::GetViewportTexture(uint32_t viewportId) const {
+    (void)viewportId;
+    return nullptr;  // device buffers are owned by tri_ctx; expose them via ReadViewportPixels / bind_output
+}
+
+bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgba, std::vector<float>* depth) {
+    auto it = m_Viewports.find(viewportId);
+    if (it == m_Viewports.end() || !it->second.m_Ctx) return false;
+    ViewportContext& vc = it->second;
+    std::vector<uint8_t> bgra((size_t)vc.m_Width * vc.m_Height * 4);
+    std::vector<uint32_t> dbits;
+    if (depth) dbits.resize((size_t)vc.m_Width * vc.m_Height);
+    if (tri_readback(vc.m_Ctx, bgra.data(), depth ? dbits.data() : nullptr) != TRI_OK) {
+        LogError("readback", tri_last_error());
+        return false;
+    }
+    rgba.resize(bgra.size());
+    for (size_t i = 0; i < bgra.size(); i += 4) {  // QuerySwapchainFormatInfo: BGRA -> RGBA
+        rgba[i + 0] = bgra[i + 2];
+        rgba[i + 1] = bgra[i + 1];
+        rgba[i + 2] = bgra[i + 0];
+        rgba[i + 3] = bgra[i + 3];
+    }
+    if (depth) {
+        depth->resize(dbits.size());
+        std::memcpy(depth->data(), dbits.data(), dbits.size() * 4);
+    }
+    return true;
+}
+
+}  // namespace Trident

@@ -1,0 +1,283 @@
+// trident_app.cpp — flat C driver over Trident::Renderer (see host/include/trident_app.h).
+// Entity set-up follows Forge's ApplicationLayer: a primitive spawned with Transform +
+// MeshComponent (ApplicationLayer.cpp:677-718), lights as LightComponent entities.
+#include "trident_app.h"
+
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "trident/Renderer.h"
+
+using namespace Trident;
+
+struct trident_app {
+    Renderer renderer;
+    ECS::Registry registry;
+    EditorCamera editor;
+    RuntimeCamera runtime;
+};
+
+namespace {
+
+glm::vec3 V3(const float* p, glm::vec3 dflt) { return p ? glm::vec3{p[0], p[1], p[2]} : dflt; }
+
+template <typename F>
+int Guard(trident_app* app, F&& f) {
+    if (!app) return TRI_E_INVALID;
+    try {
+        return f();
+    } catch (const std::exception&) {
+        return TRI_E_INVALID;
+    }
+}
+
+}  // namespace
+
+extern "C" {
+
+int trident_app_create(uint32_t raster_flags, trident_app** out) {
+    if (!out) return TRI_E_INVALID;
+    *out = nullptr;
+    try {
+        auto* app = new trident_app();
+        app->renderer.Init();
+        app->renderer.SetRasterFlags(raster_flags);
+        app->renderer.SetActiveRegistry(&app->registry);
+        app->renderer.SetEditorCamera(&app->editor);
+        app->renderer.SetRuntimeCamera(&app->runtime);
+        *out = app;
+        return TRI_OK;
+    } catch (const std::exception&) {
+        return TRI_E_OOM;
+    }
+}
+
+void trident_app_destroy(trident_app* app) {
+    if (!app) return;
+    app->renderer.Shutdown();
+    delete app;
+}
+
+int trident_app_append_mesh(trident_app* app, const tri_vertex* vertices, uint32_t vertex_count,
+                            const uint32_t* indices, uint32_t index_count, const float base_color[4], float metallic,
+                            float roughness, const char* texture_path, uint32_t* mesh_index) {
+    return Guard(app, [&] {
+        if ((!vertices && vertex_count) || (!indices && index_count) || index_count % 3) return TRI_E_INVALID;
+        Geometry::Mesh mesh;
+        mesh.Vertices.resize(vertex_count);
+        if (vertex_count) std::memcpy(static_cast<void*>(mesh.Vertices.data()), vertices, (size_t)vertex_count * sizeof(Vertex));
+        mesh.Indices.assign(indices, indices + index_count);
+        mesh.MaterialIndex = 0;  // local to this append; AppendMeshes offsets it
+        Geometry::Material mat;
+        if (base_color) mat.BaseColorFactor = {base_color[0], base_color[1], base_color[2], base_color[3]};
+        mat.MetallicFactor = metallic;
+        mat.RoughnessFactor = roughness;
+        std::vector<std::string> textures;
+        if (texture_path && *texture_path) {
+            textures.emplace_back(texture_path);
+            mat.BaseColorTextureIndex = 0;
+        }
+        const size_t before = app->renderer.GetModelCount();
+        app->renderer.AppendMeshes({mesh}, {mat}, textures);
+        if (mesh_index) *mesh_index = static_cast<uint32_t>(before);
+        return TRI_OK;
+    });
+}
+
+int trident_app_upload_texture(trident_app* app, const char* path, const uint8_t* rgba, uint32_t width,
+                               uint32_t height) {
+    return Guard(app, [&] {
+        if (!path || !rgba || !width || !height) return TRI_E_INVALID;
+        Loader::TextureData t;
+        t.Width = (int)width;
+        t.Height = (int)height;
+        t.Pixels.assign(rgba, rgba + (size_t)width * height * 4);
+        app->renderer.UploadTexture(path, t);
+        return TRI_OK;
+    });
+}
+
+int trident_app_add_mesh_entity(trident_app* app, int primitive, uint32_t mesh_index, const float position[3],
+                                const float rotation_deg[3], const float scale[3], uint32_t* entity) {
+    return Guard(app, [&] {
+        if (primitive < 0 || primitive > 3) return TRI_E_INVALID;
+        const ECS::Entity e = app->registry.CreateEntity();
+        Transform& t = app->registry.AddComponent<Transform>(e);
+        t.Position = V3(position, glm::vec3{0.0f});
+        t.Rotation = V3(rotation_deg, glm::vec3{0.0f});
+        t.Scale = V3(scale, glm::vec3{1.0f});
+        MeshComponent& m = app->registry.AddComponent<MeshComponent>(e);
+        m.m_Primitive = static_cast<MeshComponent::PrimitiveType>(primitive);
+        if (primitive == 0) m.m_MeshIndex = mesh_index;
+        if (entity) *entity = e;
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_entity_texture(trident_app* app, uint32_t entity, const char* texture_path) {
+    return Guard(app, [&] {
+        TextureComponent& t = app->registry.AddComponent<TextureComponent>(entity);
+        t.m_TexturePath = texture_path ? texture_path : "";
+        t.m_TextureSlot = -1;
+        t.m_IsDirty = true;
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_entity_transform(trident_app* app, uint32_t entity, const float position[3],
+                                     const float rotation_deg[3], const float scale[3]) {
+    return Guard(app, [&] {
+        if (!app->registry.HasComponent<Transform>(entity)) return TRI_E_INVALID;
+        Transform& t = app->registry.GetComponent<Transform>(entity);
+        t.Position = V3(position, t.Position);
+        t.Rotation = V3(rotation_deg, t.Rotation);
+        t.Scale = V3(scale, t.Scale);
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_entity_visible(trident_app* app, uint32_t entity, int visible) {
+    return Guard(app, [&] {
+        if (!app->registry.HasComponent<MeshComponent>(entity)) return TRI_E_INVALID;
+        app->registry.GetComponent<MeshComponent>(entity).m_Visible = visible != 0;
+        return TRI_OK;
+    });
+}
+
+int trident_app_add_light(trident_app* app, int type, const float position[3], const float direction[3],
+                          const float color[3], float intensity, float range, int enabled, uint32_t* entity) {
+    return Guard(app, [&] {
+        if (type != TRIDENT_LIGHT_DIRECTIONAL && type != TRIDENT_LIGHT_POINT) return TRI_E_INVALID;
+        const ECS::Entity e = app->registry.CreateEntity();
+        Transform& t = app->registry.AddComponent<Transform>(e);
+        t.Position = V3(position, glm::vec3{0.0f});
+        LightComponent& l = app->registry.AddComponent<LightComponent>(e);
+        l.m_Type = static_cast<LightComponent::Type>(type);
+        l.m_Direction = V3(direction, l.m_Direction);
+        l.m_Color = V3(color, l.m_Color);
+        l.m_Intensity = intensity;
+        l.m_Range = range;
+        l.m_Enabled = enabled != 0;
+        if (entity) *entity = e;
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_camera(trident_app* app, int which, const float position[3], const float rotation_deg[3],
+                           float fov_deg, float near_clip, float far_clip, int ready) {
+    return Guard(app, [&] {
+        if (which != 0 && which != 1) return TRI_E_INVALID;
+        Camera& cam = which == 0 ? static_cast<Camera&>(app->editor) : static_cast<Camera&>(app->runtime);
+        cam.SetPosition(V3(position, cam.GetPosition()));
+        cam.SetRotation(V3(rotation_deg, cam.GetRotation()));
+        cam.SetFieldOfView(fov_deg);
+        cam.SetClipPlanes(near_clip, far_clip);
+        if (which == 1) app->renderer.SetRuntimeCameraReady(ready != 0);
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_viewport(trident_app* app, uint32_t viewport_id, uint32_t width, uint32_t height) {
+    return Guard(app, [&] {
+        if (width > TRI_MAX_DIM || height > TRI_MAX_DIM) return TRI_E_INVALID;
+        ViewportInfo info;
+        info.Size = {(float)width, (float)height};
+        app->renderer.SetViewport(viewport_id, info);
+        // The viewport panel resizes the camera that renders into it (ApplicationLayer.cpp:253-290).
+        if (width && height) {
+            const glm::vec2 s{(float)width, (float)height};
+            if (viewport_id == 2u) app->runtime.SetViewportSize(s);
+            else app->editor.SetViewportSize(s);
+        }
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_clear_color(trident_app* app, const float rgba[4]) {
+    return Guard(app, [&] {
+        if (!rgba) return TRI_E_INVALID;
+        app->renderer.SetClearColor({rgba[0], rgba[1], rgba[2], rgba[3]});
+        return TRI_OK;
+    });
+}
+
+int trident_app_draw_frame(trident_app* app) {
+    return Guard(app, [&] {
+        app->renderer.DrawFrame();
+        return TRI_OK;
+    });
+}
+
+int trident_app_read_pixels(trident_app* app, uint32_t viewport_id, uint8_t* rgba, float* depth) {
+    return Guard(app, [&] {
+        if (!rgba) return TRI_E_INVALID;
+        std::vector<uint8_t> px;
+        std::vector<float> d;
+        if (!app->renderer.ReadViewportPixels(viewport_id, px, depth ? &d : nullptr)) return TRI_E_STATE;
+        std::memcpy(rgba, px.data(), px.size());
+        if (depth) std::memcpy(depth, d.data(), d.size() * sizeof(float));
+        return TRI_OK;
+    });
+}
+
+int trident_app_frame_inputs(trident_app* app, uint32_t viewport_id, tri_global_ubo* ubo, tri_draw* draws,
+                             uint32_t capacity, uint32_t* draw_count) {
+    return Guard(app, [&] {
+        if (!ubo || !draw_count) return TRI_E_INVALID;
+        std::vector<tri_draw> list;
+        if (!app->renderer.BuildFrameInputs(viewport_id, *ubo, list)) return TRI_E_STATE;
+        *draw_count = (uint32_t)list.size();
+        if (list.size() > capacity || (!draws && !list.empty())) return list.size() > capacity ? TRI_E_OVERFLOW : TRI_E_INVALID;
+        if (!list.empty()) std::memcpy(draws, list.data(), list.size() * sizeof(tri_draw));
+        return TRI_OK;
+    });
+}
+
+int trident_app_geometry(trident_app* app, const tri_vertex** vertices, size_t* vertex_count,
+                         const uint32_t** indices, size_t* index_count, tri_mesh_range* ranges, uint32_t capacity,
+                         uint32_t* range_count) {
+    return Guard(app, [&] {
+        if (!vertices || !vertex_count || !indices || !index_count || !range_count) return TRI_E_INVALID;
+        *vertices = app->renderer.GetVertexBuffer().data();
+        *vertex_count = app->renderer.GetVertexBuffer().size();
+        *indices = app->renderer.GetIndexBuffer().data();
+        *index_count = app->renderer.GetIndexBuffer().size();
+        const std::vector<tri_mesh_range> r = app->renderer.GetMeshRanges();
+        *range_count = (uint32_t)r.size();
+        if (r.size() > capacity) return TRI_E_OVERFLOW;
+        if (!r.empty() && ranges) std::memcpy(ranges, r.data(), r.size() * sizeof(tri_mesh_range));
+        return TRI_OK;
+    });
+}
+
+int trident_app_materials(trident_app* app, tri_material_record* out, uint32_t capacity, uint32_t* count) {
+    return Guard(app, [&] {
+        if (!count) return TRI_E_INVALID;
+        const auto& mats = app->renderer.GetMaterials();
+        *count = (uint32_t)mats.size();
+        if (mats.size() > capacity) return TRI_E_OVERFLOW;
+        for (size_t i = 0; i < mats.size() && out; ++i)
+            out[i] = {{mats[i].BaseColorFactor.x, mats[i].BaseColorFactor.y, mats[i].BaseColorFactor.z,
+                       mats[i].BaseColorFactor.w},
+                      {mats[i].MetallicFactor, mats[i].RoughnessFactor, 1.0f, 0.0f}};
+        return TRI_OK;
+    });
+}
+
+int trident_app_frame_timing(trident_app* app, double out[7]) {
+    return Guard(app, [&] {
+        if (!out) return TRI_E_INVALID;
+        const FrameTimingStats& s = app->renderer.GetFrameTimingStats();
+        out[0] = s.MinimumMilliseconds;
+        out[1] = s.MaximumMilliseconds;
+        out[2] = s.AverageMilliseconds;
+        out[3] = s.MinimumFPS;
+        out[4] = s.MaximumFPS;
+        out[5] = s.AverageFPS;
+        out[6] = (double)app->renderer.GetFrameTimingHistoryCount();
+        return TRI_OK;
+    });
+}
+
+}  // extern "C"

@@ -1,0 +1,182 @@
+"""Python binding of the C++ Trident::Renderer shim (libtrident_renderer.so, host/include/trident_app.h).
+
+The shim is the reference's renderer API (Renderer/RenderCommand over an ECS registry and the
+editor/runtime cameras) restated in C++ on top of the HIP C-ABI. This binding drives it the way
+Trident-Forge's ApplicationLayer does, for tests. No CPU fallback: the library must be built.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+from . import abi
+from .raster import PKG_ROOT, TriError
+
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libtrident_renderer.so")
+
+PRIMITIVE = {"none": 0, "cube": 1, "sphere": 2, "quad": 3}
+LIGHT = {"directional": 0, "point": 1}
+
+_f3 = C.POINTER(C.c_float)
+_APP_FUNCTIONS = [
+    ("trident_app_create", C.c_int, [C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("trident_app_destroy", None, [C.c_void_p]),
+    ("trident_app_append_mesh", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, _f3, C.c_float,
+                                          C.c_float, C.c_char_p, C.POINTER(C.c_uint32)]),
+    ("trident_app_upload_texture", C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.c_uint32]),
+    ("trident_app_add_mesh_entity", C.c_int, [C.c_void_p, C.c_int, C.c_uint32, _f3, _f3, _f3, C.POINTER(C.c_uint32)]),
+    ("trident_app_set_entity_texture", C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p]),
+    ("trident_app_set_entity_transform", C.c_int, [C.c_void_p, C.c_uint32, _f3, _f3, _f3]),
+    ("trident_app_set_entity_visible", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
+    ("trident_app_add_light", C.c_int, [C.c_void_p, C.c_int, _f3, _f3, _f3, C.c_float, C.c_float, C.c_int,
+                                        C.POINTER(C.c_uint32)]),
+    ("trident_app_set_camera", C.c_int, [C.c_void_p, C.c_int, _f3, _f3, C.c_float, C.c_float, C.c_float, C.c_int]),
+    ("trident_app_set_viewport", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]),
+    ("trident_app_set_clear_color", C.c_int, [C.c_void_p, _f3]),
+    ("trident_app_draw_frame", C.c_int, [C.c_void_p]),
+    ("trident_app_read_pixels", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("trident_app_frame_inputs", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(abi.TriGlobalUbo), C.c_void_p, C.c_uint32,
+                                           C.POINTER(C.c_uint32)]),
+    ("trident_app_geometry", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t), C.POINTER(C.c_void_p),
+                                       C.POINTER(C.c_size_t), C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("trident_app_materials", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("trident_app_frame_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+]
+
+_lib = None
+
+
+def load_library(path=LIB_PATH):
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise ImportError(f"Trident renderer shim not built: {path} (run __graft_entry__.build())")
+    lib = C.CDLL(path)
+    for name, res, args in _APP_FUNCTIONS:
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def _check(rc, what):
+    if rc != abi.TRI_OK:
+        raise TriError(rc, what)
+
+
+def _vec(v):
+    return None if v is None else (C.c_float * len(v))(*[float(x) for x in v])
+
+
+class TridentApp:
+    """One Renderer + ECS registry + editor/runtime cameras (Forge's ApplicationLayer, reduced)."""
+
+    def __init__(self, raster_flags=0):
+        self._lib = load_library()
+        h = C.c_void_p()
+        _check(self._lib.trident_app_create(raster_flags, C.byref(h)), "trident_app_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            self._lib.trident_app_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def append_mesh(self, vertices, indices, base_color=(1, 1, 1, 1), metallic=1.0, roughness=1.0, texture=None):
+        v = np.ascontiguousarray(vertices, abi.VERTEX_DTYPE)
+        i = np.ascontiguousarray(indices, np.uint32)
+        out = C.c_uint32()
+        _check(self._lib.trident_app_append_mesh(self._h, v.ctypes.data, v.shape[0], i.ctypes.data, i.size,
+                                                 _vec(base_color), metallic, roughness,
+                                                 texture.encode() if texture else None, C.byref(out)),
+               "append_mesh")
+        return out.value
+
+    def upload_texture(self, path, rgba):
+        rgba = np.ascontiguousarray(rgba, np.uint8)
+        _check(self._lib.trident_app_upload_texture(self._h, path.encode(), rgba.ctypes.data, rgba.shape[1],
+                                                    rgba.shape[0]), "upload_texture")
+
+    def add_mesh_entity(self, primitive="none", mesh_index=0, position=(0, 0, 0), rotation=(0, 0, 0), scale=(1, 1, 1)):
+        e = C.c_uint32()
+        _check(self._lib.trident_app_add_mesh_entity(self._h, PRIMITIVE[primitive], mesh_index, _vec(position),
+                                                     _vec(rotation), _vec(scale), C.byref(e)), "add_mesh_entity")
+        return e.value
+
+    def set_entity_texture(self, entity, path):
+        _check(self._lib.trident_app_set_entity_texture(self._h, entity, path.encode()), "set_entity_texture")
+
+    def set_entity_transform(self, entity, position=None, rotation=None, scale=None):
+        _check(self._lib.trident_app_set_entity_transform(self._h, entity, _vec(position), _vec(rotation), _vec(scale)),
+               "set_entity_transform")
+
+    def set_entity_visible(self, entity, visible):
+        _check(self._lib.trident_app_set_entity_visible(self._h, entity, 1 if visible else 0), "set_entity_visible")
+
+    def add_light(self, type, position=(0, 0, 0), direction=(-0.5, -1.0, -0.3), color=(1.0, 0.98, 0.92),
+                  intensity=5.0, range=10.0, enabled=True):
+        e = C.c_uint32()
+        _check(self._lib.trident_app_add_light(self._h, LIGHT[type], _vec(position), _vec(direction), _vec(color),
+                                               intensity, range, 1 if enabled else 0, C.byref(e)), "add_light")
+        return e.value
+
+    def set_camera(self, which, position, rotation=(0, 0, 0), fov=60.0, near=0.1, far=1000.0, ready=True):
+        _check(self._lib.trident_app_set_camera(self._h, {"editor": 0, "runtime": 1}[which], _vec(position),
+                                                _vec(rotation), fov, near, far, 1 if ready else 0), "set_camera")
+
+    def set_viewport(self, viewport_id, width, height):
+        _check(self._lib.trident_app_set_viewport(self._h, viewport_id, width, height), "set_viewport")
+
+    def set_clear_color(self, rgba):
+        _check(self._lib.trident_app_set_clear_color(self._h, _vec(rgba)), "set_clear_color")
+
+    def draw_frame(self):
+        _check(self._lib.trident_app_draw_frame(self._h), "draw_frame")
+
+    def read_pixels(self, viewport_id, width, height, depth=True):
+        rgba = np.zeros((height, width, 4), np.uint8)
+        d = np.zeros((height, width), np.float32) if depth else None
+        _check(self._lib.trident_app_read_pixels(self._h, viewport_id, rgba.ctypes.data,
+                                                 d.ctypes.data if depth else None), "read_pixels")
+        return rgba, d
+
+    def frame_inputs(self, viewport_id, capacity=4096):
+        ubo = abi.TriGlobalUbo()
+        draws = (abi.TriDraw * capacity)()
+        n = C.c_uint32()
+        _check(self._lib.trident_app_frame_inputs(self._h, viewport_id, C.byref(ubo), draws, capacity, C.byref(n)),
+               "frame_inputs")
+        return ubo, list(draws[: n.value])
+
+    def geometry(self, capacity=4096):
+        vp, ip = C.c_void_p(), C.c_void_p()
+        nv, ni = C.c_size_t(), C.c_size_t()
+        ranges = np.zeros(capacity, abi.MESH_RANGE_DTYPE)
+        nr = C.c_uint32()
+        _check(self._lib.trident_app_geometry(self._h, C.byref(vp), C.byref(nv), C.byref(ip), C.byref(ni),
+                                              ranges.ctypes.data, capacity, C.byref(nr)), "geometry")
+        vb = np.frombuffer((C.c_uint8 * (nv.value * abi.VERTEX_DTYPE.itemsize)).from_address(vp.value),
+                           abi.VERTEX_DTYPE).copy() if nv.value else np.zeros(0, abi.VERTEX_DTYPE)
+        ib = np.ctypeslib.as_array((C.c_uint32 * ni.value).from_address(ip.value)).copy() if ni.value else \
+            np.zeros(0, np.uint32)
+        return vb, ib, ranges[: nr.value].copy()
+
+    def materials(self, capacity=1024):
+        recs = (abi.TriMaterialRecord * capacity)()
+        n = C.c_uint32()
+        _check(self._lib.trident_app_materials(self._h, recs, capacity, C.byref(n)), "materials")
+        return [(tuple(r.base_color_factor), tuple(r.material_factors)) for r in recs[: n.value]]
+
+    def frame_timing(self):
+        out = (C.c_double * 7)()
+        _check(self._lib.trident_app_frame_timing(self._h, out), "frame_timing")
+        keys = ("min_ms", "max_ms", "avg_ms", "min_fps", "max_fps", "avg_fps", "samples")
+        return dict(zip(keys, list(out)))

@@ -1,0 +1,232 @@
+"""The C++ Trident::Renderer shim (3d-renderer_amd/host) against the oracle's restatement of the
+reference's frame preparation.
+
+CPU tests check what DrawFrame would submit — the concatenated geometry (UploadMeshFromCache), the
+draw list (GatherMeshDraws + the push-constant loop, Renderer.cpp:2910-2994, :5110-5151), the
+global UBO (UpdateUniformBuffer, :5822-5925) and the per-viewport camera routing (:4545-4574) — and
+need no GPU. GPU tests render through the shim and compare the frame with the oracle on the
+shim's own inputs (depth bit-exact, colour within 1 LSB, as tests/test_parity_gpu.py).
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+W, H = 640, 480
+
+
+@pytest.fixture(scope="module")
+def app_mod():
+    from trident_raster import app
+
+    app.load_library()
+    return app
+
+
+def ubo_bytes(u):
+    return bytes(memoryview(u))
+
+
+def c1_app(app_mod, frame=0, flags=0, w=W, h=H):
+    a = app_mod.TridentApp(flags)
+    a.set_camera("editor", (0.0, 3.0, 8.0))
+    a.set_viewport(1, w, h)
+    e = a.add_mesh_entity("cube", position=(0.0, 3.0, -2.0), rotation=(0.0, 30.0 * frame, 0.0))
+    return a, e
+
+
+def test_c1_frame_inputs_match_scene(app_mod):
+    from trident_raster import abi, scenes
+
+    for frame in (0, 1, 3):
+        a, _ = c1_app(app_mod, frame)
+        ubo, draws = a.frame_inputs(1)
+        ref = scenes.scene_c1_cube(frame, W, H)
+        assert ubo_bytes(ubo) == ubo_bytes(ref.ubo)
+        assert len(draws) == 1
+        got, want = draws[0], ref.draws[0]
+        assert got.mesh_index == 0
+        assert bytes(memoryview(got.pc)) == bytes(memoryview(want.pc))
+        vb, ib, ranges = a.geometry()
+        assert vb.tobytes() == ref.vertices.tobytes()
+        assert np.array_equal(ib, ref.indices)
+        assert ranges.tolist() == ref.meshes.tolist()
+        assert a.materials() == [tuple(map(tuple, m)) for m in ref.materials]
+        a.close()
+        assert abi.TRI_OK == 0
+
+
+def test_primitive_meshes(app_mod):
+    from trident_raster import scenes
+
+    a = app_mod.TridentApp()
+    a.set_viewport(1, W, H)
+    a.add_mesh_entity("sphere", position=(-1, 0, 0))
+    a.add_mesh_entity("quad", position=(1, 0, 0))
+    a.add_mesh_entity("sphere", position=(0, 1, 0))  # shares the cached sphere
+    a.frame_inputs(1)
+    vb, ib, ranges = a.geometry()
+    assert len(ranges) == 2  # sphere + quad, created once each
+    sv, si = scenes.uv_sphere_mesh()
+    n = len(sv)
+    assert np.array_equal(ib[: si.size], si)
+    np.testing.assert_allclose(vb["position"][:n], sv["position"], atol=2e-7)
+    np.testing.assert_allclose(vb["texcoord"][:n], sv["texcoord"], atol=0)
+    assert ranges[1]["first_index"] == si.size and ranges[1]["index_count"] == 6
+    assert ranges[1]["base_vertex"] == n
+    assert ib[si.size:].tolist() == [0, 1, 2, 0, 2, 3]  # mesh-local indices, base_vertex carries the offset
+    _, draws = a.frame_inputs(1)
+    assert [d.mesh_index for d in draws] == [0, 1, 0]
+    # primitives use metallic 0 / roughness 1 (Renderer.cpp:1900-1906)
+    assert all(m[1][:2] == (0.0, 1.0) for m in a.materials())
+
+
+def test_lights_pack_like_update_uniform_buffer(app_mod, oracle):
+    a = app_mod.TridentApp()
+    a.set_camera("editor", (1.0, 2.0, 3.0), (-10.0, 20.0, 0.0), fov=50.0, near=0.05, far=200.0)
+    a.set_viewport(1, 800, 600)
+    lights = [
+        dict(type="point", position=(1, 2, 3), color=(1, 0.5, 0.25), intensity=3.0, range=7.0),
+        dict(type="directional", direction=(0.2, -1.0, 0.1), color=(0.9, 0.9, 1.0), intensity=2.5),
+        dict(type="directional", direction=(1, 0, 0), color=(1, 0, 0), intensity=9.0),  # only the first counts
+        dict(type="point", position=(-4, 1, 0), color=(0.2, 1, 0.2), intensity=6.0, range=0.0, enabled=False),
+    ] + [dict(type="point", position=(k, 0, -k), color=(1, 1, 1), intensity=1.0 + k, range=2.0 + k) for k in range(9)]
+    for L in lights:
+        a.add_light(L["type"], position=L.get("position", (0, 0, 0)), direction=L.get("direction", (-0.5, -1, -0.3)),
+                    color=L["color"], intensity=L["intensity"], range=L.get("range", 10.0),
+                    enabled=L.get("enabled", True))
+    ubo, _ = a.frame_inputs(1)
+    view, proj, _ = oracle.editor_camera((1.0, 2.0, 3.0), (-10.0, 20.0, 0.0), 50.0, (800, 600), 0.05, 200.0)
+    want = oracle.pack_ubo(view, proj, (1.0, 2.0, 3.0), lights)
+    assert ubo_bytes(ubo) == ubo_bytes(want)
+    assert ubo.light_counts[0] == 1 and ubo.light_counts[1] == 8
+
+
+def test_fallback_sun_without_lights(app_mod):
+    a, _ = c1_app(app_mod)
+    ubo, _ = a.frame_inputs(1)
+    assert ubo.light_counts[0] == 1 and ubo.light_counts[1] == 0
+    assert tuple(ubo.directional_light_color) == pytest.approx((1.0, 0.98, 0.92, 5.0))
+
+
+def test_viewport_camera_routing(app_mod, oracle):
+    a = app_mod.TridentApp()
+    a.set_camera("editor", (0, 3, 8))
+    a.set_camera("runtime", (2, 1, 4), (0, 15, 0), fov=70.0, ready=False)
+    a.set_viewport(1, 640, 480)
+    a.set_viewport(2, 320, 240)
+    a.set_viewport(7, 640, 480)
+    a.add_mesh_entity("cube")
+    ev, ep, _ = oracle.editor_camera((0, 3, 8), (0, 0, 0), 60.0, (640, 480))
+    rv, rp = oracle.runtime_camera((2, 1, 4), (0, 15, 0), 70.0, (320, 240))
+    # runtime camera not ready: viewport 2 falls back to the editor camera
+    u2, _ = a.frame_inputs(2)
+    assert np.array_equal(np.frombuffer(u2.view, np.float32), ev.reshape(-1))
+    a.set_camera("runtime", (2, 1, 4), (0, 15, 0), fov=70.0, ready=True)
+    u1, _ = a.frame_inputs(1)
+    u2, _ = a.frame_inputs(2)
+    u7, _ = a.frame_inputs(7)
+    assert np.array_equal(np.frombuffer(u1.view, np.float32), ev.reshape(-1))
+    assert np.array_equal(np.frombuffer(u1.projection, np.float32), ep.reshape(-1))
+    assert np.array_equal(np.frombuffer(u2.view, np.float32), rv.reshape(-1))
+    assert np.array_equal(np.frombuffer(u2.projection, np.float32), rp.reshape(-1))
+    assert tuple(u2.camera_position) == (2.0, 1.0, 4.0, 1.0)
+    assert np.array_equal(np.frombuffer(u7.view, np.float32), ev.reshape(-1))  # others: editor first
+
+
+def test_texture_slots_and_overrides(app_mod):
+    a = app_mod.TridentApp()
+    a.set_viewport(1, 64, 64)
+    tex = np.full((4, 4, 4), 200, np.uint8)
+    a.upload_texture("assets\\bricks.png", tex)  # path normalised to forward slashes
+    a.upload_texture("assets/grass.png", tex)
+    from trident_raster import scenes
+
+    v, i = scenes.cube_mesh()
+    m0 = a.append_mesh(v, i, base_color=(1, 0, 0, 1), metallic=0.3, roughness=0.6, texture="assets/grass.png")
+    m1 = a.append_mesh(v, i, texture="missing.png")
+    e0 = a.add_mesh_entity("none", m0)
+    e1 = a.add_mesh_entity("none", m1)
+    e2 = a.add_mesh_entity("none", m1)
+    a.set_entity_texture(e2, "assets/bricks.png")
+    e3 = a.add_mesh_entity("none", 99)  # out-of-range mesh index: skipped
+    e4 = a.add_mesh_entity("none", m0)
+    a.set_entity_visible(e4, False)
+    _, draws = a.frame_inputs(1)
+    assert [d.mesh_index for d in draws] == [m0, m1, m1]
+    assert [d.pc.texture_slot for d in draws] == [2, 0, 1]
+    assert [d.pc.material_index for d in draws] == [0, 1, 1]
+    assert a.materials()[0] == ((1.0, 0.0, 0.0, 1.0), (pytest.approx(0.3), pytest.approx(0.6), 1.0, 0.0))
+    assert (e0, e1, e3) == (0, 1, 3)
+
+
+def test_draw_frame_records_timing_without_device(app_mod):
+    import conftest
+
+    if conftest.gpu_available():
+        pytest.skip("host-only behaviour")
+    a, _ = c1_app(app_mod)
+    for _ in range(3):
+        a.draw_frame()  # no device: the viewport target cannot be created, the frame is skipped
+    t = a.frame_timing()
+    assert t["samples"] == 3 and t["avg_ms"] >= 0.0
+    with pytest.raises(Exception):
+        a.read_pixels(1, W, H)
+
+
+# ---------------------------------------------------------------------------------------------
+# GPU: frames rendered through the shim == oracle on the same inputs
+# ---------------------------------------------------------------------------------------------
+def shim_scene(a, viewport, w, h, textures=()):
+    from trident_raster import scenes
+
+    ubo, draws = a.frame_inputs(viewport)
+    vb, ib, ranges = a.geometry()
+    return scenes.Scene(f"shim_vp{viewport}", w, h, vb, ib, ranges, draws, ubo,
+                        materials=[(m[0], m[1]) for m in a.materials()], textures=list(textures))
+
+
+def assert_shim_parity(a, oracle, viewport, w, h, textures=(), min_covered=100):
+    rgba, depth = a.read_pixels(viewport, w, h)
+    oc, od, _ = oracle.render(shim_scene(a, viewport, w, h, textures))
+    assert np.array_equal(depth.view(np.uint32), od), "depth mismatch"
+    ob = oc[..., [2, 1, 0, 3]]  # oracle BGRA -> RGBA
+    diff = np.abs(rgba.astype(np.int16) - ob.astype(np.int16))
+    assert int(diff.max(initial=0)) <= 1
+    assert int((od != 0x3F800000).sum()) >= min_covered
+
+
+@pytest.mark.gpu
+def test_gpu_shim_c1_frames(app_mod, oracle):
+    a, e = c1_app(app_mod)
+    for frame in range(4):
+        a.set_entity_transform(e, rotation=(0.0, 30.0 * frame, 0.0))
+        a.draw_frame()
+        assert_shim_parity(a, oracle, 1, W, H, min_covered=1000)
+    t = a.frame_timing()
+    assert t["samples"] == 4 and t["avg_fps"] > 0
+
+
+@pytest.mark.gpu
+def test_gpu_shim_two_viewports_and_textures(app_mod, oracle):
+    from trident_raster import scenes
+
+    a = app_mod.TridentApp()
+    a.set_camera("editor", (0, 1, 6))
+    a.set_camera("runtime", (3, 2, 5), (-10, 30, 0), fov=55.0, ready=True)
+    a.set_viewport(1, 480, 320)
+    a.set_viewport(2, 256, 200)
+    yy, xx = np.mgrid[0:8, 0:8]
+    checker = np.where(((xx + yy) % 2)[..., None] == 0, 230, 25).astype(np.uint8).repeat(4, -1)
+    checker[..., 3] = 255
+    a.upload_texture("checker.png", checker)
+    v, i = scenes.uv_sphere_mesh(24, 32, 1.0)
+    m = a.append_mesh(v, i, base_color=(0.9, 0.8, 0.7, 1), metallic=0.2, roughness=0.5, texture="checker.png")
+    a.add_mesh_entity("none", m, position=(0, 0.5, 0))
+    a.add_mesh_entity("cube", position=(-1.5, 0, 0), rotation=(10, 20, 30))
+    q = a.add_mesh_entity("quad", position=(1.5, 0, 0), scale=(1.5, 1.5, 1))
+    a.set_entity_texture(q, "checker.png")
+    a.add_light("point", position=(0, 2, 2), color=(1, 0.9, 0.8), intensity=8.0, range=6.0)
+    a.draw_frame()
+    assert_shim_parity(a, oracle, 1, 480, 320, textures=[(1, checker)], min_covered=5000)
+    assert_shim_parity(a, oracle, 2, 256, 200, textures=[(1, checker)], min_covered=1000)
