@@ -6,8 +6,7 @@
 
 One step = one frame of Trident's graphics-pipeline stage: the per-frame UBO + draw-list update
 (UpdateUniformBuffer / push constants, Renderer.cpp:5822-6051, :5110-5151) and the five gfx950
-kernels (vs_transform, tri_setup_bin, bin scan, scatter, tile_raster_shade) over geometry resident
-in HBM; N > 1 = sort-first row bands (geometry replicated) + an RCCL all-gather of the BGRA8 bands
+kernels (k_vertex, k_setup, k_clip, k_raster) over geometry resident in HBM; N > 1 = sort-first row bands (geometry replicated) + an RCCL all-gather of the BGRA8 bands
 into the full frame on every rank. value = whole frames per second (strong scaling: a frame's work
 is fixed, N GPUs share it). Rank 0 prints ONE JSON line.
 """
@@ -36,6 +35,37 @@ def build_scene(name):
     raise SystemExit(f"unknown config {name}")
 
 
+def band_rows(height, world, rank):
+    """Rank's row band [y0, y1): equal contiguous bands (all_gather_into_tensor needs equal sizes)."""
+    if height % world:
+        raise ValueError(f"height {height} does not split into {world} equal row bands")
+    rows = height // world
+    return rank * rows, (rank + 1) * rows
+
+
+def gather_bands(frame, band, world):
+    """Assemble the full frame on every rank from the per-rank BGRA8 bands (RCCL all-gather over xGMI
+    with the nccl backend; gloo in the CPU tests). Band r lands at rows [r*rows, (r+1)*rows)."""
+    if world == 1:
+        return band
+    import torch.distributed as dist
+
+    dist.all_gather_into_tensor(frame, band)
+    return frame
+
+
+def max_over_ranks(value, device, dist_on):
+    """The job's time is the slowest rank's time."""
+    if not dist_on:
+        return value
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
 class BandRenderer:
     """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers."""
 
@@ -44,10 +74,9 @@ class BandRenderer:
         from trident_raster import raster, scenes
 
         H, W = scene.height, scene.width
-        assert H % world == 0, "row bands must be equal for all_gather_into_tensor"
-        rows = H // world
+        self.band = band_rows(H, world, rank)
+        rows = self.band[1] - self.band[0]
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
-        self.band = (rank * rows, (rank + 1) * rows)
         self.dev = torch.device("cuda", device_index)
         self.color = torch.empty(rows * W, dtype=torch.int32, device=self.dev)
         self.depth = torch.empty(rows * W, dtype=torch.float32, device=self.dev)
@@ -62,10 +91,7 @@ class BandRenderer:
         self.r.set_frame(s.ubo, s.clear)  # per-frame uniform update
         self.r.set_draws(s.draws)         # per-frame draw list (push constants)
         self.r.render()
-        if self.world > 1:
-            import torch.distributed as dist
-
-            dist.all_gather_into_tensor(self.frame, self.color)
+        gather_bands(self.frame, self.color, self.world)
 
 
 def timed_run(br, steps, warmup, dist_on):
@@ -91,11 +117,7 @@ def timed_run(br, steps, warmup, dist_on):
     br.r.synchronize()  # surfaces TRI_E_OVERFLOW if any timed frame overflowed
     timing = br.r.timing()
     br.r.set_timing(False)
-    if dist_on:
-        t = torch.tensor([dt], dtype=torch.float64, device=br.dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-    return dt, timing
+    return max_over_ranks(dt, br.dev, dist_on), timing
 
 
 def cpu_baseline(scene, seconds):
