@@ -4,10 +4,10 @@
 //                          Trident Vertex that reach the output; Vertex.h:9-78)
 //   VsSkin    32 B/vertex  {bone indices, bone weights}, only when any draw has BoneCount > 0
 //   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation
+//   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, z_ndc, 1/w}
 //   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
-//   TriRec    64 B/record  snapped screen vertices, NDC z, 1/w, (prim<<3|sub), 3 vary slots
-//   brange     8 B/record  (bx0|by0<<16, bx1|by1<<16) in 64x64-pixel bins
-//   bin_list   4 B/entry   record ids per bin (order-free: visibility is resolved by a 64-bit key)
+//   bin_list   4 B/entry   primitive ids per bin (order-free: visibility is resolved by a 64-bit key)
+//   TriRec    64 B/record  clipped sub-triangles only: snapped vertices, z, 1/w, prim<<3|sub, slots
 //   colour     4 B/pixel   B8G8R8A8_UNORM;  depth 4 B/pixel D32_SFLOAT bits
 #pragma once
 
@@ -18,10 +18,8 @@
 #define TRI_BIN (1 << TRI_BIN_LOG2)
 #define TRI_BLOCK 256
 #define TRI_PRIM_MAX ((1u << 29) - 1u)
-#define TRI_REC_CULLED 0xFFFFFFFFu
-#define TRI_REC_CLIPPED 0xFFFFFFFEu
-#define TRI_BR_CULLED 0xFFFFFFFFu
-#define TRI_BR_CLIPPED 0xFFFFFFFEu
+// bin-queue entry: a primitive id, or TRI_ENTRY_CLIPPED | index of a clipped sub-triangle's record
+#define TRI_ENTRY_CLIPPED 0x80000000u
 #define TRI_MAX_CLIP_VERTS 12
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f
@@ -69,9 +67,11 @@ struct __attribute__((aligned(16))) TriRec {
     int32_t Y[3];
     float z[3];
     float iw[3];
-    uint32_t prim_sub;  // prim << 3 | sub; TRI_REC_CULLED; TRI_REC_CLIPPED (v[0] = first sub-record)
+    uint32_t prim_sub;  // prim << 3 | sub (sub = fan index of a clipped sub-triangle)
     uint32_t v[3];      // vary slots (post orientation swap)
 };
+// A set-up triangle. Unclipped triangles are rebuilt in registers from their snapped vertices
+// wherever they are needed; only clipped sub-triangles are stored (TriDeviceBuffers::recs).
 static_assert(sizeof(TriRec) == 64, "TriRec must be one 64-byte line");
 
 // Per-draw vertex-stage constants (push constant + hoisted normal matrix).

@@ -3,8 +3,8 @@
 //   k_vertex   vs_transform   Default.vert:60-105, one lane per (draw, referenced vertex)
 //   k_setup    tri_setup_bin  primitive assembly + trivial reject + cull + bbox on the per-vertex
 //                             snapped coordinates (Pipeline.cpp:611-643), binned into per-bin queues
-//                             (LDS histogram, one global atomic per touched (chunk, bin)); triangles
-//                             that need homogeneous clipping are queued for k_clip
+//                             (wave-aggregated atomics: one per (wave, bin)); nothing else is stored
+//                             per triangle. Triangles that need homogeneous clipping go to k_clip
 //   k_clip     rare path: Sutherland-Hodgman against w>=WMIN, z>=0 and the guard band + fan
 //   k_raster   tile_raster_shade: one workgroup per 32x32 (or 64x64) bin; coverage + early-Z in LDS
 //              with 64-bit (depth, primitive-order) keys (== in-order LESS_OR_EQUAL,
@@ -216,92 +216,106 @@ __device__ __forceinline__ void note_bin_overflow(const TriDeviceBuffers& b, uin
     atomicMax(&b.counters->bin_max, needed);
 }
 
-// One workgroup bins a chunk of TRI_BLOCK * ppt consecutive primitives: setup per primitive, an LDS
-// histogram over the bins they touch (plus a list of touched bins), ONE global atomicAdd per touched
-// bin to reserve a contiguous range of that bin's queue, then the queue writes. Entry order inside a
-// bin is free: k_raster resolves visibility with (depth, primitive order) keys.
+// Wave-aggregated queue reservation: every lane with `want` gets one slot in bin `bin`. Lanes of the
+// wave that target the same bin form a group; each group's leader issues ONE atomicAdd for the whole
+// group (all leaders at once, one round trip), and members take consecutive slots after it. Must be
+// reached by the whole wave (uniform control flow).
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+__device__ __forceinline__ uint32_t wave_reserve(uint32_t* counts, uint32_t bin, bool want) {
+    uint64_t pending = __ballot(want);
+    const uint32_t lane = lanes_below(~0ull);
+    uint32_t leader = lane, rank = 0, cnt = 0;
+    while (pending) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(pending);
+        const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)l);
+        const uint64_t grp = __ballot(want && bin == lb) & pending;
+        if (want && bin == lb) {
+            leader = l;
+            rank = lanes_below(grp);
+        }
+        if (lane == l) cnt = (uint32_t)__builtin_popcountll(grp);
+        pending &= ~grp;
+    }
+    uint32_t base = 0;
+    if (want && lane == leader) base = atomicAdd(&counts[bin], cnt);
+    base = (uint32_t)__shfl((int)base, (int)leader);
+    return base + rank;
+}
+
+// One lane per primitive (ppt primitives per lane): assembly from the snapped vertices, trivial
+// reject, cull, bbox, then one bin-queue entry per touched bin via wave_reserve. Nothing else is
+// written for a visible triangle: k_raster rebuilds it from `snap`. Triangles needing homogeneous
+// clipping go to the clip queue for k_clip. Entry order inside a bin is free: k_raster resolves
+// visibility with (depth, primitive order) keys.
 __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
-    extern __shared__ uint32_t lds[];
-    uint32_t* hist = lds;                                           // nbins counters -> queue cursors
-    uint16_t* touched = reinterpret_cast<uint16_t*>(lds + fp.nbins);  // bins touched by this chunk
-    __shared__ uint32_t red[4];
-    for (int i = threadIdx.x; i < fp.nbins; i += TRI_BLOCK) hist[i] = 0;
-    if (threadIdx.x == 0) { red[0] = 0; red[1] = 0; red[2] = 0; red[3] = 0; }
+    __shared__ uint32_t red[3];
+    if (threadIdx.x < 3) red[threadIdx.x] = 0;
     __syncthreads();
-    uint32_t nsetup = 0, nclip = 0;
+    uint32_t nsetup = 0, nclip = 0, nentries = 0;
+    const uint32_t cap = fp.bin_cap;
     const uint32_t chunk0 = blockIdx.x * (uint32_t)(TRI_BLOCK * fp.ppt);
-    uint2 brk[TRI_MAX_PPT];
-#pragma unroll
-    for (int k = 0; k < TRI_MAX_PPT; ++k) {
-        brk[k] = make_uint2(TRI_BR_CULLED, 0u);
+    for (int k = 0; k < fp.ppt; ++k) {  // uniform trip count: wave_reserve needs the whole wave
         const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
-        if (k >= fp.ppt || p >= fp.nprims) continue;
-        const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
-        const TriDrawDev& dr = b.draws[d];
-        const uint32_t t = p - b.draw_pbase[d];
-        const uint32_t* ip = b.indices + dr.first_index + 3ull * t;
-        const uint32_t vb = b.draw_vbase[d] - dr.min_index;
-        const uint32_t sl0 = vb + ip[0], sl1 = vb + ip[1], sl2 = vb + ip[2];
-        const TriSnap a0 = b.snap[sl0], a1 = b.snap[sl1], a2 = b.snap[sl2];
-        const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
-        TriRec r;
-        uint2 br = make_uint2(TRI_BR_CULLED, 0u);
         bool ok = false;
-        // invalid vertex, or trivial reject: all three vertices outside one clip half-space
-        if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
-            if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
-                ++nclip;
-                const uint32_t q = atomicAdd(&b.counters->clip_queue, 1u);
-                if (q < fp.ovf_rec_cap) b.clip_queue[q] = p;
-                else atomicOr(&b.counters->flags, TRI_OVF_CLIP_QUEUE);
-            } else {
-                const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
-                const int32_t Y[3] = {a0.y, a1.y, a2.y};
-                const float z[3] = {a0.z, a1.z, a2.z};
-                const float iw[3] = {a0.iw, a1.iw, a2.iw};
-                ok = setup_snapped(fp, X, Y, z, iw, sl0, sl1, sl2, p << 3, r, br);
+        uint2 br = make_uint2(0u, 0u);
+        if (p < fp.nprims) {
+            const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
+            const TriDrawDev& dr = b.draws[d];
+            const uint32_t* ip = b.indices + dr.first_index + 3ull * (p - b.draw_pbase[d]);
+            const uint32_t vb = b.draw_vbase[d] - dr.min_index;
+            const uint32_t sl0 = vb + ip[0], sl1 = vb + ip[1], sl2 = vb + ip[2];
+            const TriSnap a0 = b.snap[sl0], a1 = b.snap[sl1], a2 = b.snap[sl2];
+            const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
+            // invalid vertex, or trivial reject: all three vertices outside one clip half-space
+            if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
+                if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
+                    ++nclip;
+                    const uint32_t q = atomicAdd(&b.counters->clip_queue, 1u);
+                    if (q < fp.ovf_rec_cap) b.clip_queue[q] = p;
+                    else atomicOr(&b.counters->flags, TRI_OVF_CLIP_QUEUE);
+                } else {
+                    const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
+                    const int32_t Y[3] = {a0.y, a1.y, a2.y};
+                    const float z[3] = {a0.z, a1.z, a2.z};
+                    const float iw[3] = {a0.iw, a1.iw, a2.iw};
+                    TriRec r;
+                    ok = setup_snapped(fp, X, Y, z, iw, sl0, sl1, sl2, p << 3, r, br);
+                }
             }
         }
-        if (ok) {
-            ++nsetup;
-            brk[k] = br;
-            for_bins(br, fp.nbx, [&](uint32_t bi) {
-                if (atomicAdd(&hist[bi], 1u) == 0u) touched[atomicAdd(&red[2], 1u)] = (uint16_t)bi;
-            });
-        } else {
-            r.prim_sub = TRI_REC_CULLED;
+        nsetup += ok ? 1u : 0u;
+        uint32_t bx = br.x & 0xFFFFu, by = br.x >> 16;
+        const uint32_t bx0 = bx, bx1 = br.y & 0xFFFFu, by1 = br.y >> 16;
+        bool has = ok;
+        while (__ballot(has)) {  // one bin per lane per round
+            const uint32_t bi = by * (uint32_t)fp.nbx + bx;
+            const uint32_t pos = wave_reserve(b.bin_count, bi, has);
+            if (has) {
+                if (pos < cap) b.bin_list[(size_t)bi * cap + pos] = p;
+                else note_bin_overflow(b, pos + 1);
+                ++nentries;
+                if (bx < bx1) {
+                    ++bx;
+                } else if (by < by1) {
+                    bx = bx0;
+                    ++by;
+                } else {
+                    has = false;
+                }
+            }
         }
-        b.recs[p] = r;
     }
     if (nsetup) atomicAdd(&red[0], nsetup);
     if (nclip) atomicAdd(&red[1], nclip);
-    __syncthreads();
-    const uint32_t ntouched = red[2];
-    const uint32_t cap = fp.bin_cap;
-    uint32_t entries = 0;
-    for (uint32_t i = threadIdx.x; i < ntouched; i += TRI_BLOCK) {  // reserve queue ranges
-        const uint32_t bi = touched[i];
-        const uint32_t cnt = hist[bi];
-        const uint32_t base = atomicAdd(&b.bin_count[bi], cnt);
-        if (base + cnt > cap) note_bin_overflow(b, base + cnt);
-        hist[bi] = base;
-        entries += cnt;
-    }
-    if (entries) atomicAdd(&red[3], entries);
+    if (nentries) atomicAdd(&red[2], nentries);
     __syncthreads();
     if (threadIdx.x == 0) {
         if (red[0]) atomicAdd(&b.counters->tris_setup, red[0]);
         if (red[1]) atomicAdd(&b.counters->tris_clipped, red[1]);
-        if (red[3]) atomicAdd(&b.counters->bin_entries, red[3]);
-    }
-#pragma unroll
-    for (int k = 0; k < TRI_MAX_PPT; ++k) {  // fill the reserved ranges
-        if (brk[k].x == TRI_BR_CULLED) continue;
-        const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
-        for_bins(brk[k], fp.nbx, [&](uint32_t bi) {
-            const uint32_t pos = atomicAdd(&hist[bi], 1u);
-            if (pos < cap) b.bin_list[(size_t)bi * cap + pos] = p;
-        });
+        if (red[2]) atomicAdd(&b.counters->bin_entries, red[2]);
     }
 }
 
@@ -369,8 +383,6 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDevice
             cur ^= 1;
         }
         const ClipVert* src = buf[cur];
-        TriRec main{};
-        main.prim_sub = TRI_REC_CULLED;
         if (n >= 3) {
             const uint32_t nsub = (uint32_t)(n - 2);
             const uint32_t rbase = atomicAdd(&b.counters->ovf_records, nsub);
@@ -393,32 +405,26 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDevice
                                             (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, (s.b0 * x.w + s.b1 * y.w) + s.b2 * z.w);
                     }
                 }
-                const uint32_t first = fp.nprims + rbase;
+                b.clip_slot[prim] = rbase;  // k_raster's fragment fetch finds sub-triangle `sub` here
                 for (int k = 1; k + 1 < n; ++k) {
                     TriRec r;
-                    uint2 br = make_uint2(TRI_BR_CULLED, 0u);
+                    uint2 br;
                     const uint32_t ps = (prim << 3) | (uint32_t)(k - 1);
+                    const uint32_t rid = rbase + k - 1;
                     if (setup_from_clip(fp, src[0].c, src[k].c, src[k + 1].c, sbase, sbase + k, sbase + k + 1, ps, r,
                                         br)) {
                         ++nsetup;
-                        const uint32_t rid = first + k - 1;
+                        b.recs[rid] = r;
                         for_bins(br, fp.nbx, [&](uint32_t bi) {  // rare path: one global atomic per entry
                             const uint32_t pos = atomicAdd(&b.bin_count[bi], 1u);
-                            if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = rid;
+                            if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = TRI_ENTRY_CLIPPED | rid;
                             else note_bin_overflow(b, pos + 1);
                             ++nentries;
                         });
-                    } else {
-                        r.prim_sub = TRI_REC_CULLED;
                     }
-                    b.recs[first + k - 1] = r;
                 }
-                main.prim_sub = TRI_REC_CLIPPED;
-                main.v[0] = first;
-                main.v[1] = nsub;
             }
         }
-        b.recs[prim] = main;
     }
     if (nsetup) atomicAdd(&b.counters->tris_setup, nsetup);
     if (nentries) atomicAdd(&b.counters->bin_entries, nentries);
@@ -470,6 +476,41 @@ __device__ __forceinline__ TriRec load_rec(const TriRec* recs, uint32_t i) {
     uint4* o = reinterpret_cast<uint4*>(&r);
     o[0] = q0; o[1] = q1; o[2] = q2; o[3] = q3;
     return r;
+}
+
+// Vertex slots of primitive p (and its draw): the same assembly k_setup performed.
+__device__ __forceinline__ int prim_slots(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t p,
+                                          uint32_t sl[3]) {
+    const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
+    const TriDrawDev& dr = b.draws[d];
+    const uint32_t* ip = b.indices + dr.first_index + 3ull * (p - b.draw_pbase[d]);
+    const uint32_t vb = b.draw_vbase[d] - dr.min_index;
+    sl[0] = vb + ip[0];
+    sl[1] = vb + ip[1];
+    sl[2] = vb + ip[2];
+    return d;
+}
+
+// The record setup_snapped produced for an unclipped primitive (v1 <-> v2 swapped), rebuilt from
+// its snapped vertices instead of being stored and re-read.
+__device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3], const TriSnap& a0,
+                                                 const TriSnap& a1, const TriSnap& a2) {
+    TriRec r;
+    r.X[0] = (a0.xo << 8) >> 8; r.X[1] = (a2.xo << 8) >> 8; r.X[2] = (a1.xo << 8) >> 8;
+    r.Y[0] = a0.y; r.Y[1] = a2.y; r.Y[2] = a1.y;
+    r.z[0] = a0.z; r.z[1] = a2.z; r.z[2] = a1.z;
+    r.iw[0] = a0.iw; r.iw[1] = a2.iw; r.iw[2] = a1.iw;
+    r.v[0] = sl[0]; r.v[1] = sl[2]; r.v[2] = sl[1];
+    r.prim_sub = p << 3;
+    return r;
+}
+
+// A bin-queue entry -> its triangle.
+__device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
+    if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
+    uint32_t sl[3];
+    prim_slots(fp, b, e, sl);
+    return rec_from_snaps(e, sl, b.snap[sl[0]], b.snap[sl[1]], b.snap[sl[2]]);
 }
 
 // Fragment depth at pixel centre: plane through the snapped vertices, fixed evaluation order.
@@ -755,8 +796,12 @@ __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const T
                                                int32_t px, int32_t py, const float* lut, Frag& f) {
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
-    TriRec r = load_rec(b.recs, prim);
-    if (r.prim_sub == TRI_REC_CLIPPED) r = load_rec(b.recs, r.v[0] + (low & 7u));
+    uint32_t sl[3];
+    const int d = prim_slots(fp, b, prim, sl);
+    const TriSnap s0 = b.snap[sl[0]], s1 = b.snap[sl[1]], s2 = b.snap[sl[2]];
+    const TriRec r = ((((uint32_t)(s0.xo | s1.xo | s2.xo)) >> 24) & TRI_OC_CLIP)
+                         ? load_rec(b.recs, b.clip_slot[prim] + (low & 7u))
+                         : rec_from_snaps(prim, sl, s0, s1, s2);
     float l0, l1, l2;
     if (EXACT) {  // exact int64 edge functions (oracle order)
         const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
@@ -803,7 +848,6 @@ __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const T
     f.u = ip(a0.w, b0.w, c0.w);
     f.v = ip(a1.w, b1.w, c1.w);
     f.vcol = mk(ip(a2.x, b2.x, c2.x), ip(a2.y, b2.y, c2.y), ip(a2.z, b2.z, c2.z));
-    const int d = find_range(b.draw_pbase, (int)fp.ndraws, prim);
     const TriDrawShade ds = b.draw_shade[d];
     f.tint = make_float4(ds.tint[0], ds.tint[1], ds.tint[2], ds.tint[3]);
     f.s = sample_tex(b.textures[ds.tex_id], f.u, f.v, lut);
@@ -846,7 +890,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
     uint32_t s0 = 0, s1 = nentries;
     if (fp.ablate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
-            const TriRec r = load_rec(b.recs, queue[0]);
+            const TriRec r = load_entry(fp, b, queue[0]);
             const uint64_t key = (0x3F000000ull << 32) | key_low(r.prim_sub);
             for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = key;
         }
@@ -854,7 +898,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
     }
     for (uint32_t i = s0 + tid; i < s1; i += TRI_BLOCK) {
         const uint32_t ri = queue[i];
-        const TriRec r = load_rec(b.recs, ri);
+        const TriRec r = load_entry(fp, b, ri);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
@@ -867,7 +911,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
     __syncthreads();
     const uint32_t nb = min(nbig, (uint32_t)kBigQueue);
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        const TriRec r = load_rec(b.recs, bigq[q]);
+        const TriRec r = load_entry(fp, b, bigq[q]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         EdgeSetup e;
@@ -923,11 +967,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
 
 }  // namespace
 
-hipError_t tri_kernels_init() {
-    const int lds_max = 16384 * (int)(sizeof(uint32_t) + sizeof(uint16_t));
-    return hipFuncSetAttribute(reinterpret_cast<const void*>(&k_setup),
-                               hipFuncAttributeMaxDynamicSharedMemorySize, lds_max);
-}
+hipError_t tri_kernels_init() { return hipSuccess; }
 
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* ev) {
@@ -946,10 +986,7 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
     else
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
     rec(kStageSetup);
-    const size_t lds_bytes = (size_t)fp.nbins * (sizeof(uint32_t) + sizeof(uint16_t));
-    if (fp.nchunks > 0)
-        hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), (lds_bytes + 15) & ~(size_t)15, stream, fp,
-                           b);
+    if (fp.nchunks > 0) hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
     rec(kStageClip);
     if (fp.nchunks > 0) hipLaunchKernelGGL(k_clip, dim3(TRI_CLIP_GRID), dim3(TRI_BLOCK), 0, stream, fp, b);
     rec(kStageRaster);

@@ -19,8 +19,8 @@ struct TriDeviceBuffers {
     float4* clip;                // nslots (read only by k_clip)
     TriSnap* snap;               // nslots
     float4* vary;                // 3 * (nslots + ovf_vert_cap)
-    TriRec* recs;                // nprims + ovf_rec_cap
-    uint2* brange;               // nprims + ovf_rec_cap
+    TriRec* recs;                // ovf_rec_cap clipped sub-triangles
+    uint32_t* clip_slot;         // nprims: first sub-triangle record of a clipped primitive
     uint32_t* clip_queue;        // ovf_rec_cap primitive ids needing geometric clipping
     uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
     uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)
@@ -31,7 +31,6 @@ struct TriDeviceBuffers {
 
 enum TriStage { kStageVertex = 0, kStageSetup, kStageClip, kStageRaster, kStageCount };
 
-// Raise the dynamic-LDS limit of the binning kernel (up to 16384 bins x 6 B).
 hipError_t tri_kernels_init();
 
 // One frame = 4 dependent launches on `stream`; `events` (may be null) gets kStageCount+1 stamps:

@@ -113,6 +113,7 @@ struct tri_ctx {
     int32_t bin_log2 = 6;
     float4* d_vary = nullptr; size_t cap_vary = 0;
     TriRec* d_recs = nullptr; size_t cap_recs = 0;
+    uint32_t* d_clip_slot = nullptr; size_t cap_clip_slot = 0;
     uint32_t* d_bin_count = nullptr; size_t cap_bin_count = 0;
     uint32_t* d_bin_list = nullptr; size_t cap_bin_list = 0;
     TriCounters* d_ctr = nullptr;
@@ -298,7 +299,7 @@ int resolve_draws(tri_ctx* c) {
 
 int ensure_work_buffers(tri_ctx* c) {
     int rc;
-    const size_t nrec = (size_t)c->nprims + c->ovf_rec_cap;
+    const size_t nrec = c->ovf_rec_cap;
     const size_t nvary = 3ull * ((size_t)c->nslots + c->ovf_vert_cap);
     // per-bin queue capacity: ~8x the mean entries per bin (1.3 bins per triangle), >= 256,
     // grown from the observed maximum after an overflow (check_overflow)
@@ -308,12 +309,14 @@ int ensure_work_buffers(tri_ctx* c) {
     const size_t nlist = (size_t)c->nbins * c->bin_cap;
     if (nlist * 4 > (8ull << 30)) return fail(TRI_E_OOM, "bin queues would need %zu MB", nlist * 4 >> 20);
     bool realloc = c->cap_clip < std::max<size_t>(c->nslots, 1) || c->cap_vary < nvary || c->cap_recs < nrec ||
+                   c->cap_clip_slot < std::max<size_t>(c->nprims, 1) ||
                    c->cap_bin_list < nlist;
     if (realloc) HIP_TRY(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_clip, c->cap_clip, std::max<size_t>(c->nslots, 1)))) return rc;
     if ((rc = grow(c->d_snap, c->cap_snap, std::max<size_t>(c->nslots, 1)))) return rc;
     if ((rc = grow(c->d_vary, c->cap_vary, nvary))) return rc;
     if ((rc = grow(c->d_recs, c->cap_recs, nrec))) return rc;
+    if ((rc = grow(c->d_clip_slot, c->cap_clip_slot, std::max<size_t>(c->nprims, 1)))) return rc;
     if ((rc = grow(c->d_clip_queue, c->cap_clip_queue, c->ovf_rec_cap))) return rc;
     if ((rc = grow(c->d_bin_list, c->cap_bin_list, nlist))) return rc;
     return TRI_OK;
@@ -439,7 +442,7 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_clip_queue); f(c->d_vbase); f(c->d_pbase);
-    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs);
+    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -605,7 +608,7 @@ int tri_render(tri_ctx* c) {
     fp.W = c->W; fp.H = c->H; fp.y0 = c->y0; fp.y1 = c->y1;
     fp.nbx = c->nbx; fp.nby = c->nby; fp.nbins = c->nbins;
     fp.bin_log2 = c->bin_log2;
-    const uint32_t target_chunks = 1024;  // >= 4 binning workgroups per CU
+    const uint32_t target_chunks = 4096;  // >= 16 binning workgroups per CU
     uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
     ppt = std::min<uint32_t>(std::max<uint32_t>(ppt, 1), TRI_MAX_PPT);
     fp.ppt = (int32_t)ppt;
@@ -651,6 +654,7 @@ int tri_render(tri_ctx* c) {
     b.snap = c->d_snap;
     b.vary = c->d_vary;
     b.recs = c->d_recs;
+    b.clip_slot = c->d_clip_slot;
     b.bin_count = c->d_bin_count;
     b.bin_list = c->d_bin_list;
     b.counters = c->d_ctr;
