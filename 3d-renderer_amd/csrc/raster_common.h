@@ -124,6 +124,8 @@ struct TriShadeConst {
     float sun_rad[4];     // DirectionalLightColor.rgb * .w
     float pl_pos[TRI_MAX_POINT_LIGHTS][4];  // xyz, 1/max(radius, 1e-4)
     float pl_rad[TRI_MAX_POINT_LIGHTS][4];  // ColorIntensity.rgb * .w
+    // roughness terms of the fast BRDF: a2 - 1, a2 / pi, Schlick-GGX k and 1 - k (a = roughness^2)
+    float a2m1, a2pi, kg, omkg;
 };
 
 struct TriFrameParams {
@@ -131,7 +133,8 @@ struct TriFrameParams {
     int32_t nbx, nby, nbins, ppt;
     int32_t bin_log2;
     uint32_t ablate;  // diagnostics only (TRI_ABLATE env): 1 = skip shading, 2 = skip coverage
-    int32_t pad_b1, pad_b2;
+    uint32_t chunk_stride;  // k_setup visits chunks in the order (blockIdx * stride) mod nchunks
+    int32_t pad_b2;
     float hw, hh, gx, gy;
     uint32_t nprims, nslots, ndraws, nchunks;
     uint32_t ovf_rec_cap, ovf_vert_cap, bin_cap, bone_count;

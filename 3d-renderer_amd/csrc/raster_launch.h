@@ -15,7 +15,7 @@ struct TriDeviceBuffers {
     const uint32_t* draw_vbase;  // ndraws+1
     const uint32_t* draw_pbase;  // ndraws+1
     const TriTexDesc* textures;  // TRI_MAX_TEXTURE_SLOTS entries, aliases resolved
-    const float* srgb_lut;       // 256 entries, sRGB -> linear (computed on the host in double)
+    const float* srgb_lut;       // 256 sRGB -> linear (host, double) + 256 alpha b/255
     float4* clip;                // nslots (read only by k_clip)
     TriSnap* snap;               // nslots
     float4* vary;                // 3 * (nslots + ovf_vert_cap)
@@ -25,6 +25,7 @@ struct TriDeviceBuffers {
     uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
     uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)
     TriCounters* counters;
+    uint2* setup_stats;          // nchunks {triangles set up, bin entries} per k_setup workgroup
     uint32_t* color;             // band rows * W
     float* depth;                // band rows * W (may be null)
 };

@@ -114,6 +114,8 @@ struct tri_ctx {
     float4* d_vary = nullptr; size_t cap_vary = 0;
     TriRec* d_recs = nullptr; size_t cap_recs = 0;
     uint32_t* d_clip_slot = nullptr; size_t cap_clip_slot = 0;
+    uint2* d_setup_stats = nullptr; size_t cap_setup_stats = 0;
+    uint32_t last_nchunks = 0;
     uint32_t* d_bin_count = nullptr; size_t cap_bin_count = 0;
     uint32_t* d_bin_list = nullptr; size_t cap_bin_list = 0;
     TriCounters* d_ctr = nullptr;
@@ -170,6 +172,11 @@ void shade_constants(const tri_global_ubo& g, const tri_material_record& m, TriS
     sc.metallic = clamp01(m.material_factors[0]);
     sc.roughness = std::fmin(std::fmax(m.material_factors[1], 0.045f), 1.0f);
     sc.amb_strength = clamp01(m.material_factors[2]);
+    const float a = sc.roughness * sc.roughness, a2 = a * a, rr = sc.roughness + 1.0f;
+    sc.a2m1 = a2 - 1.0f;
+    sc.a2pi = a2 / 3.14159265359f;
+    sc.kg = rr * rr * 0.125f;
+    sc.omkg = 1.0f - sc.kg;
     for (int i = 0; i < 3; ++i) sc.amb[i] = g.ambient_color_intensity[i] * g.ambient_color_intensity[3];
     sc.has_sun = g.light_counts[0] > 0u ? 1u : 0u;
     const float lx = -g.directional_light_direction[0], ly = -g.directional_light_direction[1],
@@ -297,6 +304,20 @@ int resolve_draws(tri_ctx* c) {
     return TRI_OK;
 }
 
+// A stride near nchunks / golden ratio, coprime to nchunks (TRI_SETUP_STRIDE=1 restores linear order).
+uint32_t chunk_stride(uint32_t n) {
+    static const long env = [] {
+        const char* e = getenv("TRI_SETUP_STRIDE");
+        return e ? atol(e) : 0L;
+    }();
+    if (n <= 2) return 1;
+    if (env > 0) return (uint32_t)env % n ? (uint32_t)env % n : 1u;
+    uint32_t s = (uint32_t)((double)n * 0.6180339887) | 1u;
+    auto gcd = [](uint32_t a, uint32_t b) { while (b) { const uint32_t t = a % b; a = b; b = t; } return a; };
+    while (gcd(s, n) != 1) ++s;
+    return s % n ? s % n : 1u;
+}
+
 int ensure_work_buffers(tri_ctx* c) {
     int rc;
     const size_t nrec = c->ovf_rec_cap;
@@ -317,6 +338,7 @@ int ensure_work_buffers(tri_ctx* c) {
     if ((rc = grow(c->d_vary, c->cap_vary, nvary))) return rc;
     if ((rc = grow(c->d_recs, c->cap_recs, nrec))) return rc;
     if ((rc = grow(c->d_clip_slot, c->cap_clip_slot, std::max<size_t>(c->nprims, 1)))) return rc;
+    if ((rc = grow(c->d_setup_stats, c->cap_setup_stats, (size_t)c->nprims / TRI_BLOCK + 1))) return rc;
     if ((rc = grow(c->d_clip_queue, c->cap_clip_queue, c->ovf_rec_cap))) return rc;
     if ((rc = grow(c->d_bin_list, c->cap_bin_list, nlist))) return rc;
     return TRI_OK;
@@ -411,17 +433,18 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
     if (hipMalloc(&c->d_color_own, px * 4) != hipSuccess || hipMalloc(&c->d_depth_own, px * 4) != hipSuccess ||
         hipMalloc(&c->d_ctr, sizeof(TriCounters)) != hipSuccess ||
         hipMalloc(&c->d_texdesc, sizeof(TriTexDesc) * TRI_MAX_TEXTURE_SLOTS) != hipSuccess ||
-        hipMalloc(&c->d_lut, 256 * sizeof(float)) != hipSuccess)
+        hipMalloc(&c->d_lut, 512 * sizeof(float)) != hipSuccess)
         return bail(fail(TRI_E_OOM, "tri_create: target allocation failed"));
     c->d_color = c->d_color_own;
     c->d_depth = c->d_depth_own;
     if ((rc = grow(c->d_bin_count, c->cap_bin_count, (size_t)c->nbins))) return bail(rc);
     if (hipMemset(c->d_bin_count, 0, c->nbins * 4) != hipSuccess || hipMemset(c->d_ctr, 0, sizeof(TriCounters)) != hipSuccess)
         return bail(fail(TRI_E_HIP, "tri_create: memset failed"));
-    float lut[256];
+    float lut[512];
     for (int i = 0; i < 256; ++i) {  // R8G8B8A8_SRGB decode (sRGB EOTF), evaluated in double
         const double v = i / 255.0;
         lut[i] = (float)(v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4));
+        lut[256 + i] = (float)i / 255.0f;  // alpha: linear UNORM decode (IEEE float division)
     }
     if (hipMemcpy(c->d_lut, lut, sizeof lut, hipMemcpyHostToDevice) != hipSuccess)
         return bail(fail(TRI_E_HIP, "tri_create: LUT upload failed"));
@@ -442,7 +465,7 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_clip_queue); f(c->d_vbase); f(c->d_pbase);
-    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot);
+    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -613,6 +636,8 @@ int tri_render(tri_ctx* c) {
     ppt = std::min<uint32_t>(std::max<uint32_t>(ppt, 1), TRI_MAX_PPT);
     fp.ppt = (int32_t)ppt;
     fp.nchunks = (c->nprims + ppt * TRI_BLOCK - 1) / (ppt * TRI_BLOCK);
+    fp.chunk_stride = chunk_stride(fp.nchunks);
+    c->last_nchunks = fp.nchunks;
     fp.hw = (float)c->W * 0.5f;
     fp.hh = (float)c->H * 0.5f;
     fp.gx = (2.0f * TRI_GUARD_BAND_PX) / (float)c->W - 1.0f;
@@ -655,6 +680,7 @@ int tri_render(tri_ctx* c) {
     b.vary = c->d_vary;
     b.recs = c->d_recs;
     b.clip_slot = c->d_clip_slot;
+    b.setup_stats = c->d_setup_stats;
     b.bin_count = c->d_bin_count;
     b.bin_list = c->d_bin_list;
     b.counters = c->d_ctr;
@@ -725,9 +751,16 @@ int tri_get_frame_stats(tri_ctx* c, tri_frame_stats* out) {
     HIP_TRY(hipMemcpy(&h, c->d_ctr, sizeof h, hipMemcpyDeviceToHost));
     std::memset(out, 0, sizeof *out);
     out->triangles_in = c->nprims;
-    out->triangles_setup = h.tris_setup;
-    out->triangles_clipped = h.tris_clipped;
-    out->bin_entries = h.bin_entries;
+    std::vector<uint2> ws(c->last_nchunks);
+    if (!ws.empty()) HIP_TRY(hipMemcpy(ws.data(), c->d_setup_stats, ws.size() * sizeof(uint2), hipMemcpyDeviceToHost));
+    uint64_t setup = h.tris_setup, entries = h.bin_entries;  // k_clip's share
+    for (const uint2& w : ws) {
+        setup += w.x;
+        entries += w.y;
+    }
+    out->triangles_setup = setup;
+    out->triangles_clipped = h.clip_queue;
+    out->bin_entries = entries;
     out->vertices_shaded = c->nslots;
     out->bins_x = (uint32_t)c->nbx;
     out->bins_y = (uint32_t)c->nby;
