@@ -484,10 +484,14 @@ __device__ __forceinline__ int32_t clamp_edge(int64_t f, bool& reject) {
 
 __device__ __forceinline__ TriRec load_rec(const TriRec* recs, uint32_t i) {
     const uint4* p = reinterpret_cast<const uint4*>(recs + i);
-    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];
+    const uint4 q0 = p[0], q1 = p[1], q2 = p[2], q3 = p[3];  // field by field: stays in registers
     TriRec r;
-    uint4* o = reinterpret_cast<uint4*>(&r);
-    o[0] = q0; o[1] = q1; o[2] = q2; o[3] = q3;
+    r.X[0] = (int32_t)q0.x; r.X[1] = (int32_t)q0.y; r.X[2] = (int32_t)q0.z;
+    r.Y[0] = (int32_t)q0.w; r.Y[1] = (int32_t)q1.x; r.Y[2] = (int32_t)q1.y;
+    r.z[0] = __uint_as_float(q1.z); r.z[1] = __uint_as_float(q1.w); r.z[2] = __uint_as_float(q2.x);
+    r.iw[0] = __uint_as_float(q2.y); r.iw[1] = __uint_as_float(q2.z); r.iw[2] = __uint_as_float(q2.w);
+    r.prim_sub = q3.x;
+    r.v[0] = q3.y; r.v[1] = q3.z; r.v[2] = q3.w;
     return r;
 }
 
@@ -649,12 +653,23 @@ __device__ __forceinline__ uint32_t unorm8(float c) {
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
 }
 
-struct Frag {
-    f3 world, nrm, vcol;
-    float u, v;
-    float4 s;     // sampled texel (linear)
-    float4 tint;
+struct __attribute__((aligned(16))) V4 {
+    float x, y, z, w;
 };
+
+struct Frag {  // flat scalars: nested f3 members are ABI-coerced and defeat SROA in the pair path
+    float wx, wy, wz;  // world position
+    float nx, ny, nz;  // interpolated normal
+    float cx, cy, cz;  // vertex colour
+    float u, v;
+    float sx, sy, sz, sw;  // sampled texel (linear rgb, alpha)
+    float tx, ty, tz, tw;  // draw tint
+};
+__device__ __forceinline__ f3 fworld(const Frag& f) { return mk(f.wx, f.wy, f.wz); }
+__device__ __forceinline__ f3 fnrm(const Frag& f) { return mk(f.nx, f.ny, f.nz); }
+__device__ __forceinline__ f3 fvcol(const Frag& f) { return mk(f.cx, f.cy, f.cz); }
+__device__ __forceinline__ f3 ftex(const Frag& f) { return mk(f.sx, f.sy, f.sz); }
+__device__ __forceinline__ f3 ftint(const Frag& f) { return mk(f.tx, f.ty, f.tz); }
 
 // ---- EXACT build: Default.frag with IEEE div/sqrt/powf in the oracle's operation order ----------
 __device__ __forceinline__ float schlick_ggx(float NdotV, float roughness) {
@@ -689,12 +704,12 @@ __device__ __forceinline__ f3 eval_pbr_exact(f3 L, f3 rad, f3 N, f3 V, f3 albedo
 __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag& f) {
     const tri_global_ubo& g = fp.ubo;
     const tri_material_record& mat = fp.mat0;
-    const f3 N = norm3(norm3(f.nrm));
-    const f3 V = norm3(sub3(mk(g.camera_position[0], g.camera_position[1], g.camera_position[2]), f.world));
-    const f3 albedo = mul(mul(mul(mk(f.s.x, f.s.y, f.s.z), mk(mat.base_color_factor[0], mat.base_color_factor[1],
+    const f3 N = norm3(norm3(fnrm(f)));
+    const f3 V = norm3(sub3(mk(g.camera_position[0], g.camera_position[1], g.camera_position[2]), fworld(f)));
+    const f3 albedo = mul(mul(mul(ftex(f), mk(mat.base_color_factor[0], mat.base_color_factor[1],
                                                                mat.base_color_factor[2])),
-                              mk(f.tint.x, f.tint.y, f.tint.z)),
-                          f.vcol);
+                              ftint(f)),
+                          fvcol(f));
     const float metallic = sat(mat.material_factors[0]);
     const float roughness = fminf(fmaxf(mat.material_factors[1], 0.045f), 1.0f);
     const float amb_s = sat(mat.material_factors[2]);
@@ -711,7 +726,7 @@ __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag&
     const uint32_t np = min(g.light_counts[1], 8u);
     for (uint32_t i = 0; i < np; ++i) {
         const tri_point_light& pl = g.point_lights[i];
-        const f3 to = sub3(mk(pl.position_range[0], pl.position_range[1], pl.position_range[2]), f.world);
+        const f3 to = sub3(mk(pl.position_range[0], pl.position_range[1], pl.position_range[2]), fworld(f));
         const float dist = sqrtf(dot3(to, to));
         if (dist <= 1e-4f) continue;
         const f3 L = mk(to.x / dist, to.y / dist, to.z / dist);
@@ -733,7 +748,7 @@ __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag&
     col = mk(col.x / (col.x + 1.0f), col.y / (col.y + 1.0f), col.z / (col.z + 1.0f));
     const float gamma = 1.0f / 2.2f;
     col = mk(powf(col.x, gamma), powf(col.y, gamma), powf(col.z, gamma));
-    const float alpha = (mat.base_color_factor[3] * f.tint.w) * f.s.w;
+    const float alpha = (mat.base_color_factor[3] * f.tw) * f.sw;
     return make_float4(col.x, col.y, col.z, alpha);
 }
 
@@ -745,6 +760,7 @@ struct PbrPix {
 };
 
 __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const PbrPix& px, f3 L, f3 rad, f3& c) {
+#pragma clang fp contract(fast)  // fast build only: FMA contraction is inside the 1-LSB budget
     const f3 Hu = add(px.V, L);
     const float ih = frsq(fdot(Hu, Hu));
     const float NdotH = fmaxf(fdot(px.N, Hu) * ih, 0.0f);
@@ -767,12 +783,13 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
 }
 
 __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f) {
+#pragma clang fp contract(fast)
     PbrPix px;
-    px.N = fnorm(f.nrm);
-    px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), f.world));
-    const f3 albedo = mul(mul(mul(mk(f.s.x, f.s.y, f.s.z), mk(sc.base[0], sc.base[1], sc.base[2])),
-                              mk(f.tint.x, f.tint.y, f.tint.z)),
-                          f.vcol);
+    px.N = fnorm(fnrm(f));
+    px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), fworld(f)));
+    const f3 albedo = mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])),
+                              ftint(f)),
+                          fvcol(f));
     const float m = sc.metallic;
     const float om = 0.04f * (1.0f - m);
     px.F0 = mk(__builtin_fmaf(albedo.x, m, om), __builtin_fmaf(albedo.y, m, om), __builtin_fmaf(albedo.z, m, om));
@@ -787,7 +804,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         eval_pbr_fast(sc, px, mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]),
                       mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), c);
     for (uint32_t i = 0; i < sc.npt; ++i) {
-        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), f.world);
+        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), fworld(f));
         const float d2 = fdot(to, to);
         if (d2 <= 1e-8f) continue;  // dist <= 1e-4
         const float inv = frsq(d2);
@@ -798,21 +815,32 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     }
     const float g = 1.0f / 2.2f;
     const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
-    return make_float4(fpow(t.x, g), fpow(t.y, g), fpow(t.z, g), (sc.base[3] * f.tint.w) * f.s.w);
+    return make_float4(fpow(t.x, g), fpow(t.y, g), fpow(t.z, g), (sc.base[3] * f.tw) * f.sw);
+}
+
+__device__ __forceinline__ float interp_exact(float w0, float w1, float w2, float x0, float x1, float x2) {
+    return (w0 * x0 + w1 * x1) + w2 * x2;  // the oracle's order, no contraction
+}
+__device__ __forceinline__ float interp_fast(float w0, float w1, float w2, float x0, float x1, float x2) {
+    return __builtin_fmaf(w2, x2, __builtin_fmaf(w1, x1, w0 * x0));
 }
 
 // Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
-template <bool EXACT>
-__device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                               int32_t px, int32_t py, const float* lut, Frag& f) {
+// Writes the fragment through `put(field_index, value)` (fields in Frag order), so one body serves
+// the single-pixel Frag and the lane-pair FragP without an intermediate in scratch memory.
+template <bool EXACT, typename Put>
+__device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
+                                                  int32_t px, int32_t py, const float* lut, Put&& put) {
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
     uint32_t sl[3];
     const int d = prim_slots(fp, b, prim, sl);
     const TriSnap s0 = b.snap[sl[0]], s1 = b.snap[sl[1]], s2 = b.snap[sl[2]];
-    const TriRec r = ((((uint32_t)(s0.xo | s1.xo | s2.xo)) >> 24) & TRI_OC_CLIP)
-                         ? load_rec(b.recs, b.clip_slot[prim] + (low & 7u))
-                         : rec_from_snaps(prim, sl, s0, s1, s2);
+    TriRec r;
+    if ((((uint32_t)(s0.xo | s1.xo | s2.xo)) >> 24) & TRI_OC_CLIP)
+        r = load_rec(b.recs, b.clip_slot[prim] + (low & 7u));
+    else
+        r = rec_from_snaps(prim, sl, s0, s1, s2);
     float l0, l1, l2;
     if (EXACT) {  // exact int64 edge functions (oracle order)
         const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
@@ -847,21 +875,33 @@ __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const T
         const float iq = frcp(qs);
         w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
     }
-    const float4* va = b.vary + 3ull * r.v[0];
-    const float4* vb = b.vary + 3ull * r.v[1];
-    const float4* vc = b.vary + 3ull * r.v[2];
-    auto ip = [&](float x0, float x1, float x2) { return (w0 * x0 + w1 * x1) + w2 * x2; };
-    const float4 a0 = va[0], a1 = va[1], a2 = va[2];
-    const float4 b0 = vb[0], b1 = vb[1], b2 = vb[2];
-    const float4 c0 = vc[0], c1 = vc[1], c2 = vc[2];
-    f.world = mk(ip(a0.x, b0.x, c0.x), ip(a0.y, b0.y, c0.y), ip(a0.z, b0.z, c0.z));
-    f.nrm = mk(ip(a1.x, b1.x, c1.x), ip(a1.y, b1.y, c1.y), ip(a1.z, b1.z, c1.z));
-    f.u = ip(a0.w, b0.w, c0.w);
-    f.v = ip(a1.w, b1.w, c1.w);
-    f.vcol = mk(ip(a2.x, b2.x, c2.x), ip(a2.y, b2.y, c2.y), ip(a2.z, b2.z, c2.z));
+    // plain-float views of the varyings (HIP vector unions defeat SROA in the pixel-pair path)
+    const V4* va = reinterpret_cast<const V4*>(b.vary + 3ull * r.v[0]);
+    const V4* vb = reinterpret_cast<const V4*>(b.vary + 3ull * r.v[1]);
+    const V4* vc = reinterpret_cast<const V4*>(b.vary + 3ull * r.v[2]);
+    auto ip = [&](float x0, float x1, float x2) {
+        return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
+    };
+    const V4 a0 = va[0], a1 = va[1], a2 = va[2];
+    const V4 b0 = vb[0], b1 = vb[1], b2 = vb[2];
+    const V4 c0 = vc[0], c1 = vc[1], c2 = vc[2];
+    // field-wise stores (a struct-valued f3 store is ABI-coerced to <2 x float> + float, which
+    // keeps the pixel-pair path's fragments from being promoted to registers)
+    put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
+    put(3, ip(a1.x, b1.x, c1.x)); put(4, ip(a1.y, b1.y, c1.y)); put(5, ip(a1.z, b1.z, c1.z));
+    put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
+    const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
+    put(9, u); put(10, v);
     const TriDrawShade ds = b.draw_shade[d];
-    f.tint = make_float4(ds.tint[0], ds.tint[1], ds.tint[2], ds.tint[3]);
-    f.s = sample_tex(b.textures[ds.tex_id], f.u, f.v, lut);
+    const float4 tx = sample_tex(b.textures[ds.tex_id], u, v, lut);
+    put(11, tx.x); put(12, tx.y); put(13, tx.z); put(14, tx.w);
+    put(15, ds.tint[0]); put(16, ds.tint[1]); put(17, ds.tint[2]); put(18, ds.tint[3]);
+}
+
+template <bool EXACT>
+__device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
+                                               int32_t px, int32_t py, const float* lut, Frag& f) {
+    fetch_fragment_to<EXACT>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
 }
 
 constexpr int kBigArea = 96;  // bbox∩bin pixels above which a triangle is rasterized cooperatively

@@ -180,18 +180,20 @@ def test_first_frame_lazy_primitive_drops_earlier_draws(app_mod):
     assert [d.mesh_index for d in second] == [0, 1, 2]
 
 
-def test_draw_frame_records_timing_without_device(app_mod):
-    import conftest
-
-    if conftest.gpu_available():
-        pytest.skip("host-only behaviour")
+def test_draw_frame_records_frame_timing(app_mod):
+    """GetFrameTimingStats after DrawFrame (Renderer.cpp:6286-6343). Without a device the viewport
+    target cannot be created: the frame is skipped (logged), timing is still recorded and there is
+    nothing to read back."""
     a, _ = c1_app(app_mod)
     for _ in range(3):
-        a.draw_frame()  # no device: the viewport target cannot be created, the frame is skipped
+        a.draw_frame()
     t = a.frame_timing()
-    assert t["samples"] == 3 and t["avg_ms"] >= 0.0
-    with pytest.raises(Exception):
-        a.read_pixels(1, W, H)
+    assert t["samples"] == 3 and t["avg_ms"] >= 0.0 and t["min_ms"] <= t["avg_ms"] <= t["max_ms"]
+    try:
+        rgba, _ = a.read_pixels(1, W, H)
+    except Exception:
+        return  # no device
+    assert rgba.shape == (H, W, 4)
 
 
 # ---------------------------------------------------------------------------------------------
