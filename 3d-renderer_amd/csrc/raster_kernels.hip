@@ -124,7 +124,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
         sn.y = Y;
     }
     b.snap[slot] = sn;
-    float4* vo = b.vary + 3ull * slot;
+    float4* vo = b.vary + 3u * slot;
     vo[0] = make_float4(world.x, world.y, world.z, u);
     vo[1] = make_float4(nnx, nny, nnz, v);
     vo[2] = make_float4(in.cr, in.cg, in.cb, 0.0f);
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
         if (p < fp.nprims) {
             const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
             const TriDrawDev& dr = b.draws[d];
-            const uint32_t* ip = b.indices + dr.first_index + 3ull * (p - b.draw_pbase[d]);
+            const uint32_t* ip = b.indices + dr.first_index + 3u * (p - b.draw_pbase[d]);
             const uint32_t vb = b.draw_vbase[d] - dr.min_index;
             const uint32_t sl0 = vb + ip[0], sl1 = vb + ip[1], sl2 = vb + ip[2];
             const TriSnap a0 = b.snap[sl0], a1 = b.snap[sl1], a2 = b.snap[sl2];
@@ -366,7 +366,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDevice
         const uint32_t prim = b.clip_queue[q];
         const int d = find_range(b.draw_pbase, (int)fp.ndraws, prim);
         const TriDrawDev& dr = b.draws[d];
-        const uint32_t* ip = b.indices + dr.first_index + 3ull * (prim - b.draw_pbase[d]);
+        const uint32_t* ip = b.indices + dr.first_index + 3u * (prim - b.draw_pbase[d]);
         const uint32_t vb = b.draw_vbase[d] - dr.min_index;
         uint32_t srcv[3];
         // polygon vertex = clip position (lerped exactly like the oracle: depth stays bit-exact) +
@@ -405,11 +405,11 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDevice
                          (rbase + nsub > fp.ovf_rec_cap) ? TRI_OVF_CLIP_RECORDS : TRI_OVF_CLIP_VERTS);
             } else {
                 const uint32_t sbase = fp.nslots + vbase;
-                const float4* v0 = b.vary + 3ull * srcv[0];
-                const float4* v1 = b.vary + 3ull * srcv[1];
-                const float4* v2 = b.vary + 3ull * srcv[2];
+                const float4* v0 = b.vary + 3u * srcv[0];
+                const float4* v1 = b.vary + 3u * srcv[1];
+                const float4* v2 = b.vary + 3u * srcv[2];
                 for (int k = 0; k < n; ++k) {
-                    float4* vo = b.vary + 3ull * (sbase + k);
+                    float4* vo = b.vary + 3u * (sbase + k);
                     const ClipVert& s = src[k];
 #pragma unroll
                     for (int j = 0; j < 3; ++j) {
@@ -500,7 +500,7 @@ __device__ __forceinline__ int prim_slots(const TriFrameParams& fp, const TriDev
                                           uint32_t sl[3]) {
     const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
     const TriDrawDev& dr = b.draws[d];
-    const uint32_t* ip = b.indices + dr.first_index + 3ull * (p - b.draw_pbase[d]);
+    const uint32_t* ip = b.indices + dr.first_index + 3u * (p - b.draw_pbase[d]);
     const uint32_t vb = b.draw_vbase[d] - dr.min_index;
     sl[0] = vb + ip[0];
     sl[1] = vb + ip[1];
@@ -630,8 +630,8 @@ __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, floa
     const float a = u - fu, bb = v - fv;
     const uint32_t x0 = wrap_repeat(fu, t.w), y0 = wrap_repeat(fv, t.h);
     const uint32_t x1 = (x0 + 1 == t.w) ? 0u : x0 + 1, y1 = (y0 + 1 == t.h) ? 0u : y0 + 1;
-    const uint32_t p00 = t.texels[(uint64_t)y0 * t.w + x0], p10 = t.texels[(uint64_t)y0 * t.w + x1];
-    const uint32_t p01 = t.texels[(uint64_t)y1 * t.w + x0], p11 = t.texels[(uint64_t)y1 * t.w + x1];
+    const uint32_t p00 = t.texels[y0 * t.w + x0], p10 = t.texels[y0 * t.w + x1];
+    const uint32_t p01 = t.texels[y1 * t.w + x0], p11 = t.texels[y1 * t.w + x1];
     float4 r;
     float* rp = &r.x;
 #pragma unroll
@@ -753,33 +753,35 @@ __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag&
 }
 
 // ---- fast build: same algebra, frame constants hoisted, hardware transcendental approximations ---
-// Per light: one v_rsq (half vector) and ONE v_rcp for NDF * G_L / (4 NdotV NdotL) together.
+// Per light: one v_rsq (half vector) and ONE v_rcp for NDF * G_L / (4 NdotV NdotL) together. For unit
+// V and L, |V + L|^2 = 2 + 2 L.V, N.H = (N.V + N.L) / |V + L| and H.V = (1 + L.V) / |V + L|.
 struct PbrPix {
     f3 N, V, F0, omF0, diffK;
-    float NdotV4, gV;
+    float NdotVr, NdotV4, gV;  // NdotVr: unclamped N.V
 };
 
-__device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const PbrPix& px, f3 L, f3 rad, f3& c) {
+__device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const PbrPix& px, f3 L, f3 rad, float scale,
+                                              f3& c) {
 #pragma clang fp contract(fast)  // fast build only: FMA contraction is inside the 1-LSB budget
-    const f3 Hu = add(px.V, L);
-    const float ih = frsq(fdot(Hu, Hu));
-    const float NdotH = fmaxf(fdot(px.N, Hu) * ih, 0.0f);
-    const float HdotV = fmaxf(fdot(Hu, px.V) * ih, 0.0f);
-    const float NdotL = fmaxf(fdot(px.N, L), 0.0f);
+    const float LdotV = fdot(L, px.V);
+    const float NdotLr = fdot(px.N, L);
+    const float ih = frsq(fmaxf(__builtin_fmaf(2.0f, LdotV, 2.0f), 1e-30f));
+    const float NdotH = fmaxf((px.NdotVr + NdotLr) * ih, 0.0f);
+    const float HdotV = fmaxf(__builtin_fmaf(LdotV, ih, ih), 0.0f);
+    const float NdotL = fmaxf(NdotLr, 0.0f);
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
     const float gden = fmaxf(__builtin_fmaf(NdotL, sc.omkg, sc.kg), 1e-4f);
     const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
     // NDF * G_L * G_V / den with NDF = a2 / (pi dd^2), G_L = NdotL / gden
-    const float s = (sc.a2pi * NdotL) * px.gV * frcp(((dd * dd) * gden) * den);
+    const float sp = (sc.a2pi * NdotL) * px.gV * frcp(((dd * dd) * gden) * den);
     const float q = fmaxf(1.0f - HdotV, 0.0f);
     const float q2 = q * q;
     const float p5 = q2 * q2 * q;
-    const f3 F = mk(__builtin_fmaf(px.omF0.x, p5, px.F0.x), __builtin_fmaf(px.omF0.y, p5, px.F0.y),
-                    __builtin_fmaf(px.omF0.z, p5, px.F0.z));
-    const f3 rw = muls(rad, NdotL);
-    c.x = __builtin_fmaf(__builtin_fmaf(-px.diffK.x, F.x, __builtin_fmaf(F.x, s, px.diffK.x)), rw.x, c.x);
-    c.y = __builtin_fmaf(__builtin_fmaf(-px.diffK.y, F.y, __builtin_fmaf(F.y, s, px.diffK.y)), rw.y, c.y);
-    c.z = __builtin_fmaf(__builtin_fmaf(-px.diffK.z, F.z, __builtin_fmaf(F.z, s, px.diffK.z)), rw.z, c.z);
+    const float w = NdotL * scale;
+    // (kD albedo / pi + F s) = diffK + F (s - diffK), F = F0 + (1 - F0) p5
+    c.x = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(px.omF0.x, p5, px.F0.x), sp - px.diffK.x, px.diffK.x), rad.x * w, c.x);
+    c.y = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(px.omF0.y, p5, px.F0.y), sp - px.diffK.y, px.diffK.y), rad.y * w, c.y);
+    c.z = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(px.omF0.z, p5, px.F0.z), sp - px.diffK.z, px.diffK.z), rad.z * w, c.z);
 }
 
 __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f) {
@@ -787,31 +789,29 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     PbrPix px;
     px.N = fnorm(fnrm(f));
     px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), fworld(f)));
-    const f3 albedo = mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])),
-                              ftint(f)),
-                          fvcol(f));
+    const f3 albedo = mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])), ftint(f)), fvcol(f));
     const float m = sc.metallic;
     const float om = 0.04f * (1.0f - m);
     px.F0 = mk(__builtin_fmaf(albedo.x, m, om), __builtin_fmaf(albedo.y, m, om), __builtin_fmaf(albedo.z, m, om));
     px.omF0 = mk(1.0f - px.F0.x, 1.0f - px.F0.y, 1.0f - px.F0.z);
     px.diffK = muls(albedo, (1.0f - m) * (1.0f / kPi));
-    const float NdotV = fmaxf(fdot(px.N, px.V), 0.0f);
+    px.NdotVr = fdot(px.N, px.V);
+    const float NdotV = fmaxf(px.NdotVr, 0.0f);
     px.NdotV4 = 4.0f * NdotV;
     px.gV = NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
     f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
               sc.amb[2] * albedo.z * sc.amb_strength);
     if (sc.has_sun)
         eval_pbr_fast(sc, px, mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]),
-                      mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), c);
+                      mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), 1.0f, c);
+    const f3 wp = fworld(f);
     for (uint32_t i = 0; i < sc.npt; ++i) {
-        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), fworld(f));
+        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
         const float d2 = fdot(to, to);
         if (d2 <= 1e-8f) continue;  // dist <= 1e-4
         const float inv = frsq(d2);
         const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
-        const float att = att0 * att0;
-        eval_pbr_fast(sc, px, muls(to, inv), mk(sc.pl_rad[i][0] * att, sc.pl_rad[i][1] * att, sc.pl_rad[i][2] * att),
-                      c);
+        eval_pbr_fast(sc, px, muls(to, inv), mk(sc.pl_rad[i][0], sc.pl_rad[i][1], sc.pl_rad[i][2]), att0 * att0, c);
     }
     const float g = 1.0f / 2.2f;
     const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
@@ -876,9 +876,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
     }
     // plain-float views of the varyings (HIP vector unions defeat SROA in the pixel-pair path)
-    const V4* va = reinterpret_cast<const V4*>(b.vary + 3ull * r.v[0]);
-    const V4* vb = reinterpret_cast<const V4*>(b.vary + 3ull * r.v[1]);
-    const V4* vc = reinterpret_cast<const V4*>(b.vary + 3ull * r.v[2]);
+    const V4* va = reinterpret_cast<const V4*>(b.vary + 3u * r.v[0]);
+    const V4* vb = reinterpret_cast<const V4*>(b.vary + 3u * r.v[1]);
+    const V4* vc = reinterpret_cast<const V4*>(b.vary + 3u * r.v[2]);
     auto ip = [&](float x0, float x1, float x2) {
         return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
     };

@@ -128,6 +128,7 @@ struct tri_ctx {
     float* d_depth = nullptr;
 
     bool timing = false;
+    uint32_t timing_period = 1, timing_counter = 0;  // time every timing_period-th frame
     std::vector<TimingSet> pending;
     std::vector<TimingSet> free_sets;
     tri_timing acc{};
@@ -329,6 +330,8 @@ int ensure_work_buffers(tri_ctx* c) {
     c->bin_cap = std::max<uint32_t>(c->bin_cap, 256u);
     const size_t nlist = (size_t)c->nbins * c->bin_cap;
     if (nlist * 4 > (8ull << 30)) return fail(TRI_E_OOM, "bin queues would need %zu MB", nlist * 4 >> 20);
+    if (nvary >= (1ull << 32))  // the kernels index varyings / indices with 32-bit arithmetic
+        return fail(TRI_E_INVALID, "too many vertex invocations (%zu varyings)", nvary);
     bool realloc = c->cap_clip < std::max<size_t>(c->nslots, 1) || c->cap_vary < nvary || c->cap_recs < nrec ||
                    c->cap_clip_slot < std::max<size_t>(c->nprims, 1) ||
                    c->cap_bin_list < nlist;
@@ -689,7 +692,8 @@ int tri_render(tri_ctx* c) {
 
     hipEvent_t* ev = nullptr;
     TimingSet ts{};
-    if (c->timing) {
+    const bool timed = c->timing && (c->timing_counter++ % c->timing_period) == 0;
+    if (timed) {
         if (!c->free_sets.empty()) {
             ts = c->free_sets.back();
             c->free_sets.pop_back();
@@ -699,7 +703,7 @@ int tri_render(tri_ctx* c) {
         ev = ts.ev;
     }
     HIP_TRY(tri_launch_frame(fp, b, c->stream, ev));
-    if (c->timing) c->pending.push_back(ts);
+    if (timed) c->pending.push_back(ts);
     return TRI_OK;
 }
 
@@ -729,7 +733,10 @@ int tri_set_timing(tri_ctx* c, int enable) {
     if (!c) return fail(TRI_E_INVALID, "tri_set_timing: null context");
     int rc = collect_timing(c);
     if (rc) return rc;
+    if (enable < 0) return fail(TRI_E_INVALID, "tri_set_timing: negative period %d", enable);
     c->timing = enable != 0;
+    c->timing_period = enable > 0 ? (uint32_t)enable : 1u;
+    c->timing_counter = 0;
     c->acc = tri_timing{};
     return TRI_OK;
 }

@@ -23,11 +23,13 @@ class TriError(RuntimeError):
         self.code = code
 
 
-def load_library(path=LIB_PATH):
-    """Load the HIP rasterizer library (built by `make -C 3d-renderer_amd`)."""
+def load_library(path=None):
+    """Load the HIP rasterizer library (built by `make -C 3d-renderer_amd`). TRI_RASTER_LIB may name
+    another in-tree build of the same library (kernel-variant experiments)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("TRI_RASTER_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise ImportError(f"HIP rasterizer library not built: {path} (run __graft_entry__.build())")
     lib = C.CDLL(path)
@@ -149,8 +151,9 @@ class TriRaster:
                 if e.code != abi.TRI_E_OVERFLOW or attempt == retries:
                     raise
 
-    def set_timing(self, enable):
-        _check(_lib.tri_set_timing(self._ctx, 1 if enable else 0))
+    def set_timing(self, enable, period=1):
+        """Per-stage HIP-event timing of every `period`-th frame (enable=False: off)."""
+        _check(_lib.tri_set_timing(self._ctx, int(period) if enable else 0))
 
     def timing(self):
         t = abi.TriTiming()

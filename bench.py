@@ -94,7 +94,7 @@ class BandRenderer:
         gather_bands(self.frame, self.color, self.world)
 
 
-def timed_run(br, steps, warmup, dist_on):
+def timed_run(br, steps, warmup, dist_on, stage_timing=True, period=8):
     import torch
 
     br.r.render_frame()  # first frame sizes the internal queues (re-renders after TRI_E_OVERFLOW)
@@ -106,7 +106,8 @@ def timed_run(br, steps, warmup, dist_on):
         import torch.distributed as dist
 
         dist.barrier()
-    br.r.set_timing(True)
+    # per-kernel HIP events on every `period`-th timed frame (events on every frame cost ~9% fps)
+    br.r.set_timing(stage_timing, period)
     t0 = time.perf_counter()
     for _ in range(steps):
         br.step()
@@ -161,6 +162,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--no-stage-timing", action="store_true",
+                    help="diagnostics: no per-kernel HIP events in the timed loop (roofline fields become null)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -179,7 +182,7 @@ def main():
 
     scene = build_scene(args.config)
     br = BandRenderer(scene, rank, world, local)
-    dt, timing = timed_run(br, args.steps, args.warmup, dist_on)
+    dt, timing = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing)
     fps = args.steps / dt
     W, H = scene.width, scene.height
     stats = br.r.frame_stats()
@@ -190,7 +193,7 @@ def main():
     raster_ms = timing["ms_raster"] / frames_timed
     frame_ms = timing["ms_frame"] / frames_timed
     raster_bytes = 8.0 * W * br.rows
-    achieved = raster_bytes / (raster_ms * 1e-3) / 1e9
+    achieved = raster_bytes / (raster_ms * 1e-3) / 1e9 if raster_ms > 0 else None
     frame_bytes = scene.algorithmic_bytes(rows=br.rows)
     traffic = pmc_traffic(scene.name, br.rows / H)
 
@@ -228,11 +231,12 @@ def main():
                        "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "single GPU"},
             "mpix_per_s": fps * W * H / 1e6,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": "k_raster",
+                         "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                         "kernel": "k_raster",
                          "kernel_ms": raster_ms, "algorithmic_bytes": raster_bytes},
             "frame_roofline": {"algorithmic_bytes": frame_bytes, "gpu_ms": frame_ms,
-                               "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9,
-                               "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS},
+                               "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9 if frame_ms > 0 else None,
+                               "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if frame_ms > 0 else None},
             "stage_ms": {k: timing[k] / frames_timed for k in
                          ("ms_vertex", "ms_setup", "ms_clip", "ms_raster", "ms_frame")},
             "frame_stats": stats,

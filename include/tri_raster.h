@@ -206,7 +206,9 @@ int tri_synchronize(tri_ctx* ctx);
 int tri_readback(tri_ctx* ctx, uint8_t* bgra8, uint32_t* depth_bits);
 
 /* ---- measurement -------------------------------------------------------------------------- */
-int tri_set_timing(tri_ctx* ctx, int enable);      /* also resets the accumulators       */
+/* enable = N > 0: HIP events around every stage of every N-th frame (1 = all frames; sampling keeps
+ * the event overhead out of throughput runs); 0 = off. Also resets the accumulators. */
+int tri_set_timing(tri_ctx* ctx, int enable);
 int tri_get_timing(tri_ctx* ctx, tri_timing* out); /* synchronizes                      */
 int tri_get_frame_stats(tri_ctx* ctx, tri_frame_stats* out); /* synchronizes           */
 
