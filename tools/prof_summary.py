@@ -7,15 +7,20 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
 from collections import defaultdict
 
 
 def short(name):
-    for k in ("k_raster<false>", "k_raster<true>", "k_setup", "k_scatter", "k_vertex", "k_clip", "k_binscan",
-              "copyBuffer", "fillBuffer"):
+    """Kernel name without namespace / parameter list: k_raster<false, 5> -> k_raster (the fast
+    build, the one the bench runs), k_raster<true, 5> -> k_raster_exact."""
+    m = re.search(r"(k_[a-z_]+)(<([a-z]+)[^>]*>)?\(", name)
+    if m:
+        return m.group(1) + ("_exact" if m.group(3) == "true" else "")
+    for k in ("copyBuffer", "fillBuffer"):
         if k in name:
-            return k.replace("<false>", "").replace("<true>", "_exact")
+            return k
     return name[:40]
 
 
