@@ -141,8 +141,11 @@ struct TriFrameParams {
     uint32_t clear_bgra;
     uint32_t write_depth;
     uint32_t exact_shading;
-    uint32_t pad0;
+    uint32_t sky_size;  // skybox face size (0 = no skybox pass)
     float pv[16];
+    float sky_ip[16];   // inverse(Projection) (double on the host, rounded)
+    float sky_R[9];     // mat3(View)
+    float sky_pw[4];    // Projection row 3
     tri_global_ubo ubo;
     tri_material_record mat0;
     TriShadeConst sc;

@@ -904,6 +904,121 @@ __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const T
     fetch_fragment_to<EXACT>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
 }
 
+// ------------------------------------------------------------------------------------------
+// skybox pass (Skybox.cpp:13-79, Skybox.vert:30-41, Skybox.frag:28-35, cull FRONT / depth LEQUAL
+// without writes, recorded before the meshes, Renderer.cpp:5076-5082). Same arithmetic as the
+// oracle's sky_pixel(): a background pixel's interpolated direction is the view-space point where
+// its ray leaves the 20-unit cube; Vulkan cube sampling with seamless LINEAR filtering.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int cube_face(f3 d, float& s, float& t) {
+    const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+    int face;
+    float ma, sc, tc;
+    if (ax >= ay && ax >= az) {
+        face = d.x >= 0.0f ? 0 : 1; ma = ax; sc = d.x >= 0.0f ? -d.z : d.z; tc = -d.y;
+    } else if (ay >= az) {
+        face = d.y >= 0.0f ? 2 : 3; ma = ay; sc = d.x; tc = d.y >= 0.0f ? d.z : -d.z;
+    } else {
+        face = d.z >= 0.0f ? 4 : 5; ma = az; sc = d.z >= 0.0f ? d.x : -d.x; tc = -d.y;
+    }
+    if (!(ma > 0.0f)) { s = 0.5f; t = 0.5f; return face; }
+    s = 0.5f * (sc / ma) + 0.5f;
+    t = 0.5f * (tc / ma) + 0.5f;
+    return face;
+}
+
+__device__ __forceinline__ f3 face_dir(int face, float sc, float tc) {
+    switch (face) {
+        case 0: return mk(1.0f, -tc, -sc);
+        case 1: return mk(-1.0f, -tc, sc);
+        case 2: return mk(sc, 1.0f, tc);
+        case 3: return mk(sc, -1.0f, -tc);
+        case 4: return mk(sc, -tc, 1.0f);
+        default: return mk(-sc, -tc, -1.0f);
+    }
+}
+
+struct SkyTex {
+    const uint32_t* t;
+    int32_t n;
+    const float* lut;
+    __device__ __forceinline__ f3 texel(int face, int32_t i, int32_t j) const {
+        const uint32_t p = t[((uint32_t)face * (uint32_t)n + (uint32_t)j) * (uint32_t)n + (uint32_t)i];
+        return mk(lut[p & 0xFFu], lut[(p >> 8) & 0xFFu], lut[(p >> 16) & 0xFFu]);
+    }
+    __device__ __forceinline__ f3 across(int face, int32_t i, int32_t j) const {
+        const float sc = 2.0f * (((float)i + 0.5f) / (float)n) - 1.0f;
+        const float tc = 2.0f * (((float)j + 0.5f) / (float)n) - 1.0f;
+        float s, tt;
+        const int f2 = cube_face(face_dir(face, sc, tc), s, tt);
+        const int32_t i2 = min(max((int32_t)floorf(s * (float)n), 0), n - 1);
+        const int32_t j2 = min(max((int32_t)floorf(tt * (float)n), 0), n - 1);
+        return texel(f2, i2, j2);
+    }
+    __device__ __forceinline__ f3 fetch(int face, int32_t i, int32_t j) const {
+        const bool in_i = i >= 0 && i < n, in_j = j >= 0 && j < n;
+        if (in_i && in_j) return texel(face, i, j);
+        if (in_i || in_j) return across(face, i, j);
+        const int32_t ci = min(max(i, 0), n - 1), cj = min(max(j, 0), n - 1);
+        const f3 a = texel(face, ci, cj), b = across(face, i, cj), c = across(face, ci, j);
+        return mk(((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f);
+    }
+    __device__ __forceinline__ f3 sample(f3 d) const {
+        float s, tt;
+        const int face = cube_face(d, s, tt);
+        const float u = s * (float)n - 0.5f, v = tt * (float)n - 0.5f;
+        const float fu = floorf(u), fv = floorf(v);
+        const float a = u - fu, bb = v - fv;
+        const int32_t i0 = (int32_t)fu, j0 = (int32_t)fv;
+        const f3 t00 = fetch(face, i0, j0), t10 = fetch(face, i0 + 1, j0);
+        const f3 t01 = fetch(face, i0, j0 + 1), t11 = fetch(face, i0 + 1, j0 + 1);
+        auto lp = [](float x, float y, float w) { return x + w * (y - x); };
+        return mk(lp(lp(t00.x, t10.x, a), lp(t01.x, t11.x, a), bb), lp(lp(t00.y, t10.y, a), lp(t01.y, t11.y, a), bb),
+                  lp(lp(t00.z, t10.z, a), lp(t01.z, t11.z, a), bb));
+    }
+};
+
+// BGRA8 sky colour of pixel (px, py), or the clear colour where the skybox does not cover it.
+__device__ __noinline__ uint32_t sky_bgra(const TriFrameParams& fp, const TriDeviceBuffers& b, int32_t px, int32_t py,
+                                          const float* lut) {
+    const float xn = (float)(2 * px + 1) / (float)fp.W - 1.0f;
+    const float yn = (float)(2 * py + 1) / (float)fp.H - 1.0f;
+    const float* m = fp.sky_ip;
+    auto unproject = [&](float zn) {
+        const float x = ((m[0] * xn + m[4] * yn) + m[8] * zn) + m[12];
+        const float y = ((m[1] * xn + m[5] * yn) + m[9] * zn) + m[13];
+        const float z = ((m[2] * xn + m[6] * yn) + m[10] * zn) + m[14];
+        const float w = ((m[3] * xn + m[7] * yn) + m[11] * zn) + m[15];
+        return mk(x / w, y / w, z / w);
+    };
+    const f3 o = unproject(0.0f), o1 = unproject(1.0f);
+    const f3 r = sub3(o1, o);
+    const float* R = fp.sky_R;
+    const float oa[3] = {(R[0] * o.x + R[1] * o.y) + R[2] * o.z, (R[3] * o.x + R[4] * o.y) + R[5] * o.z,
+                         (R[6] * o.x + R[7] * o.y) + R[8] * o.z};
+    const float ra[3] = {(R[0] * r.x + R[1] * r.y) + R[2] * r.z, (R[3] * r.x + R[4] * r.y) + R[5] * r.z,
+                         (R[6] * r.x + R[7] * r.y) + R[8] * r.z};
+    const float half = 20.0f;
+    float t_in = -INFINITY, t_out = INFINITY;
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        if (ra[a] != 0.0f) {
+            const float t0 = (-half - oa[a]) / ra[a], t1 = (half - oa[a]) / ra[a];
+            t_in = fmaxf(t_in, fminf(t0, t1));
+            t_out = fminf(t_out, fmaxf(t0, t1));
+        } else if (oa[a] < -half || oa[a] > half) {
+            return fp.clear_bgra;
+        }
+    }
+    if (!(t_out >= t_in)) return fp.clear_bgra;
+    const f3 h = mk(o.x + r.x * t_out, o.y + r.y * t_out, o.z + r.z * t_out);
+    const float w = ((fp.sky_pw[0] * h.x + fp.sky_pw[1] * h.y) + fp.sky_pw[2] * h.z) + fp.sky_pw[3];
+    if (!(w > 0.0f)) return fp.clear_bgra;
+    const SkyTex sky{b.sky, (int32_t)fp.sky_size, lut};
+    const f3 c = sky.sample(norm3(h));
+    return unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (255u << 24);
+}
+
 constexpr int kBigArea = 96;  // bbox∩bin pixels above which a triangle is rasterized cooperatively
 constexpr int kBigQueue = 1024;
 
@@ -998,7 +1113,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
         uint32_t out;
         float z;
         if (key == kBgKey) {
-            out = fp.clear_bgra;
+            out = fp.sky_size ? sky_bgra(fp, b, px, py, lut) : fp.clear_bgra;
             z = 1.0f;
         } else if (fp.ablate & 1) {  // diagnostics: coverage only
             z = __uint_as_float((uint32_t)(key >> 32));

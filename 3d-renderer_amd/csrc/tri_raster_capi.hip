@@ -86,6 +86,8 @@ struct tri_ctx {
     float* d_lut = nullptr;
 
     float* d_bones = nullptr; size_t cap_bones = 0;
+    uint32_t* d_sky = nullptr; size_t cap_sky = 0;
+    uint32_t sky_size = 0;
     uint32_t nbones = 0;
 
     // per frame
@@ -194,6 +196,35 @@ void shade_constants(const tri_global_ubo& g, const tri_material_record& m, TriS
         }
         sc.pl_pos[i][3] = 1.0f / std::fmax(pl.position_range[3], 1e-4f);
     }
+}
+
+// Skybox constants: inverse(Projection) by cofactors in double (rounded to float), mat3(View) and
+// the projection's w row (same arithmetic as the oracle's sky_constants()).
+void sky_constants(const tri_global_ubo& g, float* ip, float* R, float* pw) {
+    double a[16], inv[16];
+    for (int i = 0; i < 16; ++i) a[i] = g.projection[i];
+    inv[0] = a[5] * a[10] * a[15] - a[5] * a[11] * a[14] - a[9] * a[6] * a[15] + a[9] * a[7] * a[14] + a[13] * a[6] * a[11] - a[13] * a[7] * a[10];
+    inv[4] = -a[4] * a[10] * a[15] + a[4] * a[11] * a[14] + a[8] * a[6] * a[15] - a[8] * a[7] * a[14] - a[12] * a[6] * a[11] + a[12] * a[7] * a[10];
+    inv[8] = a[4] * a[9] * a[15] - a[4] * a[11] * a[13] - a[8] * a[5] * a[15] + a[8] * a[7] * a[13] + a[12] * a[5] * a[11] - a[12] * a[7] * a[9];
+    inv[12] = -a[4] * a[9] * a[14] + a[4] * a[10] * a[13] + a[8] * a[5] * a[14] - a[8] * a[6] * a[13] - a[12] * a[5] * a[10] + a[12] * a[6] * a[9];
+    inv[1] = -a[1] * a[10] * a[15] + a[1] * a[11] * a[14] + a[9] * a[2] * a[15] - a[9] * a[3] * a[14] - a[13] * a[2] * a[11] + a[13] * a[3] * a[10];
+    inv[5] = a[0] * a[10] * a[15] - a[0] * a[11] * a[14] - a[8] * a[2] * a[15] + a[8] * a[3] * a[14] + a[12] * a[2] * a[11] - a[12] * a[3] * a[10];
+    inv[9] = -a[0] * a[9] * a[15] + a[0] * a[11] * a[13] + a[8] * a[1] * a[15] - a[8] * a[3] * a[13] - a[12] * a[1] * a[11] + a[12] * a[3] * a[9];
+    inv[13] = a[0] * a[9] * a[14] - a[0] * a[10] * a[13] - a[8] * a[1] * a[14] + a[8] * a[2] * a[13] + a[12] * a[1] * a[10] - a[12] * a[2] * a[9];
+    inv[2] = a[1] * a[6] * a[15] - a[1] * a[7] * a[14] - a[5] * a[2] * a[15] + a[5] * a[3] * a[14] + a[13] * a[2] * a[7] - a[13] * a[3] * a[6];
+    inv[6] = -a[0] * a[6] * a[15] + a[0] * a[7] * a[14] + a[4] * a[2] * a[15] - a[4] * a[3] * a[14] - a[12] * a[2] * a[7] + a[12] * a[3] * a[6];
+    inv[10] = a[0] * a[5] * a[15] - a[0] * a[7] * a[13] - a[4] * a[1] * a[15] + a[4] * a[3] * a[13] + a[12] * a[1] * a[7] - a[12] * a[3] * a[5];
+    inv[14] = -a[0] * a[5] * a[14] + a[0] * a[6] * a[13] + a[4] * a[1] * a[14] - a[4] * a[2] * a[13] - a[12] * a[1] * a[6] + a[12] * a[2] * a[5];
+    inv[3] = -a[1] * a[6] * a[11] + a[1] * a[7] * a[10] + a[5] * a[2] * a[11] - a[5] * a[3] * a[10] - a[9] * a[2] * a[7] + a[9] * a[3] * a[6];
+    inv[7] = a[0] * a[6] * a[11] - a[0] * a[7] * a[10] - a[4] * a[2] * a[11] + a[4] * a[3] * a[10] + a[8] * a[2] * a[7] - a[8] * a[3] * a[6];
+    inv[11] = -a[0] * a[5] * a[11] + a[0] * a[7] * a[9] + a[4] * a[1] * a[11] - a[4] * a[3] * a[9] - a[8] * a[1] * a[7] + a[8] * a[3] * a[5];
+    inv[15] = a[0] * a[5] * a[10] - a[0] * a[6] * a[9] - a[4] * a[1] * a[10] + a[4] * a[2] * a[9] + a[8] * a[1] * a[6] - a[8] * a[2] * a[5];
+    const double det = a[0] * inv[0] + a[1] * inv[4] + a[2] * inv[8] + a[3] * inv[12];
+    const double id = det != 0.0 ? 1.0 / det : 0.0;
+    for (int i = 0; i < 16; ++i) ip[i] = (float)(inv[i] * id);
+    for (int col = 0; col < 3; ++col)
+        for (int r = 0; r < 3; ++r) R[col * 3 + r] = g.view[col * 4 + r];
+    for (int col = 0; col < 4; ++col) pw[col] = g.projection[col * 4 + 3];
 }
 
 // glm mat4 * mat4 (column j = ((A0*B[j][0] + A1*B[j][1]) + A2*B[j][2]) + A3*B[j][3])
@@ -465,7 +496,7 @@ int tri_destroy(tri_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones);
+    f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones); f(c->d_sky);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_clip_queue); f(c->d_vbase); f(c->d_pbase);
     f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_setup_stats);
@@ -582,6 +613,23 @@ int tri_upload_bone_palette(tri_ctx* c, const float* m, uint32_t n) {
     return TRI_OK;
 }
 
+int tri_upload_skybox(tri_ctx* c, const uint8_t* faces, uint32_t n) {
+    if (!c) return fail(TRI_E_INVALID, "tri_upload_skybox: null context");
+    if (!faces || n == 0) {
+        c->sky_size = 0;
+        return TRI_OK;
+    }
+    if (n > 16384) return fail(TRI_E_INVALID, "tri_upload_skybox: face size %u too large", n);
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    const size_t texels = 6ull * n * n;
+    if ((rc = grow(c->d_sky, c->cap_sky, texels))) return rc;
+    HIP_TRY(hipMemcpy(c->d_sky, faces, texels * 4, hipMemcpyHostToDevice));
+    c->sky_size = n;
+    return TRI_OK;
+}
+
 int tri_set_frame(tri_ctx* c, const tri_global_ubo* ubo, const float clear[4]) {
     if (!c || !ubo) return fail(TRI_E_INVALID, "tri_set_frame: null argument");
     if (ubo->ai_blend_config[3] > 0.0f && ubo->ai_blend_config[0] > 0.0f)
@@ -655,6 +703,8 @@ int tri_render(tri_ctx* c) {
     fp.clear_bgra = c->clear_bgra;
     fp.write_depth = (c->cfg.flags & TRI_FLAG_NO_DEPTH_OUTPUT) ? 0u : 1u;
     fp.exact_shading = (c->cfg.flags & TRI_FLAG_EXACT_SHADING) ? 1u : 0u;
+    fp.sky_size = c->sky_size;
+    if (c->sky_size) sky_constants(c->ubo, fp.sky_ip, fp.sky_R, fp.sky_pw);
     static const uint32_t ablate = [] {  // diagnostics only: TRI_ABLATE=1 no shading, 2 no coverage
         const char* e = getenv("TRI_ABLATE");
         return e ? (uint32_t)atoi(e) : 0u;
@@ -678,6 +728,7 @@ int tri_render(tri_ctx* c) {
     b.draw_pbase = c->d_pbase;
     b.textures = c->d_texdesc;
     b.srgb_lut = c->d_lut;
+    b.sky = c->d_sky;
     b.clip = c->d_clip;
     b.snap = c->d_snap;
     b.vary = c->d_vary;

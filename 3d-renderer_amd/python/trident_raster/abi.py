@@ -158,6 +158,7 @@ CABI_FUNCTIONS = [
     ("tri_upload_materials", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("tri_upload_texture", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_upload_bone_palette", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("tri_upload_skybox", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("tri_set_frame", C.c_int, [C.c_void_p, C.POINTER(TriGlobalUbo), C.POINTER(C.c_float * 4)]),
     ("tri_set_draws", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("tri_bind_output", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),

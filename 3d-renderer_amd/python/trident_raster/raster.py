@@ -111,6 +111,16 @@ class TriRaster:
         m = np.ascontiguousarray(mats, dtype=np.float32).reshape(-1, 16)
         _check(_lib.tri_upload_bone_palette(self._ctx, _ptr(m), m.shape[0]))
 
+    def upload_skybox(self, faces):
+        """faces: uint8 [6, n, n, 4] sRGB (+X,-X,+Y,-Y,+Z,-Z), or None to remove the skybox."""
+        if faces is None:
+            _check(_lib.tri_upload_skybox(self._ctx, None, 0))
+            return
+        f = np.ascontiguousarray(faces, dtype=np.uint8)
+        if f.ndim != 4 or f.shape[0] != 6 or f.shape[1] != f.shape[2] or f.shape[3] != 4:
+            raise ValueError("skybox faces must be uint8 [6, n, n, 4]")
+        _check(_lib.tri_upload_skybox(self._ctx, _ptr(f), f.shape[1]))
+
     # ---- frame ----
     def set_frame(self, ubo, clear=(0.005, 0.005, 0.005, 1.0)):
         cl = (C.c_float * 4)(*clear)

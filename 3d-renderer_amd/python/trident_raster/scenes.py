@@ -301,6 +301,7 @@ class Scene:
     textures: list = field(default_factory=list)  # [(slot, rgba8 HxWx4)]
     clear: tuple = (0.005, 0.005, 0.005, 1.0)
     bones: np.ndarray = None
+    skybox: np.ndarray = None  # uint8 [6, n, n, 4] sRGB cubemap (+X,-X,+Y,-Y,+Z,-Z), None = no skybox pass
 
     @property
     def triangles(self):
@@ -373,5 +374,7 @@ def load_scene(rast, scene):
         rast.upload_texture(slot, tex)
     if scene.bones is not None:
         rast.upload_bone_palette(scene.bones)
+    if scene.skybox is not None:
+        rast.upload_skybox(scene.skybox)
     rast.set_frame(scene.ubo, scene.clear)
     rast.set_draws(scene.draws)

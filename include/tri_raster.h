@@ -186,6 +186,12 @@ int tri_upload_texture(tri_ctx* ctx, uint32_t slot, const uint8_t* rgba8_srgb, u
 /* Bone palette SSBO (binding 4, PrepareBonePaletteBuffer Renderer.cpp:3168-3245):
  * column-major mat4s. */
 int tri_upload_bone_palette(tri_ctx* ctx, const float* matrices, uint32_t matrix_count);
+/* Skybox cubemap (CreateSkyboxCubemap, Renderer.cpp:3818-4110; LoadFromFaces TextureLoader.cpp:
+ * 334-830): 6 faces in Vulkan layer order +X,-X,+Y,-Y,+Z,-Z, each size x size RGBA8 sRGB texels, rows
+ * top to bottom, one mip. The skybox pass (Skybox.cpp:13-79, Skybox.vert/.frag, cull FRONT, depth
+ * LEQUAL without writes) then gives every uncovered pixel its sky colour instead of the clear colour.
+ * faces = NULL or size = 0 removes the skybox. */
+int tri_upload_skybox(tri_ctx* ctx, const uint8_t* faces_rgba8_srgb, uint32_t size);
 
 /* ---- per frame --------------------------------------------------------------------------- */
 /* UpdateUniformBuffer's vkCmdUpdateBuffer (Renderer.cpp:5958) + the colour clear value

@@ -32,6 +32,7 @@ class OracleScene(C.Structure):
         ("draws", C.c_void_p), ("draw_count", C.c_uint32), ("reserved", C.c_uint32),
         ("ubo", C.POINTER(abi.TriGlobalUbo)),
         ("clear_rgba", C.c_float * 4),
+        ("sky_faces", C.c_void_p), ("sky_size", C.c_uint32), ("sky_reserved", C.c_uint32),
     ]
 
 
@@ -187,6 +188,11 @@ def render(scene, band=None, threads=None):
     ubo = scene.ubo
     sc.ubo = C.pointer(ubo)
     sc.clear_rgba = (C.c_float * 4)(*scene.clear)
+    sky = getattr(scene, "skybox", None)
+    if sky is not None:
+        sky = np.ascontiguousarray(sky, np.uint8)  # [6, n, n, 4]
+        keep.append(sky)
+        sc.sky_faces, sc.sky_size = sky.ctypes.data, sky.shape[1]
     y0, y1 = band if band is not None else (0, scene.height)
     rows = y1 - y0
     col = np.empty((rows, scene.width, 4), np.uint8)

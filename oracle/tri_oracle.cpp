@@ -404,6 +404,168 @@ vec4 fragment_shader(const FragIn& f, const tri_push_constant& pc, const tri_glo
     return {c.x, c.y, c.z, alpha};
 }
 
+// ---- skybox pass ---------------------------------------------------------------------------------
+// Skybox.cpp:13-79 (cube of half-size 1 scaled by 20, pushed as the model matrix), Skybox.vert:30-41
+// (gl_Position = (P * mat4(mat3(View)) * world).xyww, outDirection = mat3(View) * world),
+// Skybox.frag:28-35 (texture(samplerCube, normalize(dir)).rgb, alpha 1), pipeline
+// Pipeline.cpp:727-880 (cull FRONT, depth LEQUAL, no depth write), recorded before the meshes
+// (Renderer.cpp:5076-5082). Every pixel whose ray leaves the cube in front of the camera gets the
+// sky; the interpolated direction at a pixel is the view-space exit point of that pixel's ray, which
+// is computed here analytically. Cube sampling is Vulkan's: major-axis face selection, LINEAR
+// within the face (sRGB decoded before filtering, one level), seamless edges (texels across an
+// edge come from the adjacent face; a corner texel is the mean of the three that meet there).
+struct SkyConst {
+    float ip[16];  // inverse(Projection), column-major (computed in double, rounded)
+    float R[9];    // mat3(View), column-major
+    float pw[4];   // Projection row 3 (clip w of a view-space point)
+};
+
+// 4x4 inverse by cofactors in double (column-major in/out).
+void invert4(const float* m, float* out) {
+    double a[16], inv[16];
+    for (int i = 0; i < 16; ++i) a[i] = m[i];
+    inv[0] = a[5] * a[10] * a[15] - a[5] * a[11] * a[14] - a[9] * a[6] * a[15] + a[9] * a[7] * a[14] + a[13] * a[6] * a[11] - a[13] * a[7] * a[10];
+    inv[4] = -a[4] * a[10] * a[15] + a[4] * a[11] * a[14] + a[8] * a[6] * a[15] - a[8] * a[7] * a[14] - a[12] * a[6] * a[11] + a[12] * a[7] * a[10];
+    inv[8] = a[4] * a[9] * a[15] - a[4] * a[11] * a[13] - a[8] * a[5] * a[15] + a[8] * a[7] * a[13] + a[12] * a[5] * a[11] - a[12] * a[7] * a[9];
+    inv[12] = -a[4] * a[9] * a[14] + a[4] * a[10] * a[13] + a[8] * a[5] * a[14] - a[8] * a[6] * a[13] - a[12] * a[5] * a[10] + a[12] * a[6] * a[9];
+    inv[1] = -a[1] * a[10] * a[15] + a[1] * a[11] * a[14] + a[9] * a[2] * a[15] - a[9] * a[3] * a[14] - a[13] * a[2] * a[11] + a[13] * a[3] * a[10];
+    inv[5] = a[0] * a[10] * a[15] - a[0] * a[11] * a[14] - a[8] * a[2] * a[15] + a[8] * a[3] * a[14] + a[12] * a[2] * a[11] - a[12] * a[3] * a[10];
+    inv[9] = -a[0] * a[9] * a[15] + a[0] * a[11] * a[13] + a[8] * a[1] * a[15] - a[8] * a[3] * a[13] - a[12] * a[1] * a[11] + a[12] * a[3] * a[9];
+    inv[13] = a[0] * a[9] * a[14] - a[0] * a[10] * a[13] - a[8] * a[1] * a[14] + a[8] * a[2] * a[13] + a[12] * a[1] * a[10] - a[12] * a[2] * a[9];
+    inv[2] = a[1] * a[6] * a[15] - a[1] * a[7] * a[14] - a[5] * a[2] * a[15] + a[5] * a[3] * a[14] + a[13] * a[2] * a[7] - a[13] * a[3] * a[6];
+    inv[6] = -a[0] * a[6] * a[15] + a[0] * a[7] * a[14] + a[4] * a[2] * a[15] - a[4] * a[3] * a[14] - a[12] * a[2] * a[7] + a[12] * a[3] * a[6];
+    inv[10] = a[0] * a[5] * a[15] - a[0] * a[7] * a[13] - a[4] * a[1] * a[15] + a[4] * a[3] * a[13] + a[12] * a[1] * a[7] - a[12] * a[3] * a[5];
+    inv[14] = -a[0] * a[5] * a[14] + a[0] * a[6] * a[13] + a[4] * a[1] * a[14] - a[4] * a[2] * a[13] - a[12] * a[1] * a[6] + a[12] * a[2] * a[5];
+    inv[3] = -a[1] * a[6] * a[11] + a[1] * a[7] * a[10] + a[5] * a[2] * a[11] - a[5] * a[3] * a[10] - a[9] * a[2] * a[7] + a[9] * a[3] * a[6];
+    inv[7] = a[0] * a[6] * a[11] - a[0] * a[7] * a[10] - a[4] * a[2] * a[11] + a[4] * a[3] * a[10] + a[8] * a[2] * a[7] - a[8] * a[3] * a[6];
+    inv[11] = -a[0] * a[5] * a[11] + a[0] * a[7] * a[9] + a[4] * a[1] * a[11] - a[4] * a[3] * a[9] - a[8] * a[1] * a[7] + a[8] * a[3] * a[5];
+    inv[15] = a[0] * a[5] * a[10] - a[0] * a[6] * a[9] - a[4] * a[1] * a[10] + a[4] * a[2] * a[9] + a[8] * a[1] * a[6] - a[8] * a[2] * a[5];
+    const double det = a[0] * inv[0] + a[1] * inv[4] + a[2] * inv[8] + a[3] * inv[12];
+    const double id = det != 0.0 ? 1.0 / det : 0.0;
+    for (int i = 0; i < 16; ++i) out[i] = (float)(inv[i] * id);
+}
+
+SkyConst sky_constants(const tri_global_ubo& g) {
+    SkyConst k;
+    invert4(g.projection, k.ip);
+    for (int c = 0; c < 3; ++c)
+        for (int r = 0; r < 3; ++r) k.R[c * 3 + r] = g.view[c * 4 + r];
+    for (int c = 0; c < 4; ++c) k.pw[c] = g.projection[c * 4 + 3];
+    return k;
+}
+
+// Vulkan cube face selection: face 0..5 = +X,-X,+Y,-Y,+Z,-Z; (s, t) in [0, 1] on that face.
+int cube_face(vec3 d, float& s, float& t) {
+    const float ax = std::fabs(d.x), ay = std::fabs(d.y), az = std::fabs(d.z);
+    int face;
+    float ma, sc, tc;
+    if (ax >= ay && ax >= az) {
+        face = d.x >= 0.0f ? 0 : 1; ma = ax; sc = d.x >= 0.0f ? -d.z : d.z; tc = -d.y;
+    } else if (ay >= az) {
+        face = d.y >= 0.0f ? 2 : 3; ma = ay; sc = d.x; tc = d.y >= 0.0f ? d.z : -d.z;
+    } else {
+        face = d.z >= 0.0f ? 4 : 5; ma = az; sc = d.z >= 0.0f ? d.x : -d.x; tc = -d.y;
+    }
+    if (!(ma > 0.0f)) { s = 0.5f; t = 0.5f; return face; }
+    s = 0.5f * (sc / ma) + 0.5f;
+    t = 0.5f * (tc / ma) + 0.5f;
+    return face;
+}
+
+// Direction through face-local (sc, tc) in [-1, 1]^2 (major axis component 1).
+vec3 face_dir(int face, float sc, float tc) {
+    switch (face) {
+        case 0: return {1.0f, -tc, -sc};
+        case 1: return {-1.0f, -tc, sc};
+        case 2: return {sc, 1.0f, tc};
+        case 3: return {sc, -1.0f, -tc};
+        case 4: return {sc, -tc, 1.0f};
+        default: return {-sc, -tc, -1.0f};
+    }
+}
+
+struct Sky {
+    const uint8_t* faces;
+    int32_t n;
+    vec3 texel(int face, int32_t i, int32_t j) const {  // decoded linear rgb
+        const uint8_t* p = faces + 4ull * (((uint64_t)face * n + (uint64_t)j) * n + (uint64_t)i);
+        return {g_srgb_lut[p[0]], g_srgb_lut[p[1]], g_srgb_lut[p[2]]};
+    }
+    // texel (i, j) of `face` with exactly one coordinate outside [0, n): from the adjacent face
+    vec3 across(int face, int32_t i, int32_t j) const {
+        const float sc = 2.0f * (((float)i + 0.5f) / (float)n) - 1.0f;
+        const float tc = 2.0f * (((float)j + 0.5f) / (float)n) - 1.0f;
+        float s, t;
+        const int f2 = cube_face(face_dir(face, sc, tc), s, t);
+        const int32_t i2 = std::min(std::max((int32_t)std::floor(s * (float)n), 0), n - 1);
+        const int32_t j2 = std::min(std::max((int32_t)std::floor(t * (float)n), 0), n - 1);
+        return texel(f2, i2, j2);
+    }
+    vec3 fetch(int face, int32_t i, int32_t j) const {
+        const bool in_i = i >= 0 && i < n, in_j = j >= 0 && j < n;
+        if (in_i && in_j) return texel(face, i, j);
+        if (in_i || in_j) return across(face, i, j);
+        const int32_t ci = std::min(std::max(i, 0), n - 1), cj = std::min(std::max(j, 0), n - 1);
+        const vec3 a = texel(face, ci, cj), b = across(face, i, cj), c = across(face, ci, j);
+        return {((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f};
+    }
+    vec3 sample(vec3 d) const {
+        float s, t;
+        const int face = cube_face(d, s, t);
+        const float u = s * (float)n - 0.5f, v = t * (float)n - 0.5f;
+        const float fu = std::floor(u), fv = std::floor(v);
+        const float a = u - fu, b = v - fv;
+        const int32_t i0 = (int32_t)fu, j0 = (int32_t)fv;
+        const vec3 t00 = fetch(face, i0, j0), t10 = fetch(face, i0 + 1, j0);
+        const vec3 t01 = fetch(face, i0, j0 + 1), t11 = fetch(face, i0 + 1, j0 + 1);
+        return {lerpf(lerpf(t00.x, t10.x, a), lerpf(t01.x, t11.x, a), b),
+                lerpf(lerpf(t00.y, t10.y, a), lerpf(t01.y, t11.y, a), b),
+                lerpf(lerpf(t00.z, t10.z, a), lerpf(t01.z, t11.z, a), b)};
+    }
+};
+
+// Sky colour of pixel (px, py); false where the skybox cube does not cover the pixel.
+bool sky_pixel(const SkyConst& k, const Sky& sky, uint32_t W, uint32_t H, int32_t px, int32_t py, vec3& out) {
+    const float xn = (float)(2 * px + 1) / (float)W - 1.0f;
+    const float yn = (float)(2 * py + 1) / (float)H - 1.0f;
+    auto unproject = [&](float zn, vec3& p) {
+        const float* m = k.ip;
+        const float x = ((m[0] * xn + m[4] * yn) + m[8] * zn) + m[12];
+        const float y = ((m[1] * xn + m[5] * yn) + m[9] * zn) + m[13];
+        const float z = ((m[2] * xn + m[6] * yn) + m[10] * zn) + m[14];
+        const float w = ((m[3] * xn + m[7] * yn) + m[11] * zn) + m[15];
+        p = {x / w, y / w, z / w};
+    };
+    vec3 o, o1;
+    unproject(0.0f, o);
+    unproject(1.0f, o1);
+    const vec3 r = o1 - o;
+    // into cube space (inverse of the rotation mat3(View) = its transpose)
+    const float* R = k.R;
+    const vec3 oc = {(R[0] * o.x + R[1] * o.y) + R[2] * o.z, (R[3] * o.x + R[4] * o.y) + R[5] * o.z,
+                     (R[6] * o.x + R[7] * o.y) + R[8] * o.z};
+    const vec3 rc = {(R[0] * r.x + R[1] * r.y) + R[2] * r.z, (R[3] * r.x + R[4] * r.y) + R[5] * r.z,
+                     (R[6] * r.x + R[7] * r.y) + R[8] * r.z};
+    const float half = 20.0f;
+    float t_in = -INFINITY, t_out = INFINITY;
+    const float oa[3] = {oc.x, oc.y, oc.z}, ra[3] = {rc.x, rc.y, rc.z};
+    for (int a = 0; a < 3; ++a) {
+        if (ra[a] != 0.0f) {
+            const float t0 = (-half - oa[a]) / ra[a], t1 = (half - oa[a]) / ra[a];
+            t_in = std::max(t_in, std::min(t0, t1));
+            t_out = std::min(t_out, std::max(t0, t1));
+        } else if (oa[a] < -half || oa[a] > half) {
+            return false;
+        }
+    }
+    if (!(t_out >= t_in)) return false;
+    const vec3 h = o + r * t_out;  // view-space exit point == interpolated outDirection
+    const float w = ((k.pw[0] * h.x + k.pw[1] * h.y) + k.pw[2] * h.z) + k.pw[3];
+    if (!(w > 0.0f)) return false;  // behind the camera: clipped
+    out = sky.sample(normalize(h));
+    return true;
+}
+
 inline uint32_t unorm8(float c) {
     const float cc = std::fmin(std::fmax(c, 0.0f), 1.0f);  // NaN -> 0
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
@@ -584,6 +746,9 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
     // ---- fragment shading of the surviving fragment (no blending, no discard: the last passing
     //      fragment's colour is the pixel colour) ----
     const uint32_t clear = pack_bgra({sc->clear_rgba[0], sc->clear_rgba[1], sc->clear_rgba[2], sc->clear_rgba[3]});
+    const bool has_sky = sc->sky_faces != nullptr && sc->sky_size > 0;
+    const SkyConst skk = sky_constants(g);
+    const Sky sky{sc->sky_faces, (int32_t)sc->sky_size};
     std::atomic<uint32_t> next_row{0};
     auto shade_worker = [&]() {
         for (;;) {
@@ -597,7 +762,11 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
                 if (out_depth) out_depth[idx] = dbits;
                 const int32_t ti = vis[idx];
                 if (ti < 0) {
-                    if (out_bgra) out_bgra[idx] = clear;
+                    vec3 skc;
+                    if (out_bgra)
+                        out_bgra[idx] = (has_sky && sky_pixel(skk, sky, W, H, (int32_t)px, py, skc))
+                                            ? pack_bgra({skc.x, skc.y, skc.z, 1.0f})
+                                            : clear;
                     continue;
                 }
                 const RTri& t = tris[ti];

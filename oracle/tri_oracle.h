@@ -45,6 +45,11 @@ typedef struct oracle_scene {
     uint32_t reserved;
     const tri_global_ubo* ubo;
     float clear_rgba[4];
+    /* Skybox cubemap (Renderer.cpp:3818-4110): 6 faces +X,-X,+Y,-Y,+Z,-Z of sky_size^2 RGBA8 sRGB
+     * texels, rows top to bottom. NULL / 0 = no skybox pass (background = clear colour). */
+    const uint8_t* sky_faces;
+    uint32_t sky_size;
+    uint32_t sky_reserved;
 } oracle_scene;
 
 typedef struct oracle_stats {

@@ -135,3 +135,40 @@ def empty_scene(w=128, h=96):
     return scenes.Scene("empty", w, h, np.zeros(0, abi.VERTEX_DTYPE), np.zeros(0, np.uint32),
                         np.zeros(0, abi.MESH_RANGE_DTYPE), [], scenes.pack_ubo(view, proj, (0, 0, 5)),
                         clear=(0.1, 0.2, 0.3, 1.0))
+
+
+# ---- skybox ----------------------------------------------------------------
+SOLID_0x808080 = np.tile(np.array([0x80, 0x80, 0x80, 0x00], np.uint8), (6, 1, 1, 1))  # CreateSolidColor(0x808080)
+
+
+def cubemap_faces(n=16, seed=11):
+    """A cubemap whose faces are distinct seeded gradients with noise (exercises filtering and the
+    seamless edges), uint8 [6, n, n, 4] sRGB, faces +X,-X,+Y,-Y,+Z,-Z."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:n, 0:n].astype(np.float32) / max(n - 1, 1)
+    faces = np.empty((6, n, n, 4), np.uint8)
+    for f in range(6):
+        base = rng.integers(30, 200, size=3)
+        g = np.stack([base[0] + 50 * xx, base[1] + 50 * yy, base[2] + 25 * (xx + yy)], -1)
+        g += rng.integers(-8, 9, size=g.shape)
+        faces[f, ..., :3] = np.clip(g, 0, 255).astype(np.uint8)
+        faces[f, ..., 3] = 255
+    return faces
+
+
+def skybox_only(w=320, h=240, fov=100.0, rot=(0.0, 0.0, 0.0), faces=None):
+    """No meshes: every pixel is the skybox pass (Renderer.cpp:5076-5082 before any mesh draw)."""
+    s = scenes.scene_c1_cube(0, w, h)
+    view, proj = scenes.editor_camera((0.0, 3.0, 8.0), rot, fov, (w, h), 0.1, 1000.0)
+    s.ubo = scenes.pack_ubo(view, proj, (0.0, 3.0, 8.0))
+    s.draws = []
+    s.name = f"skybox_only_{w}x{h}_fov{fov:g}"
+    s.skybox = cubemap_faces() if faces is None else faces
+    return s
+
+
+def c1_cube_skybox(frame=1, w=640, h=480):
+    s = scenes.scene_c1_cube(frame, w, h)
+    s.skybox = cubemap_faces(32, seed=5)
+    s.name = "c1_cube_skybox"
+    return s
