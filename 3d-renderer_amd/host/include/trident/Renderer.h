@@ -64,6 +64,10 @@ public:
     size_t GetOrCreatePrimitiveMeshIndex(MeshComponent::PrimitiveType primitiveType);
 
     void SetClearColor(const glm::vec4& color) { m_ClearColor = color; }
+    // Replaces the skybox cubemap (CreateSkyboxCubemap, Renderer.cpp:3818-4110). Init installs the
+    // reference's fallback, a solid 0x808080 cubemap (:3925-3926). An invalid cubemap is rejected
+    // and logged; returns false in that case.
+    bool SetSkyboxCubemap(const Loader::CubemapTextureData& cubemap);
     glm::vec4 GetClearColor() const { return m_ClearColor; }
 
     size_t GetModelCount() const { return m_ModelCount; }
@@ -114,7 +118,7 @@ private:
         ViewportInfo m_Info{};
         tri_ctx* m_Ctx = nullptr;
         uint32_t m_Width = 0, m_Height = 0;
-        uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0;
+        uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0, m_SkyboxGeneration = 0;
     };
 
     void UploadMeshFromCache();
@@ -142,6 +146,8 @@ private:
     std::vector<tri_vertex> m_VertexBuffer;
     std::vector<uint32_t> m_IndexBuffer;
     uint64_t m_GeometryGeneration = 1, m_TextureGeneration = 1, m_MaterialGeneration = 1;
+    Loader::CubemapTextureData m_SkyboxCubemap;
+    uint64_t m_SkyboxGeneration = 1;
 
     struct TextureSlot {
         std::string m_SourcePath;

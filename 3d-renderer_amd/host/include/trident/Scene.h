@@ -56,6 +56,25 @@ struct TextureData {  // TextureLoader output: RGBA8 (forced 4 channels), rows a
     int Channels = 4;
     std::vector<uint8_t> Pixels;
 };
+// CubemapTextureData (Loader/TextureLoader.h:30-48), LDR subset: 6 faces +X,-X,+Y,-Y,+Z,-Z of
+// m_Width x m_Height RGBA8 sRGB texels, one mip, stored face after face.
+struct CubemapTextureData {
+    uint32_t m_Width = 0;
+    uint32_t m_Height = 0;
+    uint32_t m_MipCount = 1;
+    std::vector<uint8_t> m_PixelData;
+    bool IsValid() const {
+        return m_Width > 0 && m_Width == m_Height && m_PixelData.size() >= 6ull * m_Width * m_Height * 4;
+    }
+    static CubemapTextureData CreateSolidColor(uint32_t rgba8888) {  // TextureLoader.cpp:309-330
+        CubemapTextureData d;
+        d.m_Width = d.m_Height = 1;
+        d.m_PixelData.resize(24);
+        for (int f = 0; f < 6; ++f)
+            for (int b = 0; b < 4; ++b) d.m_PixelData[4 * f + b] = (uint8_t)(rgba8888 >> (8 * b));  // little-endian memcpy
+        return d;
+    }
+};
 }  // namespace Loader
 
 struct Transform {

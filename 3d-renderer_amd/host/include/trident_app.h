@@ -48,6 +48,8 @@ int trident_app_set_camera(trident_app* app, int which, const float position[3],
                            float fov_deg, float near_clip, float far_clip, int ready);
 int trident_app_set_viewport(trident_app* app, uint32_t viewport_id, uint32_t width, uint32_t height);
 int trident_app_set_clear_color(trident_app* app, const float rgba[4]);
+/* Renderer::SetSkyboxCubemap: faces [6][size][size] RGBA8 sRGB (+X,-X,+Y,-Y,+Z,-Z). */
+int trident_app_set_skybox(trident_app* app, const uint8_t* faces, uint32_t size);
 
 int trident_app_draw_frame(trident_app* app);
 int trident_app_read_pixels(trident_app* app, uint32_t viewport_id, uint8_t* rgba, float* depth /* nullable */);

@@ -151,6 +151,11 @@ void Renderer::Init() {
     m_TextureSlots.push_back(white);
     m_TextureSlotLookup.emplace(kDefaultTextureKey, 0u);
     m_PerformanceHistory.assign(s_PerformanceHistorySize, FrameTimingSample{});
+    // CreateDefaultSkybox (Renderer.cpp:3806-3816). The reference first searches Assets/Skyboxes for
+    // KTX / PNG faces; no image decoder is linked here, so the shim starts from the reference's
+    // fallback and callers hand decoded faces to SetSkyboxCubemap.
+    m_SkyboxCubemap = Loader::CubemapTextureData::CreateSolidColor(0x808080u);
+    ++m_SkyboxGeneration;
     m_Initialised = true;
     m_Shutdown = false;
 }
@@ -163,6 +168,16 @@ void Renderer::Shutdown() {
     m_Viewports.clear();
     if (m_Initialised) m_Shutdown = true;
     m_Initialised = false;
+}
+
+bool Renderer::SetSkyboxCubemap(const Loader::CubemapTextureData& cubemap) {
+    if (!cubemap.IsValid()) {
+        LogError("SetSkyboxCubemap", "cubemap needs 6 square RGBA8 faces");
+        return false;
+    }
+    m_SkyboxCubemap = cubemap;
+    ++m_SkyboxGeneration;
+    return true;
 }
 
 // ---- geometry ---------------------------------------------------------------------------------
@@ -500,7 +515,7 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
         }
         vc.m_Width = w;
         vc.m_Height = h;
-        vc.m_GeometryGeneration = vc.m_TextureGeneration = vc.m_MaterialGeneration = 0;
+        vc.m_GeometryGeneration = vc.m_TextureGeneration = vc.m_MaterialGeneration = vc.m_SkyboxGeneration = 0;
     }
     if (vc.m_GeometryGeneration != m_GeometryGeneration) {
         const std::vector<tri_mesh_range> ranges = GetMeshRanges();
@@ -521,6 +536,15 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
             return false;
         }
         vc.m_MaterialGeneration = m_MaterialGeneration;
+    }
+    if (vc.m_SkyboxGeneration != m_SkyboxGeneration) {
+        const bool ok = m_SkyboxCubemap.IsValid();
+        if (tri_upload_skybox(vc.m_Ctx, ok ? m_SkyboxCubemap.m_PixelData.data() : nullptr,
+                              ok ? m_SkyboxCubemap.m_Width : 0) != TRI_OK) {
+            LogError("skybox cubemap", tri_last_error());
+            return false;
+        }
+        vc.m_SkyboxGeneration = m_SkyboxGeneration;
     }
     if (vc.m_TextureGeneration != m_TextureGeneration) {
         for (size_t s = 0; s < m_TextureSlots.size(); ++s) {

@@ -202,6 +202,16 @@ int trident_app_set_clear_color(trident_app* app, const float rgba[4]) {
     });
 }
 
+int trident_app_set_skybox(trident_app* app, const uint8_t* faces, uint32_t size) {
+    return Guard(app, [&] {
+        if (!faces || !size) return TRI_E_INVALID;
+        Loader::CubemapTextureData d;
+        d.m_Width = d.m_Height = size;
+        d.m_PixelData.assign(faces, faces + 6ull * size * size * 4);
+        return app->renderer.SetSkyboxCubemap(d) ? TRI_OK : TRI_E_INVALID;
+    });
+}
+
 int trident_app_draw_frame(trident_app* app) {
     return Guard(app, [&] {
         app->renderer.DrawFrame();

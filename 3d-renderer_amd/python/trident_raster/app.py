@@ -33,6 +33,7 @@ _APP_FUNCTIONS = [
     ("trident_app_set_camera", C.c_int, [C.c_void_p, C.c_int, _f3, _f3, C.c_float, C.c_float, C.c_float, C.c_int]),
     ("trident_app_set_viewport", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("trident_app_set_clear_color", C.c_int, [C.c_void_p, _f3]),
+    ("trident_app_set_skybox", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("trident_app_draw_frame", C.c_int, [C.c_void_p]),
     ("trident_app_read_pixels", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("trident_app_frame_inputs", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(abi.TriGlobalUbo), C.c_void_p, C.c_uint32,
@@ -137,6 +138,10 @@ class TridentApp:
 
     def set_clear_color(self, rgba):
         _check(self._lib.trident_app_set_clear_color(self._h, _vec(rgba)), "set_clear_color")
+
+    def set_skybox(self, faces):
+        f = np.ascontiguousarray(faces, np.uint8)
+        _check(self._lib.trident_app_set_skybox(self._h, f.ctypes.data, f.shape[1]), "set_skybox")
 
     def draw_frame(self):
         _check(self._lib.trident_app_draw_frame(self._h), "draw_frame")

@@ -315,6 +315,12 @@ class Scene:
         return 12 * self.triangles + 44 * V + 8 * self.width * rows + tex
 
 
+# CreateDefaultSkybox's fallback (Renderer.cpp:3925-3926): CreateSolidColor(0x808080) — bytes 80 80 80 00
+# on every face. The reference always records the skybox pass before the meshes, so the synthetic
+# workloads carry it too (Forge's PNG faces are assets of the reference, not available on the GPU box).
+DEFAULT_SKYBOX = np.tile(np.array([0x80, 0x80, 0x80, 0x00], np.uint8), (6, 1, 1, 1))
+
+
 def _single_mesh_ranges(nidx, material=0):
     m = np.zeros(1, abi.MESH_RANGE_DTYPE)
     m[0] = (0, nidx, 0, material)
@@ -330,7 +336,7 @@ def scene_c1_cube(frame=0, width=640, height=480):
     model = compose_transform((0.0, 3.0, -2.0), (0.0, 30.0 * frame, 0.0), (1, 1, 1))
     return Scene("c1_cube_640x480", width, height, v, idx, _single_mesh_ranges(idx.size),
                  [abi.make_draw(0, model, texture_slot=0, material_index=0)], pack_ubo(view, proj, cam),
-                 materials=[((1, 1, 1, 1), (0.0, 1.0, 1.0, 0.0))])
+                 materials=[((1, 1, 1, 1), (0.0, 1.0, 1.0, 0.0))], skybox=DEFAULT_SKYBOX)
 
 
 def scene_c2_sphere(width=1920, height=1080, rings=125, segments=200):
@@ -347,7 +353,7 @@ def scene_c2_sphere(width=1920, height=1080, rings=125, segments=200):
     ]
     return Scene(f"c2_sphere50k_{width}x{height}", width, height, v, idx, _single_mesh_ranges(idx.size),
                  [abi.make_draw(0, np.eye(4, dtype=F), material_index=0)], pack_ubo(view, proj, cam, lights),
-                 materials=[((0.9, 0.75, 0.6, 1.0), (0.3, 0.45, 1.0, 0.0))])
+                 materials=[((0.9, 0.75, 0.6, 1.0), (0.3, 0.45, 1.0, 0.0))], skybox=DEFAULT_SKYBOX)
 
 
 def scene_c3_grid(width=3840, height=2160, n=708):
@@ -363,7 +369,7 @@ def scene_c3_grid(width=3840, height=2160, n=708):
                        "color": (1.0, 0.9 - 0.1 * k, 0.7 + 0.1 * k)})
     return Scene(f"c3_grid1m_{width}x{height}", width, height, v, idx, _single_mesh_ranges(idx.size),
                  [abi.make_draw(0, np.eye(4, dtype=F), material_index=0)], pack_ubo(view, proj, cam, lights),
-                 materials=[((1.0, 1.0, 1.0, 1.0), (0.1, 0.6, 1.0, 0.0))])
+                 materials=[((1.0, 1.0, 1.0, 1.0), (0.1, 0.6, 1.0, 0.0))], skybox=DEFAULT_SKYBOX)
 
 
 def load_scene(rast, scene):

@@ -228,6 +228,7 @@ def main():
             "data": "synthetic (procedural PCG32-seeded scene; reference Assimp assets absent)",
             "config": {"workload": scene.name, "width": W, "height": H, "triangles": scene.triangles,
                        "vertices": int(scene.vertices.shape[0]), "bin": stats["bin_size"],
+                       "skybox": "solid 0x808080 fallback cubemap" if scene.skybox is not None else "none",
                        "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "single GPU"},
             "mpix_per_s": fps * W * H / 1e6,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

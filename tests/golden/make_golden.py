@@ -34,6 +34,8 @@ def cases():
     yield "skinned", sc.skinned_quad(o)
     yield "invalid", sc.invalid_inputs(o)
     yield "sphere_360p", sc.sphere_c2(640, 360, 40, 64, oracle=o)
+    yield "skybox_only", sc.skybox_only(192, 144, fov=110.0)
+    yield "c1_cube_skybox", sc.c1_cube_skybox(1, 320, 240)
 
 
 def pack(scene):
@@ -48,6 +50,8 @@ def pack(scene):
     for k, (slot, t) in enumerate(scene.textures):
         d[f"tex{k}_slot"] = np.array(slot)
         d[f"tex{k}"] = t
+    if scene.skybox is not None:
+        d["skybox"] = np.asarray(scene.skybox, np.uint8)
     return d
 
 
@@ -67,12 +71,15 @@ def unpack(z):
     return scenes.Scene("golden", int(z["width"]), int(z["height"]),
                         z["vertices"].view(abi.VERTEX_DTYPE), z["indices"], z["meshes"].view(abi.MESH_RANGE_DTYPE),
                         draws, abi.TriGlobalUbo.from_buffer_copy(z["ubo"].tobytes()), materials=mats, textures=texs,
-                        clear=tuple(float(c) for c in z["clear"]), bones=bones)
+                        clear=tuple(float(c) for c in z["clear"]), bones=bones,
+                        skybox=z["skybox"] if "skybox" in z else None)
 
 
-def main():
+def main(only=()):
     oracle_py.build()
     for name, scene in cases():
+        if only and name not in only:
+            continue
         col, dep, st = oracle_py.render(scene)
         d = pack(scene)
         d["out_bgra"], d["out_depth"] = col, dep
@@ -84,4 +91,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    main(tuple(sys.argv[1:]))  # optional fixture names: regenerate only those

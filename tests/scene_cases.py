@@ -138,7 +138,7 @@ def empty_scene(w=128, h=96):
 
 
 # ---- skybox ----------------------------------------------------------------
-SOLID_0x808080 = np.tile(np.array([0x80, 0x80, 0x80, 0x00], np.uint8), (6, 1, 1, 1))  # CreateSolidColor(0x808080)
+SOLID_0x808080 = scenes.DEFAULT_SKYBOX  # CreateSolidColor(0x808080)
 
 
 def cubemap_faces(n=16, seed=11):

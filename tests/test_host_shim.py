@@ -199,18 +199,22 @@ def test_draw_frame_records_frame_timing(app_mod):
 # ---------------------------------------------------------------------------------------------
 # GPU: frames rendered through the shim == oracle on the same inputs
 # ---------------------------------------------------------------------------------------------
-def shim_scene(a, viewport, w, h, textures=()):
+def shim_scene(a, viewport, w, h, textures=(), skybox=None):
+    """The oracle scene for what the shim submitted. skybox None = the Init fallback cubemap
+    (CreateSolidColor(0x808080), Renderer.cpp:3925-3926)."""
+    import scene_cases as sc
     from trident_raster import scenes
 
     ubo, draws = a.frame_inputs(viewport)
     vb, ib, ranges = a.geometry()
     return scenes.Scene(f"shim_vp{viewport}", w, h, vb, ib, ranges, draws, ubo,
-                        materials=[(m[0], m[1]) for m in a.materials()], textures=list(textures))
+                        materials=[(m[0], m[1]) for m in a.materials()], textures=list(textures),
+                        skybox=sc.SOLID_0x808080 if skybox is None else skybox)
 
 
-def assert_shim_parity(a, oracle, viewport, w, h, textures=(), min_covered=100):
+def assert_shim_parity(a, oracle, viewport, w, h, textures=(), min_covered=100, skybox=None):
     rgba, depth = a.read_pixels(viewport, w, h)
-    oc, od, _ = oracle.render(shim_scene(a, viewport, w, h, textures))
+    oc, od, _ = oracle.render(shim_scene(a, viewport, w, h, textures, skybox))
     assert np.array_equal(depth.view(np.uint32), od), "depth mismatch"
     ob = oc[..., [2, 1, 0, 3]]  # oracle BGRA -> RGBA
     diff = np.abs(rgba.astype(np.int16) - ob.astype(np.int16))
@@ -249,7 +253,11 @@ def test_gpu_shim_two_viewports_and_textures(app_mod, oracle):
     q = a.add_mesh_entity("quad", position=(1.5, 0, 0), scale=(1.5, 1.5, 1))
     a.set_entity_texture(q, "checker.png")
     a.add_light("point", position=(0, 2, 2), color=(1, 0.9, 0.8), intensity=8.0, range=6.0)
+    import scene_cases as sc
+
+    sky = sc.cubemap_faces(16, seed=3)
+    a.set_skybox(sky)
     a.draw_frame()  # first frame: the lazily created cube drops the sphere's draw (reference quirk)
     a.draw_frame()  # steady state: all three draws
-    assert_shim_parity(a, oracle, 1, 480, 320, textures=[(1, checker)], min_covered=5000)
-    assert_shim_parity(a, oracle, 2, 256, 200, textures=[(1, checker)], min_covered=1000)
+    assert_shim_parity(a, oracle, 1, 480, 320, textures=[(1, checker)], min_covered=5000, skybox=sky)
+    assert_shim_parity(a, oracle, 2, 256, 200, textures=[(1, checker)], min_covered=1000, skybox=sky)
