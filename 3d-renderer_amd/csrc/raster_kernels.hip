@@ -979,7 +979,9 @@ struct SkyTex {
 };
 
 // BGRA8 sky colour of pixel (px, py), or the clear colour where the skybox does not cover it.
-__device__ __noinline__ uint32_t sky_bgra(const TriFrameParams& fp, const TriDeviceBuffers& b, int32_t px, int32_t py,
+// Inlined into its own pass of k_raster (a call here costs the whole kernel a scratch stack and the
+// callee-saved register set: measured 5x slower at C3).
+__device__ __forceinline__ uint32_t sky_bgra(const TriFrameParams& fp, const TriDeviceBuffers& b, int32_t px, int32_t py,
                                           const float* lut) {
     const float xn = (float)(2 * px + 1) / (float)fp.W - 1.0f;
     const float yn = (float)(2 * py + 1) / (float)fp.H - 1.0f;
@@ -1031,12 +1033,15 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 }
 
 template <bool EXACT, int BL>
-__global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
+// 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
+// a little); 64x64 bins are LDS-limited to 3
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL == 5 ? 6 : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     __shared__ uint32_t bigq[kBigQueue];
     __shared__ float lut[512];
-    __shared__ uint32_t nbig, nentries;
+    __shared__ uint16_t skyq[BIN * BIN];
+    __shared__ uint32_t nbig, nentries, nsky;
     const int tid = threadIdx.x;
     const int bin = xcd_bin(blockIdx.x, fp.nbins);
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
@@ -1046,6 +1051,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
     for (int i = tid; i < 512; i += TRI_BLOCK) lut[i] = b.srgb_lut[i];
     if (tid == 0) {
         nbig = 0;
+        nsky = 0;
         const uint32_t cnt = b.bin_count[bin];
         b.bin_count[bin] = 0;  // queue consumed: ready for the next frame
         if (cnt > fp.bin_cap) note_bin_overflow(b, cnt);
@@ -1104,17 +1110,35 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
         }
     }
     __syncthreads();
-    // shade + store: each wave covers whole BIN-pixel row pieces -> coalesced colour/depth stores
+    // shade + store: each wave covers whole BIN-pixel row pieces -> coalesced colour/depth stores.
+    // Background pixels go to an LDS queue for the skybox pass below (lane-dense, and its registers
+    // are not live during shading).
     const int lx = tid & (BIN - 1);
+    const bool sky_on = fp.sky_size != 0;
     for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
-        if (lx >= bw) continue;
-        const uint64_t key = keys[(ly << BL) + lx];
+        const bool in = lx < bw;
+        const uint64_t key = in ? keys[(ly << BL) + lx] : 0ull;
+        const bool bg = in && key == kBgKey;
+        if (sky_on) {  // wave-aggregated append (uniform control flow here)
+            const uint64_t m = __ballot(bg);
+            if (m) {
+                const uint32_t lane = lanes_below(~0ull);
+                const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+                uint32_t base = 0;
+                if (lane == leader) base = atomicAdd(&nsky, (uint32_t)__builtin_popcountll(m));
+                base = (uint32_t)__shfl((int)base, (int)leader);
+                if (bg) skyq[base + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
+            }
+        }
+        if (!in) continue;
         const int32_t px = ox + lx, py = oy + ly;
         uint32_t out;
         float z;
-        if (key == kBgKey) {
-            out = fp.sky_size ? sky_bgra(fp, b, px, py, lut) : fp.clear_bgra;
-            z = 1.0f;
+        if (bg) {
+            const size_t o = (size_t)(py - fp.y0) * fp.W + px;
+            if (!sky_on) b.color[o] = fp.clear_bgra;
+            if (fp.write_depth) b.depth[o] = 1.0f;
+            continue;
         } else if (fp.ablate & 1) {  // diagnostics: coverage only
             z = __uint_as_float((uint32_t)(key >> 32));
             out = (uint32_t)key;
@@ -1128,6 +1152,14 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_raster(TriFrameParams fp, TriDevi
         const size_t o = (size_t)(py - fp.y0) * fp.W + px;
         b.color[o] = out;
         if (fp.write_depth) b.depth[o] = z;
+    }
+    if (!sky_on) return;
+    __syncthreads();
+    const uint32_t ns = nsky;
+    for (uint32_t i = tid; i < ns; i += TRI_BLOCK) {  // skybox pass over the queued background pixels
+        const uint32_t li = skyq[i];
+        const int32_t px = ox + (int32_t)(li & (BIN - 1)), py = oy + (int32_t)(li >> BL);
+        b.color[(size_t)(py - fp.y0) * fp.W + px] = sky_bgra(fp, b, px, py, lut);
     }
 }
 
