@@ -6,9 +6,11 @@
 
 One step = one frame of Trident's graphics-pipeline stage: the per-frame UBO + draw-list update
 (UpdateUniformBuffer / push constants, Renderer.cpp:5822-6051, :5110-5151) and the five gfx950
-kernels (k_vertex, k_setup, k_clip, k_raster) over geometry resident in HBM; N > 1 = sort-first row bands (geometry replicated) + an RCCL all-gather of the BGRA8 bands
-into the full frame on every rank. value = whole frames per second (strong scaling: a frame's work
-is fixed, N GPUs share it). Rank 0 prints ONE JSON line.
+kernels (k_vertex, k_setup, k_clip, k_raster) over geometry resident in HBM. N > 1 = sort-first
+row bands (geometry replicated) + an RCCL all-gather of the BGRA8 bands into the full frame on
+every rank, double-buffered so frame k's gather overlaps frame k+1's kernels. value = whole frames
+per second (strong scaling: a frame's work is fixed, N GPUs share it); latency_ms = one frame end
+to end without overlap. Rank 0 prints ONE JSON line.
 """
 import argparse
 import json
@@ -43,15 +45,16 @@ def band_rows(height, world, rank):
     return rank * rows, (rank + 1) * rows
 
 
-def gather_bands(frame, band, world):
+def gather_bands(frame, band, world, async_op=False):
     """Assemble the full frame on every rank from the per-rank BGRA8 bands (RCCL all-gather over xGMI
-    with the nccl backend; gloo in the CPU tests). Band r lands at rows [r*rows, (r+1)*rows)."""
+    with the nccl backend; gloo in the CPU tests). Band r lands at rows [r*rows, (r+1)*rows).
+    async_op=True returns the collective's work handle (None for world 1) instead of waiting."""
     if world == 1:
-        return band
+        return None if async_op else band
     import torch.distributed as dist
 
-    dist.all_gather_into_tensor(frame, band)
-    return frame
+    work = dist.all_gather_into_tensor(frame, band, async_op=async_op)
+    return work if async_op else frame
 
 
 def max_over_ranks(value, device, dist_on):
@@ -66,8 +69,49 @@ def max_over_ranks(value, device, dist_on):
     return float(t.item())
 
 
+class GatherRing:
+    """Double-buffered band assembly for N > 1: frame k's all-gather (on the collective's stream)
+    overlaps frame k+1's kernels (on the render stream). Before frame k+2 reuses slot k % 2, the
+    render stream waits for frame k's gather (work.wait() is a stream wait; the host does not
+    block). Throughput is then max(render, gather) per frame instead of their sum."""
+
+    def __init__(self, world, band_elems, frame_elems, make):
+        self.world = world
+        self.nbuf = 2 if world > 1 else 1
+        self.bands = [make(band_elems) for _ in range(self.nbuf)]
+        self.frames = [make(frame_elems) for _ in range(self.nbuf)] if world > 1 else self.bands
+        self.pending = [None] * self.nbuf
+        self.k = 0
+
+    def acquire(self):
+        """The band buffer frame k renders into (after frame k-2's gather released it)."""
+        i = self.k % self.nbuf
+        if self.pending[i] is not None:
+            self.pending[i].wait()
+            self.pending[i] = None
+        return self.bands[i]
+
+    def publish(self):
+        """Start frame k's gather of the band returned by acquire()."""
+        i = self.k % self.nbuf
+        self.pending[i] = gather_bands(self.frames[i], self.bands[i], self.world, async_op=True)
+        self.k += 1
+
+    def drain(self):
+        for i, w in enumerate(self.pending):
+            if w is not None:
+                w.wait()
+                self.pending[i] = None
+
+    @property
+    def frame(self):
+        """The most recently assembled frame (complete after drain())."""
+        return self.frames[(self.k - 1) % self.nbuf]
+
+
 class BandRenderer:
-    """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers."""
+    """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers, assembled
+    by a GatherRing."""
 
     def __init__(self, scene, rank, world, device_index):
         import torch
@@ -78,20 +122,39 @@ class BandRenderer:
         rows = self.band[1] - self.band[0]
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
         self.dev = torch.device("cuda", device_index)
-        self.color = torch.empty(rows * W, dtype=torch.int32, device=self.dev)
+        self.ring = GatherRing(world, rows * W, H * W,
+                               lambda n: torch.empty(n, dtype=torch.int32, device=self.dev))
         self.depth = torch.empty(rows * W, dtype=torch.float32, device=self.dev)
-        self.frame = torch.empty(H * W, dtype=torch.int32, device=self.dev) if world > 1 else self.color
         self.r = raster.TriRaster(W, H, band=self.band, device=device_index)
-        self.r.bind_output(self.color.data_ptr(), self.depth.data_ptr())
         self.r.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
         scenes.load_scene(self.r, scene)
 
     def step(self):
         s = self.scene
+        self.r.bind_output(self.ring.acquire().data_ptr(), self.depth.data_ptr())
         self.r.set_frame(s.ubo, s.clear)  # per-frame uniform update
         self.r.set_draws(s.draws)         # per-frame draw list (push constants)
         self.r.render()
-        gather_bands(self.frame, self.color, self.world)
+        self.ring.publish()
+
+    def drain(self):
+        self.ring.drain()
+
+    def latency_ms(self, frames=20):
+        """Per-frame latency without overlap: render + gather + wait, host-synchronised each frame."""
+        import torch
+
+        self.drain()
+        ts = []
+        for _ in range(frames):
+            torch.cuda.synchronize(self.dev)
+            t0 = time.perf_counter()
+            self.step()
+            self.drain()
+            torch.cuda.synchronize(self.dev)
+            ts.append((time.perf_counter() - t0) * 1e3)
+        ts.sort()
+        return ts[len(ts) // 2]
 
 
 def timed_run(br, steps, warmup, dist_on, stage_timing=True, period=8):
@@ -100,6 +163,7 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, period=8):
     br.r.render_frame()  # first frame sizes the internal queues (re-renders after TRI_E_OVERFLOW)
     for _ in range(warmup):
         br.step()
+    br.drain()
     br.r.synchronize()
     torch.cuda.synchronize(br.dev)
     if dist_on:
@@ -111,6 +175,7 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, period=8):
     t0 = time.perf_counter()
     for _ in range(steps):
         br.step()
+    br.drain()
     torch.cuda.synchronize(br.dev)
     if dist_on:
         dist.barrier()
@@ -186,6 +251,7 @@ def main():
     fps = args.steps / dt
     W, H = scene.width, scene.height
     stats = br.r.frame_stats()
+    latency = br.latency_ms()  # one frame end to end (render + gather), no overlap
 
     # roofline of the dominant kernel (k_raster = tile_raster_shade): its algorithmic bytes per
     # launch are the colour + depth it must store for its band (4 + 4 B per pixel).
@@ -231,6 +297,7 @@ def main():
                        "skybox": "solid 0x808080 fallback cubemap" if scene.skybox is not None else "none",
                        "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "single GPU"},
             "mpix_per_s": fps * W * H / 1e6,
+            "latency_ms": latency,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "kernel": "k_raster",

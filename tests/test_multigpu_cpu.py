@@ -69,6 +69,51 @@ def test_row_band_allgather_equals_full_frame(world, scene_name, oracle, tmp_pat
         assert float(np.load(tmp_path / f"slowest{r}.npy")[0]) == float(world)
 
 
+def _ring_worker(rank, world, port, out_dir):
+    """bench.GatherRing over gloo: 5 frames through the double buffer, each band stamped with
+    (frame, rank); every assembled frame must hold exactly that frame's bands."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rows, W = 3, 5
+    ring = bench.GatherRing(world, rows * W, world * rows * W, lambda n: torch.zeros(n, dtype=torch.int32))
+    assembled = []
+    for k in range(5):
+        band = ring.acquire()
+        band.fill_(1000 * k + rank)  # the "render" of frame k into this rank's band
+        ring.publish()
+        if k % 2 == 1:  # read back every other frame only after its gather completed
+            ring.drain()
+            assembled.append((k, ring.frame.clone().numpy()))
+    ring.drain()
+    assembled.append((4, ring.frame.clone().numpy()))
+    for k, fr in assembled:
+        np.save(os.path.join(out_dir, f"ring{rank}_{k}.npy"), fr)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_gather_ring_double_buffer():
+    import torch.multiprocessing as mp
+
+    import tempfile
+
+    world = 2
+    with tempfile.TemporaryDirectory() as d:
+        mp.start_processes(_ring_worker, args=(world, _free_port(), d), nprocs=world, join=True,
+                           start_method="spawn")
+        for r in range(world):
+            for k in (1, 3, 4):
+                fr = np.load(os.path.join(d, f"ring{r}_{k}.npy")).reshape(world, -1)
+                for src in range(world):
+                    assert (fr[src] == 1000 * k + src).all(), (r, k, src)
+
+
 def test_band_rows_partition():
     sys.path.insert(0, ROOT)
     import bench
