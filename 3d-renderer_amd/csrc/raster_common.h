@@ -26,6 +26,10 @@
 #define TRI_CLIP_GRID 16
 #define TRI_MAX_PPT 8  // primitives per k_setup thread
 
+#define TRI_SKY_RAY 0u
+#define TRI_SKY_PERSP 1u
+#define TRI_SKY_UNIFORM 2u
+
 // overflow flag bits (TriCounters.flags)
 #define TRI_OVF_CLIP_RECORDS 0x1u
 #define TRI_OVF_CLIP_VERTS 0x2u
@@ -142,6 +146,17 @@ struct TriFrameParams {
     uint32_t write_depth;
     uint32_t exact_shading;
     uint32_t sky_size;  // skybox face size (0 = no skybox pass)
+    // Skybox evaluation mode (fast build; the exact build always uses the oracle's ray/cube path):
+    //  TRI_SKY_RAY     unproject both clip planes, intersect the 20-unit cube (oracle sky_pixel)
+    //  TRI_SKY_PERSP   the projection's centre is the view origin (w row has no constant term), so
+    //                  every ray leaves the eye-centred cube and the sampled direction is the far
+    //                  point's homogeneous xyz: 3 dot products per pixel
+    //  TRI_SKY_UNIFORM TRI_SKY_PERSP over a cubemap whose texels are all equal: LINEAR filtering of
+    //                  equal taps returns that texel, so the sky is the constant sky_bgra
+    uint32_t sky_mode;
+    uint32_t sky_bgra;
+    uint32_t pad_s[2];
+    float sky_far[16];  // inverse(Projection) applied to (xn, yn, 1, 1): rows {x, y, z, w} as (a, b, c, 0)
     float pv[16];
     float sky_ip[16];   // inverse(Projection) (double on the host, rounded)
     float sky_R[9];     // mat3(View)

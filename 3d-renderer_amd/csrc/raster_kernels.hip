@@ -910,6 +910,7 @@ __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const T
 // oracle's sky_pixel(): a background pixel's interpolated direction is the view-space point where
 // its ray leaves the 20-unit cube; Vulkan cube sampling with seamless LINEAR filtering.
 // ------------------------------------------------------------------------------------------
+template <bool FAST = false>
 __device__ __forceinline__ int cube_face(f3 d, float& s, float& t) {
     const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
     int face;
@@ -922,8 +923,14 @@ __device__ __forceinline__ int cube_face(f3 d, float& s, float& t) {
         face = d.z >= 0.0f ? 4 : 5; ma = az; sc = d.z >= 0.0f ? d.x : -d.x; tc = -d.y;
     }
     if (!(ma > 0.0f)) { s = 0.5f; t = 0.5f; return face; }
-    s = 0.5f * (sc / ma) + 0.5f;
-    t = 0.5f * (tc / ma) + 0.5f;
+    if (FAST) {
+        const float h = 0.5f * frcp(ma);
+        s = sc * h + 0.5f;
+        t = tc * h + 0.5f;
+    } else {
+        s = 0.5f * (sc / ma) + 0.5f;
+        t = 0.5f * (tc / ma) + 0.5f;
+    }
     return face;
 }
 
@@ -963,9 +970,10 @@ struct SkyTex {
         const f3 a = texel(face, ci, cj), b = across(face, i, cj), c = across(face, ci, j);
         return mk(((a.x + b.x) + c.x) / 3.0f, ((a.y + b.y) + c.y) / 3.0f, ((a.z + b.z) + c.z) / 3.0f);
     }
+    template <bool FAST = false>
     __device__ __forceinline__ f3 sample(f3 d) const {
         float s, tt;
-        const int face = cube_face(d, s, tt);
+        const int face = cube_face<FAST>(d, s, tt);
         const float u = s * (float)n - 0.5f, v = tt * (float)n - 0.5f;
         const float fu = floorf(u), fv = floorf(v);
         const float a = u - fu, bb = v - fv;
@@ -1021,6 +1029,25 @@ __device__ __forceinline__ uint32_t sky_bgra(const TriFrameParams& fp, const Tri
     return unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (255u << 24);
 }
 
+// TRI_SKY_PERSP (fast build): the ray of a pixel starts at the eye, the centre of the skybox cube,
+// so it always leaves the cube and its exit point has the direction of the far-plane point; cube
+// sampling only uses direction ratios, so no normalisation and no cube intersection is needed.
+__device__ __forceinline__ uint32_t sky_bgra_persp(const TriFrameParams& fp, const TriDeviceBuffers& b, int32_t px,
+                                                   int32_t py, const float* lut) {
+    const float xn = (float)(2 * px + 1) / (float)fp.W - 1.0f;
+    const float yn = (float)(2 * py + 1) / (float)fp.H - 1.0f;
+    const float* m = fp.sky_far;
+    f3 d = mk(m[0] * xn + m[1] * yn + m[2], m[4] * xn + m[5] * yn + m[6], m[8] * xn + m[9] * yn + m[10]);
+    if (m[12] * xn + m[13] * yn + m[14] < 0.0f) d = mk(-d.x, -d.y, -d.z);  // homogeneous w < 0
+    const SkyTex sky{b.sky, (int32_t)fp.sky_size, lut};
+    const f3 c = sky.sample<true>(d);
+    return unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (255u << 24);
+}
+
+#ifndef TRI_RASTER_WAVES
+#define TRI_RASTER_WAVES 6  // k_raster occupancy target at 32x32 bins (waves per SIMD)
+#endif
+
 constexpr int kBigArea = 96;  // bbox∩bin pixels above which a triangle is rasterized cooperatively
 constexpr int kBigQueue = 1024;
 
@@ -1035,7 +1062,7 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 template <bool EXACT, int BL>
 // 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
 // a little); 64x64 bins are LDS-limited to 3
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL == 5 ? 6 : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL == 5 ? TRI_RASTER_WAVES : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     __shared__ uint32_t bigq[kBigQueue];
@@ -1115,11 +1142,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL ==
     // are not live during shading).
     const int lx = tid & (BIN - 1);
     const bool sky_on = fp.sky_size != 0;
+    const bool sky_const = sky_on && !EXACT && fp.sky_mode == TRI_SKY_UNIFORM;
+    const bool sky_queue = sky_on && !sky_const;
+    const uint32_t bg_bgra = sky_const ? fp.sky_bgra : fp.clear_bgra;
     for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
         const bool in = lx < bw;
         const uint64_t key = in ? keys[(ly << BL) + lx] : 0ull;
         const bool bg = in && key == kBgKey;
-        if (sky_on) {  // wave-aggregated append (uniform control flow here)
+        if (sky_queue) {  // wave-aggregated append (uniform control flow here)
             const uint64_t m = __ballot(bg);
             if (m) {
                 const uint32_t lane = lanes_below(~0ull);
@@ -1136,7 +1166,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL ==
         float z;
         if (bg) {
             const size_t o = (size_t)(py - fp.y0) * fp.W + px;
-            if (!sky_on) b.color[o] = fp.clear_bgra;
+            if (!sky_queue) b.color[o] = bg_bgra;
             if (fp.write_depth) b.depth[o] = 1.0f;
             continue;
         } else if (fp.ablate & 1) {  // diagnostics: coverage only
@@ -1153,13 +1183,15 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL ==
         b.color[o] = out;
         if (fp.write_depth) b.depth[o] = z;
     }
-    if (!sky_on) return;
+    if (!sky_queue) return;
     __syncthreads();
     const uint32_t ns = nsky;
+    const bool persp = !EXACT && fp.sky_mode == TRI_SKY_PERSP;
     for (uint32_t i = tid; i < ns; i += TRI_BLOCK) {  // skybox pass over the queued background pixels
         const uint32_t li = skyq[i];
         const int32_t px = ox + (int32_t)(li & (BIN - 1)), py = oy + (int32_t)(li >> BL);
-        b.color[(size_t)(py - fp.y0) * fp.W + px] = sky_bgra(fp, b, px, py, lut);
+        b.color[(size_t)(py - fp.y0) * fp.W + px] =
+            persp ? sky_bgra_persp(fp, b, px, py, lut) : sky_bgra(fp, b, px, py, lut);
     }
 }
 

@@ -52,6 +52,12 @@ uint32_t unorm8_host(float c) {
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
 }
 
+// R8G8B8A8_SRGB decode of one channel byte (sRGB EOTF in double, rounded): the kernels' LUT.
+float srgb_decode(int i) {
+    const double v = i / 255.0;
+    return (float)(v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4));
+}
+
 struct TimingSet {
     hipEvent_t ev[kStageCount + 1];
 };
@@ -88,6 +94,8 @@ struct tri_ctx {
     float* d_bones = nullptr; size_t cap_bones = 0;
     uint32_t* d_sky = nullptr; size_t cap_sky = 0;
     uint32_t sky_size = 0;
+    bool sky_uniform = false;  // every texel of the cubemap equal (e.g. the solid fallback)
+    uint32_t sky_uniform_bgra = 0;
     uint32_t nbones = 0;
 
     // per frame
@@ -476,8 +484,7 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
         return bail(fail(TRI_E_HIP, "tri_create: memset failed"));
     float lut[512];
     for (int i = 0; i < 256; ++i) {  // R8G8B8A8_SRGB decode (sRGB EOTF), evaluated in double
-        const double v = i / 255.0;
-        lut[i] = (float)(v <= 0.04045 ? v / 12.92 : std::pow((v + 0.055) / 1.055, 2.4));
+        lut[i] = srgb_decode(i);
         lut[256 + i] = (float)i / 255.0f;  // alpha: linear UNORM decode (IEEE float division)
     }
     if (hipMemcpy(c->d_lut, lut, sizeof lut, hipMemcpyHostToDevice) != hipSuccess)
@@ -627,6 +634,18 @@ int tri_upload_skybox(tri_ctx* c, const uint8_t* faces, uint32_t n) {
     if ((rc = grow(c->d_sky, c->cap_sky, texels))) return rc;
     HIP_TRY(hipMemcpy(c->d_sky, faces, texels * 4, hipMemcpyHostToDevice));
     c->sky_size = n;
+    const uint32_t* t = reinterpret_cast<const uint32_t*>(faces);
+    uint32_t t0;
+    std::memcpy(&t0, faces, 4);
+    c->sky_uniform = true;
+    for (size_t i = 1; i < texels && c->sky_uniform; ++i) {
+        uint32_t ti;
+        std::memcpy(&ti, t + i, 4);
+        c->sky_uniform = ti == t0;
+    }
+    // Skybox.frag writes the decoded linear colour, alpha 1, to the UNORM target
+    c->sky_uniform_bgra = unorm8_host(srgb_decode((t0 >> 16) & 0xFF)) | (unorm8_host(srgb_decode((t0 >> 8) & 0xFF)) << 8) |
+                          (unorm8_host(srgb_decode(t0 & 0xFF)) << 16) | (255u << 24);
     return TRI_OK;
 }
 
@@ -704,7 +723,18 @@ int tri_render(tri_ctx* c) {
     fp.write_depth = (c->cfg.flags & TRI_FLAG_NO_DEPTH_OUTPUT) ? 0u : 1u;
     fp.exact_shading = (c->cfg.flags & TRI_FLAG_EXACT_SHADING) ? 1u : 0u;
     fp.sky_size = c->sky_size;
-    if (c->sky_size) sky_constants(c->ubo, fp.sky_ip, fp.sky_R, fp.sky_pw);
+    if (c->sky_size) {
+        sky_constants(c->ubo, fp.sky_ip, fp.sky_R, fp.sky_pw);
+        // the projection's centre is the view origin when its w row has no constant term
+        const bool persp = fp.sky_pw[3] == 0.0f;
+        fp.sky_mode = !persp ? TRI_SKY_RAY : (c->sky_uniform ? TRI_SKY_UNIFORM : TRI_SKY_PERSP);
+        fp.sky_bgra = c->sky_uniform_bgra;
+        for (int r = 0; r < 4; ++r) {  // inverse(P) * (xn, yn, 1, 1), row r
+            fp.sky_far[4 * r + 0] = fp.sky_ip[0 * 4 + r];
+            fp.sky_far[4 * r + 1] = fp.sky_ip[1 * 4 + r];
+            fp.sky_far[4 * r + 2] = fp.sky_ip[2 * 4 + r] + fp.sky_ip[3 * 4 + r];
+        }
+    }
     static const uint32_t ablate = [] {  // diagnostics only: TRI_ABLATE=1 no shading, 2 no coverage
         const char* e = getenv("TRI_ABLATE");
         return e ? (uint32_t)atoi(e) : 0u;

@@ -123,3 +123,31 @@ def test_gpu_skybox_bands(oracle):
     s = sc.skybox_only(256, 192, fov=110.0)
     for band in [(0, 64), (64, 128), (128, 192)]:
         assert_sky_parity(s, oracle, band=band)
+
+
+def skybox_runtime_camera(ptype, w=240, h=160, ortho=12.0):
+    """RuntimeCamera projections (RuntimeCamera.cpp:177-195): GL-style perspective (ptype 0) or
+    glm::ortho (ptype 1). Orthographic rays do not start at the cube's centre, so the kernel takes
+    the general ray/cube path there; some rays miss the 20-unit cube and keep the clear colour."""
+    import oracle_py
+
+    s = sc.skybox_only(w, h, fov=70.0)
+    view, proj = oracle_py.runtime_camera((0.0, 3.0, 8.0), (10.0, 25.0, 0.0), 70.0, (w, h), 0.1, 1000.0,
+                                          ortho=ortho, ptype=ptype)
+    s.ubo = oracle_py.pack_ubo(view, proj, (0.0, 3.0, 8.0))
+    s.name = f"skybox_runtime_p{ptype}"
+    return s
+
+
+def test_orthographic_sky_has_uncovered_pixels(oracle):
+    s = skybox_runtime_camera(1, ortho=30.0)
+    col, _, _ = oracle.render(s)
+    clear = np.array([1, 1, 1, 255], np.uint8)  # unorm8(0.005) = 1
+    missed = np.all(col == clear, axis=-1)
+    assert missed.any() and (~missed).any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("ptype,ortho", [(0, 12.0), (1, 12.0), (1, 30.0)])
+def test_gpu_skybox_runtime_camera(oracle, ptype, ortho):
+    assert_sky_parity(skybox_runtime_camera(ptype, ortho=ortho), oracle)

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Build an A/B variant of the HIP library: tools/build_variant.sh NAME [extra hipcc flags...]
+# -> 3d-renderer_amd/lib/variants/NAME.so (select it with TRI_RASTER_LIB=... on the GPU box).
+set -e
+cd "$(dirname "$0")/../3d-renderer_amd"
+name=$1; shift
+mkdir -p lib/variants/obj_$name
+for s in raster_kernels tri_raster_capi; do
+  /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function "$@" \
+    -c csrc/$s.hip -o lib/variants/obj_$name/$s.o &
+done
+wait
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o lib/variants/$name.so lib/variants/obj_$name/*.o
+echo "built lib/variants/$name.so"
