@@ -6,6 +6,9 @@
 //   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation
 //   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, z_ndc, 1/w}
 //   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
+//   prim_vs   16 B/prim    {vertex slots 0..2, draw | clipped flag}, written by k_setup for the
+//                          primitives it bins or clips: k_raster's one-load route from a primitive
+//                          id to its vertices (instead of draw search -> index buffer)
 //   bin_list   4 B/entry   primitive ids per bin (order-free: visibility is resolved by a 64-bit key)
 //   TriRec    64 B/record  clipped sub-triangles only: snapped vertices, z, 1/w, prim<<3|sub, slots
 //   colour     4 B/pixel   B8G8R8A8_UNORM;  depth 4 B/pixel D32_SFLOAT bits
@@ -20,6 +23,8 @@
 #define TRI_PRIM_MAX ((1u << 29) - 1u)
 // bin-queue entry: a primitive id, or TRI_ENTRY_CLIPPED | index of a clipped sub-triangle's record
 #define TRI_ENTRY_CLIPPED 0x80000000u
+// prim_vs[p].w flag: primitive p was clipped (its fragments come from TriRec sub-triangles)
+#define TRI_PRIM_CLIPPED 0x80000000u
 #define TRI_MAX_CLIP_VERTS 12
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f

@@ -287,6 +287,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
             // invalid vertex, or trivial reject: all three vertices outside one clip half-space
             if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
                 if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
+                    b.prim_vs[p] = make_uint4(sl0, sl1, sl2, (uint32_t)d | TRI_PRIM_CLIPPED);
                     const uint32_t q = wave_append(&b.counters->clip_queue);
                     if (q < fp.ovf_rec_cap) b.clip_queue[q] = p;
                     else atomicOr(&b.counters->flags, TRI_OVF_CLIP_QUEUE);
@@ -297,6 +298,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
                     const float iw[3] = {a0.iw, a1.iw, a2.iw};
                     TriRec r;
                     ok = setup_snapped(fp, X, Y, z, iw, sl0, sl1, sl2, p << 3, r, br);
+                    if (ok) b.prim_vs[p] = make_uint4(sl0, sl1, sl2, (uint32_t)d);
                 }
             }
         }
@@ -495,19 +497,6 @@ __device__ __forceinline__ TriRec load_rec(const TriRec* recs, uint32_t i) {
     return r;
 }
 
-// Vertex slots of primitive p (and its draw): the same assembly k_setup performed.
-__device__ __forceinline__ int prim_slots(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t p,
-                                          uint32_t sl[3]) {
-    const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
-    const TriDrawDev& dr = b.draws[d];
-    const uint32_t* ip = b.indices + dr.first_index + 3u * (p - b.draw_pbase[d]);
-    const uint32_t vb = b.draw_vbase[d] - dr.min_index;
-    sl[0] = vb + ip[0];
-    sl[1] = vb + ip[1];
-    sl[2] = vb + ip[2];
-    return d;
-}
-
 // The record setup_snapped produced for an unclipped primitive (v1 <-> v2 swapped), rebuilt from
 // its snapped vertices instead of being stored and re-read.
 __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3], const TriSnap& a0,
@@ -525,8 +514,8 @@ __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3
 // A bin-queue entry -> its triangle.
 __device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
     if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
-    uint32_t sl[3];
-    prim_slots(fp, b, e, sl);
+    const uint4 pv = b.prim_vs[e];
+    const uint32_t sl[3] = {pv.x, pv.y, pv.z};
     return rec_from_snaps(e, sl, b.snap[sl[0]], b.snap[sl[1]], b.snap[sl[2]]);
 }
 
@@ -833,14 +822,14 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
                                                   int32_t px, int32_t py, const float* lut, Put&& put) {
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
-    uint32_t sl[3];
-    const int d = prim_slots(fp, b, prim, sl);
-    const TriSnap s0 = b.snap[sl[0]], s1 = b.snap[sl[1]], s2 = b.snap[sl[2]];
+    const uint4 pv = b.prim_vs[prim];
+    const uint32_t sl[3] = {pv.x, pv.y, pv.z};
+    const int d = (int)(pv.w & ~TRI_PRIM_CLIPPED);
     TriRec r;
-    if ((((uint32_t)(s0.xo | s1.xo | s2.xo)) >> 24) & TRI_OC_CLIP)
+    if (pv.w & TRI_PRIM_CLIPPED)
         r = load_rec(b.recs, b.clip_slot[prim] + (low & 7u));
     else
-        r = rec_from_snaps(prim, sl, s0, s1, s2);
+        r = rec_from_snaps(prim, sl, b.snap[sl[0]], b.snap[sl[1]], b.snap[sl[2]]);
     float l0, l1, l2;
     if (EXACT) {  // exact int64 edge functions (oracle order)
         const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;

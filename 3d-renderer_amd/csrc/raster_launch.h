@@ -22,6 +22,8 @@ struct TriDeviceBuffers {
     float4* vary;                // 3 * (nslots + ovf_vert_cap)
     TriRec* recs;                // ovf_rec_cap clipped sub-triangles
     uint32_t* clip_slot;         // nprims: first sub-triangle record of a clipped primitive
+    uint4* prim_vs;              // nprims: {vertex slot 0, 1, 2, draw | TRI_PRIM_CLIPPED} of every
+                                 // primitive k_setup passed on (visible or sent to k_clip)
     uint32_t* clip_queue;        // ovf_rec_cap primitive ids needing geometric clipping
     uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
     uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)

@@ -124,6 +124,7 @@ struct tri_ctx {
     float4* d_vary = nullptr; size_t cap_vary = 0;
     TriRec* d_recs = nullptr; size_t cap_recs = 0;
     uint32_t* d_clip_slot = nullptr; size_t cap_clip_slot = 0;
+    uint4* d_prim_vs = nullptr; size_t cap_prim_vs = 0;
     uint2* d_setup_stats = nullptr; size_t cap_setup_stats = 0;
     uint32_t last_nchunks = 0;
     uint32_t* d_bin_count = nullptr; size_t cap_bin_count = 0;
@@ -372,7 +373,7 @@ int ensure_work_buffers(tri_ctx* c) {
     if (nvary >= (1ull << 32))  // the kernels index varyings / indices with 32-bit arithmetic
         return fail(TRI_E_INVALID, "too many vertex invocations (%zu varyings)", nvary);
     bool realloc = c->cap_clip < std::max<size_t>(c->nslots, 1) || c->cap_vary < nvary || c->cap_recs < nrec ||
-                   c->cap_clip_slot < std::max<size_t>(c->nprims, 1) ||
+                   c->cap_clip_slot < std::max<size_t>(c->nprims, 1) || c->cap_prim_vs < std::max<size_t>(c->nprims, 1) ||
                    c->cap_bin_list < nlist;
     if (realloc) HIP_TRY(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_clip, c->cap_clip, std::max<size_t>(c->nslots, 1)))) return rc;
@@ -380,6 +381,7 @@ int ensure_work_buffers(tri_ctx* c) {
     if ((rc = grow(c->d_vary, c->cap_vary, nvary))) return rc;
     if ((rc = grow(c->d_recs, c->cap_recs, nrec))) return rc;
     if ((rc = grow(c->d_clip_slot, c->cap_clip_slot, std::max<size_t>(c->nprims, 1)))) return rc;
+    if ((rc = grow(c->d_prim_vs, c->cap_prim_vs, std::max<size_t>(c->nprims, 1)))) return rc;
     if ((rc = grow(c->d_setup_stats, c->cap_setup_stats, (size_t)c->nprims / TRI_BLOCK + 1))) return rc;
     if ((rc = grow(c->d_clip_queue, c->cap_clip_queue, c->ovf_rec_cap))) return rc;
     if ((rc = grow(c->d_bin_list, c->cap_bin_list, nlist))) return rc;
@@ -506,7 +508,7 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones); f(c->d_sky);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_clip_queue); f(c->d_vbase); f(c->d_pbase);
-    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_setup_stats);
+    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
@@ -764,6 +766,7 @@ int tri_render(tri_ctx* c) {
     b.vary = c->d_vary;
     b.recs = c->d_recs;
     b.clip_slot = c->d_clip_slot;
+    b.prim_vs = c->d_prim_vs;
     b.setup_stats = c->d_setup_stats;
     b.bin_count = c->d_bin_count;
     b.bin_list = c->d_bin_list;
