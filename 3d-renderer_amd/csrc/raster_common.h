@@ -106,9 +106,10 @@ struct __attribute__((aligned(16))) TriDrawShade {
     int32_t pad[3];
 };
 
-struct TriTexDesc {
+struct __attribute__((aligned(16))) TriTexDesc {
     const uint32_t* texels;  // RGBA8 sRGB, row-major
     uint32_t w, h;
+    float solid[4];          // 1x1 textures: the decoded texel (every bilinear tap is that texel)
 };
 
 struct TriCounters {  // per-frame fields are zeroed before every frame; `flags`/`bin_max` are sticky
@@ -160,7 +161,8 @@ struct TriFrameParams {
     //                  equal taps returns that texel, so the sky is the constant sky_bgra
     uint32_t sky_mode;
     uint32_t sky_bgra;
-    uint32_t pad_s[2];
+    uint32_t need_lut;  // some texture larger than 1x1 or a sampled skybox: k_raster stages the sRGB LUT
+    uint32_t pad_s;
     float sky_far[16];  // inverse(Projection) applied to (xn, yn, 1, 1): rows {x, y, z, w} as (a, b, c, 0)
     float pv[16];
     float sky_ip[16];   // inverse(Projection) (double on the host, rounded)

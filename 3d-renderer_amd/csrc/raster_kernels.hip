@@ -609,10 +609,8 @@ __device__ __forceinline__ uint32_t wrap_repeat(float f, uint32_t n) {  // REPEA
 
 // texture(): R8G8B8A8_SRGB decode before LINEAR filtering, REPEAT, level 0 (Renderer.cpp:3592-3607)
 __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, float v0, const float* lut) {
-    if (t.w == 1 && t.h == 1) {  // 1x1 (the default white slot): all four taps are texel (0,0)
-        const uint32_t p = t.texels[0];
-        return make_float4(lut[p & 0xFFu], lut[(p >> 8) & 0xFFu], lut[(p >> 16) & 0xFFu], lut[256 + (p >> 24)]);
-    }
+    if (t.w == 1 && t.h == 1)  // 1x1 (the default white slot): all four taps are texel (0,0)
+        return make_float4(t.solid[0], t.solid[1], t.solid[2], t.solid[3]);
     const float u = u0 * (float)t.w - 0.5f;
     const float v = v0 * (float)t.h - 0.5f;
     const float fu = floorf(u), fv = floorf(v);
@@ -1064,7 +1062,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL ==
     const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
     const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);
     for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = kBgKey;
-    for (int i = tid; i < 512; i += TRI_BLOCK) lut[i] = b.srgb_lut[i];
+    if (fp.need_lut)
+        for (int i = tid; i < 512; i += TRI_BLOCK) lut[i] = b.srgb_lut[i];
     if (tid == 0) {
         nbig = 0;
         nsky = 0;

@@ -87,6 +87,7 @@ struct tri_ctx {
     // texture slots; slot 0 = default 1x1 white
     uint32_t* d_tex[TRI_MAX_TEXTURE_SLOTS] = {};
     uint32_t tex_w[TRI_MAX_TEXTURE_SLOTS] = {}, tex_h[TRI_MAX_TEXTURE_SLOTS] = {};
+    uint32_t tex_solid[TRI_MAX_TEXTURE_SLOTS] = {};  // texel of a 1x1 slot (RGBA8)
     TriTexDesc* d_texdesc = nullptr;
     bool tex_dirty = true;
     float* d_lut = nullptr;
@@ -256,6 +257,9 @@ int upload_texture_table(tri_ctx* c) {
         h[s].texels = c->d_tex[src];
         h[s].w = c->tex_w[src];
         h[s].h = c->tex_h[src];
+        const uint32_t p = c->tex_solid[src];
+        for (int k = 0; k < 3; ++k) h[s].solid[k] = srgb_decode((p >> (8 * k)) & 0xFF);
+        h[s].solid[3] = (float)(p >> 24) / 255.0f;  // alpha: linear UNORM decode
     }
     HIP_TRY(hipStreamSynchronize(c->stream));
     HIP_TRY(hipMemcpy(c->d_texdesc, h, sizeof h, hipMemcpyHostToDevice));
@@ -606,6 +610,7 @@ int tri_upload_texture(tri_ctx* c, uint32_t slot, const uint8_t* rgba, uint32_t 
     HIP_TRY(hipMemcpy(c->d_tex[slot], rgba, (size_t)w * h * 4, hipMemcpyHostToDevice));
     c->tex_w[slot] = w;
     c->tex_h[slot] = h;
+    std::memcpy(&c->tex_solid[slot], rgba, 4);
     c->tex_dirty = true;
     return TRI_OK;
 }
@@ -731,12 +736,15 @@ int tri_render(tri_ctx* c) {
         const bool persp = fp.sky_pw[3] == 0.0f;
         fp.sky_mode = !persp ? TRI_SKY_RAY : (c->sky_uniform ? TRI_SKY_UNIFORM : TRI_SKY_PERSP);
         fp.sky_bgra = c->sky_uniform_bgra;
+        fp.need_lut = fp.sky_mode != TRI_SKY_UNIFORM || fp.exact_shading;
         for (int r = 0; r < 4; ++r) {  // inverse(P) * (xn, yn, 1, 1), row r
             fp.sky_far[4 * r + 0] = fp.sky_ip[0 * 4 + r];
             fp.sky_far[4 * r + 1] = fp.sky_ip[1 * 4 + r];
             fp.sky_far[4 * r + 2] = fp.sky_ip[2 * 4 + r] + fp.sky_ip[3 * 4 + r];
         }
     }
+    for (int t = 0; t < TRI_MAX_TEXTURE_SLOTS && !fp.need_lut; ++t)
+        fp.need_lut = c->d_tex[t] && (c->tex_w[t] != 1 || c->tex_h[t] != 1);
     static const uint32_t ablate = [] {  // diagnostics only: TRI_ABLATE=1 no shading, 2 no coverage
         const char* e = getenv("TRI_ABLATE");
         return e ? (uint32_t)atoi(e) : 0u;

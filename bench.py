@@ -113,12 +113,12 @@ class BandRenderer:
     """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers, assembled
     by a GatherRing."""
 
-    def __init__(self, scene, rank, world, device_index):
+    def __init__(self, scene, rank, world, device_index, band_world=None):
         import torch
         from trident_raster import raster, scenes
 
         H, W = scene.height, scene.width
-        self.band = band_rows(H, world, rank)
+        self.band = band_rows(H, band_world or world, rank)
         rows = self.band[1] - self.band[0]
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
         self.dev = torch.device("cuda", device_index)
@@ -227,6 +227,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
+    ap.add_argument("--sim-world", type=int, default=0,
+                    help="diagnostics (1 GPU, no collective): render only band --sim-rank of an N-way split")
+    ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--no-stage-timing", action="store_true",
                     help="diagnostics: no per-kernel HIP events in the timed loop (roofline fields become null)")
     args = ap.parse_args()
@@ -246,7 +249,10 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     scene = build_scene(args.config)
-    br = BandRenderer(scene, rank, world, local)
+    if args.sim_world and world == 1:
+        br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world)
+    else:
+        br = BandRenderer(scene, rank, world, local)
     dt, timing = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing)
     fps = args.steps / dt
     W, H = scene.width, scene.height
