@@ -28,7 +28,6 @@
 #define TRI_MAX_CLIP_VERTS 12
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f
-#define TRI_CLIP_GRID 16
 #define TRI_MAX_PPT 8  // primitives per k_setup thread
 
 #define TRI_SKY_RAY 0u
@@ -39,7 +38,6 @@
 #define TRI_OVF_CLIP_RECORDS 0x1u
 #define TRI_OVF_CLIP_VERTS 0x2u
 #define TRI_OVF_BIN_LIST 0x4u
-#define TRI_OVF_CLIP_QUEUE 0x8u
 
 struct __attribute__((aligned(16))) TriVsIn {
     float px, py, pz, nx;
@@ -118,7 +116,7 @@ struct TriCounters {  // per-frame fields are zeroed before every frame; `flags`
     uint32_t tris_setup;
     uint32_t tris_clipped;
     uint32_t bin_entries;
-    uint32_t clip_queue;
+    uint32_t pad;
     uint32_t bin_max;  // largest per-bin entry count seen (sizes the bin queues after an overflow)
     uint32_t flags;
 };

@@ -4,8 +4,9 @@
 //   k_setup    tri_setup_bin  primitive assembly + trivial reject + cull + bbox on the per-vertex
 //                             snapped coordinates (Pipeline.cpp:611-643), binned into per-bin queues
 //                             (wave-aggregated atomics: one per (wave, bin)); nothing else is stored
-//                             per triangle. Triangles that need homogeneous clipping go to k_clip
-//   k_clip     rare path: Sutherland-Hodgman against w>=WMIN, z>=0 and the guard band + fan
+//                             per triangle. Triangles that need homogeneous clipping (rare) are
+//                             clipped by their wave in place: Sutherland-Hodgman against w>=WMIN,
+//                             z>=0 and the guard band + fan, one primitive per wave at a time
 //   k_raster   tile_raster_shade: one workgroup per 32x32 (or 64x64) bin; coverage + early-Z in LDS
 //              with 64-bit (depth, primitive-order) keys (== in-order LESS_OR_EQUAL,
 //              Pipeline.cpp:655-658), then Default.frag:123-192 once per visible pixel, coalesced
@@ -62,7 +63,7 @@ __device__ __forceinline__ uint32_t outcode(const TriFrameParams& fp, float4 c);
 
 __device__ __forceinline__ void reset_counters(TriCounters* c) {
     c->ovf_records = 0; c->ovf_verts = 0; c->tris_setup = 0; c->tris_clipped = 0;
-    c->bin_entries = 0; c->clip_queue = 0;  // `flags` / `bin_max` are sticky (cleared by the host)
+    c->bin_entries = 0;  // `flags` / `bin_max` are sticky (cleared by the host)
 }
 
 __global__ void k_reset(TriDeviceBuffers b) { reset_counters(b.counters); }
@@ -224,17 +225,6 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// One slot per active lane in a single global queue: one atomic per wave (divergent code is fine).
-__device__ __forceinline__ uint32_t wave_append(uint32_t* counter) {
-    const uint64_t m = __ballot(1);
-    const uint32_t lane = lanes_below(~0ull);
-    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(counter, (uint32_t)__builtin_popcountll(m));
-    base = (uint32_t)__shfl((int)base, (int)leader);
-    return base + lanes_below(m);
-}
-
 __device__ __forceinline__ uint32_t wave_reserve(uint32_t* counts, uint32_t bin, bool want) {
     uint64_t pending = __ballot(want);
     const uint32_t lane = lanes_below(~0ull);
@@ -256,13 +246,156 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* counts, uint32_t bin,
     return base + rank;
 }
 
+// ------------------------------------------------------------------------------------------
+// Homogeneous clipping (oracle clip_polygon: Sutherland-Hodgman against w >= WMIN, z >= 0 and the
+// guard band, then a fan), done by the whole wave for one primitive at a time inside k_setup: lane i
+// holds polygon vertex i, the output order of the sequential algorithm is rebuilt with ballots, and
+// the two polygon buffers live in a per-wave LDS slice. No separate launch, no per-lane arrays.
+// ------------------------------------------------------------------------------------------
+struct ClipVert {
+    float4 c;
+    float b0, b1, b2;  // barycentric weights on the source triangle (for the varyings)
+};
+constexpr int kClipStride = 8;  // floats per LDS polygon vertex
+constexpr int kWavesPerBlock = TRI_BLOCK / 64;
+
+__device__ __forceinline__ ClipVert lerp_cv(const ClipVert& a, const ClipVert& b, float t) {
+    ClipVert o;
+#define L(f) o.f = a.f + t * (b.f - a.f)
+    L(c.x); L(c.y); L(c.z); L(c.w); L(b0); L(b1); L(b2);
+#undef L
+    return o;
+}
+
+__device__ __forceinline__ float plane_dist(const TriFrameParams& fp, int plane, float4 c) {
+    switch (plane) {
+        case 0: return c.w - TRI_WMIN;
+        case 1: return c.z;
+        case 2: return c.x + fp.gx * c.w;
+        case 3: return fp.gx * c.w - c.x;
+        case 4: return c.y + fp.gy * c.w;
+        default: return fp.gy * c.w - c.y;
+    }
+}
+
+__device__ __forceinline__ void cv_store(float* p, const ClipVert& v) {
+    p[0] = v.c.x; p[1] = v.c.y; p[2] = v.c.z; p[3] = v.c.w; p[4] = v.b0; p[5] = v.b1; p[6] = v.b2;
+}
+__device__ __forceinline__ ClipVert cv_load(const float* p) {
+    ClipVert v;
+    v.c = make_float4(p[0], p[1], p[2], p[3]);
+    v.b0 = p[4]; v.b1 = p[5]; v.b2 = p[6];
+    return v;
+}
+// LDS traffic between lanes of one wave: DS instructions of a wave execute in order, so a
+// compiler barrier is all that is needed between a lane's store and another lane's load.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Clip primitive `prim` (vertex slots sl[3]) with the whole wave; lanes that set up a fan
+// sub-triangle bin it. Must be reached by the whole wave.
+__device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const TriDeviceBuffers& b, float* poly,
+                                               uint32_t prim, uint32_t sl0, uint32_t sl1, uint32_t sl2,
+                                               uint32_t& nsetup, uint32_t& nentries) {
+    const uint32_t lane = lanes_below(~0ull);
+    const uint64_t below = (lane == 63) ? 0x7FFFFFFFFFFFFFFFull : ((1ull << lane) - 1ull);
+    float* buf[2] = {poly, poly + TRI_MAX_CLIP_VERTS * kClipStride};
+    if (lane < 3) {
+        ClipVert v;
+        v.c = b.clip[lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2)];
+        v.b0 = lane == 0 ? 1.0f : 0.0f;
+        v.b1 = lane == 1 ? 1.0f : 0.0f;
+        v.b2 = lane == 2 ? 1.0f : 0.0f;
+        cv_store(buf[0] + lane * kClipStride, v);
+    }
+    int n = 3, cur = 0;
+    for (int plane = 0; plane < 6 && n > 0; ++plane) {
+        wave_lds_sync();
+        const bool act = (int)lane < n;
+        ClipVert a{}, nb{};
+        float da = 0.0f, db = 0.0f;
+        if (act) {
+            a = cv_load(buf[cur] + lane * kClipStride);
+            nb = cv_load(buf[cur] + ((int)lane + 1 < n ? lane + 1 : 0) * kClipStride);
+            da = plane_dist(fp, plane, a.c);
+            db = plane_dist(fp, plane, nb.c);
+        }
+        const bool in = act && da >= 0.0f;
+        const bool cross = act && ((da >= 0.0f) != (db >= 0.0f));
+        const uint64_t m_in = __ballot(in), m_cr = __ballot(cross);
+        const int pos = __builtin_popcountll(m_in & below) + __builtin_popcountll(m_cr & below);
+        wave_lds_sync();
+        if (in && pos < TRI_MAX_CLIP_VERTS) cv_store(buf[cur ^ 1] + pos * kClipStride, a);
+        const int pos2 = pos + (in ? 1 : 0);
+        if (cross && pos2 < TRI_MAX_CLIP_VERTS) {
+            const float t = da / (da - db);
+            cv_store(buf[cur ^ 1] + pos2 * kClipStride, lerp_cv(a, nb, t));
+        }
+        n = min(__builtin_popcountll(m_in) + __builtin_popcountll(m_cr), TRI_MAX_CLIP_VERTS);
+        cur ^= 1;
+    }
+    wave_lds_sync();
+    if (n < 3) return;
+    const uint32_t nsub = (uint32_t)(n - 2);
+    uint32_t rbase = 0, vbase = 0;
+    if (lane == 0) {
+        rbase = atomicAdd(&b.counters->ovf_records, nsub);
+        vbase = atomicAdd(&b.counters->ovf_verts, (uint32_t)n);
+    }
+    rbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)rbase);
+    vbase = (uint32_t)__builtin_amdgcn_readfirstlane((int)vbase);
+    if (rbase + nsub > fp.ovf_rec_cap || vbase + (uint32_t)n > fp.ovf_vert_cap) {
+        if (lane == 0)
+            atomicOr(&b.counters->flags, (rbase + nsub > fp.ovf_rec_cap) ? TRI_OVF_CLIP_RECORDS : TRI_OVF_CLIP_VERTS);
+        return;
+    }
+    const uint32_t sbase = fp.nslots + vbase;
+    const float* src = buf[cur];
+    if ((int)lane < n) {  // varyings of polygon vertex `lane` from the source triangle's barycentrics
+        const ClipVert s = cv_load(src + lane * kClipStride);
+        const float4* v0 = b.vary + 3u * sl0;
+        const float4* v1 = b.vary + 3u * sl1;
+        const float4* v2 = b.vary + 3u * sl2;
+        float4* vo = b.vary + 3u * (sbase + lane);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) {
+            const float4 x = v0[j], y = v1[j], z = v2[j];
+            vo[j] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
+                                (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, (s.b0 * x.w + s.b1 * y.w) + s.b2 * z.w);
+        }
+    }
+    if (lane == 0) b.clip_slot[prim] = rbase;  // k_raster's fragment fetch finds sub-triangle `sub` here
+    if (lane < nsub) {  // fan sub-triangle k = lane + 1: (v0, vk, vk+1)
+        const uint32_t k = lane + 1;
+        TriRec r;
+        uint2 br;
+        const uint32_t ps = (prim << 3) | (k - 1);
+        const uint32_t rid = rbase + k - 1;
+        const float4 c0 = cv_load(src).c, ck = cv_load(src + k * kClipStride).c,
+                     ck1 = cv_load(src + (k + 1) * kClipStride).c;
+        if (setup_from_clip(fp, c0, ck, ck1, sbase, sbase + k, sbase + k + 1, ps, r, br)) {
+            ++nsetup;
+            b.recs[rid] = r;
+            for_bins(br, fp.nbx, [&](uint32_t bi) {  // rare path: one global atomic per entry
+                const uint32_t pos = atomicAdd(&b.bin_count[bi], 1u);
+                if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = TRI_ENTRY_CLIPPED | rid;
+                else note_bin_overflow(b, pos + 1);
+                ++nentries;
+            });
+        }
+    }
+}
+
 // One lane per primitive (ppt primitives per lane): assembly from the snapped vertices, trivial
 // reject, cull, bbox, then one bin-queue entry per touched bin via wave_reserve. Nothing else is
 // written for a visible triangle: k_raster rebuilds it from `snap`. Triangles needing homogeneous
-// clipping go to the clip queue for k_clip. Entry order inside a bin is free: k_raster resolves
-// visibility with (depth, primitive order) keys.
+// clipping are clipped right here by their wave (clip_prim_wave). Entry order inside a bin is free:
+// k_raster resolves visibility with (depth, primitive order) keys.
 __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t red[2];
+    __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
     __syncthreads();
     uint32_t nsetup = 0, nentries = 0;
@@ -274,23 +407,22 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
     const uint32_t chunk0 = chunk * (uint32_t)(TRI_BLOCK * fp.ppt);
     for (int k = 0; k < fp.ppt; ++k) {  // uniform trip count: wave_reserve needs the whole wave
         const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
-        bool ok = false;
+        bool ok = false, needs_clip = false;
+        uint32_t sl0 = 0, sl1 = 0, sl2 = 0;
         uint2 br = make_uint2(0u, 0u);
         if (p < fp.nprims) {
             const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
             const TriDrawDev& dr = b.draws[d];
             const uint32_t* ip = b.indices + dr.first_index + 3u * (p - b.draw_pbase[d]);
             const uint32_t vb = b.draw_vbase[d] - dr.min_index;
-            const uint32_t sl0 = vb + ip[0], sl1 = vb + ip[1], sl2 = vb + ip[2];
+            sl0 = vb + ip[0]; sl1 = vb + ip[1]; sl2 = vb + ip[2];
             const TriSnap a0 = b.snap[sl0], a1 = b.snap[sl1], a2 = b.snap[sl2];
             const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
             // invalid vertex, or trivial reject: all three vertices outside one clip half-space
             if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
                 if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
                     b.prim_vs[p] = make_uint4(sl0, sl1, sl2, (uint32_t)d | TRI_PRIM_CLIPPED);
-                    const uint32_t q = wave_append(&b.counters->clip_queue);
-                    if (q < fp.ovf_rec_cap) b.clip_queue[q] = p;
-                    else atomicOr(&b.counters->flags, TRI_OVF_CLIP_QUEUE);
+                    needs_clip = true;
                 } else {
                     const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
                     const int32_t Y[3] = {a0.y, a1.y, a2.y};
@@ -303,6 +435,19 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
             }
         }
         nsetup += ok ? 1u : 0u;
+        uint64_t cm = __ballot(needs_clip);  // rare: the wave clips its primitives one at a time
+        if (cm) {
+            if (lanes_below(~0ull) == 0) atomicAdd(&b.counters->tris_clipped, (uint32_t)__builtin_popcountll(cm));
+            float* poly = clip_poly[threadIdx.x >> 6];
+            while (cm) {
+                const int src = __builtin_ctzll(cm);
+                cm &= cm - 1;
+                clip_prim_wave(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p, src),
+                               (uint32_t)__builtin_amdgcn_readlane((int)sl0, src),
+                               (uint32_t)__builtin_amdgcn_readlane((int)sl1, src),
+                               (uint32_t)__builtin_amdgcn_readlane((int)sl2, src), nsetup, nentries);
+            }
+        }
         uint32_t bx = br.x & 0xFFFFu, by = br.x >> 16;
         const uint32_t bx0 = bx, bx1 = br.y & 0xFFFFu, by1 = br.y >> 16;
         bool has = ok && !(fp.ablate & 4);  // diagnostics: 4 = setup without binning
@@ -332,117 +477,6 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
     // Statistics go to a per-workgroup slot with a plain store: same-address global atomics from
     // every workgroup serialise across the XCDs (measured: +34 us per frame at 4K/1M).
     if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(red[0], red[1]);
-}
-
-// ------------------------------------------------------------------------------------------
-// k_clip: homogeneous Sutherland-Hodgman + fan (oracle clip_polygon), rare path
-// ------------------------------------------------------------------------------------------
-struct ClipVert {
-    float4 c;
-    float b0, b1, b2;
-};
-
-__device__ __forceinline__ ClipVert lerp_cv(const ClipVert& a, const ClipVert& b, float t) {
-    ClipVert o;
-#define L(f) o.f = a.f + t * (b.f - a.f)
-    L(c.x); L(c.y); L(c.z); L(c.w); L(b0); L(b1); L(b2);
-#undef L
-    return o;
-}
-
-__device__ __forceinline__ float plane_dist(const TriFrameParams& fp, int plane, float4 c) {
-    switch (plane) {
-        case 0: return c.w - TRI_WMIN;
-        case 1: return c.z;
-        case 2: return c.x + fp.gx * c.w;
-        case 3: return fp.gx * c.w - c.x;
-        case 4: return c.y + fp.gy * c.w;
-        default: return fp.gy * c.w - c.y;
-    }
-}
-
-__global__ __launch_bounds__(TRI_BLOCK) void k_clip(TriFrameParams fp, TriDeviceBuffers b) {
-    const uint32_t nq = min(b.counters->clip_queue, fp.ovf_rec_cap);
-    uint32_t nsetup = 0, nentries = 0;
-    for (uint32_t q = blockIdx.x * TRI_BLOCK + threadIdx.x; q < nq; q += gridDim.x * TRI_BLOCK) {
-        const uint32_t prim = b.clip_queue[q];
-        const int d = find_range(b.draw_pbase, (int)fp.ndraws, prim);
-        const TriDrawDev& dr = b.draws[d];
-        const uint32_t* ip = b.indices + dr.first_index + 3u * (prim - b.draw_pbase[d]);
-        const uint32_t vb = b.draw_vbase[d] - dr.min_index;
-        uint32_t srcv[3];
-        // polygon vertex = clip position (lerped exactly like the oracle: depth stays bit-exact) +
-        // barycentric weights on the source triangle (for the varyings: colour-only effect)
-        ClipVert buf[2][TRI_MAX_CLIP_VERTS];
-        for (int k = 0; k < 3; ++k) {
-            srcv[k] = vb + ip[k];
-            buf[0][k].c = b.clip[srcv[k]];
-            buf[0][k].b0 = k == 0 ? 1.0f : 0.0f;
-            buf[0][k].b1 = k == 1 ? 1.0f : 0.0f;
-            buf[0][k].b2 = k == 2 ? 1.0f : 0.0f;
-        }
-        int n = 3, cur = 0;
-        for (int plane = 0; plane < 6 && n > 0; ++plane) {
-            int m = 0;
-            for (int i = 0; i < n; ++i) {
-                const ClipVert a = buf[cur][i];
-                const ClipVert bb = buf[cur][i + 1 < n ? i + 1 : 0];
-                const float da = plane_dist(fp, plane, a.c), db = plane_dist(fp, plane, bb.c);
-                if (da >= 0.0f && m < TRI_MAX_CLIP_VERTS) buf[cur ^ 1][m++] = a;
-                if ((da >= 0.0f) != (db >= 0.0f) && m < TRI_MAX_CLIP_VERTS) {
-                    const float t = da / (da - db);
-                    buf[cur ^ 1][m++] = lerp_cv(a, bb, t);
-                }
-            }
-            n = m;
-            cur ^= 1;
-        }
-        const ClipVert* src = buf[cur];
-        if (n >= 3) {
-            const uint32_t nsub = (uint32_t)(n - 2);
-            const uint32_t rbase = atomicAdd(&b.counters->ovf_records, nsub);
-            const uint32_t vbase = atomicAdd(&b.counters->ovf_verts, (uint32_t)n);
-            if (rbase + nsub > fp.ovf_rec_cap || vbase + (uint32_t)n > fp.ovf_vert_cap) {
-                atomicOr(&b.counters->flags,
-                         (rbase + nsub > fp.ovf_rec_cap) ? TRI_OVF_CLIP_RECORDS : TRI_OVF_CLIP_VERTS);
-            } else {
-                const uint32_t sbase = fp.nslots + vbase;
-                const float4* v0 = b.vary + 3u * srcv[0];
-                const float4* v1 = b.vary + 3u * srcv[1];
-                const float4* v2 = b.vary + 3u * srcv[2];
-                for (int k = 0; k < n; ++k) {
-                    float4* vo = b.vary + 3u * (sbase + k);
-                    const ClipVert& s = src[k];
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) {
-                        const float4 x = v0[j], y = v1[j], z = v2[j];
-                        vo[j] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
-                                            (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, (s.b0 * x.w + s.b1 * y.w) + s.b2 * z.w);
-                    }
-                }
-                b.clip_slot[prim] = rbase;  // k_raster's fragment fetch finds sub-triangle `sub` here
-                for (int k = 1; k + 1 < n; ++k) {
-                    TriRec r;
-                    uint2 br;
-                    const uint32_t ps = (prim << 3) | (uint32_t)(k - 1);
-                    const uint32_t rid = rbase + k - 1;
-                    if (setup_from_clip(fp, src[0].c, src[k].c, src[k + 1].c, sbase, sbase + k, sbase + k + 1, ps, r,
-                                        br)) {
-                        ++nsetup;
-                        b.recs[rid] = r;
-                        for_bins(br, fp.nbx, [&](uint32_t bi) {  // rare path: one global atomic per entry
-                            const uint32_t pos = atomicAdd(&b.bin_count[bi], 1u);
-                            if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = TRI_ENTRY_CLIPPED | rid;
-                            else note_bin_overflow(b, pos + 1);
-                            ++nentries;
-                        });
-                    }
-                }
-            }
-        }
-    }
-    if (nsetup) atomicAdd(&b.counters->tris_setup, nsetup);
-    if (nentries) atomicAdd(&b.counters->bin_entries, nentries);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1205,8 +1239,7 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
     rec(kStageSetup);
     if (fp.nchunks > 0) hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
-    rec(kStageClip);
-    if (fp.nchunks > 0) hipLaunchKernelGGL(k_clip, dim3(TRI_CLIP_GRID), dim3(TRI_BLOCK), 0, stream, fp, b);
+    rec(kStageClip);  // clipping runs inside k_setup: this stage is empty
     rec(kStageRaster);
     const dim3 g(fp.nbins), t(TRI_BLOCK);
     if (fp.bin_log2 == 5) {

@@ -17,14 +17,13 @@ struct TriDeviceBuffers {
     const TriTexDesc* textures;  // TRI_MAX_TEXTURE_SLOTS entries, aliases resolved
     const uint32_t* sky;         // 6 * sky_size^2 RGBA8 sRGB texels (+X,-X,+Y,-Y,+Z,-Z)
     const float* srgb_lut;       // 256 sRGB -> linear (host, double) + 256 alpha b/255
-    float4* clip;                // nslots (read only by k_clip)
+    float4* clip;                // nslots (read only when a primitive is clipped)
     TriSnap* snap;               // nslots
     float4* vary;                // 3 * (nslots + ovf_vert_cap)
     TriRec* recs;                // ovf_rec_cap clipped sub-triangles
     uint32_t* clip_slot;         // nprims: first sub-triangle record of a clipped primitive
     uint4* prim_vs;              // nprims: {vertex slot 0, 1, 2, draw | TRI_PRIM_CLIPPED} of every
-                                 // primitive k_setup passed on (visible or sent to k_clip)
-    uint32_t* clip_queue;        // ovf_rec_cap primitive ids needing geometric clipping
+                                 // primitive k_setup passed on (visible or clipped)
     uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
     uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)
     TriCounters* counters;
@@ -37,7 +36,7 @@ enum TriStage { kStageVertex = 0, kStageSetup, kStageClip, kStageRaster, kStageC
 
 hipError_t tri_kernels_init();
 
-// One frame = 4 dependent launches on `stream`; `events` (may be null) gets kStageCount+1 stamps:
-// [vertex | setup+binning | clip | raster].
+// One frame = 3 dependent launches on `stream` (k_vertex, k_setup with in-wave clipping, k_raster);
+// `events` (may be null) gets kStageCount+1 stamps: [vertex | setup+binning+clip | (empty) | raster].
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* events);

@@ -110,7 +110,6 @@ struct tri_ctx {
     // resolved draws
     TriDrawDev* d_draws = nullptr; size_t cap_draws = 0;
     TriDrawShade* d_draw_shade = nullptr; size_t cap_draw_shade = 0;
-    uint32_t* d_clip_queue = nullptr; size_t cap_clip_queue = 0;
     uint32_t* d_vbase = nullptr; size_t cap_vbase = 0;
     uint32_t* d_pbase = nullptr; size_t cap_pbase = 0;
     void* h_stage = nullptr; size_t cap_stage = 0;  // pinned upload staging
@@ -387,7 +386,6 @@ int ensure_work_buffers(tri_ctx* c) {
     if ((rc = grow(c->d_clip_slot, c->cap_clip_slot, std::max<size_t>(c->nprims, 1)))) return rc;
     if ((rc = grow(c->d_prim_vs, c->cap_prim_vs, std::max<size_t>(c->nprims, 1)))) return rc;
     if ((rc = grow(c->d_setup_stats, c->cap_setup_stats, (size_t)c->nprims / TRI_BLOCK + 1))) return rc;
-    if ((rc = grow(c->d_clip_queue, c->cap_clip_queue, c->ovf_rec_cap))) return rc;
     if ((rc = grow(c->d_bin_list, c->cap_bin_list, nlist))) return rc;
     return TRI_OK;
 }
@@ -417,7 +415,7 @@ int check_overflow(tri_ctx* c) {
     if (!h.flags) return TRI_OK;
     const uint32_t zero = 0;
     HIP_TRY(hipMemcpy(&c->d_ctr->flags, &zero, 4, hipMemcpyHostToDevice));
-    if (h.flags & (TRI_OVF_CLIP_RECORDS | TRI_OVF_CLIP_QUEUE)) c->ovf_rec_cap *= 4;
+    if (h.flags & TRI_OVF_CLIP_RECORDS) c->ovf_rec_cap *= 4;
     if (h.flags & TRI_OVF_CLIP_VERTS) c->ovf_vert_cap *= 4;
     if (h.flags & TRI_OVF_BIN_LIST) {
         c->bin_cap = std::max<uint32_t>(c->bin_cap * 2, h.bin_max + h.bin_max / 4);
@@ -511,7 +509,7 @@ int tri_destroy(tri_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones); f(c->d_sky);
     for (auto& t : c->d_tex) f(t);
-    f(c->d_draws); f(c->d_draw_shade); f(c->d_clip_queue); f(c->d_vbase); f(c->d_pbase);
+    f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase);
     f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own);
@@ -763,7 +761,6 @@ int tri_render(tri_ctx* c) {
     b.indices = c->d_idx;
     b.draws = c->d_draws;
     b.draw_shade = c->d_draw_shade;
-    b.clip_queue = c->d_clip_queue;
     b.draw_vbase = c->d_vbase;
     b.draw_pbase = c->d_pbase;
     b.textures = c->d_texdesc;
@@ -852,13 +849,13 @@ int tri_get_frame_stats(tri_ctx* c, tri_frame_stats* out) {
     out->triangles_in = c->nprims;
     std::vector<uint2> ws(c->last_nchunks);
     if (!ws.empty()) HIP_TRY(hipMemcpy(ws.data(), c->d_setup_stats, ws.size() * sizeof(uint2), hipMemcpyDeviceToHost));
-    uint64_t setup = h.tris_setup, entries = h.bin_entries;  // k_clip's share
+    uint64_t setup = h.tris_setup, entries = h.bin_entries;  // per-frame counters (0 unless a kernel adds)
     for (const uint2& w : ws) {
         setup += w.x;
         entries += w.y;
     }
     out->triangles_setup = setup;
-    out->triangles_clipped = h.clip_queue;
+    out->triangles_clipped = h.tris_clipped;
     out->bin_entries = entries;
     out->vertices_shaded = c->nslots;
     out->bins_x = (uint32_t)c->nbx;
