@@ -784,8 +784,11 @@ struct PbrPix {
 __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const PbrPix& px, f3 L, f3 rad, float scale,
                                               f3& c) {
 #pragma clang fp contract(fast)  // fast build only: FMA contraction is inside the 1-LSB budget
-    const float LdotV = fdot(L, px.V);
     const float NdotLr = fdot(px.N, L);
+    // N.L <= 0 makes the light's weight 0 and every term finite: c + X * 0 == c exactly, so a wave
+    // whose lanes all face away skips the rest (Default.frag evaluates it to the same zero)
+    if (!(NdotLr > 0.0f)) return;
+    const float LdotV = fdot(L, px.V);
     const float ih = frsq(fmaxf(__builtin_fmaf(2.0f, LdotV, 2.0f), 1e-30f));
     const float NdotH = fmaxf((px.NdotVr + NdotLr) * ih, 0.0f);
     const float HdotV = fmaxf(__builtin_fmaf(LdotV, ih, ih), 0.0f);
@@ -832,6 +835,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         if (d2 <= 1e-8f) continue;  // dist <= 1e-4
         const float inv = frsq(d2);
         const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
+        if (!(att0 > 0.0f)) continue;  // beyond the light's range: (1 - d/r)^2 = 0 adds exactly nothing
         eval_pbr_fast(sc, px, muls(to, inv), mk(sc.pl_rad[i][0], sc.pl_rad[i][1], sc.pl_rad[i][2]), att0 * att0, c);
     }
     const float g = 1.0f / 2.2f;
