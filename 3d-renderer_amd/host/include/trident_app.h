@@ -51,6 +51,23 @@ int trident_app_set_clear_color(trident_app* app, const float rgba[4]);
 /* Renderer::SetSkyboxCubemap: faces [6][size][size] RGBA8 sRGB (+X,-X,+Y,-Y,+Z,-Z). */
 int trident_app_set_skybox(trident_app* app, const uint8_t* faces, uint32_t size);
 
+/* Model import as Forge's drop handler (ModelLoader: .obj/.mtl, .gltf, .glb): entities per mesh
+ * instance. Up to `capacity` spawned entity ids go to `entities`; *count gets how many were spawned. */
+int trident_app_import_model(trident_app* app, const char* path, uint32_t* entities, uint32_t capacity,
+                             uint32_t* count);
+/* `.trident` scene files (Scene::Save / Scene::Load, ECS/Scene.cpp:80-151). Load replaces every
+ * entity and rebuilds imported geometry from the SourceAsset paths; *entity_count may be null. */
+int trident_app_save_scene(trident_app* app, const char* path, const char* scene_name);
+int trident_app_load_scene(trident_app* app, const char* path, uint32_t* entity_count);
+/* The runtime camera follows the scene's primary CameraComponent entity (the first camera entity
+ * when none is primary): Transform position / rotation, projection, field of view, clip planes. */
+int trident_app_use_scene_camera(trident_app* app);
+/* Component inspection for tests: Transform (9 floats) and MeshComponent {mesh_index, primitive,
+ * source mesh index} of an entity; TRI_E_INVALID when absent. */
+int trident_app_entity_transform(trident_app* app, uint32_t entity, float out[9]);
+int trident_app_entity_mesh(trident_app* app, uint32_t entity, uint64_t out[3]);
+int trident_app_entity_count(trident_app* app, uint32_t* count);
+
 int trident_app_draw_frame(trident_app* app);
 int trident_app_read_pixels(trident_app* app, uint32_t viewport_id, uint8_t* rgba, float* depth /* nullable */);
 

@@ -7,6 +7,7 @@
 // and frame timing (:6286-6343). Vulkan command recording is replaced by tri_set_frame /
 // tri_set_draws / tri_render on one tri_ctx per viewport.
 #include "trident/Renderer.h"
+#include "trident/ModelLoader.h"
 
 #include <algorithm>
 #include <cmath>
@@ -324,9 +325,16 @@ int32_t Renderer::ResolveTextureSlot(const std::string& texturePath) {
     if (key.empty()) return 0;
     auto it = m_TextureSlotLookup.find(key);
     if (it != m_TextureSlotLookup.end()) return static_cast<int32_t>(it->second);
-    // No image decoder is linked on this path (stb is not vendored): unknown paths fall back to the
-    // default slot, exactly like a failed load in the reference (Renderer.cpp:3740-3745).
-    LogError("ResolveTextureSlot", (key + " not uploaded; using the default slot").c_str());
+    // Load on first use (ResolveTextureSlot -> TextureLoader::Load, Renderer.cpp:3700-3745). Formats
+    // stb would decode but that are not restated here (PNG, JPEG) fail like a failed load in the
+    // reference: the default slot (:3740-3745).
+    const Loader::TextureData data = Loader::TextureLoader::Load(key);
+    if (data.Width > 0) {
+        UploadTexture(key, data);
+        it = m_TextureSlotLookup.find(key);
+        if (it != m_TextureSlotLookup.end()) return static_cast<int32_t>(it->second);
+    }
+    LogError("ResolveTextureSlot", (key + " could not be loaded; using the default slot").c_str());
     m_TextureSlotLookup.emplace(key, 0u);
     return 0;
 }

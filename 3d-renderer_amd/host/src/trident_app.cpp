@@ -6,8 +6,10 @@
 #include <cstring>
 #include <exception>
 #include <string>
+#include <vector>
 
 #include "trident/Renderer.h"
+#include "trident/SceneFile.h"
 
 using namespace Trident;
 
@@ -209,6 +211,97 @@ int trident_app_set_skybox(trident_app* app, const uint8_t* faces, uint32_t size
         d.m_Width = d.m_Height = size;
         d.m_PixelData.assign(faces, faces + 6ull * size * size * 4);
         return app->renderer.SetSkyboxCubemap(d) ? TRI_OK : TRI_E_INVALID;
+    });
+}
+
+int trident_app_import_model(trident_app* app, const char* path, uint32_t* entities, uint32_t capacity,
+                             uint32_t* count) {
+    return Guard(app, [&] {
+        if (!path) return TRI_E_INVALID;
+        std::vector<ECS::Entity> spawned;
+        const bool ok = ImportModel(app->renderer, app->registry, path, &spawned);
+        if (count) *count = (uint32_t)spawned.size();
+        for (size_t i = 0; entities && i < spawned.size() && i < capacity; ++i) entities[i] = spawned[i];
+        return ok ? TRI_OK : TRI_E_INVALID;
+    });
+}
+
+int trident_app_save_scene(trident_app* app, const char* path, const char* scene_name) {
+    return Guard(app, [&] {
+        if (!path) return TRI_E_INVALID;
+        Scene scene(app->registry, &app->renderer, scene_name ? scene_name : "Untitled");
+        scene.Save(path);
+        return TRI_OK;
+    });
+}
+
+int trident_app_load_scene(trident_app* app, const char* path, uint32_t* entity_count) {
+    return Guard(app, [&] {
+        if (!path) return TRI_E_INVALID;
+        Scene scene(app->registry, &app->renderer);
+        if (!scene.Load(path)) return TRI_E_INVALID;
+        if (entity_count) *entity_count = (uint32_t)scene.GetLoadedEntityCount();
+        return TRI_OK;
+    });
+}
+
+int trident_app_use_scene_camera(trident_app* app) {
+    return Guard(app, [&] {
+        ECS::Entity chosen = 0;
+        bool found = false;
+        for (ECS::Entity e : app->registry.GetEntities()) {
+            if (!app->registry.HasComponent<CameraComponent>(e)) continue;
+            if (!found || app->registry.GetComponent<CameraComponent>(e).m_Primary) {
+                const bool primary = app->registry.GetComponent<CameraComponent>(e).m_Primary;
+                if (!found || primary) chosen = e;
+                found = true;
+                if (primary) break;
+            }
+        }
+        if (!found) return TRI_E_INVALID;
+        const CameraComponent& c = app->registry.GetComponent<CameraComponent>(chosen);
+        RuntimeCamera& cam = app->runtime;
+        if (app->registry.HasComponent<Transform>(chosen)) {
+            const Transform& t = app->registry.GetComponent<Transform>(chosen);
+            cam.SetPosition(t.Position);
+            cam.SetRotation(t.Rotation);
+        }
+        cam.SetProjectionType(c.m_ProjectionType);
+        cam.SetFieldOfView(c.m_FieldOfView);
+        cam.SetOrthographicSize(c.m_OrthographicSize);
+        cam.SetClipPlanes(c.m_NearClip, c.m_FarClip);
+        app->renderer.SetRuntimeCameraReady(true);
+        return TRI_OK;
+    });
+}
+
+int trident_app_entity_transform(trident_app* app, uint32_t entity, float out[9]) {
+    return Guard(app, [&] {
+        if (!out || !app->registry.HasComponent<Transform>(entity)) return TRI_E_INVALID;
+        const Transform& t = app->registry.GetComponent<Transform>(entity);
+        const float v[9] = {t.Position.x, t.Position.y, t.Position.z, t.Rotation.x, t.Rotation.y,
+                            t.Rotation.z, t.Scale.x, t.Scale.y, t.Scale.z};
+        std::memcpy(out, v, sizeof v);
+        return TRI_OK;
+    });
+}
+
+int trident_app_entity_mesh(trident_app* app, uint32_t entity, uint64_t out[3]) {
+    return Guard(app, [&] {
+        if (!out || !app->registry.HasComponent<MeshComponent>(entity)) return TRI_E_INVALID;
+        const MeshComponent& m = app->registry.GetComponent<MeshComponent>(entity);
+        out[0] = (uint64_t)m.m_MeshIndex;
+        out[1] = (uint64_t)m.m_Primitive;
+        out[2] = (uint64_t)m.m_SourceMeshIndex;
+        return TRI_OK;
+    });
+}
+
+int trident_app_entity_count(trident_app* app, uint32_t* count) {
+    return Guard(app, [&] {
+        if (!count) return TRI_E_INVALID;
+        *count = (uint32_t)app->registry.GetEntities().size();
+        return TRI_OK;
     });
 }
 

@@ -42,6 +42,13 @@ _APP_FUNCTIONS = [
                                        C.POINTER(C.c_size_t), C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("trident_app_materials", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
     ("trident_app_frame_timing", C.c_int, [C.c_void_p, C.POINTER(C.c_double)]),
+    ("trident_app_import_model", C.c_int, [C.c_void_p, C.c_char_p, C.c_void_p, C.c_uint32, C.POINTER(C.c_uint32)]),
+    ("trident_app_save_scene", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p]),
+    ("trident_app_load_scene", C.c_int, [C.c_void_p, C.c_char_p, C.POINTER(C.c_uint32)]),
+    ("trident_app_use_scene_camera", C.c_int, [C.c_void_p]),
+    ("trident_app_entity_transform", C.c_int, [C.c_void_p, C.c_uint32, _f3]),
+    ("trident_app_entity_mesh", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]),
+    ("trident_app_entity_count", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
 ]
 
 _lib = None
@@ -185,3 +192,38 @@ class TridentApp:
         _check(self._lib.trident_app_frame_timing(self._h, out), "frame_timing")
         keys = ("min_ms", "max_ms", "avg_ms", "min_fps", "max_fps", "avg_fps", "samples")
         return dict(zip(keys, list(out)))
+
+    # ---- ingestion: ModelLoader + .trident scenes ----
+    def import_model(self, path, capacity=4096):
+        ents = (C.c_uint32 * capacity)()
+        n = C.c_uint32()
+        _check(self._lib.trident_app_import_model(self._h, str(path).encode(), ents, capacity, C.byref(n)),
+               f"import_model({path})")
+        return list(ents[: min(n.value, capacity)])
+
+    def save_scene(self, path, name="Untitled"):
+        _check(self._lib.trident_app_save_scene(self._h, str(path).encode(), name.encode()), "save_scene")
+
+    def load_scene(self, path):
+        n = C.c_uint32()
+        _check(self._lib.trident_app_load_scene(self._h, str(path).encode(), C.byref(n)), f"load_scene({path})")
+        return n.value
+
+    def use_scene_camera(self):
+        _check(self._lib.trident_app_use_scene_camera(self._h), "use_scene_camera")
+
+    def entity_transform(self, entity):
+        out = (C.c_float * 9)()
+        _check(self._lib.trident_app_entity_transform(self._h, entity, out), "entity_transform")
+        v = list(out)
+        return tuple(v[0:3]), tuple(v[3:6]), tuple(v[6:9])
+
+    def entity_mesh(self, entity):
+        out = (C.c_uint64 * 3)()
+        _check(self._lib.trident_app_entity_mesh(self._h, entity, out), "entity_mesh")
+        return {"mesh_index": out[0], "primitive": out[1], "source_mesh_index": out[2]}
+
+    def entity_count(self):
+        n = C.c_uint32()
+        _check(self._lib.trident_app_entity_count(self._h, C.byref(n)), "entity_count")
+        return n.value
