@@ -1221,6 +1221,39 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL ==
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// presentation blit (Renderer.cpp:5346-5361, vkCmdBlitImage with VK_FILTER_LINEAR): one lane per
+// destination texel; the source coordinate of its centre is (x + 0.5) * (W / dw), filtered
+// bilinearly over clamp-to-edge taps on UNORM values (b / 255), rounded to UNORM8. Same float
+// operation order as the oracle's blit_linear (bit-exact). Rows are coalesced per wave.
+// ------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__ src, int32_t w, int32_t h,
+                                                    uint32_t* __restrict__ dst, int32_t dw, int32_t dh, float sx,
+                                                    float sy, const float* __restrict__ lut) {
+    const int32_t x = (int32_t)(blockIdx.x * 64 + (threadIdx.x & 63));
+    const int32_t y = (int32_t)(blockIdx.y * 4 + (threadIdx.x >> 6));
+    if (x >= dw || y >= dh) return;
+    const float u = ((float)x + 0.5f) * sx - 0.5f;
+    const float v = ((float)y + 0.5f) * sy - 0.5f;
+    const float fu = floorf(u), fv = floorf(v);
+    const float a = u - fu, bb = v - fv;
+    const int32_t i0 = (int32_t)fu, j0 = (int32_t)fv;
+    const int32_t xa = min(max(i0, 0), w - 1), xb = min(max(i0 + 1, 0), w - 1);
+    const int32_t ya = min(max(j0, 0), h - 1), yb = min(max(j0 + 1, 0), h - 1);
+    const uint32_t p00 = src[(size_t)ya * w + xa], p10 = src[(size_t)ya * w + xb];
+    const uint32_t p01 = src[(size_t)yb * w + xa], p11 = src[(size_t)yb * w + xb];
+    uint32_t out = 0;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const float t00 = lut[(p00 >> (8 * c)) & 0xFFu], t10 = lut[(p10 >> (8 * c)) & 0xFFu];
+        const float t01 = lut[(p01 >> (8 * c)) & 0xFFu], t11 = lut[(p11 >> (8 * c)) & 0xFFu];
+        const float l0 = t00 + a * (t10 - t00);
+        const float l1 = t01 + a * (t11 - t01);
+        out |= unorm8(l0 + bb * (l1 - l0)) << (8 * c);
+    }
+    dst[(size_t)y * dw + x] = out;
+}
+
 }  // namespace
 
 hipError_t tri_kernels_init() { return hipSuccess; }
@@ -1254,5 +1287,13 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         else hipLaunchKernelGGL((k_raster<false, 6>), g, t, 0, stream, fp, b);
     }
     rec(kStageCount);
+    return hipGetLastError();
+}
+
+hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* dst, int32_t dw, int32_t dh,
+                           const float* unorm_lut, hipStream_t stream) {
+    const float sx = (float)w / (float)dw, sy = (float)h / (float)dh;
+    const dim3 g((uint32_t)((dw + 63) / 64), (uint32_t)((dh + 3) / 4));
+    hipLaunchKernelGGL(k_blit, g, dim3(TRI_BLOCK), 0, stream, src, w, h, dst, dw, dh, sx, sy, unorm_lut);
     return hipGetLastError();
 }

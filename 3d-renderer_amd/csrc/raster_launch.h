@@ -40,3 +40,7 @@ hipError_t tri_kernels_init();
 // `events` (may be null) gets kStageCount+1 stamps: [vertex | setup+binning+clip | (empty) | raster].
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* events);
+
+// Presentation blit (tri_blit_linear): src W x H B8G8R8A8 -> dst dw x dh, linear, clamp-to-edge.
+hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* dst, int32_t dw, int32_t dh,
+                           const float* unorm_lut, hipStream_t stream);

@@ -135,6 +135,8 @@ struct tri_ctx {
 
     uint32_t* d_color_own = nullptr;
     float* d_depth_own = nullptr;
+    uint32_t* d_present = nullptr; size_t cap_present = 0;  // tri_blit_linear's owned target
+    uint32_t present_w = 0, present_h = 0;
     uint32_t* d_color = nullptr;
     float* d_depth = nullptr;
 
@@ -512,7 +514,7 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase);
     f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
-    f(c->d_color_own); f(c->d_depth_own);
+    f(c->d_color_own); f(c->d_depth_own); f(c->d_present);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stage_free) (void)hipEventDestroy(c->stage_free);
     for (auto& v : {std::cref(c->pending), std::cref(c->free_sets)})
@@ -815,6 +817,38 @@ int tri_readback(tri_ctx* c, uint8_t* bgra, uint32_t* depth) {
             return fail(TRI_E_STATE, "tri_readback: depth output disabled by TRI_FLAG_NO_DEPTH_OUTPUT");
         HIP_TRY(hipMemcpy(depth, c->d_depth, px * 4, hipMemcpyDeviceToHost));
     }
+    return TRI_OK;
+}
+
+int tri_blit_linear(tri_ctx* c, void* dst, uint32_t width, uint32_t height) {
+    if (!c) return fail(TRI_E_INVALID, "tri_blit_linear: null context");
+    if (width == 0 || height == 0 || width > TRI_MAX_DIM || height > TRI_MAX_DIM)
+        return fail(TRI_E_INVALID, "tri_blit_linear: destination %ux%u outside 1..%d", width, height, TRI_MAX_DIM);
+    if (c->y0 != 0 || c->y1 != c->H) return fail(TRI_E_STATE, "tri_blit_linear: a row-band context has no whole frame");
+    int rc = make_current(c);
+    if (rc) return rc;
+    uint32_t* out = static_cast<uint32_t*>(dst);
+    if (!out) {
+        if ((size_t)width * height > c->cap_present) {
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        }
+        if ((rc = grow(c->d_present, c->cap_present, (size_t)width * height))) return rc;
+        out = c->d_present;
+        c->present_w = width;
+        c->present_h = height;
+    }
+    // the alpha half of the decode LUT is the UNORM8 decode b / 255 (IEEE float division)
+    HIP_TRY(tri_launch_blit(c->d_color, c->W, c->H, out, (int32_t)width, (int32_t)height, c->d_lut + 256, c->stream));
+    return TRI_OK;
+}
+
+int tri_read_present(tri_ctx* c, uint8_t* bgra) {
+    if (!c || !bgra) return fail(TRI_E_INVALID, "tri_read_present: null argument");
+    if (!c->d_present || !c->present_w) return fail(TRI_E_STATE, "tri_read_present: nothing was blitted");
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    HIP_TRY(hipMemcpy(bgra, c->d_present, (size_t)c->present_w * c->present_h * 4, hipMemcpyDeviceToHost));
     return TRI_OK;
 }
 

@@ -75,7 +75,13 @@ public:
     const FrameTimingStats& GetFrameTimingStats() const { return m_PerformanceStats; }
     size_t GetFrameTimingHistoryCount() const { return m_PerformanceSampleCount; }
 
-    void SetViewport(uint32_t viewportId, const ViewportInfo& info);
+    void SetViewport(uint32_t viewportId, const ViewportInfo& info);  // also makes it the active viewport
+    // Swapchain extent stand-in (Swapchain.cpp): when set, DrawFrame ends by blitting the active
+    // viewport onto a present image of this size with linear filtering (Renderer.cpp:5346-5361).
+    void SetPresentExtent(uint32_t width, uint32_t height) { m_PresentWidth = width; m_PresentHeight = height; }
+    // The last presented image (RGBA8 rows, BGRA reordered) and its size; false before a present.
+    bool ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height);
+    uint32_t GetActiveViewportId() const { return m_ActiveViewportId; }
     ViewportInfo GetViewport() const;
     // Vulkan returned a VkDescriptorSet for ImGui; here: the viewport's device B8G8R8A8 buffer.
     void* GetViewportTexture(uint32_t viewportId) const;
@@ -158,6 +164,9 @@ private:
 
     std::map<uint32_t, ViewportContext> m_Viewports;
     ViewportInfo m_LastViewport{};
+    uint32_t m_ActiveViewportId = 0;
+    uint32_t m_PresentWidth = 0, m_PresentHeight = 0;
+    tri_ctx* m_PresentSource = nullptr;  // viewport context the last present was blitted from
     uint32_t m_RasterFlags = 0;
 
     glm::vec3 m_AmbientColor{0.03f};

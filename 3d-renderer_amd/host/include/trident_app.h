@@ -68,6 +68,11 @@ int trident_app_entity_transform(trident_app* app, uint32_t entity, float out[9]
 int trident_app_entity_mesh(trident_app* app, uint32_t entity, uint64_t out[3]);
 int trident_app_entity_count(trident_app* app, uint32_t* count);
 
+/* Renderer::SetPresentExtent: DrawFrame then blits the active (last SetViewport) viewport onto a
+ * width x height present image (VK_FILTER_LINEAR); 0 x 0 disables. */
+int trident_app_set_present_extent(trident_app* app, uint32_t width, uint32_t height);
+int trident_app_read_present(trident_app* app, uint8_t* rgba, uint32_t width, uint32_t height);
+
 int trident_app_draw_frame(trident_app* app);
 int trident_app_read_pixels(trident_app* app, uint32_t viewport_id, uint8_t* rgba, float* depth /* nullable */);
 

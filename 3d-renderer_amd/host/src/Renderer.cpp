@@ -483,6 +483,7 @@ void Renderer::SetViewport(uint32_t viewportId, const ViewportInfo& info) {
     ctx.m_Info = info;
     ctx.m_Info.ViewportID = viewportId;
     m_LastViewport = ctx.m_Info;
+    m_ActiveViewportId = viewportId;  // Renderer.cpp:2753-2754
 }
 
 ViewportInfo Renderer::GetViewport() const { return m_LastViewport; }
@@ -607,6 +608,17 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
         }
         if (rc != TRI_OK) LogError("frame fence", tri_last_error());
     }
+    // Primary viewport -> swapchain image, VK_FILTER_LINEAR (Renderer.cpp:5346-5361).
+    m_PresentSource = nullptr;
+    auto active = m_Viewports.find(m_ActiveViewportId);
+    if (m_PresentWidth && m_PresentHeight && active != m_Viewports.end() && active->second.m_Ctx &&
+        std::find(submitted.begin(), submitted.end(), &active->second) != submitted.end()) {
+        if (tri_blit_linear(active->second.m_Ctx, nullptr, m_PresentWidth, m_PresentHeight) == TRI_OK &&
+            tri_synchronize(active->second.m_Ctx) == TRI_OK)
+            m_PresentSource = active->second.m_Ctx;
+        else
+            LogError("present blit", tri_last_error());
+    }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     RecordFrameTiming(ms);
 }
@@ -665,6 +677,25 @@ bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgb
         depth->resize(dbits.size());
         std::memcpy(depth->data(), dbits.data(), dbits.size() * 4);
     }
+    return true;
+}
+
+bool Renderer::ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height) {
+    if (!m_PresentSource) return false;
+    std::vector<uint8_t> bgra((size_t)m_PresentWidth * m_PresentHeight * 4);
+    if (tri_read_present(m_PresentSource, bgra.data()) != TRI_OK) {
+        LogError("present readback", tri_last_error());
+        return false;
+    }
+    rgba.resize(bgra.size());
+    for (size_t i = 0; i < bgra.size(); i += 4) {
+        rgba[i + 0] = bgra[i + 2];
+        rgba[i + 1] = bgra[i + 1];
+        rgba[i + 2] = bgra[i + 0];
+        rgba[i + 3] = bgra[i + 3];
+    }
+    width = m_PresentWidth;
+    height = m_PresentHeight;
     return true;
 }
 

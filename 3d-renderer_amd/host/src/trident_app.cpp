@@ -305,6 +305,26 @@ int trident_app_entity_count(trident_app* app, uint32_t* count) {
     });
 }
 
+int trident_app_set_present_extent(trident_app* app, uint32_t width, uint32_t height) {
+    return Guard(app, [&] {
+        if (width > TRI_MAX_DIM || height > TRI_MAX_DIM) return TRI_E_INVALID;
+        app->renderer.SetPresentExtent(width, height);
+        return TRI_OK;
+    });
+}
+
+int trident_app_read_present(trident_app* app, uint8_t* rgba, uint32_t width, uint32_t height) {
+    return Guard(app, [&] {
+        if (!rgba) return TRI_E_INVALID;
+        std::vector<uint8_t> px;
+        uint32_t w = 0, h = 0;
+        if (!app->renderer.ReadPresentPixels(px, w, h)) return TRI_E_STATE;
+        if (w != width || h != height) return TRI_E_INVALID;
+        std::memcpy(rgba, px.data(), px.size());
+        return TRI_OK;
+    });
+}
+
 int trident_app_draw_frame(trident_app* app) {
     return Guard(app, [&] {
         app->renderer.DrawFrame();

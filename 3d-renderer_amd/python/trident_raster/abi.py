@@ -165,6 +165,8 @@ CABI_FUNCTIONS = [
     ("tri_render", C.c_int, [C.c_void_p]),
     ("tri_synchronize", C.c_int, [C.c_void_p]),
     ("tri_readback", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("tri_blit_linear", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
+    ("tri_read_present", C.c_int, [C.c_void_p, C.c_void_p]),
     ("tri_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("tri_get_timing", C.c_int, [C.c_void_p, C.POINTER(TriTiming)]),
     ("tri_get_frame_stats", C.c_int, [C.c_void_p, C.POINTER(TriFrameStats)]),

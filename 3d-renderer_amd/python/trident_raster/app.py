@@ -49,6 +49,8 @@ _APP_FUNCTIONS = [
     ("trident_app_entity_transform", C.c_int, [C.c_void_p, C.c_uint32, _f3]),
     ("trident_app_entity_mesh", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]),
     ("trident_app_entity_count", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
+    ("trident_app_set_present_extent", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    ("trident_app_read_present", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
 ]
 
 _lib = None
@@ -227,3 +229,13 @@ class TridentApp:
         n = C.c_uint32()
         _check(self._lib.trident_app_entity_count(self._h, C.byref(n)), "entity_count")
         return n.value
+
+    # ---- presentation: active viewport -> swapchain-sized image ----
+    def set_present_extent(self, width, height):
+        _check(self._lib.trident_app_set_present_extent(self._h, width, height), "set_present_extent")
+
+    def read_present(self, width, height):
+        out = np.zeros((height, width, 4), np.uint8)
+        _check(self._lib.trident_app_read_present(self._h, out.ctypes.data, width, height), "read_present")
+        return out
+

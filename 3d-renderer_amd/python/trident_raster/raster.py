@@ -150,6 +150,17 @@ class TriRaster:
         _check(_lib.tri_readback(self._ctx, _ptr(col), _ptr(dep) if depth else None))
         return col, dep
 
+    def blit(self, width, height, dst_ptr=None):
+        """tri_blit_linear: scale the frame to width x height (VK_FILTER_LINEAR presentation blit)."""
+        _check(_lib.tri_blit_linear(self._ctx, C.c_void_p(dst_ptr) if dst_ptr else None, width, height))
+        self._present = (width, height)
+
+    def read_present(self):
+        w, h = self._present
+        out = np.empty((h, w, 4), dtype=np.uint8)
+        _check(_lib.tri_read_present(self._ctx, _ptr(out)))
+        return out
+
     def render_frame(self, retries=2):
         """render + synchronize, re-rendering once after an internal-buffer overflow (buffers grow)."""
         for attempt in range(retries + 1):

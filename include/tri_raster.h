@@ -211,6 +211,18 @@ int tri_synchronize(tri_ctx* ctx);
  * BGRA8 (width*4 bytes per row) and float32 depth bits. Either pointer may be NULL. */
 int tri_readback(tri_ctx* ctx, uint8_t* bgra8, uint32_t* depth_bits);
 
+/* Presentation blit (Renderer.cpp:5346-5361: vkCmdBlitImage of the primary viewport's offscreen
+ * target onto the swapchain image, VK_FILTER_LINEAR). Scales this context's B8G8R8A8 target to
+ * width x height: each destination texel centre maps to the source by the extent ratio, the source
+ * is filtered bilinearly on UNORM values with clamp-to-edge taps, and the result is rounded to UNORM8.
+ * `dst` is a device pointer to width*height*4 bytes, or NULL for a context-owned present image that
+ * tri_read_present copies out. Stream-ordered after the context's last tri_render. Whole frames only
+ * (a row-band context returns TRI_E_STATE). */
+int tri_blit_linear(tri_ctx* ctx, void* dst, uint32_t width, uint32_t height);
+/* Synchronous copy of the context-owned present image of the last tri_blit_linear(ctx, NULL, w, h):
+ * w*h*4 bytes of BGRA8. */
+int tri_read_present(tri_ctx* ctx, uint8_t* bgra8);
+
 /* ---- measurement -------------------------------------------------------------------------- */
 /* enable = N > 0: HIP events around every stage of every N-th frame (1 = all frames; sampling keeps
  * the event overhead out of throughput runs); 0 = off. Also resets the accumulators. */

@@ -78,6 +78,8 @@ def load():
         lib.oracle_runtime_camera.restype = None
         lib.oracle_runtime_camera.argtypes = [fl3, fl3, C.c_float, C.c_float, C.c_float, C.c_float, C.c_float,
                                               C.c_float, C.c_int, fl3, fl3]
+        lib.oracle_blit_linear.restype = None
+        lib.oracle_blit_linear.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]
         lib.oracle_pack_global_ubo.restype = None
         lib.oracle_pack_global_ubo.argtypes = [fl3, fl3, fl3, C.c_int, fl3, C.c_float, C.POINTER(OracleLight),
                                                C.c_uint32, C.POINTER(abi.TriGlobalUbo)]
@@ -203,3 +205,14 @@ def render(scene, band=None, threads=None):
     if rc != 0:
         raise RuntimeError(f"oracle_render failed: {rc}")
     return col, dep, {k: getattr(st, k) for k, _ in OracleStats._fields_}
+
+
+def blit_linear(bgra, dw, dh):
+    """vkCmdBlitImage with VK_FILTER_LINEAR (Renderer.cpp:5346-5361): uint8 [h, w, 4] -> [dh, dw, 4]."""
+    lib = load()
+    src = np.ascontiguousarray(bgra, np.uint8)
+    h, w = src.shape[:2]
+    out = np.zeros((dh, dw, 4), np.uint8)
+    lib.oracle_blit_linear(src.ctypes.data, w, h, out.ctypes.data, dw, dh)
+    return out
+

@@ -1035,3 +1035,32 @@ extern "C" void oracle_pack_global_ubo(const float view[16], const float proj[16
     out->light_counts[0] = (ndir > 0 || fallback) ? 1u : 0u;
     out->light_counts[1] = npt;
 }
+
+// vkCmdBlitImage(primary offscreen target -> swapchain image, VK_FILTER_LINEAR), Renderer.cpp:5346-5361.
+// Vulkan "Image Blits": destination texel centre (x + 0.5) scaled by src/dst extent into the source,
+// bilinear filtering of UNORM values over clamp-to-edge taps, UNORM8 round-to-nearest on the write.
+extern "C" void oracle_blit_linear(const uint32_t* src, uint32_t w, uint32_t h, uint32_t* dst, uint32_t dw,
+                                   uint32_t dh) {
+    const float sx = (float)w / (float)dw, sy = (float)h / (float)dh;
+    for (uint32_t y = 0; y < dh; ++y)
+        for (uint32_t x = 0; x < dw; ++x) {
+            const float u = ((float)x + 0.5f) * sx - 0.5f;
+            const float v = ((float)y + 0.5f) * sy - 0.5f;
+            const float fu = std::floor(u), fv = std::floor(v);
+            const float a = u - fu, b = v - fv;
+            const int32_t i0 = (int32_t)fu, j0 = (int32_t)fv;
+            auto cl = [](int32_t i, uint32_t n) { return (uint32_t)std::min(std::max(i, 0), (int32_t)n - 1); };
+            const uint32_t xa = cl(i0, w), xb = cl(i0 + 1, w), ya = cl(j0, h), yb = cl(j0 + 1, h);
+            const uint32_t p00 = src[(size_t)ya * w + xa], p10 = src[(size_t)ya * w + xb];
+            const uint32_t p01 = src[(size_t)yb * w + xa], p11 = src[(size_t)yb * w + xb];
+            uint32_t out = 0;
+            for (int c = 0; c < 4; ++c) {
+                auto un = [c](uint32_t p) { return (float)((p >> (8 * c)) & 0xFFu) / 255.0f; };
+                const float t00 = un(p00), t10 = un(p10), t01 = un(p01), t11 = un(p11);
+                const float l0 = t00 + a * (t10 - t00);
+                const float l1 = t01 + a * (t11 - t01);
+                out |= unorm8(l0 + b * (l1 - l0)) << (8 * c);
+            }
+            dst[(size_t)y * dw + x] = out;
+        }
+}

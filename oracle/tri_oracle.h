@@ -104,6 +104,11 @@ void oracle_pack_global_ubo(const float view[16], const float proj[16], const fl
                             int has_camera, const float ambient_color[3], float ambient_intensity,
                             const oracle_light* lights, uint32_t light_count, tri_global_ubo* out);
 
+/* The presentation blit (Renderer.cpp:5346-5361, vkCmdBlitImage with VK_FILTER_LINEAR, Vulkan spec
+ * "Image Blits": destination texel centres scaled into the source, bilinear over clamp-to-edge taps of
+ * UNORM values, UNORM8 round-to-nearest). src: w*h BGRA8 texels, dst: dw*dh. */
+void oracle_blit_linear(const uint32_t* src, uint32_t w, uint32_t h, uint32_t* dst, uint32_t dw, uint32_t dh);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,115 @@
+"""Second viewport + presentation blit. The editor renders every viewport, then
+blits the primary one onto the swapchain image with vkCmdBlitImage(..., VK_FILTER_LINEAR)
+(Renderer.cpp:5208-5221, :5346-5361); the primary viewport is the one SetViewport was called for
+last (:2751-2754).
+
+CPU: known answers of the oracle's blit restatement (Vulkan "Image Blits": destination texel centres
+scaled into the source, bilinear over clamp-to-edge taps of UNORM values, UNORM8 rounding). GPU: the
+HIP blit (tri_blit_linear) and the shim's present image against that restatement, bit-exact.
+Parity against a Vulkan driver's blit is unpinned (no Vulkan here; its filter precision is
+implementation-defined).
+"""
+import numpy as np
+import pytest
+
+import scene_cases as sc
+
+
+def blit_ref(src, dw, dh):
+    """numpy float32 restatement with the oracle's operation order (checks the C restatement)."""
+    h, w = src.shape[:2]
+    f32 = np.float32
+    sx, sy = f32(w) / f32(dw), f32(h) / f32(dh)
+    x = np.arange(dw, dtype=f32)
+    y = np.arange(dh, dtype=f32)
+    u = (x + f32(0.5)) * sx - f32(0.5)
+    v = (y + f32(0.5)) * sy - f32(0.5)
+    fu, fv = np.floor(u), np.floor(v)
+    a, b = (u - fu).astype(f32), (v - fv).astype(f32)
+    i0, j0 = fu.astype(np.int64), fv.astype(np.int64)
+    xa, xb = np.clip(i0, 0, w - 1), np.clip(i0 + 1, 0, w - 1)
+    ya, yb = np.clip(j0, 0, h - 1), np.clip(j0 + 1, 0, h - 1)
+    t = src.astype(f32) / f32(255.0)
+    t00, t10 = t[ya][:, xa], t[ya][:, xb]
+    t01, t11 = t[yb][:, xa], t[yb][:, xb]
+    A, B = a[None, :, None], b[:, None, None]
+    l0 = t00 + A * (t10 - t00)
+    l1 = t01 + A * (t11 - t01)
+    c = np.clip(l0 + B * (l1 - l0), 0, 1)
+    return np.floor(c * f32(255.0) + f32(0.5)).astype(np.uint8)
+
+
+def test_blit_identity_and_known_answers(oracle):
+    rng = np.random.default_rng(7)
+    src = rng.integers(0, 256, (37, 53, 4), dtype=np.uint8)
+    assert np.array_equal(oracle.blit_linear(src, 53, 37), src)  # same extent: a copy
+    # 2x downscale: every destination centre falls between 4 source texels at weights 1/2, 1/2
+    sq = rng.integers(0, 256, (8, 8, 4), dtype=np.uint8)
+    half = oracle.blit_linear(sq, 4, 4)
+    avg = sq.reshape(4, 2, 4, 2, 4).astype(np.float64).mean(axis=(1, 3))
+    assert np.abs(half.astype(np.float64) - avg).max() <= 0.5 + 1e-6
+    # upscale: clamp-to-edge keeps the corner texels
+    up = oracle.blit_linear(sq, 32, 32)
+    assert np.array_equal(up[0, 0], sq[0, 0]) and np.array_equal(up[-1, -1], sq[-1, -1])
+
+
+@pytest.mark.parametrize("shape", [(480, 640, 720, 1280), (480, 640, 240, 320), (37, 53, 177, 333), (64, 64, 1, 1)])
+def test_blit_restatements_agree(oracle, shape):
+    h, w, dh, dw = shape
+    src = np.random.default_rng(h * w + dw).integers(0, 256, (h, w, 4), dtype=np.uint8)
+    assert np.array_equal(oracle.blit_linear(src, dw, dh), blit_ref(src, dw, dh))
+
+
+# ---- GPU ----------------------------------------------------------------------------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("dw,dh", [(1280, 720), (320, 240), (333, 177), (640, 480)])
+def test_gpu_blit_matches_oracle(oracle, dw, dh):
+    from trident_raster import raster, scenes
+
+    s = sc.c1_cube_skybox(1)
+    with raster.TriRaster(s.width, s.height) as r:
+        scenes.load_scene(r, s)
+        r.render_frame()
+        col, _ = r.readback(depth=False)
+        r.blit(dw, dh)
+        got = r.read_present()
+    assert np.array_equal(got, oracle.blit_linear(col, dw, dh))
+
+
+@pytest.mark.gpu
+def test_gpu_blit_rejects_bands():
+    from trident_raster import raster, scenes
+
+    s = sc.c1_cube_skybox(1)
+    with raster.TriRaster(s.width, s.height, band=(0, 240)) as r:
+        scenes.load_scene(r, s)
+        r.render_frame()
+        with pytest.raises(raster.TriError):
+            r.blit(320, 240)
+
+
+@pytest.mark.gpu
+def test_gpu_shim_presents_the_active_viewport(oracle):
+    """Scene (id 1) and Game (id 2) viewports render every frame; the one SetViewport touched last is
+    blitted to the swapchain-sized present image."""
+    from trident_raster import app
+
+    a = app.TridentApp()
+    a.set_camera("editor", (0.0, 3.0, 8.0))
+    a.set_camera("runtime", (2.0, 2.0, 6.0), (-10.0, 20.0, 0.0), fov=70.0, ready=True)
+    a.set_viewport(2, 320, 200)
+    a.set_viewport(1, 480, 270)  # active
+    a.add_mesh_entity("cube", position=(0.0, 3.0, -2.0), rotation=(0.0, 30.0, 0.0))
+    a.add_mesh_entity("sphere", position=(1.5, 3.0, -1.0))
+    a.set_present_extent(960, 540)
+    a.draw_frame()
+    a.draw_frame()
+    vp1, _ = a.read_pixels(1, 480, 270, depth=False)
+    present = a.read_present(960, 540)
+    want = oracle.blit_linear(vp1[..., [2, 1, 0, 3]], 960, 540)[..., [2, 1, 0, 3]]  # RGBA <-> BGRA
+    assert np.array_equal(present, want)
+    a.set_viewport(2, 320, 200)  # the Game view becomes primary
+    a.draw_frame()
+    vp2, _ = a.read_pixels(2, 320, 200, depth=False)
+    present = a.read_present(960, 540)
+    assert np.array_equal(present, oracle.blit_linear(vp2[..., [2, 1, 0, 3]], 960, 540)[..., [2, 1, 0, 3]])
