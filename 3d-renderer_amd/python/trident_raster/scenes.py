@@ -372,6 +372,37 @@ def scene_c3_grid(width=3840, height=2160, n=708):
                  materials=[((1.0, 1.0, 1.0, 1.0), (0.1, 0.6, 1.0, 0.0))], skybox=DEFAULT_SKYBOX)
 
 
+def procedural_texture(size, seed):
+    """A seeded RGBA8 sRGB texture (bands + noise), opaque: every bilinear tap differs."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:size, 0:size].astype(np.float32) / size
+    base = rng.uniform(40, 200, size=3)
+    t = np.empty((size, size, 4), np.uint8)
+    for c in range(3):
+        wave = np.sin(2 * np.pi * ((c + 1) * 3 * xx + (3 - c) * 2 * yy + rng.uniform()))
+        t[..., c] = np.clip(base[c] + 45 * wave + rng.integers(-20, 21, size=(size, size)), 0, 255)
+    t[..., 3] = 255
+    return t
+
+
+def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048):
+    """C5 within the reference's shading model: the C3 grid split into 4 meshes (row quarters), each
+    drawn with its own tex_size^2 sRGB texture slot (4 bilinear textures, uv x4 REPEAT). The shadow-map
+    pre-pass of BASELINE.json's C5 has no counterpart in the reference (LightComponent.h:33 marks
+    m_ShadowCaster reserved; Default.frag samples one texture), so it is not rendered."""
+    s = scene_c3_grid(width, height, n)
+    tris = s.indices.size // 3
+    q = [(k * tris) // 4 for k in range(5)]
+    meshes = np.zeros(4, abi.MESH_RANGE_DTYPE)
+    for k in range(4):
+        meshes[k] = (3 * q[k], 3 * (q[k + 1] - q[k]), 0, 0)
+    s.meshes = meshes
+    s.textures = [(1 + k, procedural_texture(tex_size, 0xC5 + k)) for k in range(4)]
+    s.draws = [abi.make_draw(k, np.eye(4, dtype=F), texture_slot=1 + k, material_index=0) for k in range(4)]
+    s.name = f"c5_textured4x{tex_size}_{width}x{height}"
+    return s
+
+
 def load_scene(rast, scene):
     """Upload a Scene into a TriRaster (UploadMesh + materials + textures + frame + draws)."""
     rast.upload_geometry(scene.vertices, scene.indices, scene.meshes)

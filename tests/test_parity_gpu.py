@@ -56,6 +56,16 @@ def test_primitives(oracle, flags):
     assert_parity(sc.primitives_row(oracle), oracle, min_covered=2000, flags=flags)
 
 
+def test_c5_four_textured_draws(oracle, flags):
+    """BASELINE C5's sampler stress within the reference's model: 4 draws, 4 sRGB texture slots
+    (bilinear, REPEAT), reduced size so the oracle finishes in seconds."""
+    from trident_raster import scenes
+
+    s = scenes.scene_c5_textured(640, 360, 80, 64)
+    s.skybox = None
+    assert_parity(s, oracle, min_covered=100000, flags=flags)
+
+
 def test_c2_sphere_1080p(oracle, flags):
     assert_parity(sc.sphere_c2(oracle=oracle), oracle, min_covered=300000, flags=flags)
 
