@@ -1087,7 +1087,7 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 template <bool EXACT, int BL>
 // 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
 // a little); 64x64 bins are LDS-limited to 3
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL == 5 ? TRI_RASTER_WAVES : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     __shared__ uint32_t bigq[kBigQueue];
@@ -1282,6 +1282,9 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
     if (fp.bin_log2 == 5) {
         if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 5>), g, t, 0, stream, fp, b);
         else hipLaunchKernelGGL((k_raster<false, 5>), g, t, 0, stream, fp, b);
+    } else if (fp.bin_log2 == 4) {
+        if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 4>), g, t, 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_raster<false, 4>), g, t, 0, stream, fp, b);
     } else {
         if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 6>), g, t, 0, stream, fp, b);
         else hipLaunchKernelGGL((k_raster<false, 6>), g, t, 0, stream, fp, b);

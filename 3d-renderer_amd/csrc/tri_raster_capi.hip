@@ -431,6 +431,41 @@ int check_overflow(tri_ctx* c) {
                 h.flags);
 }
 
+// Bin grid: 32x32-pixel bins while the grid stays under 16384 bins (else 64x64). Sparse frames
+// (fewer than 0.05 triangles per pixel, e.g. C2's 50k-triangle sphere at 1080p) on small grids use
+// 16x16 bins: more workgroups to balance, and few triangles span several bins. Dense bands keep 32x32
+// (16x16 measured 10-25 % slower there: more bin entries, each paying its edge set-up).
+// TRI_BIN_LOG2 (4..6) forces a size (diagnostics).
+int choose_bin_grid(tri_ctx* c) {
+    static const int forced = [] {
+        const char* e = getenv("TRI_BIN_LOG2");
+        const int v = e ? atoi(e) : 0;
+        return (v >= 4 && v <= 6) ? v : 0;
+    }();
+    auto bins = [c](int bl) {
+        const int32_t bs = 1 << bl;
+        return ((c->W + bs - 1) / bs) * ((c->y1 - c->y0 + bs - 1) / bs);
+    };
+    int bl = forced;
+    if (!bl) {
+        const double density = (double)c->nprims / ((double)c->W * (double)c->H);
+        const int32_t n32 = bins(5);
+        bl = n32 > 16384 ? 6 : ((n32 < 4096 && density < 0.05) ? 4 : 5);
+    }
+    if (bl == c->bin_log2) return TRI_OK;
+    HIP_TRY(hipStreamSynchronize(c->stream));  // queued frames still use the old grid
+    int rc;
+    const int32_t bs = 1 << bl;
+    c->bin_log2 = bl;
+    c->nbx = (c->W + bs - 1) / bs;
+    c->nby = (c->y1 - c->y0 + bs - 1) / bs;
+    c->nbins = c->nbx * c->nby;
+    c->bin_cap = 0;  // re-derived for the new grid by ensure_work_buffers
+    if ((rc = grow(c->d_bin_count, c->cap_bin_count, (size_t)c->nbins))) return rc;
+    HIP_TRY(hipMemset(c->d_bin_count, 0, (size_t)c->nbins * 4));
+    return TRI_OK;
+}
+
 }  // namespace
 
 extern "C" {
@@ -462,14 +497,7 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
     c->H = (int32_t)cfg->height;
     c->y0 = (int32_t)y0;
     c->y1 = (int32_t)y1;
-    // 32x32-pixel bins while the bin grid fits the 16384-entry LDS histograms, else 64x64
-    for (c->bin_log2 = 5; c->bin_log2 <= 6; ++c->bin_log2) {
-        const int32_t bs = 1 << c->bin_log2;
-        c->nbx = (c->W + bs - 1) / bs;
-        c->nby = (c->y1 - c->y0 + bs - 1) / bs;
-        if (c->nbx * c->nby <= 16384) break;
-    }
-    c->nbins = c->nbx * c->nby;
+    c->bin_log2 = 0;  // the bin grid is chosen at the first tri_render (choose_bin_grid)
     auto bail = [&](int rc) { tri_destroy(c); return rc; };
     int rc = make_current(c);
     if (rc) return bail(rc);
@@ -485,8 +513,7 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
         return bail(fail(TRI_E_OOM, "tri_create: target allocation failed"));
     c->d_color = c->d_color_own;
     c->d_depth = c->d_depth_own;
-    if ((rc = grow(c->d_bin_count, c->cap_bin_count, (size_t)c->nbins))) return bail(rc);
-    if (hipMemset(c->d_bin_count, 0, c->nbins * 4) != hipSuccess || hipMemset(c->d_ctr, 0, sizeof(TriCounters)) != hipSuccess)
+    if (hipMemset(c->d_ctr, 0, sizeof(TriCounters)) != hipSuccess)
         return bail(fail(TRI_E_HIP, "tri_create: memset failed"));
     float lut[512];
     for (int i = 0; i < 256; ++i) {  // R8G8B8A8_SRGB decode (sRGB EOTF), evaluated in double
@@ -701,6 +728,7 @@ int tri_render(tri_ctx* c) {
         HIP_TRY(hipMemsetAsync(c->d_skin, 0, std::max<uint64_t>(c->nverts, 1) * sizeof(TriVsSkin), c->stream));
         c->has_skin_data = true;
     }
+    if ((rc = choose_bin_grid(c))) return rc;
     if ((rc = ensure_work_buffers(c))) return rc;
 
     TriFrameParams fp;
