@@ -97,18 +97,20 @@ struct __attribute__((aligned(16))) TriDrawDev {
     uint32_t pad[3];
 };
 
-// Per-draw fragment-stage constants.
-struct __attribute__((aligned(16))) TriDrawShade {
-    float tint[4];
-    int32_t tex_id;  // texture table index (unused slots alias slot 0)
-    int32_t pad[3];
-};
-
 struct __attribute__((aligned(16))) TriTexDesc {
     const uint32_t* texels;  // RGBA8 sRGB, row-major
     uint32_t w, h;
     float solid[4];          // 1x1 textures: the decoded texel (every bilinear tap is that texel)
 };
+
+// Per-draw fragment-stage constants: the push constant's tint and the descriptor of the draw's texture
+// slot (unused slots alias slot 0), copied in on the host so a fragment reads its texture after one
+// load that depends only on the draw, not after a second, dependent descriptor load.
+struct __attribute__((aligned(16))) TriDrawShade {
+    float tint[4];
+    TriTexDesc tex;
+};
+static_assert(sizeof(TriDrawShade) == 48, "TriDrawShade: tint + texture descriptor");
 
 struct TriCounters {  // per-frame fields are zeroed before every frame; `flags`/`bin_max` are sticky
     uint32_t ovf_records;

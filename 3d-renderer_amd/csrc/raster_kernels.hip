@@ -225,10 +225,13 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-__device__ __forceinline__ uint32_t wave_reserve(uint32_t* counts, uint32_t bin, bool want) {
+// Reservation plan (ALU and ballots only): each wanting lane learns its group's leader lane and its
+// rank in the group; a leader learns its group's size.
+__device__ __forceinline__ void wave_reserve_plan(uint32_t bin, bool want, uint32_t& leader, uint32_t& rank,
+                                                  uint32_t& cnt) {
     uint64_t pending = __ballot(want);
     const uint32_t lane = lanes_below(~0ull);
-    uint32_t leader = lane, rank = 0, cnt = 0;
+    leader = lane; rank = 0; cnt = 0;
     while (pending) {
         const uint32_t l = (uint32_t)__builtin_ctzll(pending);
         const uint32_t lb = (uint32_t)__builtin_amdgcn_readlane((int)bin, (int)l);
@@ -240,11 +243,10 @@ __device__ __forceinline__ uint32_t wave_reserve(uint32_t* counts, uint32_t bin,
         if (lane == l) cnt = (uint32_t)__builtin_popcountll(grp);
         pending &= ~grp;
     }
-    uint32_t base = 0;
-    if (want && lane == leader) base = atomicAdd(&counts[bin], cnt);
-    base = (uint32_t)__shfl((int)base, (int)leader);
-    return base + rank;
 }
+
+// Binning rounds whose queue reservations k_setup keeps in flight together.
+constexpr int kResBatch = 4;
 
 // ------------------------------------------------------------------------------------------
 // Homogeneous clipping (oracle clip_polygon: Sutherland-Hodgman against w >= WMIN, z >= 0 and the
@@ -389,7 +391,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
 }
 
 // One lane per primitive (ppt primitives per lane): assembly from the snapped vertices, trivial
-// reject, cull, bbox, then one bin-queue entry per touched bin via wave_reserve. Nothing else is
+// reject, cull, bbox, then one bin-queue entry per touched bin (batched wave reservations). Nothing else is
 // written for a visible triangle: k_raster rebuilds it from `snap`. Triangles needing homogeneous
 // clipping are clipped right here by their wave (clip_prim_wave). Entry order inside a bin is free:
 // k_raster resolves visibility with (depth, primitive order) keys.
@@ -400,12 +402,13 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
     __syncthreads();
     uint32_t nsetup = 0, nentries = 0;
     const uint32_t cap = fp.bin_cap;
+    const uint32_t lane = lanes_below(~0ull);
     // Spread concurrently running workgroups over the primitive stream: meshes are usually
     // index-ordered in screen space, and neighbouring chunks hammering the same bin counters
     // serialise their atomics. The stride is coprime to nchunks, so the remap is a bijection.
     const uint32_t chunk = (uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks);
     const uint32_t chunk0 = chunk * (uint32_t)(TRI_BLOCK * fp.ppt);
-    for (int k = 0; k < fp.ppt; ++k) {  // uniform trip count: wave_reserve needs the whole wave
+    for (int k = 0; k < fp.ppt; ++k) {  // uniform trip count: the reservations need the whole wave
         const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
         bool ok = false, needs_clip = false;
         uint32_t sl0 = 0, sl1 = 0, sl2 = 0;
@@ -451,22 +454,42 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
         uint32_t bx = br.x & 0xFFFFu, by = br.x >> 16;
         const uint32_t bx0 = bx, bx1 = br.y & 0xFFFFu, by1 = br.y >> 16;
         bool has = ok && !(fp.ablate & 4);  // diagnostics: 4 = setup without binning
-        while (__ballot(has)) {  // one bin per lane per round
-            const uint32_t bi = by * (uint32_t)fp.nbx + bx;
-            uint32_t pos;
-            if (fp.ablate & 8) pos = has ? atomicAdd(&b.bin_count[bi], 1u) : 0u;  // diagnostics: no aggregation
-            else pos = wave_reserve(b.bin_count, bi, has);
-            if (has) {
-                if (pos < cap) b.bin_list[(size_t)bi * cap + pos] = p;
-                else note_bin_overflow(b, pos + 1);
-                ++nentries;
-                if (bx < bx1) {
-                    ++bx;
-                } else if (by < by1) {
-                    bx = bx0;
-                    ++by;
-                } else {
-                    has = false;
+        // One bin per lane per round. A batch of kResBatch rounds is planned with ballots and its
+        // reservations (one returning atomic per (wave, bin)) are all issued before any result is
+        // used, so the wave waits for one atomic round trip per batch instead of one per round.
+        // Diagnostics: TRI_ABLATE=8 waits per round (batches of one).
+        const int batch = (fp.ablate & 8) ? 1 : kResBatch;
+        while (__ballot(has)) {
+            uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch];
+            bool rwant[kResBatch];
+#pragma unroll
+            for (int r = 0; r < kResBatch; ++r) {
+                rwant[r] = has && r < batch;
+                rbin[r] = by * (uint32_t)fp.nbx + bx;
+                if (rwant[r]) {
+                    if (bx < bx1) {
+                        ++bx;
+                    } else if (by < by1) {
+                        bx = bx0;
+                        ++by;
+                    } else {
+                        has = false;
+                    }
+                }
+                uint32_t cnt;
+                wave_reserve_plan(rbin[r], rwant[r], rlead[r], rrank[r], cnt);
+                rbase[r] = 0;
+                if (rwant[r] && lane == rlead[r] && !(fp.ablate & 16))  // diagnostics: 16 = no atomics
+                    rbase[r] = atomicAdd(&b.bin_count[rbin[r]], cnt);
+            }
+#pragma unroll
+            for (int r = 0; r < kResBatch; ++r) {
+                const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
+                if (rwant[r]) {
+                    if (fp.ablate & 32) continue;  // diagnostics: 32 = no queue stores
+                    if (pos < cap) b.bin_list[(size_t)rbin[r] * cap + pos] = p;
+                    else note_bin_overflow(b, pos + 1);
+                    ++nentries;
                 }
             }
         }
@@ -562,11 +585,14 @@ __device__ __forceinline__ float frag_depth(const TriRec& r, const EdgeSetup& e,
     return (r.z[0] + t1) + t2;
 }
 
+// The far-plane test and the [0, 1] depth clamp on the float's bit pattern. Depth is finite here (the
+// plane comes from snapped vertices with w >= WMIN and S != 0); non-negative floats order like their
+// bits, and a negative depth (sign bit set, -0.0 included) clamps to +0.0 exactly like
+// `if (!(z > 0)) z = 0`. One v_med3_i32 instead of two float compares and selects.
 __device__ __forceinline__ bool depth_key(float z, bool far_clip, uint32_t lowbits, uint64_t& key) {
-    if (far_clip && z > 1.0f) return false;  // per-pixel far-plane (z <= w) clip
-    if (!(z > 0.0f)) z = 0.0f;
-    if (z > 1.0f) z = 1.0f;
-    key = ((uint64_t)__float_as_uint(z) << 32) | lowbits;
+    const int32_t zb = __float_as_int(z);
+    if (far_clip && zb > 0x3F800000) return false;  // per-pixel far-plane (z <= w) clip: z > 1
+    key = ((uint64_t)(uint32_t)min(max(zb, 0), 0x3F800000) << 32) | lowbits;
     return true;
 }
 
@@ -596,17 +622,27 @@ __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int3
     if (rej) return;
     const bool far_clip = (r.z[0] > 1.0f) || (r.z[1] > 1.0f) || (r.z[2] > 1.0f);
     const uint32_t low = key_low(r.prim_sub);
+    // frag_depth's pixel offsets stepped incrementally: |256 p + 128 - X0| < 2^24, so the float steps
+    // of 256 are exact and equal its int -> float conversions; same (z0 + dzdX dx) + dzdY dy order
+    const float fdx0 = (float)(256 * cx0 + 128 - r.X[0]);
+    float fdy = (float)(256 * cy0 + 128 - r.Y[0]);
+    uint32_t row = (uint32_t)(((cy0 - oy) << BL) + (cx0 - ox));
     for (int32_t py = cy0; py <= cy1; ++py) {
+        const float t2 = e.dzdY * fdy;
         int32_t f0 = F[0], f1 = F[1], f2 = F[2];
-        for (int32_t px = cx0; px <= cx1; ++px) {
+        float fdx = fdx0;
+        const uint32_t rend = row + (uint32_t)(cx1 - cx0);
+        for (uint32_t a = row; a <= rend; ++a) {
             if ((f0 | f1 | f2) >= 0) {
                 uint64_t key;
-                if (depth_key(frag_depth(r, e, px, py), far_clip, low, key))
-                    atomicMin(&keys[((py - oy) << BL) + (px - ox)], key);
+                if (depth_key((r.z[0] + e.dzdX * fdx) + t2, far_clip, low, key)) atomicMin(&keys[a], key);
             }
             f0 += e.A[0]; f1 += e.A[1]; f2 += e.A[2];
+            fdx += 256.0f;
         }
         F[0] += e.B[0]; F[1] += e.B[1]; F[2] += e.B[2];
+        fdy += 256.0f;
+        row += 1u << BL;
     }
 }
 
@@ -917,8 +953,8 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
     const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
     put(9, u); put(10, v);
-    const TriDrawShade ds = b.draw_shade[d];
-    const float4 tx = sample_tex(b.textures[ds.tex_id], u, v, lut);
+    const TriDrawShade& ds = b.draw_shade[d];
+    const float4 tx = sample_tex(ds.tex, u, v, lut);
     put(11, tx.x); put(12, tx.y); put(13, tx.z); put(14, tx.w);
     put(15, ds.tint[0]); put(16, ds.tint[1]); put(17, ds.tint[2]); put(18, ds.tint[3]);
 }

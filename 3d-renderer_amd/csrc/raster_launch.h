@@ -14,7 +14,6 @@ struct TriDeviceBuffers {
     const TriDrawShade* draw_shade;
     const uint32_t* draw_vbase;  // ndraws+1
     const uint32_t* draw_pbase;  // ndraws+1
-    const TriTexDesc* textures;  // TRI_MAX_TEXTURE_SLOTS entries, aliases resolved
     const uint32_t* sky;         // 6 * sky_size^2 RGBA8 sRGB texels (+X,-X,+Y,-Y,+Z,-Z)
     const float* srgb_lut;       // 256 sRGB -> linear (host, double) + 256 alpha b/255
     float4* clip;                // nslots (read only when a primitive is clipped)

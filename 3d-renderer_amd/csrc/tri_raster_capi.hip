@@ -88,7 +88,7 @@ struct tri_ctx {
     uint32_t* d_tex[TRI_MAX_TEXTURE_SLOTS] = {};
     uint32_t tex_w[TRI_MAX_TEXTURE_SLOTS] = {}, tex_h[TRI_MAX_TEXTURE_SLOTS] = {};
     uint32_t tex_solid[TRI_MAX_TEXTURE_SLOTS] = {};  // texel of a 1x1 slot (RGBA8)
-    TriTexDesc* d_texdesc = nullptr;
+    TriTexDesc texdesc[TRI_MAX_TEXTURE_SLOTS] = {};  // per-slot descriptors, aliases resolved
     bool tex_dirty = true;
     float* d_lut = nullptr;
 
@@ -252,7 +252,7 @@ void mat4_mul(const float* a, const float* b, float* r) {
 
 int upload_texture_table(tri_ctx* c) {
     if (!c->tex_dirty) return TRI_OK;
-    TriTexDesc h[TRI_MAX_TEXTURE_SLOTS];
+    TriTexDesc* h = c->texdesc;
     for (int s = 0; s < TRI_MAX_TEXTURE_SLOTS; ++s) {
         const int src = c->d_tex[s] ? s : 0;  // unused slots alias slot 0 (Renderer.cpp:3645-3656)
         h[s].texels = c->d_tex[src];
@@ -262,9 +262,8 @@ int upload_texture_table(tri_ctx* c) {
         for (int k = 0; k < 3; ++k) h[s].solid[k] = srgb_decode((p >> (8 * k)) & 0xFF);
         h[s].solid[3] = (float)(p >> 24) / 255.0f;  // alpha: linear UNORM decode
     }
-    HIP_TRY(hipStreamSynchronize(c->stream));
-    HIP_TRY(hipMemcpy(c->d_texdesc, h, sizeof h, hipMemcpyHostToDevice));
     c->tex_dirty = false;
+    c->draws_dirty = true;  // the per-draw shade records carry the slot descriptors
     return TRI_OK;
 }
 
@@ -287,7 +286,7 @@ int resolve_draws(tri_ctx* c) {
         std::memset(&sh, 0, sizeof sh);
         std::memcpy(sh.tint, src.pc.tint, 16);
         const int32_t slot = src.pc.texture_slot;
-        sh.tex_id = (slot >= 0 && slot < TRI_MAX_TEXTURE_SLOTS) ? slot : 0;
+        sh.tex = c->texdesc[(slot >= 0 && slot < TRI_MAX_TEXTURE_SLOTS) ? slot : 0];
         o.tex_scale[0] = src.pc.texture_scale[0];
         o.tex_scale[1] = src.pc.texture_scale[1];
         o.tex_offset[0] = src.pc.texture_offset[0];
@@ -508,7 +507,6 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
     const size_t px = (size_t)c->W * (size_t)(c->y1 - c->y0);
     if (hipMalloc(&c->d_color_own, px * 4) != hipSuccess || hipMalloc(&c->d_depth_own, px * 4) != hipSuccess ||
         hipMalloc(&c->d_ctr, sizeof(TriCounters)) != hipSuccess ||
-        hipMalloc(&c->d_texdesc, sizeof(TriTexDesc) * TRI_MAX_TEXTURE_SLOTS) != hipSuccess ||
         hipMalloc(&c->d_lut, 512 * sizeof(float)) != hipSuccess)
         return bail(fail(TRI_E_OOM, "tri_create: target allocation failed"));
     c->d_color = c->d_color_own;
@@ -536,7 +534,7 @@ int tri_destroy(tri_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_texdesc); f(c->d_lut); f(c->d_bones); f(c->d_sky);
+    f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_lut); f(c->d_bones); f(c->d_sky);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase);
     f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
@@ -793,7 +791,6 @@ int tri_render(tri_ctx* c) {
     b.draw_shade = c->d_draw_shade;
     b.draw_vbase = c->d_vbase;
     b.draw_pbase = c->d_pbase;
-    b.textures = c->d_texdesc;
     b.srgb_lut = c->d_lut;
     b.sky = c->d_sky;
     b.clip = c->d_clip;
