@@ -395,7 +395,10 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
 // written for a visible triangle: k_raster rebuilds it from `snap`. Triangles needing homogeneous
 // clipping are clipped right here by their wave (clip_prim_wave). Entry order inside a bin is free:
 // k_raster resolves visibility with (depth, primitive order) keys.
-__global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
+#ifndef TRI_SETUP_WAVES
+#define TRI_SETUP_WAVES 7  // k_setup occupancy target (waves per SIMD)
+#endif
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
@@ -408,70 +411,90 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
     // serialise their atomics. The stride is coprime to nchunks, so the remap is a bijection.
     const uint32_t chunk = (uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks);
     const uint32_t chunk0 = chunk * (uint32_t)(TRI_BLOCK * fp.ppt);
-    for (int k = 0; k < fp.ppt; ++k) {  // uniform trip count: the reservations need the whole wave
-        const uint32_t p = chunk0 + k * TRI_BLOCK + threadIdx.x;
-        bool ok = false, needs_clip = false;
-        uint32_t sl0 = 0, sl1 = 0, sl2 = 0;
-        uint2 br = make_uint2(0u, 0u);
-        if (p < fp.nprims) {
-            const int d = find_range(b.draw_pbase, (int)fp.ndraws, p);
-            const TriDrawDev& dr = b.draws[d];
-            const uint32_t* ip = b.indices + dr.first_index + 3u * (p - b.draw_pbase[d]);
-            const uint32_t vb = b.draw_vbase[d] - dr.min_index;
-            sl0 = vb + ip[0]; sl1 = vb + ip[1]; sl2 = vb + ip[2];
-            const TriSnap a0 = b.snap[sl0], a1 = b.snap[sl1], a2 = b.snap[sl2];
-            const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
-            // invalid vertex, or trivial reject: all three vertices outside one clip half-space
-            if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
-                if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
-                    b.prim_vs[p] = make_uint4(sl0, sl1, sl2, (uint32_t)d | TRI_PRIM_CLIPPED);
-                    needs_clip = true;
-                } else {
-                    const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
-                    const int32_t Y[3] = {a0.y, a1.y, a2.y};
-                    const float z[3] = {a0.z, a1.z, a2.z};
-                    const float iw[3] = {a0.iw, a1.iw, a2.iw};
-                    TriRec r;
-                    ok = setup_snapped(fp, X, Y, z, iw, sl0, sl1, sl2, p << 3, r, br);
-                    if (ok) b.prim_vs[p] = make_uint4(sl0, sl1, sl2, (uint32_t)d);
+    // Two primitives per lane, set up and binned together: both index/vertex fetch chains are in
+    // flight at once, and the queue reservations of both are batched (one atomic round trip per
+    // batch), so a wave's dependent latencies are paid once for two primitives.
+    for (int k = 0; k < fp.ppt; k += 2) {  // uniform trip count: the reservations need the whole wave
+        uint32_t p[2], sl0[2], sl1[2], sl2[2];
+        bool ok[2], needs_clip[2];
+        uint2 br[2];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            p[t] = chunk0 + (k + t) * TRI_BLOCK + threadIdx.x;
+            ok[t] = false; needs_clip[t] = false;
+            sl0[t] = sl1[t] = sl2[t] = 0;
+            br[t] = make_uint2(0u, 0u);
+            if (p[t] < fp.nprims) {
+                const int d = find_range(b.draw_pbase, (int)fp.ndraws, p[t]);
+                const TriDrawDev& dr = b.draws[d];
+                const uint32_t* ip = b.indices + dr.first_index + 3u * (p[t] - b.draw_pbase[d]);
+                const uint32_t vb = b.draw_vbase[d] - dr.min_index;
+                sl0[t] = vb + ip[0]; sl1[t] = vb + ip[1]; sl2[t] = vb + ip[2];
+                const TriSnap a0 = b.snap[sl0[t]], a1 = b.snap[sl1[t]], a2 = b.snap[sl2[t]];
+                const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
+                // invalid vertex, or trivial reject: all three vertices outside one clip half-space
+                if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
+                    if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
+                        b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | TRI_PRIM_CLIPPED);
+                        needs_clip[t] = true;
+                    } else {
+                        const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
+                        const int32_t Y[3] = {a0.y, a1.y, a2.y};
+                        const float z[3] = {a0.z, a1.z, a2.z};
+                        const float iw[3] = {a0.iw, a1.iw, a2.iw};
+                        TriRec r;
+                        ok[t] = setup_snapped(fp, X, Y, z, iw, sl0[t], sl1[t], sl2[t], p[t] << 3, r, br[t]);
+                        if (ok[t]) b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d);
+                    }
+                }
+            }
+            nsetup += ok[t] ? 1u : 0u;
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+            uint64_t cm = __ballot(needs_clip[t]);  // rare: the wave clips its primitives one at a time
+            if (cm) {
+                if (lane == 0) atomicAdd(&b.counters->tris_clipped, (uint32_t)__builtin_popcountll(cm));
+                float* poly = clip_poly[threadIdx.x >> 6];
+                while (cm) {
+                    const int src = __builtin_ctzll(cm);
+                    cm &= cm - 1;
+                    clip_prim_wave(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)sl0[t], src),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)sl1[t], src),
+                                   (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src), nsetup, nentries);
                 }
             }
         }
-        nsetup += ok ? 1u : 0u;
-        uint64_t cm = __ballot(needs_clip);  // rare: the wave clips its primitives one at a time
-        if (cm) {
-            if (lanes_below(~0ull) == 0) atomicAdd(&b.counters->tris_clipped, (uint32_t)__builtin_popcountll(cm));
-            float* poly = clip_poly[threadIdx.x >> 6];
-            while (cm) {
-                const int src = __builtin_ctzll(cm);
-                cm &= cm - 1;
-                clip_prim_wave(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p, src),
-                               (uint32_t)__builtin_amdgcn_readlane((int)sl0, src),
-                               (uint32_t)__builtin_amdgcn_readlane((int)sl1, src),
-                               (uint32_t)__builtin_amdgcn_readlane((int)sl2, src), nsetup, nentries);
-            }
-        }
-        uint32_t bx = br.x & 0xFFFFu, by = br.x >> 16;
-        const uint32_t bx0 = bx, bx1 = br.y & 0xFFFFu, by1 = br.y >> 16;
-        bool has = ok && !(fp.ablate & 4);  // diagnostics: 4 = setup without binning
-        // One bin per lane per round. A batch of kResBatch rounds is planned with ballots and its
-        // reservations (one returning atomic per (wave, bin)) are all issued before any result is
-        // used, so the wave waits for one atomic round trip per batch instead of one per round.
-        // Diagnostics: TRI_ABLATE=8 waits per round (batches of one).
+        // The lane's bins, one per round: triangle 0's bbox, then triangle 1's.
+        bool has = (ok[0] || ok[1]) && !(fp.ablate & 4);  // diagnostics: 4 = setup without binning
+        bool second = !ok[0];
+        uint2 cur = second ? br[1] : br[0];
+        uint32_t bx = cur.x & 0xFFFFu, by = cur.x >> 16;
+        uint32_t bx0 = bx, bx1 = cur.y & 0xFFFFu, by1 = cur.y >> 16;
+        // A batch of kResBatch rounds is planned with ballots and its reservations (one returning
+        // atomic per (wave, bin)) are all issued before any result is used, so a wave waits for one
+        // atomic round trip per batch instead of one per round. Diagnostics: TRI_ABLATE=8 waits per
+        // round (batches of one).
         const int batch = (fp.ablate & 8) ? 1 : kResBatch;
         while (__ballot(has)) {
-            uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch];
+            uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch], rent[kResBatch];
             bool rwant[kResBatch];
 #pragma unroll
             for (int r = 0; r < kResBatch; ++r) {
                 rwant[r] = has && r < batch;
                 rbin[r] = by * (uint32_t)fp.nbx + bx;
+                rent[r] = second ? p[1] : p[0];
                 if (rwant[r]) {
                     if (bx < bx1) {
                         ++bx;
                     } else if (by < by1) {
                         bx = bx0;
                         ++by;
+                    } else if (!second && ok[1]) {
+                        second = true;
+                        bx = bx0 = br[1].x & 0xFFFFu; by = br[1].x >> 16;
+                        bx1 = br[1].y & 0xFFFFu; by1 = br[1].y >> 16;
                     } else {
                         has = false;
                     }
@@ -487,7 +510,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_setup(TriFrameParams fp, TriDevic
                 const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
                 if (rwant[r]) {
                     if (fp.ablate & 32) continue;  // diagnostics: 32 = no queue stores
-                    if (pos < cap) b.bin_list[(size_t)rbin[r] * cap + pos] = p;
+                    if (pos < cap) b.bin_list[(size_t)rbin[r] * cap + pos] = rent[r];
                     else note_bin_overflow(b, pos + 1);
                     ++nentries;
                 }

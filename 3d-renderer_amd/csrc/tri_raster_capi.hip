@@ -736,7 +736,7 @@ int tri_render(tri_ctx* c) {
     fp.bin_log2 = c->bin_log2;
     const uint32_t target_chunks = 4096;  // >= 16 binning workgroups per CU
     uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
-    ppt = std::min<uint32_t>(std::max<uint32_t>(ppt, 1), TRI_MAX_PPT);
+    ppt = std::min<uint32_t>(std::max<uint32_t>((ppt + 1) & ~1u, 2), TRI_MAX_PPT);  // k_setup takes pairs
     fp.ppt = (int32_t)ppt;
     fp.nchunks = (c->nprims + ppt * TRI_BLOCK - 1) / (ppt * TRI_BLOCK);
     fp.chunk_stride = chunk_stride(fp.nchunks);
