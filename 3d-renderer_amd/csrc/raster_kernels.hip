@@ -44,6 +44,35 @@ __device__ __forceinline__ int find_range(const uint32_t* base, int n, uint32_t 
     return lo;
 }
 
+// Raw buffer loads for k_raster's per-fragment gathers: a wave-uniform descriptor built from kernel
+// arguments (SGPRs) and a 32-bit byte offset per lane, so a 16-byte record is ONE load instruction
+// with no 64-bit address arithmetic (the compiler splits a plain struct load into per-field loads
+// when fields are used on different paths, and serialises the prim_vs -> vertex chain on it).
+// The host keeps every buffer read this way below 4 GiB (ensure_work_buffers).
+typedef __amdgpu_buffer_rsrc_t Rsrc;
+__device__ __forceinline__ Rsrc make_rsrc(const void* p, uint64_t bytes) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)(uint32_t)bytes, 0x00020000);
+}
+__device__ __forceinline__ uint4 ld128(Rsrc r, uint32_t off) {
+    const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
+    return make_uint4(v[0], v[1], v[2], v[3]);
+}
+struct FetchBufs {  // k_raster's gather sources
+    Rsrc prim_vs, snap, vary, shade;
+};
+__device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const TriDeviceBuffers& b) {
+    FetchBufs f;
+    f.prim_vs = make_rsrc(b.prim_vs, 16ull * fp.nprims);
+    f.snap = make_rsrc(b.snap, 16ull * fp.nslots);
+    f.vary = make_rsrc(b.vary, 48ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
+    f.shade = make_rsrc(b.draw_shade, (uint64_t)sizeof(TriDrawShade) * fp.ndraws);
+    return f;
+}
+__device__ __forceinline__ TriSnap ld_snap(const FetchBufs& fb, uint32_t slot) {
+    const uint4 q = ld128(fb.snap, slot * 16u);
+    return TriSnap{(int32_t)q.x, (int32_t)q.y, __uint_as_float(q.z), __uint_as_float(q.w)};
+}
+
 // ((c0*x + c1*y) + c2*z) + c3*w, column-major, no FMA (matches the oracle bit-for-bit)
 __device__ __forceinline__ float4 mat_vec_seq(const float* m, float4 v) {
     float4 r;
@@ -594,9 +623,10 @@ __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3
 // A bin-queue entry -> its triangle.
 __device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
     if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
-    const uint4 pv = b.prim_vs[e];
+    const FetchBufs fb = fetch_bufs(fp, b);
+    const uint4 pv = ld128(fb.prim_vs, e * 16u);
     const uint32_t sl[3] = {pv.x, pv.y, pv.z};
-    return rec_from_snaps(e, sl, b.snap[sl[0]], b.snap[sl[1]], b.snap[sl[2]]);
+    return rec_from_snaps(e, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
 }
 
 // Fragment depth at pixel centre: plane through the snapped vertices, fixed evaluation order.
@@ -917,14 +947,15 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
                                                   int32_t px, int32_t py, const float* lut, Put&& put) {
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
-    const uint4 pv = b.prim_vs[prim];
+    const FetchBufs fb = fetch_bufs(fp, b);
+    const uint4 pv = ld128(fb.prim_vs, prim * 16u);
     const uint32_t sl[3] = {pv.x, pv.y, pv.z};
-    const int d = (int)(pv.w & ~TRI_PRIM_CLIPPED);
+    const uint32_t d = pv.w & ~TRI_PRIM_CLIPPED;
     TriRec r;
     if (pv.w & TRI_PRIM_CLIPPED)
         r = load_rec(b.recs, b.clip_slot[prim] + (low & 7u));
     else
-        r = rec_from_snaps(prim, sl, b.snap[sl[0]], b.snap[sl[1]], b.snap[sl[2]]);
+        r = rec_from_snaps(prim, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
     float l0, l1, l2;
     if (EXACT) {  // exact int64 edge functions (oracle order)
         const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
@@ -960,15 +991,16 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
     }
     // plain-float views of the varyings (HIP vector unions defeat SROA in the pixel-pair path)
-    const V4* va = reinterpret_cast<const V4*>(b.vary + 3u * r.v[0]);
-    const V4* vb = reinterpret_cast<const V4*>(b.vary + 3u * r.v[1]);
-    const V4* vc = reinterpret_cast<const V4*>(b.vary + 3u * r.v[2]);
+    auto ldv = [&](uint32_t slot, uint32_t j) -> V4 {
+        const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);
+        return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
+    };
     auto ip = [&](float x0, float x1, float x2) {
         return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
     };
-    const V4 a0 = va[0], a1 = va[1], a2 = va[2];
-    const V4 b0 = vb[0], b1 = vb[1], b2 = vb[2];
-    const V4 c0 = vc[0], c1 = vc[1], c2 = vc[2];
+    const V4 a0 = ldv(r.v[0], 0), a1 = ldv(r.v[0], 1), a2 = ldv(r.v[0], 2);
+    const V4 b0 = ldv(r.v[1], 0), b1 = ldv(r.v[1], 1), b2 = ldv(r.v[1], 2);
+    const V4 c0 = ldv(r.v[2], 0), c1 = ldv(r.v[2], 1), c2 = ldv(r.v[2], 2);
     // field-wise stores (a struct-valued f3 store is ABI-coerced to <2 x float> + float, which
     // keeps the pixel-pair path's fragments from being promoted to registers)
     put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
@@ -976,10 +1008,16 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
     const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
     put(9, u); put(10, v);
-    const TriDrawShade& ds = b.draw_shade[d];
-    const float4 tx = sample_tex(ds.tex, u, v, lut);
+    const uint4 st = ld128(fb.shade, d * 48u), sd = ld128(fb.shade, d * 48u + 16u), ss = ld128(fb.shade, d * 48u + 32u);
+    TriTexDesc td;
+    td.texels = reinterpret_cast<const uint32_t*>(((uint64_t)sd.y << 32) | sd.x);
+    td.w = sd.z; td.h = sd.w;
+    td.solid[0] = __uint_as_float(ss.x); td.solid[1] = __uint_as_float(ss.y);
+    td.solid[2] = __uint_as_float(ss.z); td.solid[3] = __uint_as_float(ss.w);
+    const float4 tx = sample_tex(td, u, v, lut);
     put(11, tx.x); put(12, tx.y); put(13, tx.z); put(14, tx.w);
-    put(15, ds.tint[0]); put(16, ds.tint[1]); put(17, ds.tint[2]); put(18, ds.tint[3]);
+    put(15, __uint_as_float(st.x)); put(16, __uint_as_float(st.y)); put(17, __uint_as_float(st.z));
+    put(18, __uint_as_float(st.w));
 }
 
 template <bool EXACT>

@@ -374,8 +374,11 @@ int ensure_work_buffers(tri_ctx* c) {
     c->bin_cap = std::max<uint32_t>(c->bin_cap, 256u);
     const size_t nlist = (size_t)c->nbins * c->bin_cap;
     if (nlist * 4 > (8ull << 30)) return fail(TRI_E_OOM, "bin queues would need %zu MB", nlist * 4 >> 20);
-    if (nvary >= (1ull << 32))  // the kernels index varyings / indices with 32-bit arithmetic
-        return fail(TRI_E_INVALID, "too many vertex invocations (%zu varyings)", nvary);
+    // k_raster gathers varyings, snapped vertices and prim_vs records through raw buffer loads with
+    // 32-bit byte offsets
+    if (nvary * 16 > 0xFFFFFFFFull || (uint64_t)c->nprims * 16 > 0xFFFFFFFFull)
+        return fail(TRI_E_INVALID, "too many vertex invocations or primitives (%zu varyings, %u primitives)", nvary,
+                    c->nprims);
     bool realloc = c->cap_clip < std::max<size_t>(c->nslots, 1) || c->cap_vary < nvary || c->cap_recs < nrec ||
                    c->cap_clip_slot < std::max<size_t>(c->nprims, 1) || c->cap_prim_vs < std::max<size_t>(c->nprims, 1) ||
                    c->cap_bin_list < nlist;
