@@ -162,7 +162,7 @@ struct TriFrameParams {
     uint32_t sky_mode;
     uint32_t sky_bgra;
     uint32_t need_lut;  // some texture larger than 1x1 or a sampled skybox: k_raster stages the sRGB LUT
-    uint32_t pad_s;
+    uint32_t one_draw;  // exactly one draw: draw0 / vbase0 / pbase0 carry it (kernel arguments, scalar loads)
     float sky_far[16];  // inverse(Projection) applied to (xn, yn, 1, 1): rows {x, y, z, w} as (a, b, c, 0)
     float pv[16];
     float sky_ip[16];   // inverse(Projection) (double on the host, rounded)
@@ -171,4 +171,5 @@ struct TriFrameParams {
     tri_global_ubo ubo;
     tri_material_record mat0;
     TriShadeConst sc;
+    TriDrawDev draw0;  // the draw when one_draw (its vertex and primitive slots start at 0)
 };

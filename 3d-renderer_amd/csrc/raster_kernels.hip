@@ -97,18 +97,23 @@ __device__ __forceinline__ void reset_counters(TriCounters* c) {
 
 __global__ void k_reset(TriDeviceBuffers b) { reset_counters(b.counters); }
 
-__global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
-    const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
-    if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
-    if (slot >= fp.nslots) return;
-    const int d = find_range(b.draw_vbase, (int)fp.ndraws, slot);
-    const TriDrawDev& dr = b.draws[d];
-    const int64_t gi = (int64_t)dr.base_vertex + (int64_t)(dr.min_index + (slot - b.draw_vbase[d]));
+// Default.vert for vertex slot `slot` of draw `dr` (whose first slot is `vbase`).
+__device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
+                                            const TriDrawDev& dr, uint32_t vbase) {
+    const int64_t gi = (int64_t)dr.base_vertex + (int64_t)(dr.min_index + (slot - vbase));
     if (gi < 0 || (uint64_t)gi >= b.vertex_count) {
         b.snap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
         return;
     }
-    const TriVsIn in = b.vin[gi];
+    // three 16-byte loads (a plain struct load is split into overlapping per-field loads)
+    const Rsrc vr = make_rsrc(b.vin, 48ull * b.vertex_count);
+    const uint4 q0 = ld128(vr, (uint32_t)gi * 48u), q1 = ld128(vr, (uint32_t)gi * 48u + 16u),
+                q2 = ld128(vr, (uint32_t)gi * 48u + 32u);
+    TriVsIn in;
+    in.px = __uint_as_float(q0.x); in.py = __uint_as_float(q0.y); in.pz = __uint_as_float(q0.z);
+    in.nx = __uint_as_float(q0.w); in.ny = __uint_as_float(q1.x); in.nz = __uint_as_float(q1.y);
+    in.cr = __uint_as_float(q1.z); in.cg = __uint_as_float(q1.w); in.cb = __uint_as_float(q2.x);
+    in.u = __uint_as_float(q2.y); in.v = __uint_as_float(q2.z);
     float4 sp = make_float4(in.px, in.py, in.pz, 1.0f);
     float snx = in.nx, sny = in.ny, snz = in.nz;
     if (dr.bone_count > 0 && b.vskin) {  // Default.vert:64-85
@@ -158,6 +163,18 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
     vo[0] = make_float4(world.x, world.y, world.z, u);
     vo[1] = make_float4(nnx, nny, nnz, v);
     vo[2] = make_float4(in.cr, in.cg, in.cb, 0.0f);
+}
+
+__global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
+    const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
+    if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
+    if (slot >= fp.nslots) return;
+    if (fp.one_draw) {  // the draw's constants are kernel arguments: scalar loads, no dependent fetch
+        vertex_slot(fp, b, slot, fp.draw0, 0u);
+    } else {
+        const int d = find_range(b.draw_vbase, (int)fp.ndraws, slot);
+        vertex_slot(fp, b, slot, b.draws[d], b.draw_vbase[d]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -454,10 +471,18 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             sl0[t] = sl1[t] = sl2[t] = 0;
             br[t] = make_uint2(0u, 0u);
             if (p[t] < fp.nprims) {
-                const int d = find_range(b.draw_pbase, (int)fp.ndraws, p[t]);
-                const TriDrawDev& dr = b.draws[d];
-                const uint32_t* ip = b.indices + dr.first_index + 3u * (p[t] - b.draw_pbase[d]);
-                const uint32_t vb = b.draw_vbase[d] - dr.min_index;
+                int d = 0;
+                const uint32_t* ip;
+                uint32_t vb;
+                if (fp.one_draw) {  // kernel-argument constants: the index fetch starts at once
+                    ip = b.indices + fp.draw0.first_index + 3u * p[t];
+                    vb = 0u - fp.draw0.min_index;
+                } else {
+                    d = find_range(b.draw_pbase, (int)fp.ndraws, p[t]);
+                    const TriDrawDev& dr = b.draws[d];
+                    ip = b.indices + dr.first_index + 3u * (p[t] - b.draw_pbase[d]);
+                    vb = b.draw_vbase[d] - dr.min_index;
+                }
                 sl0[t] = vb + ip[0]; sl1[t] = vb + ip[1]; sl2[t] = vb + ip[2];
                 const TriSnap a0 = b.snap[sl0[t]], a1 = b.snap[sl1[t]], a2 = b.snap[sl2[t]];
                 const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;

@@ -116,6 +116,7 @@ struct tri_ctx {
     hipEvent_t stage_free = nullptr;
     uint32_t ndraws = 0, nslots = 0, nprims = 0;
     bool any_skin = false;
+    TriDrawDev draw0{};  // the resolved draw when there is exactly one (passed by value to the kernels)
 
     // work buffers
     float4* d_clip = nullptr; size_t cap_clip = 0;
@@ -342,6 +343,7 @@ int resolve_draws(tri_ctx* c) {
     if (!c->stage_free) HIP_TRY(hipEventCreateWithFlags(&c->stage_free, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(c->stage_free, c->stream));
     c->ndraws = n;
+    if (n == 1) c->draw0 = dd[0];
     c->nslots = (uint32_t)vslots;
     c->nprims = (uint32_t)prims;
     c->any_skin = skin;
@@ -563,6 +565,9 @@ int tri_upload_geometry(tri_ctx* c, const tri_vertex* v, uint64_t nv, const uint
                         const tri_mesh_range* meshes, uint32_t nm) {
     if (!c) return fail(TRI_E_INVALID, "tri_upload_geometry: null context");
     if ((nv && !v) || (ni && !idx) || (nm && !meshes)) return fail(TRI_E_INVALID, "tri_upload_geometry: null array");
+    if (nv * sizeof(TriVsIn) > 0xFFFFFFFFull)  // k_vertex reads the records with 32-bit byte offsets
+        return fail(TRI_E_INVALID, "tri_upload_geometry: %llu vertices exceed the 4 GiB vertex-record buffer",
+                    (unsigned long long)nv);
     int rc = make_current(c);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
@@ -751,6 +756,8 @@ int tri_render(tri_ctx* c) {
     fp.nprims = c->nprims;
     fp.nslots = c->nslots;
     fp.ndraws = c->ndraws;
+    fp.one_draw = c->ndraws == 1 ? 1u : 0u;
+    if (fp.one_draw) fp.draw0 = c->draw0;
     fp.ovf_rec_cap = c->ovf_rec_cap;
     fp.ovf_vert_cap = c->ovf_vert_cap;
     fp.bin_cap = c->bin_cap;
