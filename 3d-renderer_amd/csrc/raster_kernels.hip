@@ -906,7 +906,7 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
     const float ih = frsq(fmaxf(__builtin_fmaf(2.0f, LdotV, 2.0f), 1e-30f));
     const float NdotH = fmaxf((px.NdotVr + NdotLr) * ih, 0.0f);
     const float HdotV = fmaxf(__builtin_fmaf(LdotV, ih, ih), 0.0f);
-    const float NdotL = fmaxf(NdotLr, 0.0f);
+    const float NdotL = NdotLr;  // > 0 here: max(N.L, 0) is the identity
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
     const float gden = fmaxf(__builtin_fmaf(NdotL, sc.omkg, sc.kg), 1e-4f);
     const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
