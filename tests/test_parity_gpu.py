@@ -125,6 +125,22 @@ def test_row_bands_assemble_to_full_frame(nbands):
     assert np.array_equal(np.concatenate([p[1] for p in parts]), full_d)
 
 
+@pytest.mark.parametrize("case", ["near_clip", "primitives", "textured"])
+def test_row_bands_clip_draws_textures(oracle, case):
+    """Row bands with clipped primitives, several draws and textured draws assemble to the full
+    frame bit for bit, and each band matches the oracle's band (set-up counts included)."""
+    s = {"near_clip": lambda: sc.near_clip_grid(), "primitives": lambda: sc.primitives_row(oracle),
+         "textured": lambda: sc.textured_grid()}[case]()
+    full_c, full_d, _ = render_gpu(s)
+    cuts = np.linspace(0, s.height, 5).astype(int)
+    parts = []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        parts.append(render_gpu(s, band=(int(a), int(b))))
+        assert_parity(s, oracle, band=(int(a), int(b)), min_covered=0)
+    assert np.array_equal(np.concatenate([p[0] for p in parts]), full_c)
+    assert np.array_equal(np.concatenate([p[1] for p in parts]), full_d)
+
+
 def test_repeat_render_is_deterministic():
     from trident_raster import raster, scenes
 
