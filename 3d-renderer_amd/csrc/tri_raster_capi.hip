@@ -401,7 +401,14 @@ int collect_timing(tri_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (TimingSet& t : c->pending) {
         float ms[kStageCount], tot;
-        for (int i = 0; i < kStageCount; ++i) HIP_TRY(hipEventElapsedTime(&ms[i], t.ev[i], t.ev[i + 1]));
+        for (int i = 0; i < kStageCount; ++i) {
+            if (i == kStageClip) {  // no event: the stage is empty (clipping runs inside k_setup)
+                ms[i] = 0.0f;
+                continue;
+            }
+            const int next = i == kStageSetup ? kStageRaster : i + 1;
+            HIP_TRY(hipEventElapsedTime(&ms[i], t.ev[i], t.ev[next]));
+        }
         HIP_TRY(hipEventElapsedTime(&tot, t.ev[0], t.ev[kStageCount]));
         c->acc.ms_vertex += ms[kStageVertex];
         c->acc.ms_setup += ms[kStageSetup];

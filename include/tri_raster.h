@@ -141,7 +141,7 @@ typedef struct tri_timing {
     uint64_t frames;        /* frames timed since the last reset                  */
     double ms_vertex;       /* vs_transform (+ per-vertex divide / viewport / snap) */
     double ms_setup;        /* tri_setup_bin (setup + cull + per-bin queues)       */
-    double ms_clip;         /* homogeneous clipping of the (rare) straddling tris  */
+    double ms_clip;         /* always 0: clipping runs inside k_setup (in ms_setup)  */
     double ms_raster;       /* tile_raster_shade (coverage + early-Z + PBR + store) */
     double ms_frame;        /* first kernel start to last kernel end              */
     double reserved;
