@@ -1206,15 +1206,57 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
     return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
 }
 
+// Balanced coverage (16x16 bins, i.e. sparse frames; dense 32x32 bands keep the per-lane walk, where
+// C3's ~4-px rows made the per-job overhead cost more than the divergence it removed: 127 -> 136 us,
+// while C2 went 16.8k -> 19.0k fps): a pass takes up to kCovPass queue entries; each entry's edge/depth constants at its
+// clipped bbox corner go to LDS, and its bbox rows become jobs spread evenly over the workgroup, so a
+// wave no longer issues its longest triangle's whole bbox walk while most lanes idle. A row job steps
+// exactly like raster_serial (integer edge functions, float depth offsets in steps of 256: exact), so
+// the keys are bit-identical.
+#ifndef TRI_COV_BALANCED
+#define TRI_COV_BALANCED 1
+#endif
+constexpr int kCovPass = 160;   // entries per pass (LDS: 64 B each)
+constexpr int kCovJobs = 1024;  // row jobs per pass (u16: entry << 6 | row); rows beyond stay with their lane
+struct __attribute__((aligned(16))) CovEntry {
+    int32_t A[3], B[3], F[3];
+    float dzdX, dzdY, z0, fdx0, fdy0;
+    uint32_t low;
+    uint32_t pk;  // row0 (12 bits) | width - 1 (6 bits) << 12 | far_clip << 18
+};
+static_assert(sizeof(CovEntry) == 64, "CovEntry: 64 bytes");
+
+template <int BL>
+__device__ __forceinline__ void cov_row(const CovEntry& c, uint32_t r, uint64_t* keys) {
+    int32_t f0 = c.F[0] + c.B[0] * (int32_t)r, f1 = c.F[1] + c.B[1] * (int32_t)r, f2 = c.F[2] + c.B[2] * (int32_t)r;
+    const float t2 = c.dzdY * (c.fdy0 + 256.0f * (float)r);
+    const bool far_clip = (c.pk >> 18) & 1u;
+    const uint32_t row = (c.pk & 0xFFFu) + (r << BL);
+    const uint32_t rend = row + ((c.pk >> 12) & 0x3Fu);
+    float fdx = c.fdx0;
+    for (uint32_t a = row; a <= rend; ++a) {
+        if ((f0 | f1 | f2) >= 0) {
+            uint64_t key;
+            if (depth_key((c.z0 + c.dzdX * fdx) + t2, far_clip, c.low, key)) atomicMin(&keys[a], key);
+        }
+        f0 += c.A[0]; f1 += c.A[1]; f2 += c.A[2];
+        fdx += 256.0f;
+    }
+}
+
 template <bool EXACT, int BL>
 // 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
 // a little); 64x64 bins are LDS-limited to 3
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
-    __shared__ uint32_t bigq[kBigQueue];
+    constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
+    __shared__ uint32_t bigq[kBalanced ? kBigQueue / 2 : kBigQueue];
     __shared__ float lut[512];
-    __shared__ uint16_t skyq[BIN * BIN];
+    constexpr int kJobWords = (kBalanced && kCovJobs > BIN * BIN ? kCovJobs : BIN * BIN);
+    __shared__ uint16_t skyq[kJobWords];  // the coverage pass's row jobs, then the skybox queue
+    __shared__ CovEntry cov[kBalanced ? kCovPass : 1];
+    __shared__ uint32_t wsum[TRI_BLOCK / 64];
     __shared__ uint32_t nbig, nentries, nsky;
     const int tid = threadIdx.x;
     const int bin = xcd_bin(blockIdx.x, fp.nbins);
@@ -1243,6 +1285,78 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         }
         s1 = s0;
     }
+  if constexpr (kBalanced) {
+    uint16_t* jobs = skyq;
+    const uint32_t lane = lanes_below(~0ull);
+    for (uint32_t base = s0; base < s1; base += kCovPass) {  // uniform trip count
+        const uint32_t i = base + tid;
+        uint32_t nrows = 0;
+        TriRec r;
+        int32_t cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
+        if (tid < kCovPass && i < s1) {
+            const uint32_t ri = queue[i];
+            r = load_entry(fp, b, ri);
+            rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
+            if (cx0 <= cx1 && cy0 <= cy1) {
+                bool big = false;
+                if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > kBigArea) {
+                    const uint32_t q = atomicAdd(&nbig, 1u);
+                    if (q < kBigQueue / 2) { bigq[q] = ri; big = true; }
+                }
+                if (!big) {
+                    EdgeSetup e;
+                    edge_setup(r, e);
+                    bool rej = false;
+                    CovEntry c;
+#pragma unroll
+                    for (int k = 0; k < 3; ++k) {
+                        c.F[k] = clamp_edge((int64_t)e.A[k] * cx0 + (int64_t)e.B[k] * cy0 + e.D[k], rej);
+                        c.A[k] = e.A[k];
+                        c.B[k] = e.B[k];
+                    }
+                    if (!rej) {
+                        c.dzdX = e.dzdX; c.dzdY = e.dzdY; c.z0 = r.z[0];
+                        c.fdx0 = (float)(256 * cx0 + 128 - r.X[0]);
+                        c.fdy0 = (float)(256 * cy0 + 128 - r.Y[0]);
+                        c.low = key_low(r.prim_sub);
+                        const bool far_clip = (r.z[0] > 1.0f) || (r.z[1] > 1.0f) || (r.z[2] > 1.0f);
+                        c.pk = (uint32_t)(((cy0 - oy) << BL) + (cx0 - ox)) | ((uint32_t)(cx1 - cx0) << 12) |
+                               (far_clip ? 1u << 18 : 0u);
+                        cov[tid] = c;
+                        nrows = (uint32_t)(cy1 - cy0 + 1);
+                    }
+                }
+            }
+        }
+        // exclusive prefix sum of the row counts over the workgroup
+        uint32_t incl = nrows;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
+            if ((int)lane >= o) incl += t;
+        }
+        if (lane == 63) wsum[tid >> 6] = incl;
+        __syncthreads();
+        uint32_t start = incl - nrows, total = 0;
+#pragma unroll
+        for (int w = 0; w < TRI_BLOCK / 64; ++w) {
+            const uint32_t ws = wsum[w];
+            if (w < (tid >> 6)) start += ws;
+            total += ws;
+        }
+        for (uint32_t k = 0; k < nrows && start + k < (uint32_t)kCovJobs; ++k)
+            jobs[start + k] = (uint16_t)((tid << 6) | k);
+        __syncthreads();
+        const uint32_t njobs = min(total, (uint32_t)kCovJobs);
+        for (uint32_t j = tid; j < njobs; j += TRI_BLOCK) {
+            const uint32_t jb = jobs[j];
+            cov_row<BL>(cov[jb >> 6], jb & 63u, keys);
+        }
+        for (uint32_t k = (start < (uint32_t)kCovJobs ? (uint32_t)kCovJobs - start : 0u); k < nrows; ++k)
+            cov_row<BL>(cov[tid], k, keys);  // rows past the job table: the owner walks them
+        __syncthreads();  // cov / jobs / wsum are reused by the next pass
+    }
+  } else {
     for (uint32_t i = s0 + tid; i < s1; i += TRI_BLOCK) {
         const uint32_t ri = queue[i];
         const TriRec r = load_entry(fp, b, ri);
@@ -1256,7 +1370,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);
     }
     __syncthreads();
-    const uint32_t nb = min(nbig, (uint32_t)kBigQueue);
+  }
+    const uint32_t nb = min(nbig, (uint32_t)(kBalanced ? kBigQueue / 2 : kBigQueue));
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
         const TriRec r = load_entry(fp, b, bigq[q]);
         int32_t cx0, cx1, cy0, cy1;
