@@ -688,9 +688,13 @@ __device__ __forceinline__ uint32_t key_low(uint32_t prim_sub) {
     return ((TRI_PRIM_MAX - (prim_sub >> 3)) << 3) | (prim_sub & 7u);
 }
 
+// Rows cy0 + sub, cy0 + sub + step, ... of the bbox (sub < step: `step` lanes share a triangle). The
+// row starts are stepped exactly (integer edge values; float offsets in multiples of 256), so any
+// split gives the same keys as one lane walking every row.
 template <int BL>
 __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int32_t cx1, int32_t cy0, int32_t cy1,
-                                              int32_t ox, int32_t oy, uint64_t* keys) {
+                                              int32_t ox, int32_t oy, uint64_t* keys, int32_t sub = 0,
+                                              int32_t step = 1) {
     EdgeSetup e;
     edge_setup(r, e);
     bool rej = false;
@@ -703,9 +707,11 @@ __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int3
     // frag_depth's pixel offsets stepped incrementally: |256 p + 128 - X0| < 2^24, so the float steps
     // of 256 are exact and equal its int -> float conversions; same (z0 + dzdX dx) + dzdY dy order
     const float fdx0 = (float)(256 * cx0 + 128 - r.X[0]);
-    float fdy = (float)(256 * cy0 + 128 - r.Y[0]);
-    uint32_t row = (uint32_t)(((cy0 - oy) << BL) + (cx0 - ox));
-    for (int32_t py = cy0; py <= cy1; ++py) {
+    float fdy = (float)(256 * (cy0 + sub) + 128 - r.Y[0]);
+    uint32_t row = (uint32_t)(((cy0 + sub - oy) << BL) + (cx0 - ox));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) F[k] += e.B[k] * sub;
+    for (int32_t py = cy0 + sub; py <= cy1; py += step) {
         const float t2 = e.dzdY * fdy;
         int32_t f0 = F[0], f1 = F[1], f2 = F[2];
         float fdx = fdx0;
@@ -718,9 +724,9 @@ __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int3
             f0 += e.A[0]; f1 += e.A[1]; f2 += e.A[2];
             fdx += 256.0f;
         }
-        F[0] += e.B[0]; F[1] += e.B[1]; F[2] += e.B[2];
-        fdy += 256.0f;
-        row += 1u << BL;
+        F[0] += e.B[0] * step; F[1] += e.B[1] * step; F[2] += e.B[2] * step;
+        fdy += 256.0f * (float)step;
+        row += (uint32_t)step << BL;
     }
 }
 
@@ -1213,6 +1219,9 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 // wave no longer issues its longest triangle's whole bbox walk while most lanes idle. A row job steps
 // exactly like raster_serial (integer edge functions, float depth offsets in steps of 256: exact), so
 // the keys are bit-identical.
+#ifndef TRI_COV_SHARE
+#define TRI_COV_SHARE 2  // 32x32 bins: lanes per triangle when the bin has at most TRI_BLOCK / share entries
+#endif
 #ifndef TRI_COV_BALANCED
 #define TRI_COV_BALANCED 1
 #endif
@@ -1357,17 +1366,24 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         __syncthreads();  // cov / jobs / wsum are reused by the next pass
     }
   } else {
-    for (uint32_t i = s0 + tid; i < s1; i += TRI_BLOCK) {
+    // `share` lanes per triangle when the bin has few entries (lanes would idle otherwise); each takes
+    // every share-th row of its bbox. Uniform per workgroup.
+    const int share = TRI_COV_SHARE > 1 && (s1 - s0) * TRI_COV_SHARE <= TRI_BLOCK ? TRI_COV_SHARE : 1;
+    const int sub = tid % share;
+    for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) {
         const uint32_t ri = queue[i];
         const TriRec r = load_entry(fp, b, ri);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
         if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > kBigArea) {
+            if (sub != 0) continue;  // the first lane of the group hands it over
             const uint32_t q = atomicAdd(&nbig, 1u);
             if (q < kBigQueue) { bigq[q] = ri; continue; }
+            raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);  // queue full: this lane walks it all
+            continue;
         }
-        raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);
+        raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys, sub, share);
     }
     __syncthreads();
   }
