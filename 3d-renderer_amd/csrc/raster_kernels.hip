@@ -1220,7 +1220,10 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 // exactly like raster_serial (integer edge functions, float depth offsets in steps of 256: exact), so
 // the keys are bit-identical.
 #ifndef TRI_COV_SHARE
-#define TRI_COV_SHARE 2  // 32x32 bins: lanes per triangle when the bin has at most TRI_BLOCK / share entries
+#define TRI_COV_SHARE 2  // 32x32 bins: lanes per triangle when the bin has at most TRI_COV_SHARE_MAX entries
+#endif
+#ifndef TRI_COV_SHARE_MAX
+#define TRI_COV_SHARE_MAX (TRI_BLOCK / TRI_COV_SHARE)  // one entry per lane group
 #endif
 #ifndef TRI_COV_BALANCED
 #define TRI_COV_BALANCED 1
@@ -1368,7 +1371,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
   } else {
     // `share` lanes per triangle when the bin has few entries (lanes would idle otherwise); each takes
     // every share-th row of its bbox. Uniform per workgroup.
-    const int share = TRI_COV_SHARE > 1 && (s1 - s0) * TRI_COV_SHARE <= TRI_BLOCK ? TRI_COV_SHARE : 1;
+    const int share = TRI_COV_SHARE > 1 && (s1 - s0) <= TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
     const int sub = tid % share;
     for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) {
         const uint32_t ri = queue[i];
