@@ -26,6 +26,13 @@
 // prim_vs[p].w flag: primitive p was clipped (its fragments come from TriRec sub-triangles)
 #define TRI_PRIM_CLIPPED 0x80000000u
 #define TRI_MAX_CLIP_VERTS 12
+// Clipping a triangle by 6 planes yields at most 3 + 6 = 9 vertices; a numerically non-convex
+// polygon can come out longer and is cut to its first 9 (oracle clip_polygon does the same). The fan
+// then has at most 7 sub-triangles, whose index fits the 3-bit `sub` field of a visibility key with
+// sub = 7 left unused, so no key of primitive 0 can equal the background key (depth 1, low 0xFFFFFFFF).
+#define TRI_MAX_CLIP_POLY 9
+static_assert(TRI_MAX_CLIP_POLY - 2 <= 7, "clipped sub-triangle index must fit 3 bits without reaching 7");
+static_assert(TRI_MAX_CLIP_POLY <= TRI_MAX_CLIP_VERTS, "clip polygon buffers");
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f
 #define TRI_MAX_PPT 8  // primitives per k_setup thread
@@ -142,7 +149,7 @@ struct TriFrameParams {
     int32_t W, H, y0, y1;
     int32_t nbx, nby, nbins, ppt;
     int32_t bin_log2;
-    uint32_t ablate;  // diagnostics only (TRI_ABLATE env): 1 = skip shading, 2 = skip coverage
+    uint32_t pad_a;
     uint32_t chunk_stride;  // k_setup visits chunks in the order (blockIdx * stride) mod nchunks
     int32_t pad_b2;
     float hw, hh, gx, gy;

@@ -24,6 +24,15 @@
 
 namespace {
 
+// Diagnostics builds only (tools/build_variant.sh NAME -DTRI_ABLATE=N): 1 = coverage without shading,
+// 2 = shading without coverage, 4 = set-up without binning, 8 = one reservation round per batch,
+// 16 = no reservation atomics, 32 = no queue stores. The shipped library is built with 0, so none of
+// these tests survives into its ISA.
+#ifndef TRI_ABLATE
+#define TRI_ABLATE 0
+#endif
+constexpr uint32_t kAblate = TRI_ABLATE;
+
 constexpr uint64_t kBgKey = (0x3F800000ull << 32) | 0xFFFFFFFFull;  // depth 1.0, lowest priority
 constexpr float kPi = 3.14159265359f;                                  // Default.frag:65
 
@@ -386,6 +395,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
     }
     wave_lds_sync();
     if (n < 3) return;
+    n = min(n, TRI_MAX_CLIP_POLY);
     const uint32_t nsub = (uint32_t)(n - 2);
     uint32_t rbase = 0, vbase = 0;
     if (lane == 0) {
@@ -521,7 +531,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             }
         }
         // The lane's bins, one per round: triangle 0's bbox, then triangle 1's.
-        bool has = (ok[0] || ok[1]) && !(fp.ablate & 4);  // diagnostics: 4 = setup without binning
+        bool has = (ok[0] || ok[1]) && !(kAblate & 4);  // diagnostics: 4 = setup without binning
         bool second = !ok[0];
         uint2 cur = second ? br[1] : br[0];
         uint32_t bx = cur.x & 0xFFFFu, by = cur.x >> 16;
@@ -530,7 +540,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
         // atomic per (wave, bin)) are all issued before any result is used, so a wave waits for one
         // atomic round trip per batch instead of one per round. Diagnostics: TRI_ABLATE=8 waits per
         // round (batches of one).
-        const int batch = (fp.ablate & 8) ? 1 : kResBatch;
+        const int batch = (kAblate & 8) ? 1 : kResBatch;
         while (__ballot(has)) {
             uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch], rent[kResBatch];
             bool rwant[kResBatch];
@@ -556,14 +566,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 uint32_t cnt;
                 wave_reserve_plan(rbin[r], rwant[r], rlead[r], rrank[r], cnt);
                 rbase[r] = 0;
-                if (rwant[r] && lane == rlead[r] && !(fp.ablate & 16))  // diagnostics: 16 = no atomics
+                if (rwant[r] && lane == rlead[r] && !(kAblate & 16))  // diagnostics: 16 = no atomics
                     rbase[r] = atomicAdd(&b.bin_count[rbin[r]], cnt);
             }
 #pragma unroll
             for (int r = 0; r < kResBatch; ++r) {
                 const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
                 if (rwant[r]) {
-                    if (fp.ablate & 32) continue;  // diagnostics: 32 = no queue stores
+                    if (kAblate & 32) continue;  // diagnostics: 32 = no queue stores
                     if (pos < cap) b.bin_list[(size_t)rbin[r] * cap + pos] = rent[r];
                     else note_bin_overflow(b, pos + 1);
                     ++nentries;
@@ -1225,6 +1235,8 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 #ifndef TRI_COV_SHARE_MAX
 #define TRI_COV_SHARE_MAX (TRI_BLOCK / TRI_COV_SHARE)  // one entry per lane group
 #endif
+static_assert((TRI_COV_SHARE & (TRI_COV_SHARE - 1)) == 0 && TRI_BLOCK % TRI_COV_SHARE == 0,
+              "TRI_COV_SHARE must be a power of two dividing the workgroup (each lane group owns one entry)");
 #ifndef TRI_COV_BALANCED
 #define TRI_COV_BALANCED 1
 #endif
@@ -1289,7 +1301,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     __syncthreads();
     const uint32_t* queue = b.bin_list + (size_t)bin * fp.bin_cap;
     uint32_t s0 = 0, s1 = nentries;
-    if (fp.ablate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
+    if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
             const TriRec r = load_entry(fp, b, queue[0]);
             const uint64_t key = (0x3F000000ull << 32) | key_low(r.prim_sub);
@@ -1451,7 +1463,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
             if (!sky_queue) b.color[o] = bg_bgra;
             if (fp.write_depth) b.depth[o] = 1.0f;
             continue;
-        } else if (fp.ablate & 1) {  // diagnostics: coverage only
+        } else if (kAblate & 1) {  // diagnostics: coverage only
             z = __uint_as_float((uint32_t)(key >> 32));
             out = (uint32_t)key;
         } else {

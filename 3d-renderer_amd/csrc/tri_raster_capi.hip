@@ -788,11 +788,6 @@ int tri_render(tri_ctx* c) {
     }
     for (int t = 0; t < TRI_MAX_TEXTURE_SLOTS && !fp.need_lut; ++t)
         fp.need_lut = c->d_tex[t] && (c->tex_w[t] != 1 || c->tex_h[t] != 1);
-    static const uint32_t ablate = [] {  // diagnostics only: TRI_ABLATE=1 no shading, 2 no coverage
-        const char* e = getenv("TRI_ABLATE");
-        return e ? (uint32_t)atoi(e) : 0u;
-    }();
-    fp.ablate = ablate;
     std::memcpy(fp.pv, c->pv, 64);
     fp.ubo = c->ubo;
     fp.mat0 = c->mat0;

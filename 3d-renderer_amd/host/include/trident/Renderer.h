@@ -118,6 +118,9 @@ private:
         glm::mat4 m_ModelMatrix{1.0f};
         const MeshComponent* m_Component = nullptr;
         const TextureComponent* m_TextureComponent = nullptr;
+        const AnimationComponent* m_AnimationComponent = nullptr;
+        uint32_t m_BoneOffset = 0;
+        uint32_t m_BoneCount = 0;
         ECS::Entity m_Entity = 0;
     };
     struct ViewportContext {
@@ -125,6 +128,7 @@ private:
         tri_ctx* m_Ctx = nullptr;
         uint32_t m_Width = 0, m_Height = 0;
         uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0, m_SkyboxGeneration = 0;
+        std::vector<float> m_BonePalette;  // the palette last uploaded to this viewport's context
     };
 
     void UploadMeshFromCache();
@@ -132,6 +136,7 @@ private:
     size_t CreatePrimitiveMeshInCache(MeshComponent::PrimitiveType primitiveType);
     void ResolveMaterialTextureSlots(const std::vector<std::string>& textures, size_t offset, size_t count);
     void GatherMeshDraws();
+    void PrepareBonePaletteBuffer();
     void UpdateUniformBuffer(const Camera* camera, tri_global_ubo& out) const;
     void BuildDrawList(std::vector<tri_draw>& out) const;
     const Camera* GetActiveCamera(const ViewportContext& context) const;
@@ -147,6 +152,8 @@ private:
     std::vector<Geometry::Material> m_Materials;
     std::vector<MeshDrawInfo> m_MeshDrawInfo;
     std::vector<MeshDrawCommand> m_MeshDrawCommands;
+    static constexpr uint32_t s_MaxBonesPerSkeleton = 128;  // Renderer.h:291
+    std::vector<float> m_BonePalette;  // PrepareBonePaletteBuffer's scratch: per-draw palettes, back to back
     size_t m_PrimitiveMeshIndices[3] = {SIZE_MAX, SIZE_MAX, SIZE_MAX};
     bool m_IsUploadingMeshes = false;
     std::vector<tri_vertex> m_VertexBuffer;

@@ -115,6 +115,13 @@ struct LightComponent {
     bool m_Reserved1 = false;
 };
 
+// AnimationComponent (ECS/Components/AnimationComponent.h:29-73), the part the renderer reads: the
+// skinning palette the CPU animation system writes each frame (m_BoneMatrices, column-major mat4s).
+// Clip/skeleton bookkeeping stays with the animation system, which is outside the hot path.
+struct AnimationComponent {
+    std::vector<glm::mat4> m_BoneMatrices{};
+};
+
 struct TagComponent {
     std::string m_Tag;
 };

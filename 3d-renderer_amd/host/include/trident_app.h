@@ -40,6 +40,9 @@ int trident_app_set_entity_texture(trident_app* app, uint32_t entity, const char
 int trident_app_set_entity_transform(trident_app* app, uint32_t entity, const float position[3],
                                      const float rotation_deg[3], const float scale[3]);
 int trident_app_set_entity_visible(trident_app* app, uint32_t entity, int visible);
+/* AnimationComponent::m_BoneMatrices of an entity (count column-major mat4s; 0 clears the palette):
+ * the draw skins with them (PrepareBonePaletteBuffer, Renderer.cpp:3168-3245). */
+int trident_app_set_entity_bones(trident_app* app, uint32_t entity, const float* matrices, uint32_t count);
 int trident_app_add_light(trident_app* app, int type, const float position[3], const float direction[3],
                           const float color[3], float intensity, float range, int enabled, uint32_t* entity);
 

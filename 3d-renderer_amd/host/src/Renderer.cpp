@@ -378,9 +378,33 @@ void Renderer::GatherMeshDraws() {  // Renderer.cpp:2910-2994
             }
             cmd.m_TextureComponent = &t;
         }
+        if (m_Registry->HasComponent<AnimationComponent>(e))
+            cmd.m_AnimationComponent = &m_Registry->GetComponent<AnimationComponent>(e);
         cmd.m_Component = &c;
         cmd.m_Entity = e;
         m_MeshDrawCommands.push_back(cmd);
+    }
+}
+
+// Renderer.cpp:3168-3245: each animated draw gets a slice [offset, offset + count) of one palette
+// (count clamped to s_MaxBonesPerSkeleton); draws without a palette keep offset 0 / count 0.
+void Renderer::PrepareBonePaletteBuffer() {
+    m_BonePalette.clear();
+    uint32_t total = 0;
+    for (MeshDrawCommand& cmd : m_MeshDrawCommands) {
+        cmd.m_BoneOffset = 0;
+        cmd.m_BoneCount = 0;
+        if (!cmd.m_AnimationComponent || cmd.m_AnimationComponent->m_BoneMatrices.empty()) continue;
+        const auto& src = cmd.m_AnimationComponent->m_BoneMatrices;
+        const uint32_t n = (uint32_t)std::min<size_t>(src.size(), s_MaxBonesPerSkeleton);
+        cmd.m_BoneOffset = total;
+        cmd.m_BoneCount = n;
+        total += n;
+        for (uint32_t b = 0; b < n; ++b) {
+            float m[16];
+            CopyMat(src[b], m);
+            m_BonePalette.insert(m_BonePalette.end(), m, m + 16);
+        }
     }
 }
 
@@ -405,6 +429,8 @@ void Renderer::BuildDrawList(std::vector<tri_draw>& out) const {  // Renderer.cp
             slot = m_Materials[info.m_MaterialIndex].BaseColorTextureSlot;
         pc.texture_slot = slot;
         pc.material_index = info.m_MaterialIndex;
+        pc.bone_offset = static_cast<int32_t>(cmd.m_BoneOffset);  // :5145-5146
+        pc.bone_count = static_cast<int32_t>(cmd.m_BoneCount);
         out.push_back(d);
     }
 }
@@ -573,6 +599,7 @@ bool Renderer::BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::v
     auto it = m_Viewports.find(viewportId);
     if (it == m_Viewports.end()) return false;
     GatherMeshDraws();
+    PrepareBonePaletteBuffer();
     UpdateUniformBuffer(GetActiveCamera(it->second), ubo);
     BuildDrawList(draws);
     return true;
@@ -582,6 +609,7 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     const auto t0 = std::chrono::steady_clock::now();
     if (!m_Initialised || m_Shutdown) return;
     GatherMeshDraws();
+    PrepareBonePaletteBuffer();
     std::vector<tri_draw> draws;
     BuildDrawList(draws);
     const float clear[4] = {m_ClearColor.x, m_ClearColor.y, m_ClearColor.z, m_ClearColor.w};
@@ -589,6 +617,13 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     for (auto& it : m_Viewports) {  // RecordCommandBuffer's per-viewport render passes
         ViewportContext& vc = it.second;
         if (!PrepareViewport(vc)) continue;
+        if (vc.m_BonePalette != m_BonePalette) {  // the bone SSBO (binding 4) of this frame
+            if (tri_upload_bone_palette(vc.m_Ctx, m_BonePalette.data(), (uint32_t)(m_BonePalette.size() / 16)) != TRI_OK) {
+                LogError("bone palette", tri_last_error());
+                continue;
+            }
+            vc.m_BonePalette = m_BonePalette;
+        }
         tri_global_ubo ubo;
         UpdateUniformBuffer(GetActiveCamera(vc), ubo);
         if (tri_set_frame(vc.m_Ctx, &ubo, clear) != TRI_OK ||

@@ -147,6 +147,20 @@ int trident_app_set_entity_visible(trident_app* app, uint32_t entity, int visibl
     });
 }
 
+int trident_app_set_entity_bones(trident_app* app, uint32_t entity, const float* matrices, uint32_t count) {
+    return Guard(app, [&] {
+        if (count && !matrices) return TRI_E_INVALID;
+        AnimationComponent& a = app->registry.HasComponent<AnimationComponent>(entity)
+                                    ? app->registry.GetComponent<AnimationComponent>(entity)
+                                    : app->registry.AddComponent<AnimationComponent>(entity);
+        a.m_BoneMatrices.resize(count);
+        for (uint32_t b = 0; b < count; ++b)
+            for (int c = 0; c < 4; ++c)
+                for (int r = 0; r < 4; ++r) a.m_BoneMatrices[b][c][r] = matrices[16 * b + 4 * c + r];
+        return TRI_OK;
+    });
+}
+
 int trident_app_add_light(trident_app* app, int type, const float position[3], const float direction[3],
                           const float color[3], float intensity, float range, int enabled, uint32_t* entity) {
     return Guard(app, [&] {

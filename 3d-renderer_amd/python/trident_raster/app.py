@@ -28,6 +28,7 @@ _APP_FUNCTIONS = [
     ("trident_app_set_entity_texture", C.c_int, [C.c_void_p, C.c_uint32, C.c_char_p]),
     ("trident_app_set_entity_transform", C.c_int, [C.c_void_p, C.c_uint32, _f3, _f3, _f3]),
     ("trident_app_set_entity_visible", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
+    ("trident_app_set_entity_bones", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
     ("trident_app_add_light", C.c_int, [C.c_void_p, C.c_int, _f3, _f3, _f3, C.c_float, C.c_float, C.c_int,
                                         C.POINTER(C.c_uint32)]),
     ("trident_app_set_camera", C.c_int, [C.c_void_p, C.c_int, _f3, _f3, C.c_float, C.c_float, C.c_float, C.c_int]),
@@ -130,6 +131,12 @@ class TridentApp:
 
     def set_entity_visible(self, entity, visible):
         _check(self._lib.trident_app_set_entity_visible(self._h, entity, 1 if visible else 0), "set_entity_visible")
+
+    def set_entity_bones(self, entity, matrices):
+        """AnimationComponent::m_BoneMatrices: float32 [n, 4, 4] column-major mat4s (m[col][row])."""
+        m = np.ascontiguousarray(matrices, dtype=np.float32).reshape(-1, 16)
+        _check(self._lib.trident_app_set_entity_bones(self._h, entity, m.ctypes.data if m.size else None,
+                                                      m.shape[0]), "set_entity_bones")
 
     def add_light(self, type, position=(0, 0, 0), direction=(-0.5, -1.0, -0.3), color=(1.0, 0.98, 0.92),
                   intensity=5.0, range=10.0, enabled=True):

@@ -128,19 +128,31 @@ class BandRenderer:
                                lambda n: torch.empty(n, dtype=torch.int32, device=self.dev))
         self.depth = torch.empty(rows * W, dtype=torch.float32, device=self.dev)
         self.r = raster.TriRaster(W, H, band=self.band, device=device_index)
-        self.r.set_stream(torch.cuda.current_stream(self.dev).cuda_stream)
+        # A dedicated render stream (a non-zero handle) that is torch's current stream while a frame is
+        # enqueued and published: RCCL's all-gather then waits on the stream k_raster wrote the band on,
+        # and work.wait() in GatherRing.acquire orders that same stream behind the gather that read the
+        # slot. (Torch's default stream is handle 0, which tri_set_stream takes as "the context's own
+        # non-blocking stream" — unordered with the collective.)
+        self.stream = torch.cuda.Stream(self.dev)
+        self.r.set_stream(self.stream.cuda_stream)
         scenes.load_scene(self.r, scene)
 
     def step(self):
+        import torch
+
         s = self.scene
-        self.r.bind_output(self.ring.acquire().data_ptr(), self.depth.data_ptr())
-        self.r.set_frame(s.ubo, s.clear)  # per-frame uniform update
-        self.r.set_draws(s.draws)         # per-frame draw list (push constants)
-        self.r.render()
-        self.ring.publish()
+        with torch.cuda.stream(self.stream):
+            self.r.bind_output(self.ring.acquire().data_ptr(), self.depth.data_ptr())
+            self.r.set_frame(s.ubo, s.clear)  # per-frame uniform update
+            self.r.set_draws(s.draws)         # per-frame draw list (push constants)
+            self.r.render()
+            self.ring.publish()
 
     def drain(self):
-        self.ring.drain()
+        import torch
+
+        with torch.cuda.stream(self.stream):
+            self.ring.drain()
 
     def latency_ms(self, frames=20):
         """Per-frame latency without overlap: render + gather + wait, host-synchronised each frame."""
@@ -159,7 +171,11 @@ class BandRenderer:
         return ts[len(ts) // 2]
 
 
-def timed_run(br, steps, warmup, dist_on, stage_timing=True, period=16):
+def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256):
+    """Time exactly `steps` frames (no per-kernel events inside the timed region), then, outside it,
+    a separate pass of `event_frames` frames with HIP events around every kernel of every frame:
+    the per-kernel durations (roofline.kernel_ms) rest on that many samples, not on the few frames a
+    short timed run would leave."""
     import torch
 
     br.r.render_frame()  # first frame sizes the internal queues (re-renders after TRI_E_OVERFLOW)
@@ -172,9 +188,6 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, period=16):
         import torch.distributed as dist
 
         dist.barrier()
-    # per-kernel HIP events on every `period`-th timed frame (events on every frame cost ~9% fps,
-    # every 8th ~1.5 % at N = 1 and ~3.5 % on an 8-way band)
-    br.r.set_timing(stage_timing, period)
     t0 = time.perf_counter()
     for _ in range(steps):
         br.step()
@@ -184,8 +197,14 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, period=16):
         dist.barrier()
     dt = time.perf_counter() - t0
     br.r.synchronize()  # surfaces TRI_E_OVERFLOW if any timed frame overflowed
-    timing = br.r.timing()
-    br.r.set_timing(False)
+    timing = None
+    if stage_timing:
+        br.r.set_timing(True, 1)
+        for _ in range(event_frames):
+            br.step()
+        br.drain()
+        timing = br.r.timing()
+        br.r.set_timing(False)
     return max_over_ranks(dt, br.dev, dist_on), timing
 
 
@@ -195,7 +214,11 @@ def cpu_baseline(scene, seconds):
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
-    threads = min(os.cpu_count() or 1, int(os.environ.get("OMP_NUM_THREADS", "16") or 16), 16)
+    # every host core ("all host cores, core count stated"); capped at 256 threads to
+    # stay far inside the GPU box's per-job task limit. A cgroup CPU quota below that (the box's CPU
+    # share) shows up as threads that do not all run at once, which is part of the measurement.
+    host_cpus = os.cpu_count() or 1
+    threads = min(host_cpus, 256)
     oracle_py.render(scene, threads=threads)  # warm-up frame (page-in, allocator)
     n, t0 = 0, time.perf_counter()
     while True:
@@ -204,7 +227,12 @@ def cpu_baseline(scene, seconds):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = host_cpus
+    return {"value": n / dt, "unit": "frames/s", "cores": threads, "host_cpus": host_cpus,
+            "affinity_cpus": affinity, "kind": "port",
             "sample": f"{n} full {scene.width}x{scene.height} frame(s) of {scene.name} "
                       f"({scene.triangles} tris) rendered by oracle/tri_oracle.cpp, {dt:.1f} s"}
 
@@ -264,6 +292,8 @@ def main():
 
     # roofline of the dominant kernel (k_raster = tile_raster_shade): its algorithmic bytes per
     # launch are the colour + depth it must store for its band (4 + 4 B per pixel).
+    if timing is None:
+        timing = {"frames": 0, "ms_vertex": 0.0, "ms_setup": 0.0, "ms_clip": 0.0, "ms_raster": 0.0, "ms_frame": 0.0}
     frames_timed = max(int(timing["frames"]), 1)
     raster_ms = timing["ms_raster"] / frames_timed
     # whole-frame figure on the throughput clock: with two frames in flight the event span of one
@@ -321,7 +351,8 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "kernel": "k_raster",
-                         "kernel_ms": raster_ms, "algorithmic_bytes": raster_bytes},
+                         "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]),
+                         "algorithmic_bytes": raster_bytes},
             "frame_roofline": {"algorithmic_bytes": frame_bytes, "ms_per_frame": frame_ms,
                                "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9 if frame_ms > 0 else None,
                                "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if frame_ms > 0 else None},

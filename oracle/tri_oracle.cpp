@@ -252,6 +252,9 @@ int clip_polygon(const Setup& su, const VsOut in[3], VsOut* out /* >= 9 */) {
         n = m;
         std::swap(src, dst);
     }
+    // a triangle clipped by 6 planes has at most 9 vertices; a numerically non-convex polygon is cut
+    // to its first 9 (fan sub-triangle indices 0..6, as the kernels' 3-bit key field requires)
+    n = std::min(n, 9);
     for (int k = 0; k < n; ++k) out[k] = src[k];
     return n;
 }

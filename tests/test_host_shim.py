@@ -196,10 +196,58 @@ def test_draw_frame_records_frame_timing(app_mod):
     assert rgba.shape == (H, W, 4)
 
 
+def bone_palette(n, seed):
+    """n column-major bone matrices: small rotations about Y plus translations."""
+    rng = np.random.default_rng(seed)
+    out = np.zeros((n, 4, 4), np.float32)
+    for b in range(n):
+        a = rng.uniform(-0.4, 0.4)
+        c, s_ = np.cos(a), np.sin(a)
+        m = np.eye(4, dtype=np.float32)
+        m[0, 0], m[0, 2], m[2, 0], m[2, 2] = c, -s_, s_, c  # m[col][row]
+        m[3, :3] = rng.uniform(-0.3, 0.3, 3)
+        out[b] = m
+    return out
+
+
+def skinned_app(app_mod, flags=0, w=W, h=H):
+    """Two animated entities (AnimationComponent palettes of 3 and 200 bones, the second clamped to
+    s_MaxBonesPerSkeleton = 128) around a static cube."""
+    from trident_raster import scenes
+
+    a = app_mod.TridentApp(flags)
+    a.set_camera("editor", (0.0, 0.5, 4.0))
+    a.set_viewport(1, w, h)
+
+    v, i = scenes.uv_sphere_mesh(12, 16, 0.6)
+    rng = np.random.default_rng(5)
+    v["bone_indices"] = rng.integers(0, 3, size=(v.size, 4))
+    wts = rng.uniform(0.0, 1.0, size=(v.size, 4)).astype(np.float32)
+    v["bone_weights"] = wts / wts.sum(-1, keepdims=True)
+    m = a.append_mesh(v, i, base_color=(0.8, 0.7, 0.9, 1), metallic=0.1, roughness=0.6)
+    e1 = a.add_mesh_entity("none", m, position=(-0.8, 0.3, 0))
+    a.add_mesh_entity("cube", position=(0, -0.6, -1.0))
+    e2 = a.add_mesh_entity("none", m, position=(0.8, 0.3, 0))
+    p1, p2 = bone_palette(3, 1), bone_palette(200, 2)
+    a.set_entity_bones(e1, p1)
+    a.set_entity_bones(e2, p2)
+    return a, np.concatenate([p1, p2[:128]]).reshape(-1, 16)
+
+
+def test_bone_palette_offsets(app_mod):
+    """PrepareBonePaletteBuffer (Renderer.cpp:3168-3245): animated draws get consecutive palette slices,
+    counts clamp to 128, static draws keep 0 / 0 (pushed at :5145-5146)."""
+    a, _ = skinned_app(app_mod)
+    a.frame_inputs(1)  # first frame creates the lazy cube primitive
+    _, draws = a.frame_inputs(1)
+    got = [(d.pc.bone_offset, d.pc.bone_count) for d in draws]
+    assert got == [(0, 3), (0, 0), (3, 128)]
+
+
 # ---------------------------------------------------------------------------------------------
 # GPU: frames rendered through the shim == oracle on the same inputs
 # ---------------------------------------------------------------------------------------------
-def shim_scene(a, viewport, w, h, textures=(), skybox=None):
+def shim_scene(a, viewport, w, h, textures=(), skybox=None, bones=None):
     """The oracle scene for what the shim submitted. skybox None = the Init fallback cubemap
     (CreateSolidColor(0x808080), Renderer.cpp:3925-3926)."""
     import scene_cases as sc
@@ -209,12 +257,12 @@ def shim_scene(a, viewport, w, h, textures=(), skybox=None):
     vb, ib, ranges = a.geometry()
     return scenes.Scene(f"shim_vp{viewport}", w, h, vb, ib, ranges, draws, ubo,
                         materials=[(m[0], m[1]) for m in a.materials()], textures=list(textures),
-                        skybox=sc.SOLID_0x808080 if skybox is None else skybox)
+                        skybox=sc.SOLID_0x808080 if skybox is None else skybox, bones=bones)
 
 
-def assert_shim_parity(a, oracle, viewport, w, h, textures=(), min_covered=100, skybox=None):
+def assert_shim_parity(a, oracle, viewport, w, h, textures=(), min_covered=100, skybox=None, bones=None):
     rgba, depth = a.read_pixels(viewport, w, h)
-    oc, od, _ = oracle.render(shim_scene(a, viewport, w, h, textures, skybox))
+    oc, od, _ = oracle.render(shim_scene(a, viewport, w, h, textures, skybox, bones))
     assert np.array_equal(depth.view(np.uint32), od), "depth mismatch"
     ob = oc[..., [2, 1, 0, 3]]  # oracle BGRA -> RGBA
     diff = np.abs(rgba.astype(np.int16) - ob.astype(np.int16))
@@ -261,3 +309,12 @@ def test_gpu_shim_two_viewports_and_textures(app_mod, oracle):
     a.draw_frame()  # steady state: all three draws
     assert_shim_parity(a, oracle, 1, 480, 320, textures=[(1, checker)], min_covered=5000, skybox=sky)
     assert_shim_parity(a, oracle, 2, 256, 200, textures=[(1, checker)], min_covered=1000, skybox=sky)
+
+
+@pytest.mark.gpu
+def test_gpu_shim_skinned_entities(app_mod, oracle):
+    """Animated entities drawn through the shim skin with their AnimationComponent palettes."""
+    a, palette = skinned_app(app_mod)
+    a.draw_frame()
+    a.draw_frame()
+    assert_shim_parity(a, oracle, 1, W, H, min_covered=5000, bones=palette)
