@@ -45,6 +45,7 @@ static_assert(TRI_MAX_CLIP_POLY <= TRI_MAX_CLIP_VERTS, "clip polygon buffers");
 #define TRI_OVF_CLIP_RECORDS 0x1u
 #define TRI_OVF_CLIP_VERTS 0x2u
 #define TRI_OVF_BIN_LIST 0x4u
+#define TRI_OVF_SHADOW_BIN_LIST 0x8u
 
 struct __attribute__((aligned(16))) TriVsIn {
     float px, py, pz, nx;
@@ -125,7 +126,7 @@ struct TriCounters {  // per-frame fields are zeroed before every frame; `flags`
     uint32_t tris_setup;
     uint32_t tris_clipped;
     uint32_t bin_entries;
-    uint32_t pad;
+    uint32_t sbin_max;  // largest shadow-map bin entry count seen (sticky, like bin_max)
     uint32_t bin_max;  // largest per-bin entry count seen (sizes the bin queues after an overflow)
     uint32_t flags;
 };
@@ -179,4 +180,12 @@ struct TriFrameParams {
     tri_material_record mat0;
     TriShadeConst sc;
     TriDrawDev draw0;  // the draw when one_draw (its vertex and primitive slots start at 0)
+    // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
+    uint32_t shadow_on, s_size, s_nbx, s_nbins;
+    uint32_t s_bin_cap;
+    float s_hw;    // s_size / 2 (light NDC -> texel, the main pass's viewport transform)
+    float s_g;     // guard band in light NDC: 2 * TRI_GUARD_BAND_PX / s_size - 1
+    float s_bias;  // depth bias of the lookup compare
+    float s_slope; // slope-scaled depth bias of the depth pass
+    float lvp[16]; // light ortho * light view (affine)
 };

@@ -99,6 +99,29 @@ __device__ __forceinline__ void snap_compute(const TriFrameParams& fp, float4 c,
                                              float& iw);
 __device__ __forceinline__ uint32_t outcode(const TriFrameParams& fp, float4 c);
 
+// Shadow pre-pass, per vertex slot: the light-NDC position (light_view_proj is affine, so w = 1 and the
+// main pass's perspective divide is the identity), kept for the fragment lookup, and its snap to the
+// s_size x s_size map (oracle shadow_raster_triangle: X = rint((x * S/2 + S/2) * 256)) with outcode
+// bits for the map's four sides and TRI_OC_CLIP beyond the guard band (such casters are dropped).
+__device__ __forceinline__ void shadow_vertex(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
+                                              float4 world) {
+    const float4 l = mat_vec_seq(fp.lvp, world);
+    b.lpos[slot] = make_float4(l.x, l.y, l.z, 0.0f);
+    uint32_t oc = 0;
+    if (l.x + 1.0f < 0.0f) oc |= TRI_OC_XNEG;
+    if (1.0f - l.x < 0.0f) oc |= TRI_OC_XPOS;
+    if (l.y + 1.0f < 0.0f) oc |= TRI_OC_YNEG;
+    if (1.0f - l.y < 0.0f) oc |= TRI_OC_YPOS;
+    if (l.x < -fp.s_g || l.x > fp.s_g || l.y < -fp.s_g || l.y > fp.s_g) oc |= TRI_OC_CLIP;
+    TriSnap sn{(int32_t)(oc << 24), 0, l.z, 1.0f};
+    if (!(oc & TRI_OC_CLIP)) {
+        const int32_t X = (int32_t)rintf((l.x * fp.s_hw + fp.s_hw) * 256.0f);
+        sn.xo = (X & 0x00FFFFFF) | (int32_t)(oc << 24);
+        sn.y = (int32_t)rintf((l.y * fp.s_hw + fp.s_hw) * 256.0f);
+    }
+    b.lsnap[slot] = sn;
+}
+
 __device__ __forceinline__ void reset_counters(TriCounters* c) {
     c->ovf_records = 0; c->ovf_verts = 0; c->tris_setup = 0; c->tris_clipped = 0;
     c->bin_entries = 0;  // `flags` / `bin_max` are sticky (cleared by the host)
@@ -112,6 +135,7 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
     const int64_t gi = (int64_t)dr.base_vertex + (int64_t)(dr.min_index + (slot - vbase));
     if (gi < 0 || (uint64_t)gi >= b.vertex_count) {
         b.snap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
+        if (fp.shadow_on) b.lsnap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
         return;
     }
     // three 16-byte loads (a plain struct load is split into overlapping per-field loads)
@@ -172,6 +196,7 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
     vo[0] = make_float4(world.x, world.y, world.z, u);
     vo[1] = make_float4(nnx, nny, nnz, v);
     vo[2] = make_float4(in.cr, in.cg, in.cb, 0.0f);
+    if (fp.shadow_on) shadow_vertex(fp, b, slot, world);
 }
 
 __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
@@ -353,6 +378,7 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Clip primitive `prim` (vertex slots sl[3]) with the whole wave; lanes that set up a fan
 // sub-triangle bin it. Must be reached by the whole wave.
+template <bool LPOS>
 __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const TriDeviceBuffers& b, float* poly,
                                                uint32_t prim, uint32_t sl0, uint32_t sl1, uint32_t sl2,
                                                uint32_t& nsetup, uint32_t& nentries) {
@@ -423,6 +449,12 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
             vo[j] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
                                 (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, (s.b0 * x.w + s.b1 * y.w) + s.b2 * z.w);
         }
+        if constexpr (LPOS) {  // shadow pre-pass on: the polygon vertex's light-space position, same weights
+            const float4 x = b.lpos[sl0], y = b.lpos[sl1], z = b.lpos[sl2];
+            b.lpos[sbase + lane] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x,
+                                               (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
+                                               (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, 0.0f);
+        }
     }
     if (lane == 0) b.clip_slot[prim] = rbase;  // k_raster's fragment fetch finds sub-triangle `sub` here
     if (lane < nsub) {  // fan sub-triangle k = lane + 1: (v0, vk, vk+1)
@@ -446,6 +478,27 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
     }
 }
 
+// Shadow pre-pass set-up of a triangle from its map snaps (oracle shadow_raster_triangle): no culling,
+// only zero-area triangles drop; the bbox of texel centres inside the map, as 32x32 bin ranges.
+__device__ __forceinline__ bool shadow_bins(const TriFrameParams& fp, const int32_t X[3], const int32_t Y[3], uint2& br) {
+    const int64_t S = (int64_t)(X[1] - X[0]) * (int64_t)(Y[2] - Y[0]) -
+                      (int64_t)(Y[1] - Y[0]) * (int64_t)(X[2] - X[0]);
+    if (S == 0) return false;
+    const int32_t xmin = min(X[0], min(X[1], X[2])), xmax = max(X[0], max(X[1], X[2]));
+    const int32_t ymin = min(Y[0], min(Y[1], Y[2])), ymax = max(Y[0], max(Y[1], Y[2]));
+    const int32_t n1 = (int32_t)fp.s_size - 1;
+    const int32_t px0 = max(-floor_shift8(128 - xmin), 0), px1 = min(floor_shift8(xmax - 128), n1);
+    const int32_t py0 = max(-floor_shift8(128 - ymin), 0), py1 = min(floor_shift8(ymax - 128), n1);
+    if (px0 > px1 || py0 > py1) return false;
+    br = make_uint2((uint32_t)(px0 >> 5) | ((uint32_t)(py0 >> 5) << 16), (uint32_t)(px1 >> 5) | ((uint32_t)(py1 >> 5) << 16));
+    return true;
+}
+
+__device__ __forceinline__ void note_shadow_bin_overflow(const TriDeviceBuffers& b, uint32_t needed) {
+    atomicOr(&b.counters->flags, TRI_OVF_SHADOW_BIN_LIST);
+    atomicMax(&b.counters->sbin_max, needed);
+}
+
 // One lane per primitive (ppt primitives per lane): assembly from the snapped vertices, trivial
 // reject, cull, bbox, then one bin-queue entry per touched bin (batched wave reservations). Nothing else is
 // written for a visible triangle: k_raster rebuilds it from `snap`. Triangles needing homogeneous
@@ -454,13 +507,22 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
 #ifndef TRI_SETUP_WAVES
 #define TRI_SETUP_WAVES 7  // k_setup occupancy target (waves per SIMD)
 #endif
+// SHADOW = the shadow pre-pass's set-up (oracle shadow_raster_triangle): the light-NDC snaps, no
+// culling, no clipping (guard-band violators are dropped), bins of the s_size^2 map's own queues.
+// LPOS (main pass with the pre-pass on): clipped polygon vertices also get light-space positions
+// (a separate instantiation keeps that code, and its registers, out of frames without shadows).
+template <bool SHADOW, bool LPOS>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t red[2];
-    __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
+    __shared__ float clip_poly[SHADOW ? 1 : kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
     __syncthreads();
     uint32_t nsetup = 0, nentries = 0;
-    const uint32_t cap = fp.bin_cap;
+    const uint32_t cap = SHADOW ? fp.s_bin_cap : fp.bin_cap;
+    const uint32_t nbx = SHADOW ? fp.s_nbx : (uint32_t)fp.nbx;
+    uint32_t* const bin_count = SHADOW ? b.sbin_count : b.bin_count;
+    uint32_t* const bin_list = SHADOW ? b.sbin_list : b.bin_list;
+    const TriSnap* const snp = SHADOW ? b.lsnap : b.snap;
     const uint32_t lane = lanes_below(~0ull);
     // Spread concurrently running workgroups over the primitive stream: meshes are usually
     // index-ordered in screen space, and neighbouring chunks hammering the same bin counters
@@ -494,10 +556,17 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                     vb = b.draw_vbase[d] - dr.min_index;
                 }
                 sl0[t] = vb + ip[0]; sl1[t] = vb + ip[1]; sl2[t] = vb + ip[2];
-                const TriSnap a0 = b.snap[sl0[t]], a1 = b.snap[sl1[t]], a2 = b.snap[sl2[t]];
+                const TriSnap a0 = snp[sl0[t]], a1 = snp[sl1[t]], a2 = snp[sl2[t]];
                 const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
                 // invalid vertex, or trivial reject: all three vertices outside one clip half-space
-                if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
+                if constexpr (SHADOW) {
+                    if (!((oc0 | oc1 | oc2) & (TRI_OC_BAD | TRI_OC_CLIP)) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
+                        const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
+                        const int32_t Y[3] = {a0.y, a1.y, a2.y};
+                        ok[t] = shadow_bins(fp, X, Y, br[t]);
+                        if (ok[t]) b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d);
+                    }
+                } else if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
                     if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
                         b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | TRI_PRIM_CLIPPED);
                         needs_clip[t] = true;
@@ -515,7 +584,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             nsetup += ok[t] ? 1u : 0u;
         }
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < 2 && !SHADOW; ++t) {
             uint64_t cm = __ballot(needs_clip[t]);  // rare: the wave clips its primitives one at a time
             if (cm) {
                 if (lane == 0) atomicAdd(&b.counters->tris_clipped, (uint32_t)__builtin_popcountll(cm));
@@ -523,7 +592,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 while (cm) {
                     const int src = __builtin_ctzll(cm);
                     cm &= cm - 1;
-                    clip_prim_wave(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
+                    clip_prim_wave<LPOS>(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
                                    (uint32_t)__builtin_amdgcn_readlane((int)sl0[t], src),
                                    (uint32_t)__builtin_amdgcn_readlane((int)sl1[t], src),
                                    (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src), nsetup, nentries);
@@ -547,7 +616,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
 #pragma unroll
             for (int r = 0; r < kResBatch; ++r) {
                 rwant[r] = has && r < batch;
-                rbin[r] = by * (uint32_t)fp.nbx + bx;
+                rbin[r] = by * nbx + bx;
                 rent[r] = second ? p[1] : p[0];
                 if (rwant[r]) {
                     if (bx < bx1) {
@@ -567,26 +636,29 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 wave_reserve_plan(rbin[r], rwant[r], rlead[r], rrank[r], cnt);
                 rbase[r] = 0;
                 if (rwant[r] && lane == rlead[r] && !(kAblate & 16))  // diagnostics: 16 = no atomics
-                    rbase[r] = atomicAdd(&b.bin_count[rbin[r]], cnt);
+                    rbase[r] = atomicAdd(&bin_count[rbin[r]], cnt);
             }
 #pragma unroll
             for (int r = 0; r < kResBatch; ++r) {
                 const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
                 if (rwant[r]) {
                     if (kAblate & 32) continue;  // diagnostics: 32 = no queue stores
-                    if (pos < cap) b.bin_list[(size_t)rbin[r] * cap + pos] = rent[r];
+                    if (pos < cap) bin_list[(size_t)rbin[r] * cap + pos] = rent[r];
+                    else if (SHADOW) note_shadow_bin_overflow(b, pos + 1);
                     else note_bin_overflow(b, pos + 1);
                     ++nentries;
                 }
             }
         }
     }
-    if (nsetup) atomicAdd(&red[0], nsetup);
-    if (nentries) atomicAdd(&red[1], nentries);
-    __syncthreads();
-    // Statistics go to a per-workgroup slot with a plain store: same-address global atomics from
-    // every workgroup serialise across the XCDs (measured: +34 us per frame at 4K/1M).
-    if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(red[0], red[1]);
+    if constexpr (!SHADOW) {
+        if (nsetup) atomicAdd(&red[0], nsetup);
+        if (nentries) atomicAdd(&red[1], nentries);
+        __syncthreads();
+        // Statistics go to a per-workgroup slot with a plain store: same-address global atomics from
+        // every workgroup serialise across the XCDs (measured: +34 us per frame at 4K/1M).
+        if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(red[0], red[1]);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -815,6 +887,7 @@ struct Frag {  // flat scalars: nested f3 members are ABI-coerced and defeat SRO
     float u, v;
     float sx, sy, sz, sw;  // sampled texel (linear rgb, alpha)
     float tx, ty, tz, tw;  // draw tint
+    float vis;             // shadow pre-pass: fraction of the sun's light reaching the fragment (1 without it)
 };
 __device__ __forceinline__ f3 fworld(const Frag& f) { return mk(f.wx, f.wy, f.wz); }
 __device__ __forceinline__ f3 fnrm(const Frag& f) { return mk(f.nx, f.ny, f.nz); }
@@ -870,8 +943,9 @@ __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag&
     if (g.light_counts[0] > 0u) {
         const f3 L = norm3(mk(-g.directional_light_direction[0], -g.directional_light_direction[1],
                               -g.directional_light_direction[2]));
-        const f3 rad = muls(mk(g.directional_light_color[0], g.directional_light_color[1], g.directional_light_color[2]),
-                            g.directional_light_color[3]);
+        const f3 rad = muls(muls(mk(g.directional_light_color[0], g.directional_light_color[1], g.directional_light_color[2]),
+                                 g.directional_light_color[3]),
+                            f.vis);
         direct = add(direct, eval_pbr_exact(L, rad, N, V, albedo, metallic, roughness, F0));
     }
     const uint32_t np = min(g.light_counts[1], 8u);
@@ -955,9 +1029,9 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.gV = NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
     f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
               sc.amb[2] * albedo.z * sc.amb_strength);
-    if (sc.has_sun)
+    if (sc.has_sun && f.vis > 0.0f)  // vis = 0 (fully shadowed): the sun adds exactly nothing
         eval_pbr_fast(sc, px, mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]),
-                      mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), 1.0f, c);
+                      mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), f.vis, c);
     const f3 wp = fworld(f);
     for (uint32_t i = 0; i < sc.npt; ++i) {
         const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
@@ -980,10 +1054,55 @@ __device__ __forceinline__ float interp_fast(float w0, float w1, float w2, float
     return __builtin_fmaf(w2, x2, __builtin_fmaf(w1, x1, w0 * x0));
 }
 
+// Perspective-correct barycentric weights of pixel (px, py) in the oracle's order: exact int64 edge
+// functions at the pixel centre, IEEE divides (the EXACT build's interpolation; the shadow lookup uses
+// them in both builds so its compare sees the oracle's light-space depth bit for bit).
+__device__ __forceinline__ void exact_weights(const TriRec& r, int32_t px, int32_t py, float& w0, float& w1, float& w2) {
+    const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
+    int64_t e[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int i = k, j = (k + 1) % 3;
+        const int64_t a = (int64_t)r.Y[i] - r.Y[j];
+        const int64_t bb = (int64_t)r.X[j] - r.X[i];
+        const int64_t c = -(a * r.X[i] + bb * r.Y[i]);
+        e[k] = a * Xp + bb * Yp + c;
+    }
+    const int64_t S = (int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
+                      (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]);
+    const float fS = (float)S;
+    const float l0 = (float)e[1] / fS, l1 = (float)e[2] / fS, l2 = (float)e[0] / fS;
+    const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
+    const float qs = (q0 + q1) + q2;
+    w0 = q0 / qs; w1 = q1 / qs; w2 = q2 / qs;
+}
+
+// Shadow lookup (oracle shadow_visibility): the fraction of the 2x2 bilinear depth compare
+// (zref - bias <= map) that passes at light-NDC point (lx, ly, lz); 1 outside the map. IEEE mul/add in
+// the oracle's order (this file is compiled without contraction).
+__device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint32_t* smap, float lx, float ly, float lz) {
+    const float u = lx * 0.5f + 0.5f, v = ly * 0.5f + 0.5f;
+    if (!(u >= 0.0f && u <= 1.0f && v >= 0.0f && v <= 1.0f)) return 1.0f;
+    const int32_t n = (int32_t)fp.s_size;
+    const float fx = u * (float)n - 0.5f, fy = v * (float)n - 0.5f;
+    const float x0 = floorf(fx), y0 = floorf(fy);
+    const float a = fx - x0, bb = fy - y0;
+    const int32_t i0 = (int32_t)x0, j0 = (int32_t)y0;
+    const float zref = lz - fp.s_bias;
+    const int32_t ia = min(max(i0, 0), n - 1), ib = min(max(i0 + 1, 0), n - 1);
+    const int32_t ja = min(max(j0, 0), n - 1), jb = min(max(j0 + 1, 0), n - 1);
+    const float c00 = zref <= __uint_as_float(smap[(size_t)ja * n + ia]) ? 1.0f : 0.0f;
+    const float c10 = zref <= __uint_as_float(smap[(size_t)ja * n + ib]) ? 1.0f : 0.0f;
+    const float c01 = zref <= __uint_as_float(smap[(size_t)jb * n + ia]) ? 1.0f : 0.0f;
+    const float c11 = zref <= __uint_as_float(smap[(size_t)jb * n + ib]) ? 1.0f : 0.0f;
+    const float l0 = c00 + a * (c10 - c00), l1 = c01 + a * (c11 - c01);
+    return l0 + bb * (l1 - l0);
+}
+
 // Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
 // Writes the fragment through `put(field_index, value)` (fields in Frag order), so one body serves
 // the single-pixel Frag and the lane-pair FragP without an intermediate in scratch memory.
-template <bool EXACT, typename Put>
+template <bool EXACT, bool SHADOW, typename Put>
 __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
                                                   int32_t px, int32_t py, const float* lut, Put&& put) {
     const uint32_t low = (uint32_t)key;
@@ -997,40 +1116,33 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         r = load_rec(b.recs, b.clip_slot[prim] + (low & 7u));
     else
         r = rec_from_snaps(prim, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
-    float l0, l1, l2;
-    if (EXACT) {  // exact int64 edge functions (oracle order)
-        const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
-        int64_t e[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            const int i = k, j = (k + 1) % 3;
-            const int64_t a = (int64_t)r.Y[i] - r.Y[j];
-            const int64_t bb = (int64_t)r.X[j] - r.X[i];
-            const int64_t c = -(a * r.X[i] + bb * r.Y[i]);
-            e[k] = a * Xp + bb * Yp + c;
-        }
-        const int64_t S = (int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
-                          (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]);
-        const float fS = (float)S;
-        l0 = (float)e[1] / fS; l1 = (float)e[2] / fS; l2 = (float)e[0] / fS;
+    float w0, w1, w2;
+    if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
+        exact_weights(r, px, py, w0, w1, w2);
     } else {  // float edge functions relative to vertex 0 (operands < 2^24: exact conversions)
         const float dx = (float)(256 * px + 128 - r.X[0]), dy = (float)(256 * py + 128 - r.Y[0]);
         const float fX1 = (float)(r.X[1] - r.X[0]), fY1 = (float)(r.Y[1] - r.Y[0]);
         const float fX2 = (float)(r.X[2] - r.X[0]), fY2 = (float)(r.Y[2] - r.Y[0]);
         const float iS = frcp(fX1 * fY2 - fY1 * fX2);
-        l2 = (fX1 * dy - fY1 * dx) * iS;
-        l1 = (fY2 * dx - fX2 * dy) * iS;
-        l0 = 1.0f - l1 - l2;
-    }
-    const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
-    const float qs = (q0 + q1) + q2;
-    float w0, w1, w2;
-    if (EXACT) {
-        w0 = q0 / qs; w1 = q1 / qs; w2 = q2 / qs;
-    } else {
-        const float iq = frcp(qs);
+        const float l2 = (fX1 * dy - fY1 * dx) * iS;
+        const float l1 = (fY2 * dx - fX2 * dy) * iS;
+        const float l0 = 1.0f - l1 - l2;
+        const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
+        const float iq = frcp((q0 + q1) + q2);
         w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
     }
+    float vis = 1.0f;
+    if constexpr (SHADOW) {  // light-space position at the pixel with the oracle's weights, then the compare
+        float e0 = w0, e1 = w1, e2 = w2;
+        if (!EXACT) exact_weights(r, px, py, e0, e1, e2);
+        const Rsrc lr = make_rsrc(b.lpos, 16ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
+        const uint4 L0 = ld128(lr, r.v[0] * 16u), L1 = ld128(lr, r.v[1] * 16u), L2 = ld128(lr, r.v[2] * 16u);
+        auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
+            return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
+        };
+        vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
+    }
+    put(19, vis);
     // plain-float views of the varyings (HIP vector unions defeat SROA in the pixel-pair path)
     auto ldv = [&](uint32_t slot, uint32_t j) -> V4 {
         const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);
@@ -1061,10 +1173,10 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     put(18, __uint_as_float(st.w));
 }
 
-template <bool EXACT>
+template <bool EXACT, bool SHADOW>
 __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
                                                int32_t px, int32_t py, const float* lut, Frag& f) {
-    fetch_fragment_to<EXACT>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
+    fetch_fragment_to<EXACT, SHADOW>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1268,7 +1380,7 @@ __device__ __forceinline__ void cov_row(const CovEntry& c, uint32_t r, uint64_t*
     }
 }
 
-template <bool EXACT, int BL>
+template <bool EXACT, int BL, bool SHADOW>
 // 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
 // a little); 64x64 bins are LDS-limited to 3
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
@@ -1469,7 +1581,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         } else {
             z = __uint_as_float((uint32_t)(key >> 32));
             Frag f;
-            fetch_fragment<EXACT>(fp, b, key, px, py, lut, f);
+            fetch_fragment<EXACT, SHADOW>(fp, b, key, px, py, lut, f);
             const float4 c = EXACT ? fs_exact(fp, f) : fs_fast(fp.sc, f);
             out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
         }
@@ -1486,6 +1598,142 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         const int32_t px = ox + (int32_t)(li & (BIN - 1)), py = oy + (int32_t)(li >> BL);
         b.color[(size_t)(py - fp.y0) * fp.W + px] =
             persp ? sky_bgra_persp(fp, b, px, py, lut) : sky_bgra(fp, b, px, py, lut);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// shadow pre-pass raster (oracle shadow_raster_triangle): one workgroup per 32x32 bin of the s_size^2
+// map, the bin's depth tile in LDS (min over covering fragments of the [0, 1]-clamped plane depth, as
+// uint32 bits: order-free), then one coalesced store of the tile. The triangle of a queue entry is
+// rebuilt from its three map snaps (prim_vs -> lsnap), oriented like the set-up (v1 <-> v2 swapped when
+// S < 0, kept when S > 0: no culling).
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ TriRec load_shadow_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
+    const Rsrc pvr = make_rsrc(b.prim_vs, 16ull * fp.nprims), snr = make_rsrc(b.lsnap, 16ull * fp.nslots);
+    const uint4 pv = ld128(pvr, e * 16u);
+    const uint4 q0 = ld128(snr, pv.x * 16u), q1 = ld128(snr, pv.y * 16u), q2 = ld128(snr, pv.z * 16u);
+    const int32_t X0 = ((int32_t)q0.x << 8) >> 8, X1 = ((int32_t)q1.x << 8) >> 8, X2 = ((int32_t)q2.x << 8) >> 8;
+    const int32_t Y0 = (int32_t)q0.y, Y1 = (int32_t)q1.y, Y2 = (int32_t)q2.y;
+    const int64_t S = (int64_t)(X1 - X0) * (int64_t)(Y2 - Y0) - (int64_t)(Y1 - Y0) * (int64_t)(X2 - X0);
+    const bool sw = S < 0;
+    TriRec r;
+    r.X[0] = X0; r.Y[0] = Y0; r.z[0] = __uint_as_float(q0.z);
+    r.X[1] = sw ? X2 : X1; r.Y[1] = sw ? Y2 : Y1; r.z[1] = __uint_as_float(sw ? q2.z : q1.z);
+    r.X[2] = sw ? X1 : X2; r.Y[2] = sw ? Y1 : Y2; r.z[2] = __uint_as_float(sw ? q1.z : q2.z);
+    r.iw[0] = r.iw[1] = r.iw[2] = 1.0f;
+    r.prim_sub = e << 3;
+    r.v[0] = r.v[1] = r.v[2] = 0;
+    return r;
+}
+
+// Depth clamp to [0, 1] on the float bits (finite depth: the plane of snapped vertices with S != 0):
+// negative (sign set, -0 included) -> +0, above 1 -> 1.
+__device__ __forceinline__ uint32_t clamp_depth_bits(float z) {
+    return (uint32_t)min(max(__float_as_int(z), 0), 0x3F800000);
+}
+
+// Slope-scaled depth bias of a caster (depthBiasSlopeFactor): slope * its largest depth change per texel.
+__device__ __forceinline__ float slope_offset(const TriFrameParams& fp, const EdgeSetup& e) {
+    return fp.s_slope * (fmaxf(fabsf(e.dzdX), fabsf(e.dzdY)) * 256.0f);
+}
+
+__device__ __forceinline__ void shadow_serial(const TriFrameParams& fp, const TriRec& r, int32_t cx0, int32_t cx1,
+                                              int32_t cy0, int32_t cy1, int32_t ox, int32_t oy, uint32_t* dep,
+                                              int32_t sub, int32_t step) {
+    EdgeSetup e;
+    edge_setup(r, e);
+    const float off = slope_offset(fp, e);
+    bool rej = false;
+    int32_t F[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) F[k] = clamp_edge((int64_t)e.A[k] * cx0 + (int64_t)e.B[k] * cy0 + e.D[k], rej);
+    if (rej) return;
+    const float fdx0 = (float)(256 * cx0 + 128 - r.X[0]);
+    float fdy = (float)(256 * (cy0 + sub) + 128 - r.Y[0]);
+    uint32_t row = (uint32_t)(((cy0 + sub - oy) << 5) + (cx0 - ox));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) F[k] += e.B[k] * sub;
+    for (int32_t py = cy0 + sub; py <= cy1; py += step) {
+        const float t2 = e.dzdY * fdy;
+        int32_t f0 = F[0], f1 = F[1], f2 = F[2];
+        float fdx = fdx0;
+        const uint32_t rend = row + (uint32_t)(cx1 - cx0);
+        for (uint32_t a = row; a <= rend; ++a) {
+            if ((f0 | f1 | f2) >= 0) atomicMin(&dep[a], clamp_depth_bits(((r.z[0] + e.dzdX * fdx) + t2) + off));
+            f0 += e.A[0]; f1 += e.A[1]; f2 += e.A[2];
+            fdx += 256.0f;
+        }
+        F[0] += e.B[0] * step; F[1] += e.B[1] * step; F[2] += e.B[2] * step;
+        fdy += 256.0f * (float)step;
+        row += (uint32_t)step << 5;
+    }
+}
+
+__global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TriFrameParams fp, TriDeviceBuffers b) {
+    constexpr int BIN = 32;
+    __shared__ uint32_t dep[BIN * BIN];
+    __shared__ uint32_t bigq[kBigQueue];
+    __shared__ uint32_t nbig, nentries;
+    const int tid = threadIdx.x;
+    const int bin = xcd_bin(blockIdx.x, (int)fp.s_nbins);
+    const int32_t S = (int32_t)fp.s_size;
+    const int32_t ox = (bin % (int)fp.s_nbx) * BIN, oy = (bin / (int)fp.s_nbx) * BIN;
+    const int32_t bw = min(BIN, S - ox), bh = min(BIN, S - oy);
+    for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) dep[i] = 0x3F800000u;  // clear 1.0
+    if (tid == 0) {
+        nbig = 0;
+        const uint32_t cnt = b.sbin_count[bin];
+        b.sbin_count[bin] = 0;  // consumed: ready for the next frame
+        if (cnt > fp.s_bin_cap) note_shadow_bin_overflow(b, cnt);
+        nentries = min(cnt, fp.s_bin_cap);
+    }
+    __syncthreads();
+    const uint32_t* queue = b.sbin_list + (size_t)bin * fp.s_bin_cap;
+    const uint32_t n = nentries;
+    const int share = TRI_COV_SHARE > 1 && n <= (uint32_t)TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
+    const int sub = tid % share;
+    for (uint32_t i = tid / share; i < n; i += TRI_BLOCK / share) {
+        const uint32_t ri = queue[i];
+        const TriRec r = load_shadow_entry(fp, b, ri);
+        int32_t cx0, cx1, cy0, cy1;
+        rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
+        if (cx0 > cx1 || cy0 > cy1) continue;
+        if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > kBigArea) {
+            if (sub != 0) continue;
+            const uint32_t q = atomicAdd(&nbig, 1u);
+            if (q < kBigQueue) { bigq[q] = ri; continue; }
+            shadow_serial(fp, r, cx0, cx1, cy0, cy1, ox, oy, dep, 0, 1);
+            continue;
+        }
+        shadow_serial(fp, r, cx0, cx1, cy0, cy1, ox, oy, dep, sub, share);
+    }
+    __syncthreads();
+    const uint32_t nb = min(nbig, (uint32_t)kBigQueue);
+    for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the texels
+        const TriRec r = load_shadow_entry(fp, b, bigq[q]);
+        int32_t cx0, cx1, cy0, cy1;
+        rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
+        EdgeSetup e;
+        edge_setup(r, e);
+        bool rej = false;
+        int32_t F[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) F[k] = clamp_edge((int64_t)e.A[k] * cx0 + (int64_t)e.B[k] * cy0 + e.D[k], rej);
+        if (rej) continue;  // uniform across the workgroup
+        const float off = slope_offset(fp, e);
+        const int32_t rw = cx1 - cx0 + 1, rh = cy1 - cy0 + 1;
+        for (int j = tid; j < rw * rh; j += TRI_BLOCK) {
+            const int32_t dy = j / rw, dx = j - dy * rw;
+            if ((F[0] + e.A[0] * dx + e.B[0] * dy | F[1] + e.A[1] * dx + e.B[1] * dy | F[2] + e.A[2] * dx + e.B[2] * dy) >= 0) {
+                const int32_t px = cx0 + dx, py = cy0 + dy;
+                atomicMin(&dep[((py - oy) << 5) + (px - ox)], clamp_depth_bits(frag_depth(r, e, px, py) + off));
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) {
+        const int32_t ly = i >> 5, lx = i & 31;
+        if (lx < bw && ly < bh) b.shadow_map[(size_t)(oy + ly) * S + ox + lx] = dep[i];
     }
 }
 
@@ -1526,10 +1774,17 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__
 
 hipError_t tri_kernels_init() { return hipSuccess; }
 
+template <bool EXACT, int BL>
+static void launch_raster(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream) {
+    const dim3 g(fp.nbins), t(TRI_BLOCK);
+    if (fp.shadow_on) hipLaunchKernelGGL((k_raster<EXACT, BL, true>), g, t, 0, stream, fp, b);
+    else hipLaunchKernelGGL((k_raster<EXACT, BL, false>), g, t, 0, stream, fp, b);
+}
+
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* ev) {
     static const bool debug_sync = getenv("TRI_DEBUG_SYNC") != nullptr;
-    static const char* names[] = {"vertex", "setup", "clip", "raster", "end"};
+    static const char* names[] = {"vertex", "shadow", "setup", "raster", "end"};
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], stream);
         if (debug_sync) {
@@ -1542,21 +1797,26 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         hipLaunchKernelGGL(k_vertex, dim3((fp.nslots + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
     else
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
+    if (fp.shadow_on) {  // shadow pre-pass: set-up + binning into the map's queues, then the depth raster
+        rec(kStageShadow);
+        if (fp.nchunks > 0) hipLaunchKernelGGL((k_setup<true, false>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
+        hipLaunchKernelGGL(k_shadow_raster, dim3(fp.s_nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
+    }
     rec(kStageSetup);
-    if (fp.nchunks > 0) hipLaunchKernelGGL(k_setup, dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
-    // clipping runs inside k_setup: the clip stage is empty and gets no event of its own (an extra
-    // event pair cost ~5 us of the sampled frame); collect_timing reports it as 0
+    if (fp.nchunks > 0) {
+        if (fp.shadow_on) hipLaunchKernelGGL((k_setup<false, true>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_setup<false, false>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
+    }
     rec(kStageRaster);
-    const dim3 g(fp.nbins), t(TRI_BLOCK);
     if (fp.bin_log2 == 5) {
-        if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 5>), g, t, 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_raster<false, 5>), g, t, 0, stream, fp, b);
+        if (fp.exact_shading) launch_raster<true, 5>(fp, b, stream);
+        else launch_raster<false, 5>(fp, b, stream);
     } else if (fp.bin_log2 == 4) {
-        if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 4>), g, t, 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_raster<false, 4>), g, t, 0, stream, fp, b);
+        if (fp.exact_shading) launch_raster<true, 4>(fp, b, stream);
+        else launch_raster<false, 4>(fp, b, stream);
     } else {
-        if (fp.exact_shading) hipLaunchKernelGGL((k_raster<true, 6>), g, t, 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_raster<false, 6>), g, t, 0, stream, fp, b);
+        if (fp.exact_shading) launch_raster<true, 6>(fp, b, stream);
+        else launch_raster<false, 6>(fp, b, stream);
     }
     rec(kStageCount);
     return hipGetLastError();

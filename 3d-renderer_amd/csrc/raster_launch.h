@@ -29,14 +29,22 @@ struct TriDeviceBuffers {
     uint2* setup_stats;          // nchunks {triangles set up, bin entries} per k_setup workgroup
     uint32_t* color;             // band rows * W
     float* depth;                // band rows * W (may be null)
+    // shadow-map pre-pass (only when TriFrameParams::shadow_on)
+    float4* lpos;                // nslots + ovf_vert_cap: light-NDC position per vertex slot (xyz, 0)
+    TriSnap* lsnap;              // nslots: the light-NDC position snapped to the map ({X | outcode << 24, Y, z, 1})
+    uint32_t* sbin_count;        // s_nbins shadow-map bin counters (zeroed by k_shadow_raster)
+    uint32_t* sbin_list;         // s_nbins * s_bin_cap primitive ids
+    uint32_t* shadow_map;        // s_size * s_size float32 depth bits
 };
 
-enum TriStage { kStageVertex = 0, kStageSetup, kStageClip, kStageRaster, kStageCount };
+// Event stamps of one frame: [vertex | shadow pre-pass (when on) | setup + binning + clip | raster].
+enum TriStage { kStageVertex = 0, kStageShadow, kStageSetup, kStageRaster, kStageCount };
 
 hipError_t tri_kernels_init();
 
-// One frame = 3 dependent launches on `stream` (k_vertex, k_setup with in-wave clipping, k_raster);
-// `events` (may be null) gets kStageCount+1 stamps: [vertex | setup+binning+clip | (empty) | raster].
+// One frame = 3 dependent launches on `stream` (k_vertex, k_setup with in-wave clipping, k_raster),
+// 5 with the shadow pre-pass (k_setup<shadow> and k_shadow_raster after k_vertex); `events` (may be
+// null) gets kStageCount + 1 stamps (the kStageShadow stamp only when the pre-pass runs).
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* events);
 

@@ -60,6 +60,7 @@ float srgb_decode(int i) {
 
 struct TimingSet {
     hipEvent_t ev[kStageCount + 1];
+    bool shadow = false;  // the frame ran the shadow pre-pass (ev[kStageShadow] was recorded)
 };
 
 }  // namespace
@@ -133,6 +134,16 @@ struct tri_ctx {
     TriCounters* d_ctr = nullptr;
     uint32_t ovf_rec_cap = 1u << 16, ovf_vert_cap = 1u << 17;
     uint32_t bin_cap = 0;
+
+    // shadow-map pre-pass (tri_set_shadow)
+    tri_shadow_config shadow{};
+    float4* d_lpos = nullptr; size_t cap_lpos = 0;
+    TriSnap* d_lsnap = nullptr; size_t cap_lsnap = 0;
+    uint32_t* d_sbin_count = nullptr; size_t cap_sbin_count = 0;
+    uint32_t* d_sbin_list = nullptr; size_t cap_sbin_list = 0;
+    uint32_t* d_shadow = nullptr; size_t cap_shadow = 0;
+    uint32_t s_nbx = 0, s_nbins = 0, s_bin_cap = 0;
+    bool shadow_rendered = false;  // a frame with the current map size has been enqueued
 
     uint32_t* d_color_own = nullptr;
     float* d_depth_own = nullptr;
@@ -249,6 +260,59 @@ void mat4_mul(const float* a, const float* b, float* r) {
             s = s + a[3 * 4 + i] * b[j * 4 + 3];
             r[j * 4 + i] = s;
         }
+}
+
+// ---- tri_shadow_fit_ortho: glm::lookAtRH + glm::orthoRH_ZO (same operation order as the oracle's
+// restatement, oracle_shadow_fit_ortho; CPU test compares them bit for bit) ----------------------
+struct V3 { float x, y, z; };
+V3 v3sub(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+V3 v3mul(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+float v3dot(V3 a, V3 b) {  // glm compute_dot: (x + y) + z
+    const float tx = a.x * b.x, ty = a.y * b.y, tz = a.z * b.z;
+    return (tx + ty) + tz;
+}
+V3 v3cross(V3 x, V3 y) { return {x.y * y.z - y.y * x.z, x.z * y.x - y.z * x.x, x.x * y.y - y.x * x.y}; }
+V3 v3norm(V3 v) { return v3mul(v, 1.0f / std::sqrt(v3dot(v, v))); }
+
+void shadow_fit_ortho(const float dir[3], const float mn[3], const float mx[3], float out[16]) {
+    V3 d{dir[0], dir[1], dir[2]};
+    if (!(v3dot(d, d) > 1e-12f)) d = {-0.5f, -1.0f, -0.3f};
+    d = v3norm(d);
+    const V3 lo{mn[0], mn[1], mn[2]}, hi{mx[0], mx[1], mx[2]};
+    const V3 c{(lo.x + hi.x) * 0.5f, (lo.y + hi.y) * 0.5f, (lo.z + hi.z) * 0.5f};
+    const float r = std::max(std::sqrt(v3dot(v3sub(hi, lo), v3sub(hi, lo))) * 0.5f, 1e-3f);
+    const V3 eye = v3sub(c, v3mul(d, 2.0f * r));
+    const V3 up = std::fabs(d.y) > 0.99f ? V3{0.0f, 0.0f, 1.0f} : V3{0.0f, 1.0f, 0.0f};
+    // glm::lookAtRH(eye, c, up), column-major V[col*4 + row]
+    const V3 f = v3norm(v3sub(c, eye));
+    const V3 sv = v3norm(v3cross(f, up));
+    const V3 u = v3cross(sv, f);
+    float V[16] = {sv.x, u.x, -f.x, 0.0f, sv.y, u.y, -f.y, 0.0f, sv.z, u.z, -f.z, 0.0f,
+                   -v3dot(sv, eye), -v3dot(u, eye), v3dot(f, eye), 1.0f};
+    float b0[3] = {INFINITY, INFINITY, INFINITY}, b1[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < 8; ++k) {
+        const float p[4] = {(k & 1) ? hi.x : lo.x, (k & 2) ? hi.y : lo.y, (k & 4) ? hi.z : lo.z, 1.0f};
+        for (int a = 0; a < 3; ++a) {  // glm mat4 * vec4: (m0 v0 + m1 v1) + (m2 v2 + m3 v3)
+            const float add0 = V[0 * 4 + a] * p[0] + V[1 * 4 + a] * p[1];
+            const float add1 = V[2 * 4 + a] * p[2] + V[3 * 4 + a] * p[3];
+            const float q = add0 + add1;
+            b0[a] = std::min(b0[a], q);
+            b1[a] = std::max(b1[a], q);
+        }
+    }
+    float m[3];
+    for (int a = 0; a < 3; ++a) m[a] = (b1[a] - b0[a]) * 0.01f + 1e-4f;
+    // glm::orthoRH_ZO(l, r, b, t, n, f); view space looks down -z
+    const float l = b0[0] - m[0], rr = b1[0] + m[0], bt = b0[1] - m[1], tp = b1[1] + m[1];
+    const float n = -b1[2] - m[2], fr = -b0[2] + m[2];
+    float P[16] = {1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1, 0, 0, 0, 0, 1};
+    P[0] = 2.0f / (rr - l);
+    P[5] = 2.0f / (tp - bt);
+    P[10] = -1.0f / (fr - n);
+    P[12] = -(rr + l) / (rr - l);
+    P[13] = -(tp + bt) / (tp - bt);
+    P[14] = -n / (fr - n);
+    mat4_mul(P, V, out);
 }
 
 int upload_texture_table(tri_ctx* c) {
@@ -393,6 +457,22 @@ int ensure_work_buffers(tri_ctx* c) {
     if ((rc = grow(c->d_prim_vs, c->cap_prim_vs, std::max<size_t>(c->nprims, 1)))) return rc;
     if ((rc = grow(c->d_setup_stats, c->cap_setup_stats, (size_t)c->nprims / TRI_BLOCK + 1))) return rc;
     if ((rc = grow(c->d_bin_list, c->cap_bin_list, nlist))) return rc;
+    if (c->shadow.size) {
+        // map queues: ~8x the mean entries per map bin (a triangle covers ~1.3 bins), >= 256
+        const uint64_t smean = ((uint64_t)c->nprims * 13 / 10) / (uint64_t)std::max<uint32_t>(c->s_nbins, 1);
+        c->s_bin_cap = std::max<uint32_t>(c->s_bin_cap, (uint32_t)std::min<uint64_t>(((8 * smean + 64 + 63) / 64) * 64, 1u << 30));
+        c->s_bin_cap = std::max<uint32_t>(c->s_bin_cap, 256u);
+        const size_t slist = (size_t)c->s_nbins * c->s_bin_cap;
+        if (slist * 4 > (8ull << 30)) return fail(TRI_E_OOM, "shadow-map bin queues would need %zu MB", slist * 4 >> 20);
+        const size_t smap = (size_t)c->shadow.size * c->shadow.size;
+        if (c->cap_lpos < nvary / 3 || c->cap_lsnap < std::max<size_t>(c->nslots, 1) || c->cap_sbin_list < slist ||
+            c->cap_sbin_count < c->s_nbins || c->cap_shadow < smap)
+            HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((rc = grow(c->d_lpos, c->cap_lpos, nvary / 3))) return rc;
+        if ((rc = grow(c->d_lsnap, c->cap_lsnap, std::max<size_t>(c->nslots, 1)))) return rc;
+        if ((rc = grow(c->d_sbin_list, c->cap_sbin_list, slist))) return rc;
+        if ((rc = grow(c->d_shadow, c->cap_shadow, smap))) return rc;
+    }
     return TRI_OK;
 }
 
@@ -400,19 +480,16 @@ int collect_timing(tri_ctx* c) {
     if (c->pending.empty()) return TRI_OK;
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (TimingSet& t : c->pending) {
-        float ms[kStageCount], tot;
-        for (int i = 0; i < kStageCount; ++i) {
-            if (i == kStageClip) {  // no event: the stage is empty (clipping runs inside k_setup)
-                ms[i] = 0.0f;
-                continue;
-            }
-            const int next = i == kStageSetup ? kStageRaster : i + 1;
-            HIP_TRY(hipEventElapsedTime(&ms[i], t.ev[i], t.ev[next]));
-        }
+        float ms[kStageCount] = {}, tot;
+        // the shadow stamp exists only for frames that ran the pre-pass
+        HIP_TRY(hipEventElapsedTime(&ms[kStageVertex], t.ev[kStageVertex], t.ev[t.shadow ? kStageShadow : kStageSetup]));
+        if (t.shadow) HIP_TRY(hipEventElapsedTime(&ms[kStageShadow], t.ev[kStageShadow], t.ev[kStageSetup]));
+        HIP_TRY(hipEventElapsedTime(&ms[kStageSetup], t.ev[kStageSetup], t.ev[kStageRaster]));
+        HIP_TRY(hipEventElapsedTime(&ms[kStageRaster], t.ev[kStageRaster], t.ev[kStageCount]));
         HIP_TRY(hipEventElapsedTime(&tot, t.ev[0], t.ev[kStageCount]));
         c->acc.ms_vertex += ms[kStageVertex];
         c->acc.ms_setup += ms[kStageSetup];
-        c->acc.ms_clip += ms[kStageClip];
+        c->acc.ms_shadow += ms[kStageShadow];
         c->acc.ms_raster += ms[kStageRaster];
         c->acc.ms_frame += tot;
         c->acc.frames += 1;
@@ -435,6 +512,12 @@ int check_overflow(tri_ctx* c) {
         c->bin_cap = (c->bin_cap + 63) & ~63u;
         const uint32_t zmax = 0;
         HIP_TRY(hipMemcpy(&c->d_ctr->bin_max, &zmax, 4, hipMemcpyHostToDevice));
+    }
+    if (h.flags & TRI_OVF_SHADOW_BIN_LIST) {
+        c->s_bin_cap = std::max<uint32_t>(c->s_bin_cap * 2, h.sbin_max + h.sbin_max / 4);
+        c->s_bin_cap = (c->s_bin_cap + 63) & ~63u;
+        const uint32_t zmax = 0;
+        HIP_TRY(hipMemcpy(&c->d_ctr->sbin_max, &zmax, 4, hipMemcpyHostToDevice));
     }
     int rc = ensure_work_buffers(c);
     if (rc) return rc;
@@ -552,6 +635,7 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own); f(c->d_present);
+    f(c->d_lpos); f(c->d_lsnap); f(c->d_sbin_count); f(c->d_sbin_list); f(c->d_shadow);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
     if (c->stage_free) (void)hipEventDestroy(c->stage_free);
     for (auto& v : {std::cref(c->pending), std::cref(c->free_sets)})
@@ -696,6 +780,55 @@ int tri_upload_skybox(tri_ctx* c, const uint8_t* faces, uint32_t n) {
     return TRI_OK;
 }
 
+int tri_set_shadow(tri_ctx* c, const tri_shadow_config* cfg) {
+    if (!c) return fail(TRI_E_INVALID, "tri_set_shadow: null context");
+    if (!cfg || cfg->size == 0) {
+        c->shadow = tri_shadow_config{};
+        c->shadow_rendered = false;
+        return TRI_OK;
+    }
+    if (cfg->size > TRI_MAX_DIM) return fail(TRI_E_INVALID, "tri_set_shadow: map size %u > %d", cfg->size, TRI_MAX_DIM);
+    const float* m = cfg->light_view_proj;
+    if (m[3] != 0.0f || m[7] != 0.0f || m[11] != 0.0f || m[15] != 1.0f)
+        return fail(TRI_E_INVALID, "tri_set_shadow: light_view_proj must be affine (an orthographic light)");
+    for (int i = 0; i < 16; ++i)
+        if (!std::isfinite(m[i])) return fail(TRI_E_INVALID, "tri_set_shadow: non-finite light transform");
+    if (!std::isfinite(cfg->depth_bias) || !std::isfinite(cfg->slope_bias))
+        return fail(TRI_E_INVALID, "tri_set_shadow: non-finite depth bias");
+    int rc = make_current(c);
+    if (rc) return rc;
+    const uint32_t nbx = (cfg->size + 31) / 32;
+    if (cfg->size != c->shadow.size) {  // new map grid: fresh (zeroed) queue counters
+        HIP_TRY(hipStreamSynchronize(c->stream));
+        if ((rc = grow(c->d_sbin_count, c->cap_sbin_count, (size_t)nbx * nbx))) return rc;
+        HIP_TRY(hipMemset(c->d_sbin_count, 0, (size_t)nbx * nbx * 4));
+        c->s_bin_cap = 0;
+        c->shadow_rendered = false;
+    }
+    c->shadow = *cfg;
+    c->s_nbx = nbx;
+    c->s_nbins = nbx * nbx;
+    return TRI_OK;
+}
+
+int tri_shadow_fit_ortho(const float dir[3], const float mn[3], const float mx[3], float out[16]) {
+    if (!dir || !mn || !mx || !out) return fail(TRI_E_INVALID, "tri_shadow_fit_ortho: null argument");
+    for (int a = 0; a < 3; ++a)
+        if (!std::isfinite(mn[a]) || !std::isfinite(mx[a]) || mn[a] > mx[a])
+            return fail(TRI_E_INVALID, "tri_shadow_fit_ortho: bad box");
+    shadow_fit_ortho(dir, mn, mx, out);
+    return TRI_OK;
+}
+
+int tri_read_shadow_map(tri_ctx* c, uint32_t* out) {
+    if (!c || !out) return fail(TRI_E_INVALID, "tri_read_shadow_map: null argument");
+    if (!c->shadow.size || !c->shadow_rendered) return fail(TRI_E_STATE, "tri_read_shadow_map: no shadow pass rendered");
+    int rc = tri_synchronize(c);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpy(out, c->d_shadow, (size_t)c->shadow.size * c->shadow.size * 4, hipMemcpyDeviceToHost));
+    return TRI_OK;
+}
+
 int tri_set_frame(tri_ctx* c, const tri_global_ubo* ubo, const float clear[4]) {
     if (!c || !ubo) return fail(TRI_E_INVALID, "tri_set_frame: null argument");
     if (ubo->ai_blend_config[3] > 0.0f && ubo->ai_blend_config[0] > 0.0f)
@@ -788,6 +921,18 @@ int tri_render(tri_ctx* c) {
     }
     for (int t = 0; t < TRI_MAX_TEXTURE_SLOTS && !fp.need_lut; ++t)
         fp.need_lut = c->d_tex[t] && (c->tex_w[t] != 1 || c->tex_h[t] != 1);
+    if (c->shadow.size) {
+        fp.shadow_on = 1u;
+        fp.s_size = c->shadow.size;
+        fp.s_nbx = c->s_nbx;
+        fp.s_nbins = c->s_nbins;
+        fp.s_bin_cap = c->s_bin_cap;
+        fp.s_hw = (float)c->shadow.size * 0.5f;
+        fp.s_g = (2.0f * TRI_GUARD_BAND_PX) / (float)c->shadow.size - 1.0f;
+        fp.s_bias = c->shadow.depth_bias;
+        fp.s_slope = c->shadow.slope_bias;
+        std::memcpy(fp.lvp, c->shadow.light_view_proj, 64);
+    }
     std::memcpy(fp.pv, c->pv, 64);
     fp.ubo = c->ubo;
     fp.mat0 = c->mat0;
@@ -817,6 +962,11 @@ int tri_render(tri_ctx* c) {
     b.counters = c->d_ctr;
     b.color = c->d_color;
     b.depth = c->d_depth;
+    b.lpos = c->d_lpos;
+    b.lsnap = c->d_lsnap;
+    b.sbin_count = c->d_sbin_count;
+    b.sbin_list = c->d_sbin_list;
+    b.shadow_map = c->d_shadow;
 
     hipEvent_t* ev = nullptr;
     TimingSet ts{};
@@ -830,8 +980,10 @@ int tri_render(tri_ctx* c) {
         }
         ev = ts.ev;
     }
+    ts.shadow = fp.shadow_on != 0;
     HIP_TRY(tri_launch_frame(fp, b, c->stream, ev));
     if (timed) c->pending.push_back(ts);
+    if (fp.shadow_on) c->shadow_rendered = true;
     return TRI_OK;
 }
 

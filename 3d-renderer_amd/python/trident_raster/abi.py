@@ -122,7 +122,7 @@ class TriTiming(C.Structure):
         ("frames", C.c_uint64),
         ("ms_vertex", C.c_double),
         ("ms_setup", C.c_double),
-        ("ms_clip", C.c_double),
+        ("ms_shadow", C.c_double),
         ("ms_raster", C.c_double),
         ("ms_frame", C.c_double),
         ("reserved", C.c_double),
@@ -143,7 +143,25 @@ class TriFrameStats(C.Structure):
     ]
 
 
-for _s, _n in ((TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32)):
+class TriShadowConfig(C.Structure):
+    _fields_ = [
+        ("size", C.c_uint32),
+        ("flags", C.c_uint32),
+        ("depth_bias", C.c_float),
+        ("slope_bias", C.c_float),
+        ("light_view_proj", C.c_float * 16),
+    ]
+
+
+def make_shadow(light_view_proj, size=2048, depth_bias=0.001, slope_bias=2.0):
+    s = TriShadowConfig()
+    s.size, s.flags, s.depth_bias, s.slope_bias = size, 0, depth_bias, slope_bias
+    s.light_view_proj = mat_to_c(light_view_proj)
+    return s
+
+
+for _s, _n in ((TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
+               (TriShadowConfig, 80)):
     assert C.sizeof(_s) == _n, (_s, C.sizeof(_s))
 
 # every entry point include/tri_raster.h declares: (name, restype, argtypes)
@@ -170,6 +188,10 @@ CABI_FUNCTIONS = [
     ("tri_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("tri_get_timing", C.c_int, [C.c_void_p, C.POINTER(TriTiming)]),
     ("tri_get_frame_stats", C.c_int, [C.c_void_p, C.POINTER(TriFrameStats)]),
+    ("tri_set_shadow", C.c_int, [C.c_void_p, C.POINTER(TriShadowConfig)]),
+    ("tri_shadow_fit_ortho", C.c_int, [C.POINTER(C.c_float * 3), C.POINTER(C.c_float * 3), C.POINTER(C.c_float * 3),
+                                       C.POINTER(C.c_float * 16)]),
+    ("tri_read_shadow_map", C.c_int, [C.c_void_p, C.c_void_p]),
 ]
 
 

@@ -53,6 +53,16 @@ def _ptr(a):
     return C.c_void_p(a.ctypes.data) if a is not None and a.size else None
 
 
+def shadow_fit_ortho(light_dir, aabb_min, aabb_max):
+    """tri_shadow_fit_ortho (host-only): column-major light ortho * light view, as numpy [col][row]."""
+    lib = load_library()
+    f3 = lambda v: (C.c_float * 3)(*[float(x) for x in v])  # noqa: E731
+    out = (C.c_float * 16)()
+    _check(lib.tri_shadow_fit_ortho(C.byref(f3(light_dir)), C.byref(f3(aabb_min)), C.byref(f3(aabb_max)),
+                                    C.byref(out)))
+    return np.array(out[:], np.float32).reshape(4, 4)
+
+
 class TriRaster:
     """One tri_ctx: a W x H framebuffer (optionally a row band) on one HIP device."""
 
@@ -120,6 +130,16 @@ class TriRaster:
         if f.ndim != 4 or f.shape[0] != 6 or f.shape[1] != f.shape[2] or f.shape[3] != 4:
             raise ValueError("skybox faces must be uint8 [6, n, n, 4]")
         _check(_lib.tri_upload_skybox(self._ctx, _ptr(f), f.shape[1]))
+
+    def set_shadow(self, cfg):
+        """tri_set_shadow: an abi.TriShadowConfig, or None to switch the shadow pre-pass off."""
+        _check(_lib.tri_set_shadow(self._ctx, C.byref(cfg) if cfg is not None else None))
+        self._shadow_size = int(cfg.size) if cfg is not None else 0
+
+    def read_shadow_map(self):
+        out = np.empty((self._shadow_size, self._shadow_size), np.uint32)
+        _check(_lib.tri_read_shadow_map(self._ctx, _ptr(out)))
+        return out
 
     # ---- frame ----
     def set_frame(self, ubo, clear=(0.005, 0.005, 0.005, 1.0)):

@@ -302,6 +302,7 @@ class Scene:
     clear: tuple = (0.005, 0.005, 0.005, 1.0)
     bones: np.ndarray = None
     skybox: np.ndarray = None  # uint8 [6, n, n, 4] sRGB cubemap (+X,-X,+Y,-Y,+Z,-Z), None = no skybox pass
+    shadow: abi.TriShadowConfig = None  # shadow-map pre-pass (tri_set_shadow), None = off
 
     @property
     def triangles(self):
@@ -312,7 +313,8 @@ class Scene:
         rows = self.height if rows is None else rows
         V = int(self.vertices.shape[0])
         tex = sum(int(t.shape[0] * t.shape[1] * 4) for _, t in self.textures if t.size > 4)
-        return 12 * self.triangles + 44 * V + 8 * self.width * rows + tex
+        shadow = 0 if self.shadow is None else 8 * int(self.shadow.size) ** 2  # map write + read (§8(d) C5)
+        return 12 * self.triangles + 44 * V + 8 * self.width * rows + tex + shadow
 
 
 # CreateDefaultSkybox's fallback (Renderer.cpp:3925-3926): CreateSolidColor(0x808080) — bytes 80 80 80 00
@@ -385,11 +387,38 @@ def procedural_texture(size, seed):
     return t
 
 
-def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048):
-    """C5 within the reference's shading model: the C3 grid split into 4 meshes (row quarters), each
-    drawn with its own tex_size^2 sRGB texture slot (4 bilinear textures, uv x4 REPEAT). The shadow-map
-    pre-pass of BASELINE.json's C5 has no counterpart in the reference (LightComponent.h:33 marks
-    m_ShadowCaster reserved; Default.frag samples one texture), so it is not rendered."""
+def world_aabb(scene):
+    """World-space box of every drawn vertex (the shim fits the shadow frustum to the same box)."""
+    lo = np.full(3, np.inf, np.float32)
+    hi = np.full(3, -np.inf, np.float32)
+    for d in scene.draws:
+        m = scene.meshes[d.mesh_index]
+        idx = scene.indices[int(m["first_index"]):int(m["first_index"]) + int(m["index_count"])]
+        if idx.size == 0:
+            continue
+        p = scene.vertices["position"][idx.astype(np.int64) + int(m["base_vertex"])].astype(np.float32)
+        M = np.array(d.pc.model, np.float32).reshape(4, 4)  # [col][row]
+        w = p @ M[:3, :3] + M[3, :3]
+        lo, hi = np.minimum(lo, w.min(0)), np.maximum(hi, w.max(0))
+    return lo, hi
+
+
+def with_shadow(scene, size=2048, depth_bias=0.001, slope_bias=2.0):
+    """Turn on the shadow pre-pass for the scene's directional light: the light transform is the one
+    the shim fits (tri_shadow_fit_ortho over the world box of the draws)."""
+    from . import raster
+
+    lo, hi = world_aabb(scene)
+    lvp = raster.shadow_fit_ortho(list(scene.ubo.directional_light_direction)[:3], lo, hi)
+    scene.shadow = abi.make_shadow(lvp, size, depth_bias, slope_bias)
+    return scene
+
+
+def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048, shadow_size=2048):
+    """C5: the C3 grid split into 4 meshes (row quarters), each drawn with its own tex_size^2 sRGB
+    texture slot (4 bilinear textures, uv x4 REPEAT), plus the shadow_size^2 shadow-map pre-pass for the
+    sun (tri_set_shadow; the reference only reserves LightComponent::m_ShadowCaster, so the pass follows
+    DESIGN.md §5d). shadow_size 0 leaves the pre-pass off."""
     s = scene_c3_grid(width, height, n)
     tris = s.indices.size // 3
     q = [(k * tris) // 4 for k in range(5)]
@@ -400,6 +429,9 @@ def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048):
     s.textures = [(1 + k, procedural_texture(tex_size, 0xC5 + k)) for k in range(4)]
     s.draws = [abi.make_draw(k, np.eye(4, dtype=F), texture_slot=1 + k, material_index=0) for k in range(4)]
     s.name = f"c5_textured4x{tex_size}_{width}x{height}"
+    if shadow_size:
+        with_shadow(s, shadow_size)
+        s.name = f"c5_textured4x{tex_size}_shadow{shadow_size}_{width}x{height}"
     return s
 
 
@@ -413,5 +445,6 @@ def load_scene(rast, scene):
         rast.upload_bone_palette(scene.bones)
     if scene.skybox is not None:
         rast.upload_skybox(scene.skybox)
+    rast.set_shadow(scene.shadow)
     rast.set_frame(scene.ubo, scene.clear)
     rast.set_draws(scene.draws)

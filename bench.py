@@ -293,7 +293,7 @@ def main():
     # roofline of the dominant kernel (k_raster = tile_raster_shade): its algorithmic bytes per
     # launch are the colour + depth it must store for its band (4 + 4 B per pixel).
     if timing is None:
-        timing = {"frames": 0, "ms_vertex": 0.0, "ms_setup": 0.0, "ms_clip": 0.0, "ms_raster": 0.0, "ms_frame": 0.0}
+        timing = {"frames": 0, "ms_vertex": 0.0, "ms_setup": 0.0, "ms_shadow": 0.0, "ms_raster": 0.0, "ms_frame": 0.0}
     frames_timed = max(int(timing["frames"]), 1)
     raster_ms = timing["ms_raster"] / frames_timed
     # whole-frame figure on the throughput clock: with two frames in flight the event span of one
@@ -357,7 +357,7 @@ def main():
                                "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9 if frame_ms > 0 else None,
                                "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if frame_ms > 0 else None},
             "stage_ms": {k: timing[k] / frames_timed for k in
-                         ("ms_vertex", "ms_setup", "ms_clip", "ms_raster", "ms_frame")},
+                         ("ms_vertex", "ms_setup", "ms_shadow", "ms_raster", "ms_frame")},
             "frame_stats": stats,
             "secondary": secondary,
             "cpu_baseline": cpu,

@@ -141,7 +141,7 @@ typedef struct tri_timing {
     uint64_t frames;        /* frames timed since the last reset                  */
     double ms_vertex;       /* vs_transform (+ per-vertex divide / viewport / snap) */
     double ms_setup;        /* tri_setup_bin (setup + cull + per-bin queues)       */
-    double ms_clip;         /* always 0: clipping runs inside k_setup (in ms_setup)  */
+    double ms_shadow;       /* shadow-map pre-pass (0 without it; clipping is in ms_setup) */
     double ms_raster;       /* tile_raster_shade (coverage + early-Z + PBR + store) */
     double ms_frame;        /* first kernel start to last kernel end              */
     double reserved;
@@ -155,6 +155,29 @@ typedef struct tri_frame_stats {
     uint64_t vertices_shaded;   /* vertex-shader invocations                       */
     uint32_t bins_x, bins_y, bin_size, reserved;
 } tri_frame_stats;
+
+/* Shadow-map pre-pass (BASELINE.json config 5). The reference reserves the switch
+ * (LightComponent::m_ShadowCaster, Trident/src/ECS/Components/LightComponent.h:33) but renders no shadow
+ * map, so this pass is defined here and restated by the oracle:
+ *   - every frame, before the main pass, the draws' triangles are rasterised depth-only into a
+ *     size x size D32 map by the orthographic light transform `light_view_proj` (column-major, affine:
+ *     its last row must be exactly 0,0,0,1): texel (i, j) covers light NDC x in [2i/size - 1, 2(i+1)/size - 1),
+ *     y likewise; the main pass's raster rules (8-bit snap, top-left fill, plane depth), no culling,
+ *     depth clamp instead of near/far clipping, a slope-scaled depth bias (Vulkan depthBiasSlopeFactor
+ *     semantics: + slope_bias * the triangle's largest depth change per texel, before the clamp),
+ *     LEQUAL (the map keeps the minimum depth, clear 1.0);
+ *     triangles reaching beyond the guard band (|x|, |y| > 2*16000/size - 1 in light NDC) cast nothing;
+ *   - in Default.frag the directional light's radiance is scaled by the fraction of a 2x2 bilinear
+ *     depth compare (zref - depth_bias <= map) that passes, zref being the fragment's light-space depth;
+ *     fragments outside the map are lit. Point lights and ambient are unchanged. */
+typedef struct tri_shadow_config {
+    uint32_t size;              /* map edge in texels (e.g. 2048); 0 disables the pre-pass         */
+    uint32_t flags;             /* reserved, 0                                                      */
+    float depth_bias;           /* light-NDC depth subtracted before the compare (e.g. 0.002)       */
+    float slope_bias;           /* depthBiasSlopeFactor of the depth pass: each caster's depth is   *
+                                 * raised by slope_bias * max(|dz/dx|, |dz/dy|) per texel (e.g. 2) */
+    float light_view_proj[16];  /* column-major light ortho * light view                            */
+} tri_shadow_config;
 
 typedef struct tri_ctx tri_ctx;
 
@@ -192,6 +215,19 @@ int tri_upload_bone_palette(tri_ctx* ctx, const float* matrices, uint32_t matrix
  * LEQUAL without writes) then gives every uncovered pixel its sky colour instead of the clear colour.
  * faces = NULL or size = 0 removes the skybox. */
 int tri_upload_skybox(tri_ctx* ctx, const uint8_t* faces_rgba8_srgb, uint32_t size);
+
+/* Shadow-map pre-pass for the directional light (see tri_shadow_config). NULL or size 0 disables it
+ * (the default: C1-C3 frames are exactly the reference's). size <= TRI_MAX_DIM. */
+int tri_set_shadow(tri_ctx* ctx, const tri_shadow_config* config);
+/* Host-only helper (no device): the orthographic light transform the shim fits for a shadow-casting
+ * directional light travelling along `light_dir` (the UBO's DirectionalLightDirection) over the world
+ * box [aabb_min, aabb_max]: glm::lookAtRH from 2 * radius behind the box centre, then glm::orthoRH_ZO
+ * over the box corners in light view space (1% margin), so every corner lands inside the map. */
+int tri_shadow_fit_ortho(const float light_dir[3], const float aabb_min[3], const float aabb_max[3],
+                         float out_light_view_proj[16]);
+/* Synchronous copy of the last rendered shadow map: size*size float32 depth bits, row j = light NDC y
+ * increasing. TRI_E_STATE when no shadow pass is configured. */
+int tri_read_shadow_map(tri_ctx* ctx, uint32_t* depth_bits);
 
 /* ---- per frame --------------------------------------------------------------------------- */
 /* UpdateUniformBuffer's vkCmdUpdateBuffer (Renderer.cpp:5958) + the colour clear value
@@ -238,6 +274,7 @@ static_assert(sizeof(tri_push_constant) == 128, "RenderablePushConstant is 128 b
 static_assert(sizeof(tri_draw) == 144, "tri_draw layout");
 static_assert(sizeof(tri_global_ubo) == 480, "GlobalUniformBuffer is 480 bytes");
 static_assert(sizeof(tri_material_record) == 32, "MaterialUniformBuffer is 32 bytes");
+static_assert(sizeof(tri_shadow_config) == 80, "tri_shadow_config layout");
 #endif
 
 #endif /* TRI_RASTER_H */

@@ -33,6 +33,7 @@ class OracleScene(C.Structure):
         ("ubo", C.POINTER(abi.TriGlobalUbo)),
         ("clear_rgba", C.c_float * 4),
         ("sky_faces", C.c_void_p), ("sky_size", C.c_uint32), ("sky_reserved", C.c_uint32),
+        ("shadow", C.POINTER(abi.TriShadowConfig)), ("out_shadow_map", C.c_void_p),
     ]
 
 
@@ -80,6 +81,8 @@ def load():
                                               C.c_float, C.c_int, fl3, fl3]
         lib.oracle_blit_linear.restype = None
         lib.oracle_blit_linear.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]
+        lib.oracle_shadow_fit_ortho.restype = None
+        lib.oracle_shadow_fit_ortho.argtypes = [fl3, fl3, fl3, fl3]
         lib.oracle_pack_global_ubo.restype = None
         lib.oracle_pack_global_ubo.argtypes = [fl3, fl3, fl3, C.c_int, fl3, C.c_float, C.POINTER(OracleLight),
                                                C.c_uint32, C.POINTER(abi.TriGlobalUbo)]
@@ -158,8 +161,17 @@ def pack_ubo(view, proj, cam, lights=(), has_camera=True, ambient=(0.03, 0.03, 0
     return u
 
 
-def render(scene, band=None, threads=None):
-    """Render a trident_raster.scenes.Scene. Returns (bgra uint8 [rows,W,4], depth bits uint32 [rows,W], stats)."""
+def shadow_fit_ortho(light_dir, aabb_min, aabb_max):
+    lib = load()
+    d, dp = _f(light_dir); a, ap = _f(aabb_min); b, bp = _f(aabb_max)
+    out = np.zeros(16, np.float32)
+    lib.oracle_shadow_fit_ortho(dp, ap, bp, out.ctypes.data_as(C.POINTER(C.c_float)))
+    return out.reshape(4, 4)
+
+
+def render(scene, band=None, threads=None, shadow_map_out=None):
+    """Render a trident_raster.scenes.Scene. Returns (bgra uint8 [rows,W,4], depth bits uint32 [rows,W], stats).
+    shadow_map_out: optional uint32 [size, size] array that receives the shadow pre-pass's map."""
     lib = load()
     if threads is None:
         threads = min(os.cpu_count() or 1, 16)
@@ -195,6 +207,12 @@ def render(scene, band=None, threads=None):
         sky = np.ascontiguousarray(sky, np.uint8)  # [6, n, n, 4]
         keep.append(sky)
         sc.sky_faces, sc.sky_size = sky.ctypes.data, sky.shape[1]
+    shadow = getattr(scene, "shadow", None)
+    if shadow is not None:
+        sc.shadow = C.pointer(shadow)
+        if shadow_map_out is not None:
+            assert shadow_map_out.dtype == np.uint32 and shadow_map_out.size == shadow.size * shadow.size
+            sc.out_shadow_map = shadow_map_out.ctypes.data
     y0, y1 = band if band is not None else (0, scene.height)
     rows = y1 - y0
     col = np.empty((rows, scene.width, 4), np.uint8)

@@ -42,18 +42,8 @@ struct VsOut {
     vec3 normal;
     vec2 uv;
     vec3 color;
+    vec3 lpos;  // light-space (shadow-map NDC) position: light_view_proj * world (shadow pass only)
 };
-
-inline VsOut lerp_vs(const VsOut& a, const VsOut& b, float t) {
-    auto l = [t](float x, float y) { return x + t * (y - x); };
-    VsOut r;
-    r.clip = {l(a.clip.x, b.clip.x), l(a.clip.y, b.clip.y), l(a.clip.z, b.clip.z), l(a.clip.w, b.clip.w)};
-    r.world = {l(a.world.x, b.world.x), l(a.world.y, b.world.y), l(a.world.z, b.world.z)};
-    r.normal = {l(a.normal.x, b.normal.x), l(a.normal.y, b.normal.y), l(a.normal.z, b.normal.z)};
-    r.uv = {l(a.uv.x, b.uv.x), l(a.uv.y, b.uv.y)};
-    r.color = {l(a.color.x, b.color.x), l(a.color.y, b.color.y), l(a.color.z, b.color.z)};
-    return r;
-}
 
 mat4 load_mat4(const float* p) {
     mat4 m;
@@ -77,7 +67,7 @@ inline vec4 mat_vec_seq(const mat4& m, vec4 v) {
 
 // Default.vert:60-105 for one vertex of one draw.
 VsOut vertex_shader(const tri_vertex& in, const tri_push_constant& pc, const mat4& pv,
-                    const float* bones, uint32_t bone_count) {
+                    const float* bones, uint32_t bone_count, const mat4* lvp) {
     const mat4 model = load_mat4(pc.model);
     vec4 sp{in.position[0], in.position[1], in.position[2], 1.0f};
     vec3 sn{in.normal[0], in.normal[1], in.normal[2]};
@@ -132,6 +122,11 @@ VsOut vertex_shader(const tri_vertex& in, const tri_push_constant& pc, const mat
     o.uv.y = (in.texcoord[1] * pc.texture_scale[1]) * pc.tiling_factor + pc.texture_offset[1];
     o.color = {in.color[0], in.color[1], in.color[2]};
     o.clip = mat_vec_seq(pv, world);  // (P*V)*world, Default.vert:104
+    o.lpos = {0.0f, 0.0f, 0.0f};
+    if (lvp) {  // shadow pre-pass (tri_shadow_config): the affine light transform of the same world point
+        const vec4 l = mat_vec_seq(*lvp, world);
+        o.lpos = {l.x, l.y, l.z};
+    }
     return o;
 }
 
@@ -220,15 +215,24 @@ bool setup_triangle(const Setup& su, const VsOut* const vs[3], const uint32_t vi
 }
 
 // Homogeneous Sutherland-Hodgman against w>=kWMin, z>=0 and the guard-band x/y planes, then a fan.
+// A polygon vertex carries its clip position and its barycentric weights on the source triangle, both
+// interpolated along the clipped edges (x + t * (y - x)); its varyings are then the weighted sums
+// (b0 * a0 + b1 * a1) + b2 * a2 of the source vertices' varyings. Vulkan leaves the precision of
+// clipped attributes to the implementation; this is the formulation the kernels use too.
+struct ClipV {
+    vec4 c;
+    float b0, b1, b2;
+};
+
 int clip_polygon(const Setup& su, const VsOut in[3], VsOut* out /* >= 9 */) {
-    VsOut bufA[12], bufB[12];
+    ClipV bufA[12], bufB[12];
     int n = 3;
-    for (int k = 0; k < 3; ++k) bufA[k] = in[k];
-    VsOut* src = bufA;
-    VsOut* dst = bufB;
+    for (int k = 0; k < 3; ++k) bufA[k] = {in[k].clip, k == 0 ? 1.0f : 0.0f, k == 1 ? 1.0f : 0.0f, k == 2 ? 1.0f : 0.0f};
+    ClipV* src = bufA;
+    ClipV* dst = bufB;
     for (int plane = 0; plane < 6 && n > 0; ++plane) {
-        auto dist = [&](const VsOut& v) -> float {
-            const vec4 c = v.clip;
+        auto dist = [&](const ClipV& v) -> float {
+            const vec4 c = v.c;
             switch (plane) {
                 case 0: return c.w - kWMin;
                 case 1: return c.z;
@@ -240,13 +244,15 @@ int clip_polygon(const Setup& su, const VsOut in[3], VsOut* out /* >= 9 */) {
         };
         int m = 0;
         for (int i = 0; i < n; ++i) {
-            const VsOut& a = src[i];
-            const VsOut& b = src[(i + 1) % n];
+            const ClipV& a = src[i];
+            const ClipV& b = src[(i + 1) % n];
             const float da = dist(a), db = dist(b);
             if (da >= 0.0f && m < 12) dst[m++] = a;
             if ((da >= 0.0f) != (db >= 0.0f) && m < 12) {
                 const float t = da / (da - db);
-                dst[m++] = lerp_vs(a, b, t);
+                auto l = [t](float x, float y) { return x + t * (y - x); };
+                dst[m++] = {{l(a.c.x, b.c.x), l(a.c.y, b.c.y), l(a.c.z, b.c.z), l(a.c.w, b.c.w)},
+                            l(a.b0, b.b0), l(a.b1, b.b1), l(a.b2, b.b2)};
             }
         }
         n = m;
@@ -255,7 +261,21 @@ int clip_polygon(const Setup& su, const VsOut in[3], VsOut* out /* >= 9 */) {
     // a triangle clipped by 6 planes has at most 9 vertices; a numerically non-convex polygon is cut
     // to its first 9 (fan sub-triangle indices 0..6, as the kernels' 3-bit key field requires)
     n = std::min(n, 9);
-    for (int k = 0; k < n; ++k) out[k] = src[k];
+    for (int k = 0; k < n; ++k) {
+        const ClipV& v = src[k];
+        auto w = [&](float x0, float x1, float x2) { return (v.b0 * x0 + v.b1 * x1) + v.b2 * x2; };
+        VsOut& o = out[k];
+        o.clip = v.c;
+        o.world = {w(in[0].world.x, in[1].world.x, in[2].world.x), w(in[0].world.y, in[1].world.y, in[2].world.y),
+                   w(in[0].world.z, in[1].world.z, in[2].world.z)};
+        o.normal = {w(in[0].normal.x, in[1].normal.x, in[2].normal.x), w(in[0].normal.y, in[1].normal.y, in[2].normal.y),
+                    w(in[0].normal.z, in[1].normal.z, in[2].normal.z)};
+        o.uv = {w(in[0].uv.x, in[1].uv.x, in[2].uv.x), w(in[0].uv.y, in[1].uv.y, in[2].uv.y)};
+        o.color = {w(in[0].color.x, in[1].color.x, in[2].color.x), w(in[0].color.y, in[1].color.y, in[2].color.y),
+                   w(in[0].color.z, in[1].color.z, in[2].color.z)};
+        o.lpos = {w(in[0].lpos.x, in[1].lpos.x, in[2].lpos.x), w(in[0].lpos.y, in[1].lpos.y, in[2].lpos.y),
+                  w(in[0].lpos.z, in[1].lpos.z, in[2].lpos.z)};
+    }
     return n;
 }
 
@@ -357,7 +377,7 @@ struct FragIn {
 
 // Default.frag:123-180 (AiBlendConfig.w == 0 path). Returns linear RGBA before UNORM conversion.
 vec4 fragment_shader(const FragIn& f, const tri_push_constant& pc, const tri_global_ubo& g,
-                     const tri_material_record& mat, const Texture& tex) {
+                     const tri_material_record& mat, const Texture& tex, float sun_vis) {
     const vec3 Nn = normalize(f.normal);
     const vec3 N = normalize(Nn);  // normalize(TBN * (0,0,1)) == normalize(N): T/B are dead
     const vec3 cam{g.camera_position[0], g.camera_position[1], g.camera_position[2]};
@@ -377,8 +397,9 @@ vec4 fragment_shader(const FragIn& f, const tri_push_constant& pc, const tri_glo
     if (g.light_counts[0] > 0u) {
         const vec3 L = normalize(vec3{-g.directional_light_direction[0], -g.directional_light_direction[1],
                                       -g.directional_light_direction[2]});
-        const vec3 rad = vec3{g.directional_light_color[0], g.directional_light_color[1],
-                              g.directional_light_color[2]} * g.directional_light_color[3];
+        // sun_vis: the shadow pre-pass's visibility (1 without it, so the product is exact)
+        const vec3 rad = (vec3{g.directional_light_color[0], g.directional_light_color[1],
+                               g.directional_light_color[2]} * g.directional_light_color[3]) * sun_vis;
         direct = direct + evaluate_pbr(L, rad, N, V, albedo, metallic, roughness, F0);
     }
     const uint32_t pcount = std::min(g.light_counts[1], 8u);
@@ -569,6 +590,100 @@ bool sky_pixel(const SkyConst& k, const Sky& sky, uint32_t W, uint32_t H, int32_
     return true;
 }
 
+// ---- shadow-map pre-pass (tri_shadow_config) ---------------------------------
+// Depth-only raster of every triangle by the affine light transform into a size x size map: the main
+// pass's snap / fill / plane-depth rules with the light NDC as window coordinates (w = 1), no culling
+// (a clockwise triangle is set up with its own orientation), depth clamped to [0, 1] instead of
+// near/far clipping, a slope-scaled depth bias (Vulkan depthBiasSlopeFactor: + slope * the triangle's
+// largest depth change per texel) before the clamp, guard-band violators dropped; each texel keeps the
+// minimum depth (LEQUAL with writes: the result does not depend on primitive order).
+struct ShadowMap {
+    uint32_t S = 0;
+    float bias = 0.0f;   // lookup: subtracted from the receiver's depth
+    float slope = 0.0f;  // raster: depthBiasSlopeFactor
+    std::vector<float> d;
+};
+
+void shadow_raster_triangle(ShadowMap& sm, const vec3& a, const vec3& b, const vec3& c, int32_t row0, int32_t row1) {
+    const float hs = (float)sm.S * 0.5f;
+    const float g = (2.0f * kGuardBandPx) / (float)sm.S - 1.0f;
+    const vec3 v[3] = {a, b, c};
+    int32_t X[3], Y[3];
+    float z[3];
+    for (int k = 0; k < 3; ++k) {
+        // the main pass's snap with w = 1: iw = 1 / 1, xd = x * 1
+        if (v[k].x < -g || v[k].x > g || v[k].y < -g || v[k].y > g) return;  // beyond the guard band
+        X[k] = (int32_t)std::rint((v[k].x * hs + hs) * 256.0f);
+        Y[k] = (int32_t)std::rint((v[k].y * hs + hs) * 256.0f);
+        z[k] = v[k].z;
+    }
+    auto all = [&](auto f) { return f(v[0]) && f(v[1]) && f(v[2]); };
+    if (all([](vec3 p) { return p.x + 1.0f < 0.0f; }) || all([](vec3 p) { return 1.0f - p.x < 0.0f; }) ||
+        all([](vec3 p) { return p.y + 1.0f < 0.0f; }) || all([](vec3 p) { return 1.0f - p.y < 0.0f; }))
+        return;  // trivially outside the map (covers no texel centre)
+    int64_t S = (int64_t)(X[1] - X[0]) * (int64_t)(Y[2] - Y[0]) - (int64_t)(Y[1] - Y[0]) * (int64_t)(X[2] - X[0]);
+    if (S == 0) return;
+    int o[3] = {0, 1, 2};
+    if (S < 0) { o[1] = 2; o[2] = 1; S = -S; }  // same v1 <-> v2 normalisation as the main pass
+    int32_t tX[3], tY[3];
+    float tz[3];
+    for (int k = 0; k < 3; ++k) { tX[k] = X[o[k]]; tY[k] = Y[o[k]]; tz[k] = z[o[k]]; }
+    const int32_t xmin = std::min(tX[0], std::min(tX[1], tX[2])), xmax = std::max(tX[0], std::max(tX[1], tX[2]));
+    const int32_t ymin = std::min(tY[0], std::min(tY[1], tY[2])), ymax = std::max(tY[0], std::max(tY[1], tY[2]));
+    const int32_t px0 = std::max(-floor_shift8(128 - xmin), 0), px1 = std::min(floor_shift8(xmax - 128), (int32_t)sm.S - 1);
+    const int32_t py0 = std::max(-floor_shift8(128 - ymin), row0), py1 = std::min(floor_shift8(ymax - 128), row1);
+    if (px0 > px1 || py0 > py1) return;
+    int64_t ea[3], eb[3], eD[3];
+    for (int e = 0; e < 3; ++e) {
+        const int i = e, j = (e + 1) % 3;
+        const int64_t aa = (int64_t)tY[i] - tY[j];
+        const int64_t bb = (int64_t)tX[j] - tX[i];
+        const int64_t cc = -(aa * tX[i] + bb * tY[i]);
+        const bool top_left = (aa > 0) || (aa == 0 && bb > 0);
+        ea[e] = aa; eb[e] = bb;
+        eD[e] = (cc + 128 * aa + 128 * bb - (top_left ? 0 : 1)) >> 8;
+    }
+    const float fX1 = (float)(tX[1] - tX[0]), fY1 = (float)(tY[1] - tY[0]);
+    const float fX2 = (float)(tX[2] - tX[0]), fY2 = (float)(tY[2] - tY[0]);
+    const float fS = (float)S;
+    const float dz1 = tz[1] - tz[0], dz2 = tz[2] - tz[0];
+    const float dzdX = (dz1 * fY2 - dz2 * fY1) / fS;
+    const float dzdY = (dz2 * fX1 - dz1 * fX2) / fS;
+    // slope-scaled bias: slope * the largest depth change per texel (the plane's per-1/256 slopes * 256)
+    const float off = sm.slope * (std::max(std::fabs(dzdX), std::fabs(dzdY)) * 256.0f);
+    for (int32_t py = py0; py <= py1; ++py)
+        for (int32_t px = px0; px <= px1; ++px) {
+            bool inside = true;
+            for (int e = 0; e < 3; ++e) inside = inside && (ea[e] * px + eb[e] * py + eD[e] >= 0);
+            if (!inside) continue;
+            const float t1 = dzdX * (float)(256 * px + 128 - tX[0]);
+            const float t2 = dzdY * (float)(256 * py + 128 - tY[0]);
+            float zz = ((tz[0] + t1) + t2) + off;
+            if (!(zz > 0.0f)) zz = 0.0f;  // depth clamp (also canonicalises -0)
+            if (zz > 1.0f) zz = 1.0f;
+            float& d = sm.d[(size_t)py * sm.S + px];
+            if (zz <= d) d = zz;
+        }
+}
+
+// Fraction of the 2x2 bilinear depth compare that passes at light-NDC point l (1 outside the map).
+float shadow_visibility(const ShadowMap& sm, vec3 l) {
+    const float u = l.x * 0.5f + 0.5f, v = l.y * 0.5f + 0.5f;
+    if (!(u >= 0.0f && u <= 1.0f && v >= 0.0f && v <= 1.0f)) return 1.0f;
+    const float fx = u * (float)sm.S - 0.5f, fy = v * (float)sm.S - 0.5f;
+    const float x0 = std::floor(fx), y0 = std::floor(fy);
+    const float a = fx - x0, b = fy - y0;
+    const int32_t i0 = (int32_t)x0, j0 = (int32_t)y0;
+    const float zref = l.z - sm.bias;
+    auto tap = [&](int32_t i, int32_t j) -> float {
+        i = std::min(std::max(i, 0), (int32_t)sm.S - 1);
+        j = std::min(std::max(j, 0), (int32_t)sm.S - 1);
+        return zref <= sm.d[(size_t)j * sm.S + i] ? 1.0f : 0.0f;
+    };
+    const float c00 = tap(i0, j0), c10 = tap(i0 + 1, j0), c01 = tap(i0, j0 + 1), c11 = tap(i0 + 1, j0 + 1);
+    return lerpf(lerpf(c00, c10, a), lerpf(c01, c11, a), b);
+}
+
 inline uint32_t unorm8(float c) {
     const float cc = std::fmin(std::fmax(c, 0.0f), 1.0f);  // NaN -> 0
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
@@ -612,6 +727,15 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
     tri_material_record mat0{{1, 1, 1, 1}, {1, 1, 1, 0}};  // BuildMaterialPayload default
     if (sc->material_count > 0 && sc->materials) mat0 = sc->materials[0];
 
+    const bool shadow_on = sc->shadow && sc->shadow->size > 0;
+    if (shadow_on) {
+        const float* m = sc->shadow->light_view_proj;
+        if (sc->shadow->size > TRI_MAX_DIM || m[3] != 0.0f || m[7] != 0.0f || m[11] != 0.0f || m[15] != 1.0f)
+            return TRI_E_INVALID;  // the light transform must be affine (orthographic)
+    }
+    const mat4 lvp = shadow_on ? load_mat4(sc->shadow->light_view_proj) : mat4_identity();
+    std::vector<uint32_t> shadow_prims;  // (pool index of vertex 0, 1, 2) of every valid primitive, in order
+
     // ---- vertex stage + primitive assembly, in submission order ----
     std::vector<VsOut> pool;
     std::vector<RTri> tris;
@@ -636,7 +760,8 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
             const int64_t gi = (int64_t)mr.base_vertex + v;
             valid[v - mn] = (gi >= 0 && (uint64_t)gi < sc->vertex_count);
             if (valid[v - mn])
-                pool[pool_base + (v - mn)] = vertex_shader(sc->vertices[gi], dr.pc, pv, sc->bones, sc->bone_count);
+                pool[pool_base + (v - mn)] =
+                    vertex_shader(sc->vertices[gi], dr.pc, pv, sc->bones, sc->bone_count, shadow_on ? &lvp : nullptr);
             if (v == 0xFFFFFFFFu) break;
         }
         for (uint32_t t = 0; t < nprim; ++t) {
@@ -650,6 +775,7 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
                 vid[k] = pool_base + (v - mn);
             }
             if (!ok) continue;
+            if (shadow_on) shadow_prims.insert(shadow_prims.end(), {vid[0], vid[1], vid[2]});
             const VsOut* vs[3] = {&pool[vid[0]], &pool[vid[1]], &pool[vid[2]]};
             // trivial reject: all three outside one clip half-space (0<=z<=w, -w<=x,y<=w)
             auto all_neg = [&](auto f) { return f(vs[0]->clip) < 0.0f && f(vs[1]->clip) < 0.0f && f(vs[2]->clip) < 0.0f; };
@@ -686,6 +812,34 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
         if (prim_base > kPrimMax) return TRI_E_INVALID;
     }
 
+    if (threads <= 0) threads = 1;
+    // ---- shadow-map pre-pass: rows of the map in parallel blocks, each walking every caster ----
+    ShadowMap sm;
+    if (shadow_on) {
+        sm.S = sc->shadow->size;
+        sm.bias = sc->shadow->depth_bias;
+        sm.slope = sc->shadow->slope_bias;
+        sm.d.assign((size_t)sm.S * sm.S, 1.0f);
+        constexpr int32_t kRows = 64;
+        const int32_t nb = ((int32_t)sm.S + kRows - 1) / kRows;
+        std::atomic<int32_t> next{0};
+        auto worker = [&]() {
+            for (;;) {
+                const int32_t blk = next.fetch_add(1);
+                if (blk >= nb) break;
+                const int32_t r0 = blk * kRows, r1 = std::min(r0 + kRows, (int32_t)sm.S) - 1;
+                for (size_t t = 0; t < shadow_prims.size(); t += 3)
+                    shadow_raster_triangle(sm, pool[shadow_prims[t]].lpos, pool[shadow_prims[t + 1]].lpos,
+                                           pool[shadow_prims[t + 2]].lpos, r0, r1);
+            }
+        };
+        std::vector<std::thread> ts;
+        for (int i = 1; i < threads; ++i) ts.emplace_back(worker);
+        worker();
+        for (auto& th : ts) th.join();
+        if (sc->out_shadow_map) std::memcpy(sc->out_shadow_map, sm.d.data(), sm.d.size() * 4);
+    }
+
     // ---- rasterization: in-order LEQUAL depth test (Pipeline.cpp:655-658) ----
     const uint32_t rows = band_y1 - band_y0;
     std::vector<float> depth((size_t)rows * W, 1.0f);  // depth clear 1.0 (Renderer.cpp:5037)
@@ -698,7 +852,6 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
         const uint32_t b0 = ((uint32_t)t.py0 - band_y0) / kBlock, b1 = ((uint32_t)t.py1 - band_y0) / kBlock;
         for (uint32_t b = b0; b <= b1; ++b) lists[b].push_back(i);
     }
-    if (threads <= 0) threads = 1;
     std::atomic<uint32_t> next_block{0};
     std::atomic<uint64_t> frags{0};
     auto raster_worker = [&]() {
@@ -797,7 +950,11 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
                 const tri_push_constant& pc = sc->draws[t.draw].pc;
                 int slot = pc.texture_slot;
                 const int tidx = (slot >= 0 && slot < TRI_MAX_TEXTURE_SLOTS) ? slot_map[slot] : 0;
-                const vec4 c = fragment_shader(f, pc, g, mat0, texs[tidx]);
+                float vis = 1.0f;
+                if (shadow_on && g.light_counts[0] > 0u)
+                    vis = shadow_visibility(sm, {ip(v0.lpos.x, v1.lpos.x, v2.lpos.x), ip(v0.lpos.y, v1.lpos.y, v2.lpos.y),
+                                                 ip(v0.lpos.z, v1.lpos.z, v2.lpos.z)});
+                const vec4 c = fragment_shader(f, pc, g, mat0, texs[tidx], vis);
                 if (out_bgra) out_bgra[idx] = pack_bgra(c);
             }
         }
@@ -1066,4 +1223,33 @@ extern "C" void oracle_blit_linear(const uint32_t* src, uint32_t w, uint32_t h, 
             }
             dst[(size_t)y * dw + x] = out;
         }
+}
+
+// tri_shadow_fit_ortho (include/tri_raster.h): the light transform the shim fits for a shadow-casting
+// directional light. glm::lookAtRH from 2 * radius behind the box centre along the light's direction,
+// then glm::orthoRH_ZO over the 8 box corners in light view space, widened by 1 % (+1e-4) per axis.
+extern "C" void oracle_shadow_fit_ortho(const float dir[3], const float mn[3], const float mx[3], float out[16]) {
+    vec3 d{dir[0], dir[1], dir[2]};
+    if (!(dot(d, d) > 1e-12f)) d = {-0.5f, -1.0f, -0.3f};
+    d = normalize(d);
+    const vec3 lo{mn[0], mn[1], mn[2]}, hi{mx[0], mx[1], mx[2]};
+    const vec3 c = (lo + hi) * 0.5f;
+    const float r = std::max(length(hi - lo) * 0.5f, 1e-3f);
+    const vec3 eye = c - d * (2.0f * r);
+    const vec3 up = std::fabs(d.y) > 0.99f ? vec3{0.0f, 0.0f, 1.0f} : vec3{0.0f, 1.0f, 0.0f};
+    const mat4 V = lookAtRH(eye, c, up);
+    float b0[3] = {INFINITY, INFINITY, INFINITY}, b1[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int k = 0; k < 8; ++k) {
+        const vec4 p = mul(V, vec4{(k & 1) ? hi.x : lo.x, (k & 2) ? hi.y : lo.y, (k & 4) ? hi.z : lo.z, 1.0f});
+        const float q[3] = {p.x, p.y, p.z};
+        for (int a = 0; a < 3; ++a) {
+            b0[a] = std::min(b0[a], q[a]);
+            b1[a] = std::max(b1[a], q[a]);
+        }
+    }
+    float m[3];
+    for (int a = 0; a < 3; ++a) m[a] = (b1[a] - b0[a]) * 0.01f + 1e-4f;
+    // view space looks down -z: near = -(max z) - margin, far = -(min z) + margin
+    const mat4 P = orthoRH_ZO(b0[0] - m[0], b1[0] + m[0], b0[1] - m[1], b1[1] + m[1], -b1[2] - m[2], -b0[2] + m[2]);
+    store(mul(P, V), out);
 }

@@ -50,6 +50,10 @@ typedef struct oracle_scene {
     const uint8_t* sky_faces;
     uint32_t sky_size;
     uint32_t sky_reserved;
+    /* Shadow-map pre-pass (tri_shadow_config semantics); NULL or size 0 = off.
+     * out_shadow_map (nullable) receives the size*size map (float32 depth bits). */
+    const tri_shadow_config* shadow;
+    uint32_t* out_shadow_map;
 } oracle_scene;
 
 typedef struct oracle_stats {
@@ -103,6 +107,10 @@ typedef struct oracle_light {
 void oracle_pack_global_ubo(const float view[16], const float proj[16], const float camera_pos[3],
                             int has_camera, const float ambient_color[3], float ambient_intensity,
                             const oracle_light* lights, uint32_t light_count, tri_global_ubo* out);
+
+/* tri_shadow_fit_ortho restated (lookAtRH + orthoRH_ZO over the box corners, 1% margin). */
+void oracle_shadow_fit_ortho(const float light_dir[3], const float aabb_min[3], const float aabb_max[3],
+                             float out_light_view_proj[16]);
 
 /* The presentation blit (Renderer.cpp:5346-5361, vkCmdBlitImage with VK_FILTER_LINEAR, Vulkan spec
  * "Image Blits": destination texel centres scaled into the source, bilinear over clamp-to-edge taps of

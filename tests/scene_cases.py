@@ -172,3 +172,33 @@ def c1_cube_skybox(frame=1, w=640, h=480):
     s.skybox = cubemap_faces(32, seed=5)
     s.name = "c1_cube_skybox"
     return s
+
+
+# ---- shadow-map pre-pass (BASELINE C5; tri_set_shadow) ------------------------------
+def shadow_scene(oracle, w=480, h=320, size=256, sun=(-0.45, -1.0, -0.35), bias=0.001, slope=2.0):
+    """A ground quad under a floating cube and sphere, lit by a shadow-casting sun (plus one point
+    light): the primitives (Renderer.cpp:72-246) as Forge spawns them, light frustum fitted by
+    tri_shadow_fit_ortho over the draws' world box."""
+    cam = (0.0, 4.0, 8.0)
+    view, proj, _ = oracle.editor_camera(cam, (-25.0, 0.0, 0.0), 60.0, (w, h))
+    verts, idxs, meshes = [], [], []
+    vbase = ibase = 0
+    for kind in (1, 2, 3):
+        v, i = oracle.build_primitive(kind)
+        meshes.append((ibase, i.size, vbase, len(meshes)))
+        verts.append(v)
+        idxs.append(i)
+        vbase += v.size
+        ibase += i.size
+    m = np.array(meshes, dtype=abi.MESH_RANGE_DTYPE)
+    draws = [
+        abi.make_draw(2, oracle.compose_transform((0.0, 0.0, 0.0), (-90.0, 0.0, 0.0), (12.0, 12.0, 1.0)), material_index=0),
+        abi.make_draw(0, oracle.compose_transform((-1.2, 1.4, 0.5), (15.0, 30.0, 0.0), (1.2, 1.2, 1.2)), material_index=0),
+        abi.make_draw(1, oracle.compose_transform((1.3, 1.0, -0.4), (0.0, 0.0, 0.0), (1.6, 1.6, 1.6)), material_index=0),
+    ]
+    lights = [{"type": "directional", "direction": sun, "intensity": 4.0},
+              {"type": "point", "position": (2.0, 2.5, 2.0), "range": 7.0, "intensity": 3.0}]
+    s = scenes.Scene("shadow", w, h, np.concatenate(verts), np.concatenate(idxs), m, draws,
+                     oracle.pack_ubo(view, proj, cam, lights), materials=[((0.9, 0.85, 0.8, 1.0), (0.1, 0.6, 1.0, 0.0))],
+                     skybox=SOLID_0x808080)
+    return scenes.with_shadow(s, size, bias, slope)
