@@ -68,6 +68,11 @@ public:
     // reference's fallback, a solid 0x808080 cubemap (:3925-3926). An invalid cubemap is rejected
     // and logged; returns false in that case.
     bool SetSkyboxCubemap(const Loader::CubemapTextureData& cubemap);
+    // Where CreateSkyboxCubemap looks for Skyboxes/ (the reference: "Assets", next to the executable,
+    // Renderer.cpp:3830). Changing it re-runs the discovery; GetSkyboxSource names what was loaded
+    // ("PNG fallback", "Default directory", ... or "solid 0x808080").
+    void SetAssetsDirectory(const std::string& directory);
+    const std::string& GetSkyboxSource() const { return m_SkyboxSource; }
     glm::vec4 GetClearColor() const { return m_ClearColor; }
 
     size_t GetModelCount() const { return m_ModelCount; }
@@ -131,6 +136,7 @@ private:
         std::vector<float> m_BonePalette;  // the palette last uploaded to this viewport's context
     };
 
+    void CreateSkyboxCubemap();
     void UploadMeshFromCache();
     void EnsurePrimitiveMeshesInCache();
     size_t CreatePrimitiveMeshInCache(MeshComponent::PrimitiveType primitiveType);
@@ -160,6 +166,8 @@ private:
     std::vector<uint32_t> m_IndexBuffer;
     uint64_t m_GeometryGeneration = 1, m_TextureGeneration = 1, m_MaterialGeneration = 1;
     Loader::CubemapTextureData m_SkyboxCubemap;
+    std::string m_AssetsDirectory = "Assets";
+    std::string m_SkyboxSource;
     uint64_t m_SkyboxGeneration = 1;
 
     struct TextureSlot {

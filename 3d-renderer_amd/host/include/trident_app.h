@@ -54,6 +54,19 @@ int trident_app_set_clear_color(trident_app* app, const float rgba[4]);
 /* Renderer::SetSkyboxCubemap: faces [6][size][size] RGBA8 sRGB (+X,-X,+Y,-Y,+Z,-Z). */
 int trident_app_set_skybox(trident_app* app, const uint8_t* faces, uint32_t size);
 
+/* Renderer::SetAssetsDirectory: the directory whose Skyboxes/ CreateSkyboxCubemap searches
+ * (Renderer.cpp:3830-3927); re-runs the discovery. *source (nullable, source_cap bytes) names the result. */
+int trident_app_set_assets_dir(trident_app* app, const char* directory, char* source, uint32_t source_cap);
+
+/* The loaders on their own (no app): TextureLoader::Load (flip = 1: stb's flip-on-load for 2D textures)
+ * or one cube face (flip = 0). rgba = NULL queries the size; else capacity must hold width*height*4. */
+int trident_load_image(const char* path, int flip, uint8_t* rgba, uint64_t capacity, uint32_t* width,
+                       uint32_t* height);
+/* DiscoverDefaultSkybox(assets_dir): faces [6][size][size] RGBA8 (+X,-X,+Y,-Y,+Z,-Z); faces = NULL
+ * queries *size; *size = 0 when nothing valid was found. */
+int trident_load_default_skybox(const char* assets_dir, uint8_t* faces, uint64_t capacity, uint32_t* size,
+                                char* source, uint32_t source_cap);
+
 /* Model import as Forge's drop handler (ModelLoader: .obj/.mtl, .gltf, .glb): entities per mesh
  * instance. Up to `capacity` spawned entity ids go to `entities`; *count gets how many were spawned. */
 int trident_app_import_model(trident_app* app, const char* path, uint32_t* entities, uint32_t capacity,

@@ -1,6 +1,7 @@
 // ModelLoader.cpp — OBJ/MTL and glTF 2.0 ingestion + PPM/PAM textures (see ModelLoader.h for the
 // Assimp / stb behaviour restated here and what is not).
 #include "trident/ModelLoader.h"
+#include "trident/ImageDecoder.h"
 
 #include <algorithm>
 #include <cctype>
@@ -702,11 +703,22 @@ ModelData ModelLoader::Load(const std::string& filePath) {
     return {};
 }
 
-TextureData TextureLoader::Load(const std::string& filePath) {
+namespace {
+// One image file -> top-to-bottom RGBA8 rows (PNG or PPM/PAM), unflipped. Width 0 on failure.
+TextureData DecodeImageFile(const std::string& filePath) {
     TextureData t;
     std::string s;
     if (!ReadFile(NormalizePath(filePath), s)) {
         LogError("texture file not found", filePath);
+        return t;
+    }
+    if (IsPng(s)) {
+        std::string err;
+        if (!DecodePng(s, t.Width, t.Height, t.Pixels, err)) {
+            LogError(("PNG decode failed: " + err).c_str(), filePath);
+            return TextureData{};
+        }
+        t.Channels = 4;
         return t;
     }
     size_t i = 0;
@@ -743,8 +755,8 @@ TextureData TextureLoader::Load(const std::string& filePath) {
     t.Height = h;
     t.Channels = 4;
     t.Pixels.resize((size_t)w * h * 4);
-    for (int y = 0; y < h; ++y) {  // stbi_set_flip_vertically_on_load(true)
-        const unsigned char* src = reinterpret_cast<const unsigned char*>(s.data() + i) + (size_t)(h - 1 - y) * w * depth;
+    for (int y = 0; y < h; ++y) {
+        const unsigned char* src = reinterpret_cast<const unsigned char*>(s.data() + i) + (size_t)y * w * depth;
         uint8_t* dst = t.Pixels.data() + (size_t)y * w * 4;
         for (int x = 0; x < w; ++x) {
             dst[4 * x + 0] = src[depth * x + 0];
@@ -754,6 +766,120 @@ TextureData TextureLoader::Load(const std::string& filePath) {
         }
     }
     return t;
+}
+}  // namespace
+
+TextureData TextureLoader::Load(const std::string& filePath) {
+    TextureData t = DecodeImageFile(filePath);
+    if (t.Width > 0) FlipRowsVertically(t.Pixels, t.Width, t.Height);  // stbi_set_flip_vertically_on_load(true)
+    return t;
+}
+
+CubemapTextureData SkyboxTextureLoader::LoadFromFaces(const std::array<std::string, 6>& faces) {
+    static const char* names[6] = {"+X", "-X", "+Y", "-Y", "+Z", "-Z"};
+    CubemapTextureData out;
+    for (int f = 0; f < 6; ++f) {
+        if (faces[f].empty()) {
+            LogError("cubemap face has an empty path", names[f]);
+            return {};
+        }
+        const std::string ext = Lower(fs::path(faces[f]).extension().string());
+        if (ext == ".exr") {
+            LogError("EXR cubemap faces need tinyexr (not linked)", faces[f]);
+            return {};
+        }
+        const TextureData t = DecodeImageFile(faces[f]);  // stbi_set_flip_vertically_on_load(false)
+        if (t.Width <= 0) return {};
+        if (f == 0) {
+            out.m_Width = (uint32_t)t.Width;
+            out.m_Height = (uint32_t)t.Height;
+        } else if ((uint32_t)t.Width != out.m_Width || (uint32_t)t.Height != out.m_Height) {
+            LogError("cubemap faces must share the same resolution", faces[f]);
+            return {};
+        }
+        out.m_PixelData.insert(out.m_PixelData.end(), t.Pixels.begin(), t.Pixels.end());
+    }
+    out.m_MipCount = 1;
+    return out;
+}
+
+namespace {
+const char* const kFaceTokens[6][2] = {{"posx", "px"}, {"negx", "nx"}, {"posy", "py"},
+                                       {"negy", "ny"}, {"posz", "pz"}, {"negz", "nz"}};
+
+std::vector<fs::path> SortedFiles(const fs::path& dir) {
+    std::vector<fs::path> files;
+    std::error_code ec;
+    for (const auto& e : fs::directory_iterator(dir, ec))
+        if (e.is_regular_file()) files.push_back(e.path());
+    std::sort(files.begin(), files.end());
+    return files;
+}
+}  // namespace
+
+CubemapTextureData SkyboxTextureLoader::LoadFromDirectory(const std::string& dir) {
+    std::error_code ec;
+    if (!fs::is_directory(dir, ec)) {
+        LogError("cubemap directory is invalid", dir);
+        return {};
+    }
+    std::array<std::vector<std::string>, 6> candidates;
+    for (const fs::path& p : SortedFiles(dir)) {
+        const std::string stem = Lower(p.stem().string());
+        for (int f = 0; f < 6; ++f) {  // TryMatchFaceIndex: the first face whose token matches
+            if (stem.find(kFaceTokens[f][0]) != std::string::npos || stem.find(kFaceTokens[f][1]) != std::string::npos) {
+                candidates[f].push_back(p.string());
+                break;
+            }
+        }
+    }
+    std::array<std::string, 6> faces;
+    for (int f = 0; f < 6; ++f) {
+        if (candidates[f].empty()) {
+            LogError("missing cubemap face in directory", dir);
+            return {};
+        }
+        faces[f] = candidates[f].front();  // no EXR candidates are usable here, so the first match
+    }
+    return LoadFromFaces(faces);
+}
+
+CubemapTextureData DiscoverDefaultSkybox(const std::string& assetsDir, std::string& source) {
+    source.clear();
+    const fs::path root = fs::path(assetsDir) / "Skyboxes";
+    std::error_code ec;
+    if (fs::exists(root / "DefaultSkybox.ktx", ec)) {  // Renderer.cpp:3831-3837
+        LogError("KTX cubemaps are not restated; DefaultSkybox.ktx loads as invalid", (root / "DefaultSkybox.ktx").string());
+        source = "DefaultSkybox.ktx";
+        return {};
+    }
+    if (fs::exists(root / "Default", ec)) {  // :3840-3845
+        source = "Default directory";
+        return SkyboxTextureLoader::LoadFromDirectory((root / "Default").string());
+    }
+    if (!fs::is_directory(root, ec)) return {};
+    std::array<std::string, 6> faces;  // :3848-3915: loose faces, short or long tokens
+    std::array<bool, 6> found{};
+    for (const fs::path& p : SortedFiles(root)) {
+        const std::string stem = Lower(p.stem().string());
+        for (int f = 0; f < 6; ++f) {
+            if (found[f]) continue;
+            for (const char* tok : kFaceTokens[f]) {
+                if (stem.find(tok) != std::string::npos) {
+                    faces[f] = p.string();
+                    found[f] = true;
+                    break;
+                }
+            }
+        }
+    }
+    if (!std::all_of(found.begin(), found.end(), [](bool b) { return b; })) {
+        LogError("PNG fallback skybox faces are incomplete", root.string());
+        return {};
+    }
+    CubemapTextureData d = SkyboxTextureLoader::LoadFromFaces(faces);
+    if (d.IsValid()) source = "PNG fallback";
+    return d;
 }
 
 // glm::decompose (gtx/matrix_decompose.inl) without perspective / skew use, then

@@ -152,11 +152,7 @@ void Renderer::Init() {
     m_TextureSlots.push_back(white);
     m_TextureSlotLookup.emplace(kDefaultTextureKey, 0u);
     m_PerformanceHistory.assign(s_PerformanceHistorySize, FrameTimingSample{});
-    // CreateDefaultSkybox (Renderer.cpp:3806-3816). The reference first searches Assets/Skyboxes for
-    // KTX / PNG faces; no image decoder is linked here, so the shim starts from the reference's
-    // fallback and callers hand decoded faces to SetSkyboxCubemap.
-    m_SkyboxCubemap = Loader::CubemapTextureData::CreateSolidColor(0x808080u);
-    ++m_SkyboxGeneration;
+    CreateSkyboxCubemap();  // CreateDefaultSkybox (Renderer.cpp:3806-3816)
     m_Initialised = true;
     m_Shutdown = false;
 }
@@ -171,12 +167,32 @@ void Renderer::Shutdown() {
     m_Initialised = false;
 }
 
+// Renderer.cpp:3818-3927: the discovered cubemap (KTX, Default/ directory, loose px/nx/... PNG faces),
+// else the solid 0x808080 fallback.
+void Renderer::CreateSkyboxCubemap() {
+    std::string source;
+    Loader::CubemapTextureData data = Loader::DiscoverDefaultSkybox(m_AssetsDirectory, source);
+    if (!data.IsValid()) {
+        data = Loader::CubemapTextureData::CreateSolidColor(0x808080u);
+        source = "solid 0x808080";
+    }
+    m_SkyboxCubemap = std::move(data);
+    m_SkyboxSource = source;
+    ++m_SkyboxGeneration;
+}
+
+void Renderer::SetAssetsDirectory(const std::string& directory) {
+    m_AssetsDirectory = directory;
+    if (m_Initialised) CreateSkyboxCubemap();
+}
+
 bool Renderer::SetSkyboxCubemap(const Loader::CubemapTextureData& cubemap) {
     if (!cubemap.IsValid()) {
         LogError("SetSkyboxCubemap", "cubemap needs 6 square RGBA8 faces");
         return false;
     }
     m_SkyboxCubemap = cubemap;
+    m_SkyboxSource = "SetSkyboxCubemap";
     ++m_SkyboxGeneration;
     return true;
 }

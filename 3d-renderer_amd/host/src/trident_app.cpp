@@ -10,6 +10,10 @@
 
 #include "trident/Renderer.h"
 #include "trident/SceneFile.h"
+#include "trident/ModelLoader.h"
+
+#include <algorithm>
+#include <array>
 
 using namespace Trident;
 
@@ -145,6 +149,69 @@ int trident_app_set_entity_visible(trident_app* app, uint32_t entity, int visibl
         app->registry.GetComponent<MeshComponent>(entity).m_Visible = visible != 0;
         return TRI_OK;
     });
+}
+
+namespace {
+void CopySource(const std::string& src, char* out, uint32_t cap) {
+    if (!out || cap == 0) return;
+    const size_t n = std::min<size_t>(src.size(), cap - 1);
+    std::memcpy(out, src.data(), n);
+    out[n] = 0;
+}
+}  // namespace
+
+int trident_app_set_assets_dir(trident_app* app, const char* directory, char* source, uint32_t source_cap) {
+    return Guard(app, [&] {
+        if (!directory) return TRI_E_INVALID;
+        app->renderer.SetAssetsDirectory(directory);
+        CopySource(app->renderer.GetSkyboxSource(), source, source_cap);
+        return TRI_OK;
+    });
+}
+
+int trident_load_image(const char* path, int flip, uint8_t* rgba, uint64_t capacity, uint32_t* width, uint32_t* height) {
+    if (!path || !width || !height) return TRI_E_INVALID;
+    try {
+        Loader::TextureData t;
+        if (flip) {
+            t = Loader::TextureLoader::Load(path);
+        } else {
+            std::array<std::string, 6> one;
+            one.fill(path);
+            const Loader::CubemapTextureData c = Loader::SkyboxTextureLoader::LoadFromFaces(one);
+            if (c.m_Width) {
+                t.Width = (int)c.m_Width;
+                t.Height = (int)c.m_Height;
+                t.Pixels.assign(c.m_PixelData.begin(), c.m_PixelData.begin() + (size_t)c.m_Width * c.m_Height * 4);
+            }
+        }
+        if (t.Width <= 0) return TRI_E_INVALID;
+        *width = (uint32_t)t.Width;
+        *height = (uint32_t)t.Height;
+        if (!rgba) return TRI_OK;
+        if (capacity < t.Pixels.size()) return TRI_E_OVERFLOW;
+        std::memcpy(rgba, t.Pixels.data(), t.Pixels.size());
+        return TRI_OK;
+    } catch (...) {
+        return TRI_E_INVALID;
+    }
+}
+
+int trident_load_default_skybox(const char* assets_dir, uint8_t* faces, uint64_t capacity, uint32_t* size, char* source,
+                                uint32_t source_cap) {
+    if (!assets_dir || !size) return TRI_E_INVALID;
+    try {
+        std::string src;
+        const Loader::CubemapTextureData c = Loader::DiscoverDefaultSkybox(assets_dir, src);
+        CopySource(src, source, source_cap);
+        *size = c.IsValid() ? c.m_Width : 0;
+        if (!faces || !c.IsValid()) return TRI_OK;
+        if (capacity < c.m_PixelData.size()) return TRI_E_OVERFLOW;
+        std::memcpy(faces, c.m_PixelData.data(), c.m_PixelData.size());
+        return TRI_OK;
+    } catch (...) {
+        return TRI_E_INVALID;
+    }
 }
 
 int trident_app_set_entity_bones(trident_app* app, uint32_t entity, const float* matrices, uint32_t count) {

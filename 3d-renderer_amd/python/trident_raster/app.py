@@ -29,6 +29,11 @@ _APP_FUNCTIONS = [
     ("trident_app_set_entity_transform", C.c_int, [C.c_void_p, C.c_uint32, _f3, _f3, _f3]),
     ("trident_app_set_entity_visible", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
     ("trident_app_set_entity_bones", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
+    ("trident_app_set_assets_dir", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint32]),
+    ("trident_load_image", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
+                                     C.POINTER(C.c_uint32)]),
+    ("trident_load_default_skybox", C.c_int, [C.c_char_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_char_p,
+                                              C.c_uint32]),
     ("trident_app_add_light", C.c_int, [C.c_void_p, C.c_int, _f3, _f3, _f3, C.c_float, C.c_float, C.c_int,
                                         C.POINTER(C.c_uint32)]),
     ("trident_app_set_camera", C.c_int, [C.c_void_p, C.c_int, _f3, _f3, C.c_float, C.c_float, C.c_float, C.c_int]),
@@ -131,6 +136,12 @@ class TridentApp:
 
     def set_entity_visible(self, entity, visible):
         _check(self._lib.trident_app_set_entity_visible(self._h, entity, 1 if visible else 0), "set_entity_visible")
+
+    def set_assets_dir(self, directory):
+        """Renderer::SetAssetsDirectory (skybox discovery under directory/Skyboxes); returns the source."""
+        buf = C.create_string_buffer(64)
+        _check(self._lib.trident_app_set_assets_dir(self._h, os.fsencode(directory), buf, 64), "set_assets_dir")
+        return buf.value.decode()
 
     def set_entity_bones(self, entity, matrices):
         """AnimationComponent::m_BoneMatrices: float32 [n, 4, 4] column-major mat4s (m[col][row])."""
@@ -246,3 +257,28 @@ class TridentApp:
         _check(self._lib.trident_app_read_present(self._h, out.ctypes.data, width, height), "read_present")
         return out
 
+
+
+def load_image(path, flip=True):
+    """TextureLoader::Load (flip=True, 2D textures) or one cube face (flip=False): uint8 [h, w, 4] RGBA."""
+    lib = load_library()
+    w, h = C.c_uint32(), C.c_uint32()
+    _check(lib.trident_load_image(os.fsencode(path), 1 if flip else 0, None, 0, C.byref(w), C.byref(h)), "load_image")
+    out = np.empty((h.value, w.value, 4), np.uint8)
+    _check(lib.trident_load_image(os.fsencode(path), 1 if flip else 0, out.ctypes.data, out.nbytes, C.byref(w),
+                                  C.byref(h)), "load_image")
+    return out
+
+
+def load_default_skybox(assets_dir):
+    """DiscoverDefaultSkybox (Renderer.cpp:3830-3927): (faces uint8 [6, n, n, 4] or None, source)."""
+    lib = load_library()
+    n = C.c_uint32()
+    src = C.create_string_buffer(64)
+    _check(lib.trident_load_default_skybox(os.fsencode(assets_dir), None, 0, C.byref(n), src, 64), "load_default_skybox")
+    if n.value == 0:
+        return None, src.value.decode()
+    faces = np.empty((6, n.value, n.value, 4), np.uint8)
+    _check(lib.trident_load_default_skybox(os.fsencode(assets_dir), faces.ctypes.data, faces.nbytes, C.byref(n), src, 64),
+           "load_default_skybox")
+    return faces, src.value.decode()

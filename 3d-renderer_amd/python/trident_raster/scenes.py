@@ -7,6 +7,7 @@ C2 = the reference UV-sphere builder at rings 125 x segments 200 (50,000 tris), 
 displaced 708 x 708 grid (999,698 tris). Everything is float32 numpy; glm operation order is kept for
 the matrices.
 """
+import os
 from dataclasses import dataclass, field
 
 import numpy as np
@@ -317,10 +318,27 @@ class Scene:
         return 12 * self.triangles + 44 * V + 8 * self.width * rows + tex + shadow
 
 
-# CreateDefaultSkybox's fallback (Renderer.cpp:3925-3926): CreateSolidColor(0x808080) — bytes 80 80 80 00
-# on every face. The reference always records the skybox pass before the meshes, so the synthetic
-# workloads carry it too (Forge's PNG faces are assets of the reference, not available on the GPU box).
+# CreateDefaultSkybox's last resort (Renderer.cpp:3925-3926): CreateSolidColor(0x808080) — bytes
+# 80 80 80 00 on every face.
 DEFAULT_SKYBOX = np.tile(np.array([0x80, 0x80, 0x80, 0x00], np.uint8), (6, 1, 1, 1))
+
+# The cubemap a default Forge frame shows: the reference's Assets/Skyboxes PNG faces (committed as data
+# under assets/), found and decoded by the shim's CreateSkyboxCubemap discovery (Renderer.cpp:3840-3915).
+ASSETS_DIR = os.path.normpath(os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "..", "..", "assets"))
+_REFERENCE_SKYBOX = None
+
+
+def reference_skybox():
+    """uint8 [6, 512, 512, 4]: the reference's default skybox, as the shim's discovery loads it."""
+    global _REFERENCE_SKYBOX
+    if _REFERENCE_SKYBOX is None:
+        from . import app
+
+        faces, source = app.load_default_skybox(ASSETS_DIR)
+        if faces is None or source != "PNG fallback":
+            raise FileNotFoundError(f"reference skybox faces not found under {ASSETS_DIR}/Skyboxes ({source!r})")
+        _REFERENCE_SKYBOX = faces
+    return _REFERENCE_SKYBOX
 
 
 def _single_mesh_ranges(nidx, material=0):
@@ -329,7 +347,7 @@ def _single_mesh_ranges(nidx, material=0):
     return m
 
 
-def scene_c1_cube(frame=0, width=640, height=480):
+def scene_c1_cube(frame=0, width=640, height=480, skybox=None):
     """C1: Forge's default editor camera (0,3,8) and a cube primitive spawned 10 units ahead
     (ApplicationLayer.cpp:185-193, :677-718) spinning 30 deg/frame about Y; no lights -> fallback sun."""
     cam = (0.0, 3.0, 8.0)
@@ -338,10 +356,20 @@ def scene_c1_cube(frame=0, width=640, height=480):
     model = compose_transform((0.0, 3.0, -2.0), (0.0, 30.0 * frame, 0.0), (1, 1, 1))
     return Scene("c1_cube_640x480", width, height, v, idx, _single_mesh_ranges(idx.size),
                  [abi.make_draw(0, model, texture_slot=0, material_index=0)], pack_ubo(view, proj, cam),
-                 materials=[((1, 1, 1, 1), (0.0, 1.0, 1.0, 0.0))], skybox=DEFAULT_SKYBOX)
+                 materials=[((1, 1, 1, 1), (0.0, 1.0, 1.0, 0.0))], skybox=_sky(skybox))
 
 
-def scene_c2_sphere(width=1920, height=1080, rings=125, segments=200):
+def _sky(skybox):
+    """Scene skybox argument: None = the reference's default (its PNG faces), "solid" = the 0x808080
+    fallback, or explicit faces."""
+    if skybox is None:
+        return reference_skybox()
+    if isinstance(skybox, str) and skybox == "solid":
+        return DEFAULT_SKYBOX
+    return skybox
+
+
+def scene_c2_sphere(width=1920, height=1080, rings=125, segments=200, skybox=None):
     """C2 substitute (Assimp sample scene not in the snapshot): 50k-tri UV sphere, radius 3, 2 point lights."""
     rng = PCG32(0x5EED)
     cam = (0.0, 0.0, 9.0)
@@ -355,10 +383,10 @@ def scene_c2_sphere(width=1920, height=1080, rings=125, segments=200):
     ]
     return Scene(f"c2_sphere50k_{width}x{height}", width, height, v, idx, _single_mesh_ranges(idx.size),
                  [abi.make_draw(0, np.eye(4, dtype=F), material_index=0)], pack_ubo(view, proj, cam, lights),
-                 materials=[((0.9, 0.75, 0.6, 1.0), (0.3, 0.45, 1.0, 0.0))], skybox=DEFAULT_SKYBOX)
+                 materials=[((0.9, 0.75, 0.6, 1.0), (0.3, 0.45, 1.0, 0.0))], skybox=_sky(skybox))
 
 
-def scene_c3_grid(width=3840, height=2160, n=708):
+def scene_c3_grid(width=3840, height=2160, n=708, skybox=None):
     """C3: 1M-triangle displaced grid at 4K, directional sun + 4 point lights, uv x4 (REPEAT)."""
     cam = (0.0, 0.0, 0.0)
     view, proj = editor_camera(cam, (0, 0, 0), 60.0, (width, height), 0.1, 1000.0)
@@ -371,7 +399,7 @@ def scene_c3_grid(width=3840, height=2160, n=708):
                        "color": (1.0, 0.9 - 0.1 * k, 0.7 + 0.1 * k)})
     return Scene(f"c3_grid1m_{width}x{height}", width, height, v, idx, _single_mesh_ranges(idx.size),
                  [abi.make_draw(0, np.eye(4, dtype=F), material_index=0)], pack_ubo(view, proj, cam, lights),
-                 materials=[((1.0, 1.0, 1.0, 1.0), (0.1, 0.6, 1.0, 0.0))], skybox=DEFAULT_SKYBOX)
+                 materials=[((1.0, 1.0, 1.0, 1.0), (0.1, 0.6, 1.0, 0.0))], skybox=_sky(skybox))
 
 
 def procedural_texture(size, seed):
@@ -414,12 +442,12 @@ def with_shadow(scene, size=2048, depth_bias=0.001, slope_bias=2.0):
     return scene
 
 
-def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048, shadow_size=2048):
+def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048, shadow_size=2048, skybox=None):
     """C5: the C3 grid split into 4 meshes (row quarters), each drawn with its own tex_size^2 sRGB
     texture slot (4 bilinear textures, uv x4 REPEAT), plus the shadow_size^2 shadow-map pre-pass for the
     sun (tri_set_shadow; the reference only reserves LightComponent::m_ShadowCaster, so the pass follows
     DESIGN.md §5d). shadow_size 0 leaves the pre-pass off."""
-    s = scene_c3_grid(width, height, n)
+    s = scene_c3_grid(width, height, n, skybox)
     tris = s.indices.size // 3
     q = [(k * tris) // 4 for k in range(5)]
     meshes = np.zeros(4, abi.MESH_RANGE_DTYPE)

@@ -151,3 +151,50 @@ def test_orthographic_sky_has_uncovered_pixels(oracle):
 @pytest.mark.parametrize("ptype,ortho", [(0, 12.0), (1, 12.0), (1, 30.0)])
 def test_gpu_skybox_runtime_camera(oracle, ptype, ortho):
     assert_sky_parity(skybox_runtime_camera(ptype, ortho=ortho), oracle)
+
+
+# ---- the reference's own cubemap (Trident-Forge/Assets/Skyboxes, "PNG fallback") ---------------------
+@pytest.mark.gpu
+@pytest.mark.parametrize("exact", [False, True])
+def test_gpu_reference_skybox_c1(oracle, exact):
+    """C1 at full size over the cubemap a default Forge frame shows (512^2 PNG faces found by the
+    discovery of Renderer.cpp:3840-3915 and decoded without flip, TextureLoader.cpp:773)."""
+    from trident_raster import abi, scenes
+
+    s = scenes.scene_c1_cube(1, 640, 480)
+    assert s.skybox.shape == (6, 512, 512, 4)
+    assert_sky_parity(s, oracle, flags=abi.TRI_FLAG_EXACT_SHADING if exact else 0)
+
+
+@pytest.mark.gpu
+def test_gpu_reference_skybox_c2(oracle):
+    """C2 at full size (1920x1080, 50k triangles, ~60 % of the pixels are sky)."""
+    s = sc.sphere_c2(oracle=oracle)
+    assert s.skybox.shape == (6, 512, 512, 4)
+    assert_sky_parity(s, oracle)
+
+
+@pytest.mark.gpu
+def test_gpu_shim_renders_reference_skybox(oracle):
+    """The shim's Init-time discovery under assets/ (Renderer::SetAssetsDirectory) feeds the same cubemap."""
+    import os
+
+    from trident_raster import app, scenes
+
+    a = app.TridentApp()
+    assert a.set_assets_dir(scenes.ASSETS_DIR) == "PNG fallback"
+    a.set_camera("editor", (0.0, 3.0, 8.0), (-10.0, 25.0, 0.0))
+    a.set_viewport(1, 320, 240)
+    a.add_mesh_entity("sphere", position=(0.0, 3.0, 4.0))
+    a.draw_frame()
+    a.draw_frame()
+    rgba, depth = a.read_pixels(1, 320, 240)
+    ubo, draws = a.frame_inputs(1)
+    vb, ib, ranges = a.geometry()
+    s = scenes.Scene("shim_sky", 320, 240, vb, ib, ranges, draws, ubo,
+                     materials=[(m[0], m[1]) for m in a.materials()], skybox=scenes.reference_skybox())
+    oc, od, _ = oracle.render(s)
+    assert np.array_equal(depth.view(np.uint32), od)
+    assert int(np.abs(rgba.astype(np.int16) - oc[..., [2, 1, 0, 3]].astype(np.int16)).max()) <= 1
+    assert os.path.isdir(scenes.ASSETS_DIR)
+    a.close()
