@@ -237,16 +237,51 @@ def cpu_baseline(scene, seconds):
                       f"({scene.triangles} tris) rendered by oracle/tri_oracle.cpp, {dt:.1f} s"}
 
 
-def pmc_traffic(workload, rows_frac):
-    """HBM bytes per k_raster launch from the committed rocprofv3 PMC summary (profiles/), if any."""
+def pmc_kernel(workload, kernel):
+    """Per-launch PMC means of one kernel from the committed rocprofv3 summary (profiles/pmc_summary.json,
+    written by tools/prof_summary.py from tools/profile.sh's passes), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
-            d = json.load(f)
-        e = d.get(workload, {}).get("k_raster")
-        return None if e is None else float(e["hbm_bytes_per_launch"]) * rows_frac
-    except (OSError, ValueError, KeyError):
+            return json.load(f).get(workload, {}).get(kernel)
+    except (OSError, ValueError):
         return None
+
+
+# CDNA4 VALU issue: a wave64 vector instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md),
+# 256 CUs x 4 SIMDs, 2.4 GHz peak engine clock.
+VALU_PEAK_WAVE_INSTS = 1024 * 2.4e9 / 2
+
+
+def valu_roofline(pmc, kernel_ms):
+    """The bound that binds k_raster: SQ_INSTS_VALU (wave instructions per launch, PMC) over the live
+    kernel duration, against the chip's wave-instruction issue rate."""
+    if not pmc or "SQ_INSTS_VALU" not in pmc or not kernel_ms:
+        return None
+    insts = float(pmc["SQ_INSTS_VALU"])
+    achieved = insts / (kernel_ms * 1e-3)
+    return {"bound": "valu", "kernel": "k_raster", "valu_wave_insts_per_launch": insts,
+            "achieved": achieved / 1e9, "peak": VALU_PEAK_WAVE_INSTS / 1e9, "unit": "G wave-instructions/s",
+            "frac": achieved / VALU_PEAK_WAVE_INSTS,
+            "source": "profiles/pmc_summary.json SQ_INSTS_VALU / roofline.kernel_ms"}
+
+
+def stage_ms(timing):
+    """Mean per-stage milliseconds of the event pass (zeros when stage timing is off)."""
+    keys = ("ms_vertex", "ms_shadow", "ms_setup", "ms_raster", "ms_frame")
+    if not timing or not timing.get("frames"):
+        return {k: 0.0 for k in keys}
+    n = float(timing["frames"])
+    return {k: timing[k] / n for k in keys}
+
+
+def skybox_name(scene):
+    sky = scene.skybox
+    if sky is None:
+        return "none"
+    if sky.shape[1] == 1:
+        return "solid 0x808080 fallback cubemap (CreateSolidColor)"
+    return f"reference Trident-Forge/Assets/Skyboxes PNG faces ({sky.shape[1]}^2, assets/Skyboxes)"
 
 
 def main():
@@ -289,20 +324,18 @@ def main():
     W, H = scene.width, scene.height
     stats = br.r.frame_stats()
     latency = br.latency_ms()  # one frame end to end (render + gather), no overlap
+    stage = stage_ms(timing)
 
     # roofline of the dominant kernel (k_raster = tile_raster_shade): its algorithmic bytes per
-    # launch are the colour + depth it must store for its band (4 + 4 B per pixel).
-    if timing is None:
-        timing = {"frames": 0, "ms_vertex": 0.0, "ms_setup": 0.0, "ms_shadow": 0.0, "ms_raster": 0.0, "ms_frame": 0.0}
-    frames_timed = max(int(timing["frames"]), 1)
-    raster_ms = timing["ms_raster"] / frames_timed
-    # whole-frame figure on the throughput clock: with two frames in flight the event span of one
-    # frame (first kernel start -> last kernel end) is its latency, not its cost
-    frame_ms = dt / args.steps * 1e3
+    # launch are the colour + depth it must store for its band (4 + 4 B per pixel),
+    # divided by its mean duration from HIP events on the render stream (a separate event pass).
+    raster_ms = stage["ms_raster"]
+    frame_ms = dt / args.steps * 1e3  # whole-frame figure on the throughput clock
     raster_bytes = 8.0 * W * br.rows
     achieved = raster_bytes / (raster_ms * 1e-3) / 1e9 if raster_ms > 0 else None
     frame_bytes = scene.algorithmic_bytes(rows=br.rows)
-    traffic = pmc_traffic(scene.name, br.rows / H)
+    pmc = pmc_kernel(scene.name, "k_raster")
+    traffic = None if pmc is None or "hbm_bytes_per_launch" not in pmc else pmc["hbm_bytes_per_launch"] * br.rows / H
 
     secondary = {}
     if not args.no_secondary and args.config == "c3":
@@ -312,14 +345,14 @@ def main():
             n2 = max(args.steps, 50) if key == "c2" else max(args.steps // 2, 20)
             dt2, t2 = timed_run(br2, n2, args.warmup, dist_on)
             fps2 = n2 / dt2
-            frames2 = max(t2["frames"], 1)
-            r_ms = t2["ms_raster"] / frames2
+            st2 = stage_ms(t2)
             entry = {"frames_per_s": fps2, "mpix_per_s": fps2 * s2.width * s2.height / 1e6, "ms_per_frame": 1e3 / fps2,
-                     "raster_kernel_ms": r_ms, "triangles": s2.triangles,
+                     "stage_ms": st2, "kernel_samples": int(t2["frames"]) if t2 else 0, "triangles": s2.triangles,
                      "algorithmic_bytes": s2.algorithmic_bytes(rows=br2.rows)}
-            if key == "c5":
-                entry["note"] = ("4 draws x 2048^2 sRGB textures (bilinear, REPEAT); BASELINE C5's shadow pre-pass "
-                                 "has no counterpart in the reference and is not rendered")
+            if s2.shadow is not None:
+                entry["shadow_map"] = f"{s2.shadow.size}^2 D32 pre-pass for the sun (tri_set_shadow, DESIGN.md 5d)"
+            if s2.textures:
+                entry["textures"] = f"{len(s2.textures)} x {s2.textures[0][1].shape[0]}^2 sRGB, bilinear REPEAT"
             secondary[s2.name] = entry
             br2.r.close()
             del br2
@@ -344,20 +377,20 @@ def main():
             "data": "synthetic (procedural PCG32-seeded scene; reference Assimp assets absent)",
             "config": {"workload": scene.name, "width": W, "height": H, "triangles": scene.triangles,
                        "vertices": int(scene.vertices.shape[0]), "bin": stats["bin_size"],
-                       "skybox": "solid 0x808080 fallback cubemap" if scene.skybox is not None else "none",
+                       "skybox": skybox_name(scene),
                        "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "single GPU"},
             "mpix_per_s": fps * W * H / 1e6,
             "latency_ms": latency,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "kernel": "k_raster",
-                         "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]),
+                         "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]) if timing else 0,
                          "algorithmic_bytes": raster_bytes},
+            "roofline_valu": valu_roofline(pmc, raster_ms),
             "frame_roofline": {"algorithmic_bytes": frame_bytes, "ms_per_frame": frame_ms,
                                "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9 if frame_ms > 0 else None,
                                "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if frame_ms > 0 else None},
-            "stage_ms": {k: timing[k] / frames_timed for k in
-                         ("ms_vertex", "ms_setup", "ms_shadow", "ms_raster", "ms_frame")},
+            "stage_ms": stage,
             "frame_stats": stats,
             "secondary": secondary,
             "cpu_baseline": cpu,

@@ -13,11 +13,15 @@ from collections import defaultdict
 
 
 def short(name):
-    """Kernel name without namespace / parameter list: k_raster<false, 5> -> k_raster (the fast
-    build, the one the bench runs), k_raster<true, 5> -> k_raster_exact."""
+    """Kernel name without namespace / parameter list: k_raster<false, 5, *> -> k_raster (the fast
+    build, the one the bench runs), k_raster<true, 5, *> -> k_raster_exact; k_setup<true, *> (the
+    shadow pre-pass set-up) -> k_setup_shadow, k_setup<false, *> -> k_setup."""
     m = re.search(r"(k_[a-z_]+)(<([a-z]+)[^>]*>)?\(", name)
     if m:
-        return m.group(1) + ("_exact" if m.group(3) == "true" else "")
+        first = m.group(3) == "true"
+        if m.group(1) == "k_setup":
+            return "k_setup_shadow" if first else "k_setup"
+        return m.group(1) + ("_exact" if first else "")
     for k in ("copyBuffer", "fillBuffer"):
         if k in name:
             return k

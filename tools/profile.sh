@@ -2,7 +2,7 @@
 # rocprofv3 kernel trace + separate PMC passes over a short bench run (GPU box).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof
+OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
 ARGS="${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline --no-secondary}"
 run() {  # name, rocprofv3 options...
