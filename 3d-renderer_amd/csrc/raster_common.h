@@ -102,7 +102,23 @@ struct __attribute__((aligned(16))) TriDrawDev {
     int32_t base_vertex;
     uint32_t min_index;
     uint32_t vert_count; // VS invocations for this draw (max-min+1), 0 = inactive
-    uint32_t pad[3];
+    uint32_t cl_first;   // the mesh's first cluster (TriCluster) and first vertex-block interval
+    uint32_t vblk_first;
+    uint32_t ncl;        // the mesh's cluster count (0 for an inactive draw)
+};
+
+// Cluster culling (row bands): a mesh's primitives in runs of TRI_CLUSTER_PRIMS, each with the object-
+// space box of the vertices it references and their mesh-local index range, computed once at upload.
+// Per frame k_cull marks the (draw, cluster) pairs whose projected box can reach the context's rows;
+// k_setup skips primitives of unmarked clusters before their index fetch, and k_vertex skips each 256-
+// slot vertex block none of whose referencing clusters is marked (TriVertexBlock interval).
+#define TRI_CLUSTER_PRIMS 512
+#define TRI_VBLOCK 256
+struct __attribute__((aligned(16))) TriCluster {
+    float lo[3];
+    uint32_t vmin;  // mesh-local index range of every referenced vertex (valid or not)
+    float hi[3];    // box of the valid referenced vertices; lo > hi: none is valid
+    uint32_t vmax;
 };
 
 struct __attribute__((aligned(16))) TriTexDesc {
@@ -180,6 +196,9 @@ struct TriFrameParams {
     tri_material_record mat0;
     TriShadeConst sc;
     TriDrawDev draw0;  // the draw when one_draw (its vertex and primitive slots start at 0)
+    // cluster culling (row bands): k_cull over ncl_total (draw, cluster) pairs; cull_vertex also lets
+    // k_vertex skip vertex blocks (off while the shadow pre-pass needs every caster)
+    uint32_t cull_on, cull_vertex, ncl_total, pad_c;
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
     uint32_t shadow_on, s_size, s_nbx, s_nbins;
     uint32_t s_bin_cap;

@@ -29,6 +29,11 @@ struct TriDeviceBuffers {
     uint2* setup_stats;          // nchunks {triangles set up, bin entries} per k_setup workgroup
     uint32_t* color;             // band rows * W
     float* depth;                // band rows * W (may be null)
+    // cluster culling (only when TriFrameParams::cull_on)
+    const TriCluster* clusters;  // all meshes' clusters
+    const uint2* vblk;           // per mesh vertex block: [first, last] referencing cluster (mesh-local)
+    const uint32_t* draw_cbase;  // ndraws+1: first (draw, cluster) pair of each draw
+    uint32_t* cvis;              // ncl_total visibility flags, written by k_cull each frame
     // shadow-map pre-pass (only when TriFrameParams::shadow_on)
     float4* lpos;                // nslots + ovf_vert_cap: light-NDC position per vertex slot (xyz, 0)
     TriSnap* lsnap;              // nslots: the light-NDC position snapped to the map ({X | outcode << 24, Y, z, 1})

@@ -81,6 +81,9 @@ struct tri_ctx {
     uint64_t nidx = 0;
     std::vector<tri_mesh_range> meshes;
     std::vector<uint32_t> mesh_min, mesh_max;
+    std::vector<uint32_t> mesh_cl_first, mesh_ncl, mesh_vblk_first;  // cluster culling tables per mesh
+    TriCluster* d_clusters = nullptr; size_t cap_clusters = 0;
+    uint2* d_vblk = nullptr; size_t cap_vblk = 0;
     bool geometry_set = false;
 
     tri_material_record mat0{{1, 1, 1, 1}, {1, 1, 1, 0}};
@@ -113,6 +116,9 @@ struct tri_ctx {
     TriDrawShade* d_draw_shade = nullptr; size_t cap_draw_shade = 0;
     uint32_t* d_vbase = nullptr; size_t cap_vbase = 0;
     uint32_t* d_pbase = nullptr; size_t cap_pbase = 0;
+    uint32_t* d_cbase = nullptr; size_t cap_cbase = 0;
+    uint32_t* d_cvis = nullptr; size_t cap_cvis = 0;
+    uint32_t ncl_total = 0;
     void* h_stage = nullptr; size_t cap_stage = 0;  // pinned upload staging
     hipEvent_t stage_free = nullptr;
     uint32_t ndraws = 0, nslots = 0, nprims = 0;
@@ -338,8 +344,8 @@ int resolve_draws(tri_ctx* c) {
     const uint32_t n = (uint32_t)c->draws.size();
     std::vector<TriDrawDev> dd(n);
     std::vector<TriDrawShade> ds(n);
-    std::vector<uint32_t> vb(n + 1), pb(n + 1);
-    uint64_t vslots = 0, prims = 0;
+    std::vector<uint32_t> vb(n + 1), pb(n + 1), cbase(n + 1);
+    uint64_t vslots = 0, prims = 0, ncl = 0;
     bool skin = false;
     for (uint32_t d = 0; d < n; ++d) {
         const tri_draw& src = c->draws[d];
@@ -361,6 +367,7 @@ int resolve_draws(tri_ctx* c) {
         o.bone_count = src.pc.bone_count;
         vb[d] = (uint32_t)vslots;
         pb[d] = (uint32_t)prims;
+        cbase[d] = (uint32_t)ncl;
         if (src.mesh_index >= c->meshes.size()) continue;  // Renderer.cpp:5118-5127 skip
         const tri_mesh_range& mr = c->meshes[src.mesh_index];
         if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > c->nidx) continue;
@@ -368,12 +375,17 @@ int resolve_draws(tri_ctx* c) {
         o.base_vertex = mr.base_vertex;
         o.min_index = c->mesh_min[src.mesh_index];
         o.vert_count = c->mesh_max[src.mesh_index] - o.min_index + 1;
+        o.cl_first = c->mesh_cl_first[src.mesh_index];
+        o.vblk_first = c->mesh_vblk_first[src.mesh_index];
+        o.ncl = c->mesh_ncl[src.mesh_index];
         vslots += o.vert_count;
         prims += mr.index_count / 3;
+        ncl += o.ncl;
         skin = skin || (o.bone_count > 0);
     }
     vb[n] = (uint32_t)vslots;
     pb[n] = (uint32_t)prims;
+    cbase[n] = (uint32_t)ncl;
     if (vslots > 0xFFFFFFF0ull) return fail(TRI_E_INVALID, "too many vertex-shader invocations (%llu)", (unsigned long long)vslots);
     if (prims > TRI_PRIM_MAX) return fail(TRI_E_INVALID, "too many primitives (%llu > %u)", (unsigned long long)prims, TRI_PRIM_MAX);
     int rc;
@@ -381,10 +393,13 @@ int resolve_draws(tri_ctx* c) {
     if ((rc = grow(c->d_draw_shade, c->cap_draw_shade, std::max<size_t>(n, 1)))) return rc;
     if ((rc = grow(c->d_vbase, c->cap_vbase, n + 1))) return rc;
     if ((rc = grow(c->d_pbase, c->cap_pbase, n + 1))) return rc;
+    if ((rc = grow(c->d_cbase, c->cap_cbase, n + 1))) return rc;
+    if ((rc = grow(c->d_cvis, c->cap_cvis, std::max<size_t>(ncl, 1)))) return rc;
     const size_t o_shade = n * sizeof(TriDrawDev);
     const size_t o_vb = o_shade + n * sizeof(TriDrawShade);
     const size_t o_pb = o_vb + (n + 1) * 4;
-    const size_t bytes = o_pb + (n + 1) * 4;
+    const size_t o_cb = o_pb + (n + 1) * 4;
+    const size_t bytes = o_cb + (n + 1) * 4;
     if (c->stage_free) HIP_TRY(hipEventSynchronize(c->stage_free));
     if (bytes > c->cap_stage) {
         if (c->h_stage) HIP_TRY(hipHostFree(c->h_stage));
@@ -397,6 +412,7 @@ int resolve_draws(tri_ctx* c) {
     std::memcpy(st + o_shade, ds.data(), n * sizeof(TriDrawShade));
     std::memcpy(st + o_vb, vb.data(), (n + 1) * 4);
     std::memcpy(st + o_pb, pb.data(), (n + 1) * 4);
+    std::memcpy(st + o_cb, cbase.data(), (n + 1) * 4);
     if (n) {
         HIP_TRY(hipMemcpyAsync(c->d_draws, st, n * sizeof(TriDrawDev), hipMemcpyHostToDevice, c->stream));
         HIP_TRY(hipMemcpyAsync(c->d_draw_shade, st + o_shade, n * sizeof(TriDrawShade), hipMemcpyHostToDevice,
@@ -404,12 +420,14 @@ int resolve_draws(tri_ctx* c) {
     }
     HIP_TRY(hipMemcpyAsync(c->d_vbase, st + o_vb, (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
     HIP_TRY(hipMemcpyAsync(c->d_pbase, st + o_pb, (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->d_cbase, st + o_cb, (n + 1) * 4, hipMemcpyHostToDevice, c->stream));
     if (!c->stage_free) HIP_TRY(hipEventCreateWithFlags(&c->stage_free, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(c->stage_free, c->stream));
     c->ndraws = n;
     if (n == 1) c->draw0 = dd[0];
     c->nslots = (uint32_t)vslots;
     c->nprims = (uint32_t)prims;
+    c->ncl_total = (uint32_t)ncl;
     c->any_skin = skin;
     c->draws_dirty = false;
     return TRI_OK;
@@ -631,7 +649,8 @@ int tri_destroy(tri_ctx* c) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_lut); f(c->d_bones); f(c->d_sky);
     for (auto& t : c->d_tex) f(t);
-    f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase);
+    f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase); f(c->d_cbase); f(c->d_cvis);
+    f(c->d_clusters); f(c->d_vblk);
     f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own); f(c->d_present);
@@ -708,6 +727,54 @@ int tri_upload_geometry(tri_ctx* c, const tri_vertex* v, uint64_t nv, const uint
         c->mesh_min[m] = mn;
         c->mesh_max[m] = mx;
     }
+    // cluster tables (row-band culling): runs of TRI_CLUSTER_PRIMS primitives with their object-space
+    // boxes and index ranges; per 256-slot vertex block the interval of clusters whose range meets it
+    std::vector<TriCluster> cl;
+    std::vector<uint2> vblk;
+    c->mesh_cl_first.assign(nm, 0);
+    c->mesh_ncl.assign(nm, 0);
+    c->mesh_vblk_first.assign(nm, 0);
+    for (uint32_t m = 0; m < nm; ++m) {
+        const tri_mesh_range& mr = meshes[m];
+        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > ni) continue;
+        const uint32_t ntri = mr.index_count / 3;
+        const uint32_t ncl = (ntri + TRI_CLUSTER_PRIMS - 1) / TRI_CLUSTER_PRIMS;
+        const uint32_t mn = c->mesh_min[m];
+        const uint32_t nblk = (c->mesh_max[m] - mn) / TRI_VBLOCK + 1;
+        c->mesh_cl_first[m] = (uint32_t)cl.size();
+        c->mesh_ncl[m] = ncl;
+        c->mesh_vblk_first[m] = (uint32_t)vblk.size();
+        vblk.resize(vblk.size() + nblk, make_uint2(0xFFFFFFFFu, 0u));
+        uint2* iv = vblk.data() + c->mesh_vblk_first[m];
+        for (uint32_t k = 0; k < ncl; ++k) {
+            TriCluster t;
+            for (int a = 0; a < 3; ++a) { t.lo[a] = INFINITY; t.hi[a] = -INFINITY; }
+            t.vmin = 0xFFFFFFFFu;
+            t.vmax = 0;
+            const uint32_t i0 = mr.first_index + 3 * k * TRI_CLUSTER_PRIMS;
+            const uint32_t i1 = mr.first_index + 3 * std::min(ntri, (k + 1) * TRI_CLUSTER_PRIMS);
+            for (uint32_t i = i0; i < i1; ++i) {
+                const uint32_t x = idx[i];
+                t.vmin = std::min(t.vmin, x);
+                t.vmax = std::max(t.vmax, x);
+                const int64_t gi = (int64_t)mr.base_vertex + x;
+                if (gi < 0 || (uint64_t)gi >= nv) continue;
+                for (int a = 0; a < 3; ++a) {
+                    t.lo[a] = std::fmin(t.lo[a], v[gi].position[a]);
+                    t.hi[a] = std::fmax(t.hi[a], v[gi].position[a]);
+                }
+            }
+            for (uint32_t bk = (t.vmin - mn) / TRI_VBLOCK; bk <= (t.vmax - mn) / TRI_VBLOCK; ++bk) {
+                iv[bk].x = std::min(iv[bk].x, k);
+                iv[bk].y = std::max(iv[bk].y, k);
+            }
+            cl.push_back(t);
+        }
+    }
+    if ((rc = grow(c->d_clusters, c->cap_clusters, std::max<size_t>(cl.size(), 1)))) return rc;
+    if (!cl.empty()) HIP_TRY(hipMemcpy(c->d_clusters, cl.data(), cl.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
+    if ((rc = grow(c->d_vblk, c->cap_vblk, std::max<size_t>(vblk.size(), 1)))) return rc;
+    if (!vblk.empty()) HIP_TRY(hipMemcpy(c->d_vblk, vblk.data(), vblk.size() * sizeof(uint2), hipMemcpyHostToDevice));
     c->geometry_set = true;
     c->draws_dirty = true;
     return TRI_OK;
@@ -921,6 +988,9 @@ int tri_render(tri_ctx* c) {
     }
     for (int t = 0; t < TRI_MAX_TEXTURE_SLOTS && !fp.need_lut; ++t)
         fp.need_lut = c->d_tex[t] && (c->tex_w[t] != 1 || c->tex_h[t] != 1);
+    fp.cull_on = (c->y0 != 0 || c->y1 != c->H || (c->cfg.flags & TRI_FLAG_CLUSTER_CULL)) && c->ncl_total > 0 ? 1u : 0u;
+    fp.cull_vertex = fp.cull_on && !c->shadow.size ? 1u : 0u;  // the pre-pass needs every caster
+    fp.ncl_total = c->ncl_total;
     if (c->shadow.size) {
         fp.shadow_on = 1u;
         fp.s_size = c->shadow.size;
@@ -962,6 +1032,10 @@ int tri_render(tri_ctx* c) {
     b.counters = c->d_ctr;
     b.color = c->d_color;
     b.depth = c->d_depth;
+    b.clusters = c->d_clusters;
+    b.vblk = c->d_vblk;
+    b.draw_cbase = c->d_cbase;
+    b.cvis = c->d_cvis;
     b.lpos = c->d_lpos;
     b.lsnap = c->d_lsnap;
     b.sbin_count = c->d_sbin_count;

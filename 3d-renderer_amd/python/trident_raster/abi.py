@@ -21,6 +21,7 @@ TRI_MAX_POINT_LIGHTS = 8
 TRI_MAX_TEXTURE_SLOTS = 256
 TRI_FLAG_NO_DEPTH_OUTPUT = 0x1
 TRI_FLAG_EXACT_SHADING = 0x2
+TRI_FLAG_CLUSTER_CULL = 0x4
 
 VERTEX_DTYPE = np.dtype(
     [

@@ -47,16 +47,24 @@ def band_rows(height, world, rank):
     return rank * rows, (rank + 1) * rows
 
 
-def gather_bands(frame, band, world, async_op=False):
-    """Assemble the full frame on every rank from the per-rank BGRA8 bands (RCCL all-gather over xGMI
-    with the nccl backend; gloo in the CPU tests). Band r lands at rows [r*rows, (r+1)*rows).
-    async_op=True returns the collective's work handle (None for world 1) instead of waiting."""
+def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=0):
+    """Assemble the full frame from the per-rank BGRA8 bands; band r lands at rows [r*rows, (r+1)*rows).
+    mode "gather" (default): onto the display rank `dst` only (RCCL grouped send/recv over xGMI: each
+    rank sends its 1/N of the frame once, the display rank receives N-1 bands over N-1 links at once);
+    "allgather": onto every rank (all_gather_into_tensor: (N-1)/N of the frame into every GPU).
+    Returns the work handle (None for world 1) with async_op, else the assembled frame (None on a
+    non-display rank in gather mode). gloo backs the same calls in the CPU tests."""
     if world == 1:
         return None if async_op else band
     import torch.distributed as dist
 
-    work = dist.all_gather_into_tensor(frame, band, async_op=async_op)
-    return work if async_op else frame
+    if mode == "allgather":
+        work = dist.all_gather_into_tensor(frame, band, async_op=async_op)
+        return work if async_op else frame
+    n = band.numel()
+    parts = [frame.narrow(0, r * n, n) for r in range(world)] if rank == dst else None
+    work = dist.gather(band, gather_list=parts, dst=dst, async_op=async_op)
+    return work if async_op else (frame if rank == dst else None)
 
 
 def max_over_ranks(value, device, dist_on):
@@ -77,11 +85,12 @@ class GatherRing:
     render stream waits for frame k's gather (work.wait() is a stream wait; the host does not
     block). Throughput is then max(render, gather) per frame instead of their sum."""
 
-    def __init__(self, world, band_elems, frame_elems, make):
-        self.world = world
+    def __init__(self, world, band_elems, frame_elems, make, mode="gather", rank=0, dst=0):
+        self.world, self.mode, self.rank, self.dst = world, mode, rank, dst
         self.nbuf = 2 if world > 1 else 1
         self.bands = [make(band_elems) for _ in range(self.nbuf)]
-        self.frames = [make(frame_elems) for _ in range(self.nbuf)] if world > 1 else self.bands
+        keeps_frame = world > 1 and (mode == "allgather" or rank == dst)
+        self.frames = [make(frame_elems) for _ in range(self.nbuf)] if keeps_frame else self.bands
         self.pending = [None] * self.nbuf
         self.k = 0
 
@@ -96,7 +105,8 @@ class GatherRing:
     def publish(self):
         """Start frame k's gather of the band returned by acquire()."""
         i = self.k % self.nbuf
-        self.pending[i] = gather_bands(self.frames[i], self.bands[i], self.world, async_op=True)
+        self.pending[i] = gather_bands(self.frames[i], self.bands[i], self.world, async_op=True, mode=self.mode,
+                                       rank=self.rank, dst=self.dst)
         self.k += 1
 
     def drain(self):
@@ -115,7 +125,7 @@ class BandRenderer:
     """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers, assembled
     by a GatherRing."""
 
-    def __init__(self, scene, rank, world, device_index, band_world=None):
+    def __init__(self, scene, rank, world, device_index, band_world=None, assembly="gather"):
         import torch
         from trident_raster import raster, scenes
 
@@ -124,8 +134,8 @@ class BandRenderer:
         rows = self.band[1] - self.band[0]
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
         self.dev = torch.device("cuda", device_index)
-        self.ring = GatherRing(world, rows * W, H * W,
-                               lambda n: torch.empty(n, dtype=torch.int32, device=self.dev))
+        self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
+                               mode=assembly, rank=rank)
         self.depth = torch.empty(rows * W, dtype=torch.float32, device=self.dev)
         self.r = raster.TriRaster(W, H, band=self.band, device=device_index)
         # A dedicated render stream (a non-zero handle) that is torch's current stream while a frame is
@@ -296,6 +306,8 @@ def main():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostics (1 GPU, no collective): render only band --sim-rank of an N-way split")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--assembly", choices=("gather", "allgather"), default="gather",
+                    help="N > 1: bands gathered onto the display rank 0 (default) or all-gathered onto every rank")
     ap.add_argument("--no-stage-timing", action="store_true",
                     help="diagnostics: no per-kernel HIP events in the timed loop (roofline fields become null)")
     args = ap.parse_args()
@@ -318,7 +330,7 @@ def main():
     if args.sim_world and world == 1:
         br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world)
     else:
-        br = BandRenderer(scene, rank, world, local)
+        br = BandRenderer(scene, rank, world, local, assembly=args.assembly)
     dt, timing = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing)
     fps = args.steps / dt
     W, H = scene.width, scene.height
@@ -341,7 +353,7 @@ def main():
     if not args.no_secondary and args.config == "c3":
         for key in ("c2", "c5"):  # the other BASELINE.json GPU configs, same timing protocol
             s2 = build_scene(key)
-            br2 = BandRenderer(s2, rank, world, local)
+            br2 = BandRenderer(s2, rank, world, local, assembly=args.assembly)
             n2 = max(args.steps, 50) if key == "c2" else max(args.steps // 2, 20)
             dt2, t2 = timed_run(br2, n2, args.warmup, dist_on)
             fps2 = n2 / dt2
@@ -378,7 +390,8 @@ def main():
             "config": {"workload": scene.name, "width": W, "height": H, "triangles": scene.triangles,
                        "vertices": int(scene.vertices.shape[0]), "bin": stats["bin_size"],
                        "skybox": skybox_name(scene),
-                       "parallelism": f"row-band x{world} + RCCL all-gather" if world > 1 else "single GPU"},
+                       "parallelism": (f"row-band x{world} + RCCL {'gather to rank 0' if args.assembly == 'gather' else 'all-gather'}"
+                                       if world > 1 else "single GPU")},
             "mpix_per_s": fps * W * H / 1e6,
             "latency_ms": latency,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

@@ -135,6 +135,8 @@ typedef struct tri_config {
 #define TRI_FLAG_NO_DEPTH_OUTPUT 0x1u /* skip the depth write (reference storeOp DONT_CARE) */
 #define TRI_FLAG_EXACT_SHADING 0x2u   /* Default.frag with IEEE div/sqrt/powf in the oracle's order *
                                        * (default: hardware rcp/rsq/exp/log; both within 1 LSB)     */
+#define TRI_FLAG_CLUSTER_CULL 0x4u    /* cull 512-triangle clusters by their projected boxes on whole *
+                                       * frames too (row-band contexts always do); output unchanged  */
 
 /* Per-stage accumulated device time (HIP events on the context stream) and last-frame counters. */
 typedef struct tri_timing {

@@ -178,3 +178,24 @@ def test_bin_overflow_grows_and_recovers():
         assert ei.value.code == abi.TRI_E_OVERFLOW
         r.render_frame()  # grown buffers: succeeds
     assert ref[0].shape == (720, 1280, 4)
+
+
+@pytest.mark.parametrize("case", ["grid_turned", "primitives", "invalid", "skinned", "near_clip"])
+def test_cluster_cull_is_exact(oracle, case):
+    """TRI_FLAG_CLUSTER_CULL on a whole frame (row bands always cull): frames bit-identical to the
+    unculled path and to the oracle, with geometry partly off screen, several draws, invalid vertices,
+    skinned draws (never culled) and clipped primitives."""
+    from trident_raster import abi, scenes
+
+    if case == "grid_turned":
+        s = sc.grid_c3(640, 360, 120)
+        view, proj = scenes.editor_camera((1.5, 0.5, 0.0), (8.0, 35.0, 0.0), 60.0, (640, 360))
+        s.ubo = scenes.pack_ubo(view, proj, (1.5, 0.5, 0.0), [{"type": "directional"}])
+    else:
+        s = {"primitives": lambda: sc.primitives_row(oracle), "invalid": lambda: sc.invalid_inputs(oracle),
+             "skinned": lambda: sc.skinned_quad(oracle), "near_clip": lambda: sc.near_clip_grid()}[case]()
+    plain_c, plain_d, plain_s = render_gpu(s)
+    cull_c, cull_d, cull_s = render_gpu(s, flags=abi.TRI_FLAG_CLUSTER_CULL)
+    assert np.array_equal(cull_c, plain_c) and np.array_equal(cull_d, plain_d)
+    assert cull_s["triangles_setup"] == plain_s["triangles_setup"]
+    assert_parity(s, oracle, flags=abi.TRI_FLAG_CLUSTER_CULL)
