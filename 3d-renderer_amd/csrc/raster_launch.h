@@ -56,3 +56,9 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
 // Presentation blit (tri_blit_linear): src W x H B8G8R8A8 -> dst dw x dh, linear, clamp-to-edge.
 hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* dst, int32_t dw, int32_t dh,
                            const float* unorm_lut, hipStream_t stream);
+
+// Internal accessors for the group layer (tri_group.hip): a context's stream and device.
+hipStream_t tri_internal_stream(tri_ctx* ctx);
+int tri_internal_device(tri_ctx* ctx);
+// Record an error message for tri_last_error (returns `code`).
+int tri_internal_fail(int code, const char* msg);

@@ -580,6 +580,10 @@ int choose_bin_grid(tri_ctx* c) {
 
 }  // namespace
 
+hipStream_t tri_internal_stream(tri_ctx* c) { return c->stream; }
+int tri_internal_device(tri_ctx* c) { return c->device; }
+int tri_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
+
 extern "C" {
 
 const char* tri_last_error(void) { return g_last_error.c_str(); }

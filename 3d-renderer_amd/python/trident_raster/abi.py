@@ -161,7 +161,19 @@ def make_shadow(light_view_proj, size=2048, depth_bias=0.001, slope_bias=2.0):
     return s
 
 
-for _s, _n in ((TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
+class TriGroupConfig(C.Structure):
+    _fields_ = [
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("device_count", C.c_uint32),
+        ("display", C.c_uint32),
+        ("devices", C.POINTER(C.c_int32)),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+for _s, _n in ((TriGroupConfig, 32), (TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
                (TriShadowConfig, 80)):
     assert C.sizeof(_s) == _n, (_s, C.sizeof(_s))
 
@@ -193,6 +205,22 @@ CABI_FUNCTIONS = [
     ("tri_shadow_fit_ortho", C.c_int, [C.POINTER(C.c_float * 3), C.POINTER(C.c_float * 3), C.POINTER(C.c_float * 3),
                                        C.POINTER(C.c_float * 16)]),
     ("tri_read_shadow_map", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("tri_group_create", C.c_int, [C.POINTER(TriGroupConfig), C.POINTER(C.c_void_p)]),
+    ("tri_group_destroy", C.c_int, [C.c_void_p]),
+    ("tri_group_context", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("tri_group_upload_geometry", C.c_int,
+     [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32]),
+    ("tri_group_upload_materials", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("tri_group_upload_texture", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
+    ("tri_group_upload_bone_palette", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("tri_group_upload_skybox", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("tri_group_set_shadow", C.c_int, [C.c_void_p, C.POINTER(TriShadowConfig)]),
+    ("tri_group_set_frame", C.c_int, [C.c_void_p, C.POINTER(TriGlobalUbo), C.POINTER(C.c_float * 4)]),
+    ("tri_group_set_draws", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("tri_group_render", C.c_int, [C.c_void_p]),
+    ("tri_group_synchronize", C.c_int, [C.c_void_p]),
+    ("tri_group_readback", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
+    ("tri_group_frame", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int32)]),
 ]
 
 

@@ -205,3 +205,102 @@ class TriRaster:
         s = abi.TriFrameStats()
         _check(_lib.tri_get_frame_stats(self._ctx, C.byref(s)))
         return {k: getattr(s, k) for k, _ in abi.TriFrameStats._fields_}
+
+
+class TriGroup:
+    """tri_group: one frame over N row-band contexts on the given devices (RCCL gather onto the display
+    band's device; bands sharing that device render in place)."""
+
+    def __init__(self, width, height, devices, display=0, flags=0):
+        lib = load_library()
+        n = len(devices)
+        self._devs = (C.c_int32 * n)(*devices)
+        cfg = abi.TriGroupConfig(width, height, n, display, self._devs, flags, 0)
+        g = C.c_void_p()
+        _check(lib.tri_group_create(C.byref(cfg), C.byref(g)))
+        self._g = g
+        self.width, self.height, self.n = width, height, n
+
+    def close(self):
+        if self._g:
+            _lib.tri_group_destroy(self._g)
+            self._g = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def upload_geometry(self, vertices, indices, meshes):
+        v = np.ascontiguousarray(vertices, dtype=abi.VERTEX_DTYPE)
+        i = np.ascontiguousarray(indices, dtype=np.uint32)
+        m = np.ascontiguousarray(meshes, dtype=abi.MESH_RANGE_DTYPE)
+        _check(_lib.tri_group_upload_geometry(self._g, _ptr(v), v.size, _ptr(i), i.size, _ptr(m), m.size))
+
+    def upload_materials(self, records):
+        n = len(records)
+        arr = (abi.TriMaterialRecord * max(n, 1))()
+        for k, (base, factors) in enumerate(records):
+            arr[k].base_color_factor = (C.c_float * 4)(*base)
+            arr[k].material_factors = (C.c_float * 4)(*factors)
+        _check(_lib.tri_group_upload_materials(self._g, arr, n))
+
+    def upload_texture(self, slot, rgba8):
+        t = np.ascontiguousarray(rgba8, dtype=np.uint8)
+        _check(_lib.tri_group_upload_texture(self._g, slot, _ptr(t), t.shape[1], t.shape[0]))
+
+    def upload_bone_palette(self, mats):
+        m = np.ascontiguousarray(mats, dtype=np.float32).reshape(-1, 16)
+        _check(_lib.tri_group_upload_bone_palette(self._g, _ptr(m), m.shape[0]))
+
+    def upload_skybox(self, faces):
+        if faces is None:
+            _check(_lib.tri_group_upload_skybox(self._g, None, 0))
+            return
+        f = np.ascontiguousarray(faces, dtype=np.uint8)
+        _check(_lib.tri_group_upload_skybox(self._g, _ptr(f), f.shape[1]))
+
+    def set_shadow(self, cfg):
+        _check(_lib.tri_group_set_shadow(self._g, C.byref(cfg) if cfg is not None else None))
+
+    def set_frame(self, ubo, clear=(0.005, 0.005, 0.005, 1.0)):
+        cl = (C.c_float * 4)(*clear)
+        _check(_lib.tri_group_set_frame(self._g, C.byref(ubo), C.byref(cl)))
+
+    def set_draws(self, draws):
+        arr, n = abi.draws_array(draws)
+        _check(_lib.tri_group_set_draws(self._g, arr, n))
+
+    def render(self):
+        _check(_lib.tri_group_render(self._g))
+
+    def synchronize(self):
+        _check(_lib.tri_group_synchronize(self._g))
+
+    def render_frame(self, retries=2):
+        for attempt in range(retries + 1):
+            self.render()
+            try:
+                self.synchronize()
+                return
+            except TriError as e:
+                if e.code != abi.TRI_E_OVERFLOW or attempt == retries:
+                    raise
+
+    def readback(self, depth=True):
+        col = np.empty((self.height, self.width, 4), dtype=np.uint8)
+        dep = np.empty((self.height, self.width), dtype=np.uint32) if depth else None
+        _check(_lib.tri_group_readback(self._g, _ptr(col), _ptr(dep) if depth else None))
+        return col, dep
+
+    def frame_pointer(self):
+        p, d = C.c_void_p(), C.c_int32()
+        _check(_lib.tri_group_frame(self._g, C.byref(p), C.byref(d)))
+        return p.value, d.value

@@ -464,7 +464,7 @@ def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048, shadow_size
 
 
 def load_scene(rast, scene):
-    """Upload a Scene into a TriRaster (UploadMesh + materials + textures + frame + draws)."""
+    """Upload a Scene into a TriRaster or TriGroup (UploadMesh + materials + textures + frame + draws)."""
     rast.upload_geometry(scene.vertices, scene.indices, scene.meshes)
     rast.upload_materials(scene.materials)
     for slot, tex in scene.textures:

@@ -268,6 +268,51 @@ int tri_set_timing(tri_ctx* ctx, int enable);
 int tri_get_timing(tri_ctx* ctx, tri_timing* out); /* synchronizes                      */
 int tri_get_frame_stats(tri_ctx* ctx, tri_frame_stats* out); /* synchronizes           */
 
+/* ---- multi-device frames (SURVEY 8(b) tri_config.device_count; 8(e) screen partition) ---------
+ * A tri_group renders one frame on N contexts, context r owning rows [r*H/N, (r+1)*H/N) (sort-first:
+ * geometry and uniforms replicated, every context culls clusters to its rows), and assembles the B8G8R8A8
+ * frame on the display context's device: bands on that device render straight into the frame, bands
+ * on other devices are gathered with RCCL grouped ncclSend / ncclRecv over xGMI (one communicator per
+ * distinct device, ncclCommInitAll). One host thread drives the whole group, as Renderer::DrawFrame
+ * does (the engine's single render thread, Application.cpp:82-134). */
+typedef struct tri_group tri_group;
+typedef struct tri_group_config {
+    uint32_t width;
+    uint32_t height;
+    uint32_t device_count;  /* N >= 1 bands                                                       */
+    uint32_t display;       /* index of the band whose device holds the assembled frame            */
+    const int32_t* devices; /* N HIP ordinals, NULL = 0..N-1; an ordinal may repeat (bands sharing  *
+                             * a device are assembled without copies)                               */
+    uint32_t flags;         /* TRI_FLAG_* for every band context                                    */
+    uint32_t reserved;
+} tri_group_config;
+
+int tri_group_create(const tri_group_config* config, tri_group** out_group);
+int tri_group_destroy(tri_group* group);
+/* The band context of index `band` (uploads, cameras, shadows, timing, readback of its own band). */
+int tri_group_context(tri_group* group, uint32_t band, tri_ctx** out_ctx);
+/* Broadcasts of the per-context uploads / frame inputs to every band (same semantics as the tri_* calls). */
+int tri_group_upload_geometry(tri_group* group, const tri_vertex* vertices, uint64_t vertex_count,
+                              const uint32_t* indices, uint64_t index_count, const tri_mesh_range* meshes,
+                              uint32_t mesh_count);
+int tri_group_upload_materials(tri_group* group, const tri_material_record* records, uint32_t count);
+int tri_group_upload_texture(tri_group* group, uint32_t slot, const uint8_t* rgba8_srgb, uint32_t width,
+                             uint32_t height);
+int tri_group_upload_bone_palette(tri_group* group, const float* matrices, uint32_t matrix_count);
+int tri_group_upload_skybox(tri_group* group, const uint8_t* faces_rgba8_srgb, uint32_t size);
+int tri_group_set_shadow(tri_group* group, const tri_shadow_config* config);
+int tri_group_set_frame(tri_group* group, const tri_global_ubo* ubo, const float clear_rgba[4]);
+int tri_group_set_draws(tri_group* group, const tri_draw* draws, uint32_t draw_count);
+/* Enqueue every band, then the assembly onto the display device (asynchronous). */
+int tri_group_render(tri_group* group);
+/* Wait for every band and the assembly; TRI_E_OVERFLOW as tri_synchronize (re-render the frame). */
+int tri_group_synchronize(tri_group* group);
+/* The assembled frame (width*height BGRA8, from the display device) and, optionally, the depth of
+ * every band (width*height float32 bits). Synchronous. */
+int tri_group_readback(tri_group* group, uint8_t* bgra8, uint32_t* depth_bits);
+/* The assembled frame in device memory: its pointer on the display device and that device's ordinal. */
+int tri_group_frame(tri_group* group, void** device_bgra8, int32_t* device);
+
 #ifdef __cplusplus
 } /* extern "C" */
 
@@ -277,6 +322,7 @@ static_assert(sizeof(tri_draw) == 144, "tri_draw layout");
 static_assert(sizeof(tri_global_ubo) == 480, "GlobalUniformBuffer is 480 bytes");
 static_assert(sizeof(tri_material_record) == 32, "MaterialUniformBuffer is 32 bytes");
 static_assert(sizeof(tri_shadow_config) == 80, "tri_shadow_config layout");
+static_assert(sizeof(tri_group_config) == 32, "tri_group_config layout");
 #endif
 
 #endif /* TRI_RASTER_H */

@@ -199,3 +199,24 @@ def test_cluster_cull_is_exact(oracle, case):
     assert np.array_equal(cull_c, plain_c) and np.array_equal(cull_d, plain_d)
     assert cull_s["triangles_setup"] == plain_s["triangles_setup"]
     assert_parity(s, oracle, flags=abi.TRI_FLAG_CLUSTER_CULL)
+
+
+@pytest.mark.parametrize("nbands,display", [(1, 0), (3, 1), (8, 5)])
+def test_group_bands_on_one_device_assemble_in_place(oracle, nbands, display):
+    """tri_group with every band on device 0 (the 1-GPU stand-in for N devices): bands render in place
+    into the display frame; the assembled frame and the per-band depth equal the oracle's full frame."""
+    from trident_raster import raster, scenes
+
+    s = sc.primitives_row(oracle, 320, 240)
+    with raster.TriGroup(s.width, s.height, [0] * nbands, display=display) as g:
+        scenes.load_scene(g, s)
+        g.render_frame()
+        col, dep = g.readback()
+        g.render_frame()  # steady state: a second frame over the same buffers
+        col2, dep2 = g.readback()
+        ptr, dev = g.frame_pointer()
+    oc, od, _ = oracle.render(s)
+    assert np.array_equal(dep, od) and np.array_equal(dep2, od)
+    assert int(np.abs(col.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL
+    assert np.array_equal(col, col2)
+    assert ptr and dev == 0

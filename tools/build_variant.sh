@@ -5,10 +5,10 @@ set -e
 cd "$(dirname "$0")/../3d-renderer_amd"
 name=$1; shift
 mkdir -p lib/variants/obj_$name
-for s in raster_kernels tri_raster_capi; do
+for s in raster_kernels tri_raster_capi tri_group; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function "$@" \
     -c csrc/$s.hip -o lib/variants/obj_$name/$s.o &
 done
 wait
-/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o lib/variants/$name.so lib/variants/obj_$name/*.o
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o lib/variants/$name.so lib/variants/obj_$name/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 echo "built lib/variants/$name.so"
