@@ -65,14 +65,14 @@ struct TimingSet {
 
 }  // namespace
 
-struct tri_ctx {
-    tri_config cfg{};
+// Geometry (UploadMeshFromCache, Renderer.cpp:1965-2116): one concatenated vertex buffer, one index
+// buffer, the per-mesh ranges and the cluster-culling tables. A context owns one; a tri_geometry made
+// with tri_geometry_create is the same object shared by several contexts of one device (the editor's
+// Scene and Game viewports read one vertex/index buffer, as the reference's do).
+struct tri_geometry {
     int device = 0;
-    int32_t W = 0, H = 0, y0 = 0, y1 = 0, nbx = 0, nby = 0, nbins = 0;
-    hipStream_t own_stream = nullptr;
-    hipStream_t stream = nullptr;
-
-    // geometry (UploadMeshFromCache)
+    bool shared = false;
+    uint64_t version = 0;  // bumped by every upload (contexts re-resolve their draws)
     TriVsIn* d_vin = nullptr; size_t cap_vin = 0;
     TriVsSkin* d_skin = nullptr; size_t cap_skin = 0;
     bool has_skin_data = false;
@@ -85,6 +85,18 @@ struct tri_ctx {
     TriCluster* d_clusters = nullptr; size_t cap_clusters = 0;
     uint2* d_vblk = nullptr; size_t cap_vblk = 0;
     bool geometry_set = false;
+};
+
+struct tri_ctx {
+    tri_config cfg{};
+    int device = 0;
+    int32_t W = 0, H = 0, y0 = 0, y1 = 0, nbx = 0, nby = 0, nbins = 0;
+    hipStream_t own_stream = nullptr;
+    hipStream_t stream = nullptr;
+
+    tri_geometry own_geom;
+    tri_geometry* geom = &own_geom;  // own_geom, or a shared tri_geometry (tri_bind_geometry)
+    uint64_t geom_seen = 0;          // geom->version the resolved draws were built against
 
     tri_material_record mat0{{1, 1, 1, 1}, {1, 1, 1, 0}};
 
@@ -368,16 +380,16 @@ int resolve_draws(tri_ctx* c) {
         vb[d] = (uint32_t)vslots;
         pb[d] = (uint32_t)prims;
         cbase[d] = (uint32_t)ncl;
-        if (src.mesh_index >= c->meshes.size()) continue;  // Renderer.cpp:5118-5127 skip
-        const tri_mesh_range& mr = c->meshes[src.mesh_index];
-        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > c->nidx) continue;
+        if (src.mesh_index >= c->geom->meshes.size()) continue;  // Renderer.cpp:5118-5127 skip
+        const tri_mesh_range& mr = c->geom->meshes[src.mesh_index];
+        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > c->geom->nidx) continue;
         o.first_index = (int32_t)mr.first_index;
         o.base_vertex = mr.base_vertex;
-        o.min_index = c->mesh_min[src.mesh_index];
-        o.vert_count = c->mesh_max[src.mesh_index] - o.min_index + 1;
-        o.cl_first = c->mesh_cl_first[src.mesh_index];
-        o.vblk_first = c->mesh_vblk_first[src.mesh_index];
-        o.ncl = c->mesh_ncl[src.mesh_index];
+        o.min_index = c->geom->mesh_min[src.mesh_index];
+        o.vert_count = c->geom->mesh_max[src.mesh_index] - o.min_index + 1;
+        o.cl_first = c->geom->mesh_cl_first[src.mesh_index];
+        o.vblk_first = c->geom->mesh_vblk_first[src.mesh_index];
+        o.ncl = c->geom->mesh_ncl[src.mesh_index];
         vslots += o.vert_count;
         prims += mr.index_count / 3;
         ncl += o.ncl;
@@ -578,6 +590,120 @@ int choose_bin_grid(tri_ctx* c) {
     return TRI_OK;
 }
 
+// UploadMeshFromCache into a geometry object: the caller has made its device current and drained the
+// streams that read it.
+int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uint32_t* idx, uint64_t ni,
+                    const tri_mesh_range* meshes, uint32_t nm) {
+    if ((nv && !v) || (ni && !idx) || (nm && !meshes)) return fail(TRI_E_INVALID, "tri_upload_geometry: null array");
+    if (nv * sizeof(TriVsIn) > 0xFFFFFFFFull)  // k_vertex reads the records with 32-bit byte offsets
+        return fail(TRI_E_INVALID, "tri_upload_geometry: %llu vertices exceed the 4 GiB vertex-record buffer",
+                    (unsigned long long)nv);
+    int rc;
+    // AoS 100-byte Vertex -> 48-byte shading records (+ 32-byte skin records when weights exist)
+    std::vector<TriVsIn> vin(nv);
+    std::vector<TriVsSkin> skin;
+    bool has_skin = false;
+    for (uint64_t i = 0; i < nv; ++i) {
+        const tri_vertex& s = v[i];
+        TriVsIn& o = vin[i];
+        o.px = s.position[0]; o.py = s.position[1]; o.pz = s.position[2];
+        o.nx = s.normal[0]; o.ny = s.normal[1]; o.nz = s.normal[2];
+        o.cr = s.color[0]; o.cg = s.color[1]; o.cb = s.color[2];
+        o.u = s.texcoord[0]; o.v = s.texcoord[1]; o.pad = 0.0f;
+        has_skin = has_skin || s.bone_weights[0] > 0.f || s.bone_weights[1] > 0.f || s.bone_weights[2] > 0.f ||
+                   s.bone_weights[3] > 0.f;
+    }
+    if (has_skin) {
+        skin.resize(nv);
+        for (uint64_t i = 0; i < nv; ++i) {
+            std::memcpy(skin[i].idx, v[i].bone_indices, 16);
+            std::memcpy(skin[i].w, v[i].bone_weights, 16);
+        }
+        if ((rc = grow(g->d_skin, g->cap_skin, nv))) return rc;
+        HIP_TRY(hipMemcpy(g->d_skin, skin.data(), nv * sizeof(TriVsSkin), hipMemcpyHostToDevice));
+    }
+    g->has_skin_data = has_skin;
+    if ((rc = grow(g->d_vin, g->cap_vin, std::max<uint64_t>(nv, 1)))) return rc;
+    if (nv) HIP_TRY(hipMemcpy(g->d_vin, vin.data(), nv * sizeof(TriVsIn), hipMemcpyHostToDevice));
+    if ((rc = grow(g->d_idx, g->cap_idx, std::max<uint64_t>(ni, 1)))) return rc;
+    if (ni) HIP_TRY(hipMemcpy(g->d_idx, idx, ni * 4, hipMemcpyHostToDevice));
+    g->nverts = nv;
+    g->nidx = ni;
+    g->meshes.assign(meshes, meshes + nm);
+    g->mesh_min.assign(nm, 0);
+    g->mesh_max.assign(nm, 0);
+    for (uint32_t m = 0; m < nm; ++m) {  // referenced vertex range per mesh (VS invocation range)
+        const tri_mesh_range& mr = meshes[m];
+        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > ni) continue;
+        const uint32_t cnt = (mr.index_count / 3) * 3;
+        uint32_t mn = 0xFFFFFFFFu, mx = 0;
+        for (uint32_t i = 0; i < cnt; ++i) {
+            mn = std::min(mn, idx[mr.first_index + i]);
+            mx = std::max(mx, idx[mr.first_index + i]);
+        }
+        if (mx - mn >= 0x7FFFFFFFu) return fail(TRI_E_INVALID, "mesh %u: index range too large", m);
+        g->mesh_min[m] = mn;
+        g->mesh_max[m] = mx;
+    }
+    // cluster tables (row-band culling): runs of TRI_CLUSTER_PRIMS primitives with their object-space
+    // boxes and index ranges; per 256-slot vertex block the interval of clusters whose range meets it
+    std::vector<TriCluster> cl;
+    std::vector<uint2> vblk;
+    g->mesh_cl_first.assign(nm, 0);
+    g->mesh_ncl.assign(nm, 0);
+    g->mesh_vblk_first.assign(nm, 0);
+    for (uint32_t m = 0; m < nm; ++m) {
+        const tri_mesh_range& mr = meshes[m];
+        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > ni) continue;
+        const uint32_t ntri = mr.index_count / 3;
+        const uint32_t ncl = (ntri + TRI_CLUSTER_PRIMS - 1) / TRI_CLUSTER_PRIMS;
+        const uint32_t mn = g->mesh_min[m];
+        const uint32_t nblk = (g->mesh_max[m] - mn) / TRI_VBLOCK + 1;
+        g->mesh_cl_first[m] = (uint32_t)cl.size();
+        g->mesh_ncl[m] = ncl;
+        g->mesh_vblk_first[m] = (uint32_t)vblk.size();
+        vblk.resize(vblk.size() + nblk, make_uint2(0xFFFFFFFFu, 0u));
+        uint2* iv = vblk.data() + g->mesh_vblk_first[m];
+        for (uint32_t k = 0; k < ncl; ++k) {
+            TriCluster t;
+            for (int a = 0; a < 3; ++a) { t.lo[a] = INFINITY; t.hi[a] = -INFINITY; }
+            t.vmin = 0xFFFFFFFFu;
+            t.vmax = 0;
+            const uint32_t i0 = mr.first_index + 3 * k * TRI_CLUSTER_PRIMS;
+            const uint32_t i1 = mr.first_index + 3 * std::min(ntri, (k + 1) * TRI_CLUSTER_PRIMS);
+            for (uint32_t i = i0; i < i1; ++i) {
+                const uint32_t x = idx[i];
+                t.vmin = std::min(t.vmin, x);
+                t.vmax = std::max(t.vmax, x);
+                const int64_t gi = (int64_t)mr.base_vertex + x;
+                if (gi < 0 || (uint64_t)gi >= nv) continue;
+                for (int a = 0; a < 3; ++a) {
+                    t.lo[a] = std::fmin(t.lo[a], v[gi].position[a]);
+                    t.hi[a] = std::fmax(t.hi[a], v[gi].position[a]);
+                }
+            }
+            for (uint32_t bk = (t.vmin - mn) / TRI_VBLOCK; bk <= (t.vmax - mn) / TRI_VBLOCK; ++bk) {
+                iv[bk].x = std::min(iv[bk].x, k);
+                iv[bk].y = std::max(iv[bk].y, k);
+            }
+            cl.push_back(t);
+        }
+    }
+    if ((rc = grow(g->d_clusters, g->cap_clusters, std::max<size_t>(cl.size(), 1)))) return rc;
+    if (!cl.empty()) HIP_TRY(hipMemcpy(g->d_clusters, cl.data(), cl.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
+    if ((rc = grow(g->d_vblk, g->cap_vblk, std::max<size_t>(vblk.size(), 1)))) return rc;
+    if (!vblk.empty()) HIP_TRY(hipMemcpy(g->d_vblk, vblk.data(), vblk.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    g->geometry_set = true;
+    ++g->version;
+    return TRI_OK;
+}
+
+void free_geometry(tri_geometry& g) {
+    auto f = [](void* p) { if (p) (void)hipFree(p); };
+    f(g.d_vin); f(g.d_skin); f(g.d_idx); f(g.d_clusters); f(g.d_vblk);
+    g.d_vin = nullptr; g.d_skin = nullptr; g.d_idx = nullptr; g.d_clusters = nullptr; g.d_vblk = nullptr;
+}
+
 }  // namespace
 
 hipStream_t tri_internal_stream(tri_ctx* c) { return c->stream; }
@@ -651,10 +777,10 @@ int tri_destroy(tri_ctx* c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(c->d_vin); f(c->d_skin); f(c->d_idx); f(c->d_lut); f(c->d_bones); f(c->d_sky);
+    free_geometry(c->own_geom);
+    f(c->d_lut); f(c->d_bones); f(c->d_sky);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase); f(c->d_cbase); f(c->d_cvis);
-    f(c->d_clusters); f(c->d_vblk);
     f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own); f(c->d_present);
@@ -678,108 +804,55 @@ int tri_set_stream(tri_ctx* c, void* s) {
 int tri_upload_geometry(tri_ctx* c, const tri_vertex* v, uint64_t nv, const uint32_t* idx, uint64_t ni,
                         const tri_mesh_range* meshes, uint32_t nm) {
     if (!c) return fail(TRI_E_INVALID, "tri_upload_geometry: null context");
-    if ((nv && !v) || (ni && !idx) || (nm && !meshes)) return fail(TRI_E_INVALID, "tri_upload_geometry: null array");
-    if (nv * sizeof(TriVsIn) > 0xFFFFFFFFull)  // k_vertex reads the records with 32-bit byte offsets
-        return fail(TRI_E_INVALID, "tri_upload_geometry: %llu vertices exceed the 4 GiB vertex-record buffer",
-                    (unsigned long long)nv);
     int rc = make_current(c);
     if (rc) return rc;
     HIP_TRY(hipStreamSynchronize(c->stream));
-    // AoS 100-byte Vertex -> 48-byte shading records (+ 32-byte skin records when weights exist)
-    std::vector<TriVsIn> vin(nv);
-    std::vector<TriVsSkin> skin;
-    bool has_skin = false;
-    for (uint64_t i = 0; i < nv; ++i) {
-        const tri_vertex& s = v[i];
-        TriVsIn& o = vin[i];
-        o.px = s.position[0]; o.py = s.position[1]; o.pz = s.position[2];
-        o.nx = s.normal[0]; o.ny = s.normal[1]; o.nz = s.normal[2];
-        o.cr = s.color[0]; o.cg = s.color[1]; o.cb = s.color[2];
-        o.u = s.texcoord[0]; o.v = s.texcoord[1]; o.pad = 0.0f;
-        has_skin = has_skin || s.bone_weights[0] > 0.f || s.bone_weights[1] > 0.f || s.bone_weights[2] > 0.f ||
-                   s.bone_weights[3] > 0.f;
-    }
-    if (has_skin) {
-        skin.resize(nv);
-        for (uint64_t i = 0; i < nv; ++i) {
-            std::memcpy(skin[i].idx, v[i].bone_indices, 16);
-            std::memcpy(skin[i].w, v[i].bone_weights, 16);
-        }
-        if ((rc = grow(c->d_skin, c->cap_skin, nv))) return rc;
-        HIP_TRY(hipMemcpy(c->d_skin, skin.data(), nv * sizeof(TriVsSkin), hipMemcpyHostToDevice));
-    }
-    c->has_skin_data = has_skin;
-    if ((rc = grow(c->d_vin, c->cap_vin, std::max<uint64_t>(nv, 1)))) return rc;
-    if (nv) HIP_TRY(hipMemcpy(c->d_vin, vin.data(), nv * sizeof(TriVsIn), hipMemcpyHostToDevice));
-    if ((rc = grow(c->d_idx, c->cap_idx, std::max<uint64_t>(ni, 1)))) return rc;
-    if (ni) HIP_TRY(hipMemcpy(c->d_idx, idx, ni * 4, hipMemcpyHostToDevice));
-    c->nverts = nv;
-    c->nidx = ni;
-    c->meshes.assign(meshes, meshes + nm);
-    c->mesh_min.assign(nm, 0);
-    c->mesh_max.assign(nm, 0);
-    for (uint32_t m = 0; m < nm; ++m) {  // referenced vertex range per mesh (VS invocation range)
-        const tri_mesh_range& mr = meshes[m];
-        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > ni) continue;
-        const uint32_t cnt = (mr.index_count / 3) * 3;
-        uint32_t mn = 0xFFFFFFFFu, mx = 0;
-        for (uint32_t i = 0; i < cnt; ++i) {
-            mn = std::min(mn, idx[mr.first_index + i]);
-            mx = std::max(mx, idx[mr.first_index + i]);
-        }
-        if (mx - mn >= 0x7FFFFFFFu) return fail(TRI_E_INVALID, "mesh %u: index range too large", m);
-        c->mesh_min[m] = mn;
-        c->mesh_max[m] = mx;
-    }
-    // cluster tables (row-band culling): runs of TRI_CLUSTER_PRIMS primitives with their object-space
-    // boxes and index ranges; per 256-slot vertex block the interval of clusters whose range meets it
-    std::vector<TriCluster> cl;
-    std::vector<uint2> vblk;
-    c->mesh_cl_first.assign(nm, 0);
-    c->mesh_ncl.assign(nm, 0);
-    c->mesh_vblk_first.assign(nm, 0);
-    for (uint32_t m = 0; m < nm; ++m) {
-        const tri_mesh_range& mr = meshes[m];
-        if (mr.index_count < 3 || (uint64_t)mr.first_index + mr.index_count > ni) continue;
-        const uint32_t ntri = mr.index_count / 3;
-        const uint32_t ncl = (ntri + TRI_CLUSTER_PRIMS - 1) / TRI_CLUSTER_PRIMS;
-        const uint32_t mn = c->mesh_min[m];
-        const uint32_t nblk = (c->mesh_max[m] - mn) / TRI_VBLOCK + 1;
-        c->mesh_cl_first[m] = (uint32_t)cl.size();
-        c->mesh_ncl[m] = ncl;
-        c->mesh_vblk_first[m] = (uint32_t)vblk.size();
-        vblk.resize(vblk.size() + nblk, make_uint2(0xFFFFFFFFu, 0u));
-        uint2* iv = vblk.data() + c->mesh_vblk_first[m];
-        for (uint32_t k = 0; k < ncl; ++k) {
-            TriCluster t;
-            for (int a = 0; a < 3; ++a) { t.lo[a] = INFINITY; t.hi[a] = -INFINITY; }
-            t.vmin = 0xFFFFFFFFu;
-            t.vmax = 0;
-            const uint32_t i0 = mr.first_index + 3 * k * TRI_CLUSTER_PRIMS;
-            const uint32_t i1 = mr.first_index + 3 * std::min(ntri, (k + 1) * TRI_CLUSTER_PRIMS);
-            for (uint32_t i = i0; i < i1; ++i) {
-                const uint32_t x = idx[i];
-                t.vmin = std::min(t.vmin, x);
-                t.vmax = std::max(t.vmax, x);
-                const int64_t gi = (int64_t)mr.base_vertex + x;
-                if (gi < 0 || (uint64_t)gi >= nv) continue;
-                for (int a = 0; a < 3; ++a) {
-                    t.lo[a] = std::fmin(t.lo[a], v[gi].position[a]);
-                    t.hi[a] = std::fmax(t.hi[a], v[gi].position[a]);
-                }
-            }
-            for (uint32_t bk = (t.vmin - mn) / TRI_VBLOCK; bk <= (t.vmax - mn) / TRI_VBLOCK; ++bk) {
-                iv[bk].x = std::min(iv[bk].x, k);
-                iv[bk].y = std::max(iv[bk].y, k);
-            }
-            cl.push_back(t);
-        }
-    }
-    if ((rc = grow(c->d_clusters, c->cap_clusters, std::max<size_t>(cl.size(), 1)))) return rc;
-    if (!cl.empty()) HIP_TRY(hipMemcpy(c->d_clusters, cl.data(), cl.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
-    if ((rc = grow(c->d_vblk, c->cap_vblk, std::max<size_t>(vblk.size(), 1)))) return rc;
-    if (!vblk.empty()) HIP_TRY(hipMemcpy(c->d_vblk, vblk.data(), vblk.size() * sizeof(uint2), hipMemcpyHostToDevice));
-    c->geometry_set = true;
+    c->geom = &c->own_geom;
+    c->own_geom.device = c->device;
+    return geometry_upload(&c->own_geom, v, nv, idx, ni, meshes, nm);
+}
+
+int tri_geometry_create(int32_t device, tri_geometry** out) {
+    if (!out) return fail(TRI_E_INVALID, "tri_geometry_create: null argument");
+    *out = nullptr;
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(TRI_E_HIP, "tri_geometry_create: no HIP device available");
+    int d = device;
+    if (d < 0 && hipGetDevice(&d) != hipSuccess) return fail(TRI_E_HIP, "tri_geometry_create: hipGetDevice failed");
+    if (d >= ndev) return fail(TRI_E_INVALID, "tri_geometry_create: device %d of %d", d, ndev);
+    tri_geometry* g = new tri_geometry();
+    g->device = d;
+    g->shared = true;
+    *out = g;
+    return TRI_OK;
+}
+
+int tri_geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uint32_t* idx, uint64_t ni,
+                        const tri_mesh_range* meshes, uint32_t nm) {
+    if (!g) return fail(TRI_E_INVALID, "tri_geometry_upload: null geometry");
+    HIP_TRY(hipSetDevice(g->device));
+    HIP_TRY(hipDeviceSynchronize());  // any context's stream may be reading the old buffers
+    return geometry_upload(g, v, nv, idx, ni, meshes, nm);
+}
+
+int tri_geometry_destroy(tri_geometry* g) {
+    if (!g) return TRI_OK;
+    (void)hipSetDevice(g->device);
+    (void)hipDeviceSynchronize();
+    free_geometry(*g);
+    delete g;
+    return TRI_OK;
+}
+
+int tri_bind_geometry(tri_ctx* c, tri_geometry* g) {
+    if (!c) return fail(TRI_E_INVALID, "tri_bind_geometry: null context");
+    if (g && g->device != c->device)
+        return fail(TRI_E_INVALID, "tri_bind_geometry: geometry on device %d, context on device %d", g->device, c->device);
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));
+    c->geom = g ? g : &c->own_geom;
+    c->geom_seen = 0;
     c->draws_dirty = true;
     return TRI_OK;
 }
@@ -933,17 +1006,21 @@ int tri_bind_output(tri_ctx* c, void* color, void* depth) {
 int tri_render(tri_ctx* c) {
     if (!c) return fail(TRI_E_INVALID, "tri_render: null context");
     if (!c->frame_set) return fail(TRI_E_STATE, "tri_render: tri_set_frame was not called");
-    if (!c->draws.empty() && !c->geometry_set) return fail(TRI_E_STATE, "tri_render: draws without geometry");
+    if (!c->draws.empty() && !c->geom->geometry_set) return fail(TRI_E_STATE, "tri_render: draws without geometry");
     int rc = make_current(c);
     if (rc) return rc;
     if ((rc = upload_texture_table(c))) return rc;
+    if (c->geom->version != c->geom_seen) {  // (shared) geometry changed since the draws were resolved
+        c->draws_dirty = true;
+        c->geom_seen = c->geom->version;
+    }
     if ((rc = resolve_draws(c))) return rc;
-    if (c->any_skin && !c->has_skin_data) {
+    if (c->any_skin && !c->geom->has_skin_data) {
         // a skinned draw over vertices without weights: skin matrix = 0 -> everything collapses
         // to the origin, exactly like the shader with all-zero weights; give the kernel zeros.
-        if ((rc = grow(c->d_skin, c->cap_skin, std::max<uint64_t>(c->nverts, 1)))) return rc;
-        HIP_TRY(hipMemsetAsync(c->d_skin, 0, std::max<uint64_t>(c->nverts, 1) * sizeof(TriVsSkin), c->stream));
-        c->has_skin_data = true;
+        if ((rc = grow(c->geom->d_skin, c->geom->cap_skin, std::max<uint64_t>(c->geom->nverts, 1)))) return rc;
+        HIP_TRY(hipMemsetAsync(c->geom->d_skin, 0, std::max<uint64_t>(c->geom->nverts, 1) * sizeof(TriVsSkin), c->stream));
+        c->geom->has_skin_data = true;
     }
     if ((rc = choose_bin_grid(c))) return rc;
     if ((rc = ensure_work_buffers(c))) return rc;
@@ -1013,11 +1090,11 @@ int tri_render(tri_ctx* c) {
     shade_constants(c->ubo, c->mat0, fp.sc);
 
     TriDeviceBuffers b;
-    b.vin = c->d_vin;
-    b.vskin = c->any_skin ? c->d_skin : nullptr;
+    b.vin = c->geom->d_vin;
+    b.vskin = c->any_skin ? c->geom->d_skin : nullptr;
     b.bones = c->d_bones;
-    b.vertex_count = c->nverts;
-    b.indices = c->d_idx;
+    b.vertex_count = c->geom->nverts;
+    b.indices = c->geom->d_idx;
     b.draws = c->d_draws;
     b.draw_shade = c->d_draw_shade;
     b.draw_vbase = c->d_vbase;
@@ -1036,8 +1113,8 @@ int tri_render(tri_ctx* c) {
     b.counters = c->d_ctr;
     b.color = c->d_color;
     b.depth = c->d_depth;
-    b.clusters = c->d_clusters;
-    b.vblk = c->d_vblk;
+    b.clusters = c->geom->d_clusters;
+    b.vblk = c->geom->d_vblk;
     b.draw_cbase = c->d_cbase;
     b.cvis = c->d_cvis;
     b.lpos = c->d_lpos;
@@ -1084,6 +1161,18 @@ int tri_readback(tri_ctx* c, uint8_t* bgra, uint32_t* depth) {
             return fail(TRI_E_STATE, "tri_readback: depth output disabled by TRI_FLAG_NO_DEPTH_OUTPUT");
         HIP_TRY(hipMemcpy(depth, c->d_depth, px * 4, hipMemcpyDeviceToHost));
     }
+    return TRI_OK;
+}
+
+int tri_get_output(tri_ctx* c, tri_image* out) {
+    if (!c || !out) return fail(TRI_E_INVALID, "tri_get_output: null argument");
+    out->device_ptr = c->d_color;
+    out->width = (uint32_t)c->W;
+    out->height = (uint32_t)(c->y1 - c->y0);
+    out->pitch_bytes = (uint32_t)c->W * 4u;
+    out->format = TRI_FORMAT_B8G8R8A8_UNORM;
+    out->device = c->device;
+    out->reserved = 0;
     return TRI_OK;
 }
 

@@ -88,8 +88,14 @@ public:
     bool ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height);
     uint32_t GetActiveViewportId() const { return m_ActiveViewportId; }
     ViewportInfo GetViewport() const;
-    // Vulkan returned a VkDescriptorSet for ImGui; here: the viewport's device B8G8R8A8 buffer.
+    // Vulkan returned a VkDescriptorSet for ImGui (Renderer.h:235); here: an opaque handle, a pointer to
+    // the viewport's tri_image (device pointer, size, pitch, B8G8R8A8_UNORM, device ordinal) that an ImGui
+    // HIP/GL-interop backend can display. nullptr before the viewport's first frame; valid until its next
+    // resize or Shutdown.
     void* GetViewportTexture(uint32_t viewportId) const;
+    // How many times the concatenated geometry went to the device: once per UploadMeshFromCache
+    // generation, shared by every viewport (the reference binds one vertex/index buffer for all).
+    uint64_t GetGeometryUploadCount() const { return m_GeometryUploads; }
     const Camera* GetActiveCamera() const;
     glm::mat4 GetViewportViewMatrix(uint32_t viewportId) const;
     glm::mat4 GetViewportProjectionMatrix(uint32_t viewportId) const;
@@ -134,6 +140,8 @@ private:
         uint32_t m_Width = 0, m_Height = 0;
         uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0, m_SkyboxGeneration = 0;
         std::vector<float> m_BonePalette;  // the palette last uploaded to this viewport's context
+        tri_image m_Image{};               // GetViewportTexture's handle (after the first frame)
+        bool m_HasImage = false;
     };
 
     void CreateSkyboxCubemap();
@@ -162,6 +170,9 @@ private:
     std::vector<float> m_BonePalette;  // PrepareBonePaletteBuffer's scratch: per-draw palettes, back to back
     size_t m_PrimitiveMeshIndices[3] = {SIZE_MAX, SIZE_MAX, SIZE_MAX};
     bool m_IsUploadingMeshes = false;
+    tri_geometry* m_SharedGeometry = nullptr;  // the device copy every viewport context binds
+    uint64_t m_SharedGeometryGeneration = 0;
+    uint64_t m_GeometryUploads = 0;
     std::vector<tri_vertex> m_VertexBuffer;
     std::vector<uint32_t> m_IndexBuffer;
     uint64_t m_GeometryGeneration = 1, m_TextureGeneration = 1, m_MaterialGeneration = 1;

@@ -90,6 +90,10 @@ int trident_app_set_present_extent(trident_app* app, uint32_t width, uint32_t he
 int trident_app_read_present(trident_app* app, uint8_t* rgba, uint32_t width, uint32_t height);
 
 int trident_app_draw_frame(trident_app* app);
+/* Renderer::GetViewportTexture: copies the viewport's image handle (TRI_E_STATE before its first frame). */
+int trident_app_viewport_texture(trident_app* app, uint32_t viewport_id, tri_image* out);
+/* Renderer::GetGeometryUploadCount. */
+int trident_app_geometry_uploads(trident_app* app, uint64_t* count);
 int trident_app_read_pixels(trident_app* app, uint32_t viewport_id, uint8_t* rgba, float* depth /* nullable */);
 
 /* Frame inputs DrawFrame would submit for a viewport (host-only). */

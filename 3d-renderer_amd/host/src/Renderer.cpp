@@ -163,6 +163,9 @@ void Renderer::Shutdown() {
         it.second.m_Ctx = nullptr;
     }
     m_Viewports.clear();
+    tri_geometry_destroy(m_SharedGeometry);  // after every context that bound it
+    m_SharedGeometry = nullptr;
+    m_SharedGeometryGeneration = 0;
     if (m_Initialised) m_Shutdown = true;
     m_Initialised = false;
 }
@@ -556,6 +559,7 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
     if (vc.m_Ctx && (vc.m_Width != w || vc.m_Height != h)) {  // CreateOrResizeOffscreenResources
         tri_destroy(vc.m_Ctx);
         vc.m_Ctx = nullptr;
+        vc.m_HasImage = false;
     }
     if (!vc.m_Ctx) {
         tri_config cfg{w, h, 0, 0, -1, m_RasterFlags};
@@ -569,9 +573,22 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
         vc.m_GeometryGeneration = vc.m_TextureGeneration = vc.m_MaterialGeneration = vc.m_SkyboxGeneration = 0;
     }
     if (vc.m_GeometryGeneration != m_GeometryGeneration) {
-        const std::vector<tri_mesh_range> ranges = GetMeshRanges();
-        if (tri_upload_geometry(vc.m_Ctx, m_VertexBuffer.data(), m_VertexBuffer.size(), m_IndexBuffer.data(),
-                                m_IndexBuffer.size(), ranges.data(), (uint32_t)ranges.size()) != TRI_OK) {
+        // one device copy of the concatenated buffers per generation, bound by every viewport
+        if (!m_SharedGeometry && tri_geometry_create(-1, &m_SharedGeometry) != TRI_OK) {
+            LogError("UploadMeshFromCache", tri_last_error());
+            return false;
+        }
+        if (m_SharedGeometryGeneration != m_GeometryGeneration) {
+            const std::vector<tri_mesh_range> ranges = GetMeshRanges();
+            if (tri_geometry_upload(m_SharedGeometry, m_VertexBuffer.data(), m_VertexBuffer.size(), m_IndexBuffer.data(),
+                                    m_IndexBuffer.size(), ranges.data(), (uint32_t)ranges.size()) != TRI_OK) {
+                LogError("UploadMeshFromCache", tri_last_error());
+                return false;
+            }
+            m_SharedGeometryGeneration = m_GeometryGeneration;
+            ++m_GeometryUploads;
+        }
+        if (tri_bind_geometry(vc.m_Ctx, m_SharedGeometry) != TRI_OK) {
             LogError("UploadMeshFromCache", tri_last_error());
             return false;
         }
@@ -647,6 +664,7 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
             LogError("DrawFrame", tri_last_error());
             continue;
         }
+        vc.m_HasImage = tri_get_output(vc.m_Ctx, &vc.m_Image) == TRI_OK;
         submitted.push_back(&vc);
     }
     // Frame fence (Renderer.cpp:744-760). A frame that outgrew the bin/clip queues has grown them
@@ -702,8 +720,9 @@ void Renderer::RecordFrameTiming(double ms) {  // Renderer.cpp:6286-6343
 }
 
 void* Renderer::GetViewportTexture(uint32_t viewportId) const {
-    (void)viewportId;
-    return nullptr;  // device buffers are owned by tri_ctx; expose them via ReadViewportPixels / bind_output
+    auto it = m_Viewports.find(viewportId);
+    if (it == m_Viewports.end() || !it->second.m_Ctx || !it->second.m_HasImage) return nullptr;
+    return const_cast<tri_image*>(&it->second.m_Image);
 }
 
 bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgba, std::vector<float>* depth) {

@@ -160,6 +160,24 @@ void CopySource(const std::string& src, char* out, uint32_t cap) {
 }
 }  // namespace
 
+int trident_app_viewport_texture(trident_app* app, uint32_t viewport_id, tri_image* out) {
+    return Guard(app, [&] {
+        if (!out) return TRI_E_INVALID;
+        const void* h = app->renderer.GetViewportTexture(viewport_id);
+        if (!h) return TRI_E_STATE;
+        *out = *static_cast<const tri_image*>(h);
+        return TRI_OK;
+    });
+}
+
+int trident_app_geometry_uploads(trident_app* app, uint64_t* count) {
+    return Guard(app, [&] {
+        if (!count) return TRI_E_INVALID;
+        *count = app->renderer.GetGeometryUploadCount();
+        return TRI_OK;
+    });
+}
+
 int trident_app_set_assets_dir(trident_app* app, const char* directory, char* source, uint32_t source_cap) {
     return Guard(app, [&] {
         if (!directory) return TRI_E_INVALID;

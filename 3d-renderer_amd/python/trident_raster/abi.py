@@ -161,6 +161,21 @@ def make_shadow(light_view_proj, size=2048, depth_bias=0.001, slope_bias=2.0):
     return s
 
 
+TRI_FORMAT_B8G8R8A8_UNORM = 44
+
+
+class TriImage(C.Structure):
+    _fields_ = [
+        ("device_ptr", C.c_void_p),
+        ("width", C.c_uint32),
+        ("height", C.c_uint32),
+        ("pitch_bytes", C.c_uint32),
+        ("format", C.c_uint32),
+        ("device", C.c_int32),
+        ("reserved", C.c_uint32),
+    ]
+
+
 class TriGroupConfig(C.Structure):
     _fields_ = [
         ("width", C.c_uint32),
@@ -173,7 +188,7 @@ class TriGroupConfig(C.Structure):
     ]
 
 
-for _s, _n in ((TriGroupConfig, 32), (TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
+for _s, _n in ((TriImage, 32), (TriGroupConfig, 32), (TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
                (TriShadowConfig, 80)):
     assert C.sizeof(_s) == _n, (_s, C.sizeof(_s))
 
@@ -205,6 +220,12 @@ CABI_FUNCTIONS = [
     ("tri_shadow_fit_ortho", C.c_int, [C.POINTER(C.c_float * 3), C.POINTER(C.c_float * 3), C.POINTER(C.c_float * 3),
                                        C.POINTER(C.c_float * 16)]),
     ("tri_read_shadow_map", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("tri_get_output", C.c_int, [C.c_void_p, C.POINTER(TriImage)]),
+    ("tri_geometry_create", C.c_int, [C.c_int32, C.POINTER(C.c_void_p)]),
+    ("tri_geometry_upload", C.c_int,
+     [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint32]),
+    ("tri_geometry_destroy", C.c_int, [C.c_void_p]),
+    ("tri_bind_geometry", C.c_int, [C.c_void_p, C.c_void_p]),
     ("tri_group_create", C.c_int, [C.POINTER(TriGroupConfig), C.POINTER(C.c_void_p)]),
     ("tri_group_destroy", C.c_int, [C.c_void_p]),
     ("tri_group_context", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),

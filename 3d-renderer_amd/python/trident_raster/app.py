@@ -30,6 +30,8 @@ _APP_FUNCTIONS = [
     ("trident_app_set_entity_visible", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
     ("trident_app_set_entity_bones", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
     ("trident_app_set_assets_dir", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint32]),
+    ("trident_app_viewport_texture", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(abi.TriImage)]),
+    ("trident_app_geometry_uploads", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("trident_load_image", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint32)]),
     ("trident_load_default_skybox", C.c_int, [C.c_char_p, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32), C.c_char_p,
@@ -142,6 +144,17 @@ class TridentApp:
         buf = C.create_string_buffer(64)
         _check(self._lib.trident_app_set_assets_dir(self._h, os.fsencode(directory), buf, 64), "set_assets_dir")
         return buf.value.decode()
+
+    def viewport_texture(self, viewport_id):
+        """Renderer::GetViewportTexture: the viewport's abi.TriImage handle."""
+        img = abi.TriImage()
+        _check(self._lib.trident_app_viewport_texture(self._h, viewport_id, C.byref(img)), "viewport_texture")
+        return img
+
+    def geometry_uploads(self):
+        n = C.c_uint64()
+        _check(self._lib.trident_app_geometry_uploads(self._h, C.byref(n)), "geometry_uploads")
+        return n.value
 
     def set_entity_bones(self, entity, matrices):
         """AnimationComponent::m_BoneMatrices: float32 [n, 4, 4] column-major mat4s (m[col][row])."""

@@ -153,6 +153,15 @@ class TriRaster:
     def set_stream(self, stream_ptr):
         _check(_lib.tri_set_stream(self._ctx, C.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def bind_geometry(self, geometry):
+        """tri_bind_geometry: reference a shared TriGeometry (None: back to the context's own)."""
+        _check(_lib.tri_bind_geometry(self._ctx, geometry._g if geometry is not None else None))
+
+    def output_image(self):
+        img = abi.TriImage()
+        _check(_lib.tri_get_output(self._ctx, C.byref(img)))
+        return img
+
     def bind_output(self, color_ptr, depth_ptr):
         _check(_lib.tri_bind_output(self._ctx, C.c_void_p(color_ptr) if color_ptr else None,
                                     C.c_void_p(depth_ptr) if depth_ptr else None))
@@ -205,6 +214,38 @@ class TriRaster:
         s = abi.TriFrameStats()
         _check(_lib.tri_get_frame_stats(self._ctx, C.byref(s)))
         return {k: getattr(s, k) for k, _ in abi.TriFrameStats._fields_}
+
+
+class TriGeometry:
+    """tri_geometry: meshes uploaded once on one device, bound by any number of contexts there."""
+
+    def __init__(self, device=-1):
+        lib = load_library()
+        g = C.c_void_p()
+        _check(lib.tri_geometry_create(device, C.byref(g)))
+        self._g = g
+
+    def upload(self, vertices, indices, meshes):
+        v = np.ascontiguousarray(vertices, dtype=abi.VERTEX_DTYPE)
+        i = np.ascontiguousarray(indices, dtype=np.uint32)
+        m = np.ascontiguousarray(meshes, dtype=abi.MESH_RANGE_DTYPE)
+        _check(_lib.tri_geometry_upload(self._g, _ptr(v), v.size, _ptr(i), i.size, _ptr(m), m.size))
+
+    def close(self):
+        if self._g:
+            _lib.tri_geometry_destroy(self._g)
+            self._g = None
+
+
+def copy_device_to_host(ptr, nbytes, device=0):
+    """hipMemcpy of `nbytes` at a device pointer (a tri_image handle) into a numpy byte array."""
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipSetDevice.argtypes = [C.c_int]
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    out = np.empty(nbytes, np.uint8)
+    assert hip.hipSetDevice(device) == 0
+    assert hip.hipMemcpy(out.ctypes.data, C.c_void_p(ptr), nbytes, 2) == 0  # hipMemcpyDeviceToHost
+    return out
 
 
 class TriGroup:

@@ -201,6 +201,19 @@ int tri_abi_version(void);
 int tri_upload_geometry(tri_ctx* ctx, const tri_vertex* vertices, uint64_t vertex_count,
                         const uint32_t* indices, uint64_t index_count,
                         const tri_mesh_range* meshes, uint32_t mesh_count);
+/* Shared geometry (the reference binds ONE vertex and index buffer for every viewport,
+ * Renderer.cpp:1965-2116, :5095-5108): a tri_geometry holds the uploaded meshes on one device and any
+ * number of contexts on that device reference it through tri_bind_geometry (NULL returns a context to
+ * its own geometry, which tri_upload_geometry fills). Uploading to a shared geometry waits for the
+ * device to go idle; contexts pick the new meshes up at their next tri_render. */
+typedef struct tri_geometry tri_geometry;
+int tri_geometry_create(int32_t device /* -1 = current */, tri_geometry** out_geometry);
+int tri_geometry_upload(tri_geometry* geometry, const tri_vertex* vertices, uint64_t vertex_count,
+                        const uint32_t* indices, uint64_t index_count, const tri_mesh_range* meshes,
+                        uint32_t mesh_count);
+int tri_geometry_destroy(tri_geometry* geometry); /* after every context using it is unbound/destroyed */
+int tri_bind_geometry(tri_ctx* ctx, tri_geometry* geometry);
+
 /* Material buffer payload (BuildMaterialPayload, Renderer.cpp:5927-5951). count 0 => the default
  * record {1,1,1,1},{1,1,1,0} (Renderer.cpp:5941-5943). */
 int tri_upload_materials(tri_ctx* ctx, const tri_material_record* records, uint32_t count);
@@ -248,6 +261,22 @@ int tri_synchronize(tri_ctx* ctx);
 /* Frame readback (Renderer.cpp:5297-5338, :1299-1389): synchronous copy of the band, tightly packed
  * BGRA8 (width*4 bytes per row) and float32 depth bits. Either pointer may be NULL. */
 int tri_readback(tri_ctx* ctx, uint8_t* bgra8, uint32_t* depth_bits);
+
+/* The context's colour target as an opaque image handle: what Renderer::GetViewportTexture returns
+ * instead of a VkDescriptorSet (Renderer.h:235; Forge shows it with ImGui::Image, GameViewportPanel.cpp:66,
+ * SceneViewportPanel.cpp:139). Rows top to bottom, B8G8R8A8_UNORM; valid until the context is destroyed,
+ * its output is rebound or its size changes; contents are those of the last completed tri_render. */
+#define TRI_FORMAT_B8G8R8A8_UNORM 44u /* the VkFormat value of the reference's offscreen target */
+typedef struct tri_image {
+    void* device_ptr;     /* device memory on `device`                   */
+    uint32_t width;
+    uint32_t height;      /* rows of the context (its band)              */
+    uint32_t pitch_bytes; /* bytes from one row to the next              */
+    uint32_t format;      /* TRI_FORMAT_B8G8R8A8_UNORM                   */
+    int32_t device;       /* HIP device ordinal                          */
+    uint32_t reserved;
+} tri_image;
+int tri_get_output(tri_ctx* ctx, tri_image* out);
 
 /* Presentation blit (Renderer.cpp:5346-5361: vkCmdBlitImage of the primary viewport's offscreen
  * target onto the swapchain image, VK_FILTER_LINEAR). Scales this context's B8G8R8A8 target to
@@ -323,6 +352,7 @@ static_assert(sizeof(tri_global_ubo) == 480, "GlobalUniformBuffer is 480 bytes")
 static_assert(sizeof(tri_material_record) == 32, "MaterialUniformBuffer is 32 bytes");
 static_assert(sizeof(tri_shadow_config) == 80, "tri_shadow_config layout");
 static_assert(sizeof(tri_group_config) == 32, "tri_group_config layout");
+static_assert(sizeof(tri_image) == 32, "tri_image layout");
 #endif
 
 #endif /* TRI_RASTER_H */

@@ -28,7 +28,7 @@ def test_struct_layout_matches_c_compiler(tmp_path):
         "tri_draw": abi.TriDraw, "tri_point_light": abi.TriPointLight, "tri_global_ubo": abi.TriGlobalUbo,
         "tri_material_record": abi.TriMaterialRecord, "tri_config": abi.TriConfig, "tri_timing": abi.TriTiming,
         "tri_frame_stats": abi.TriFrameStats, "tri_shadow_config": abi.TriShadowConfig,
-        "tri_group_config": abi.TriGroupConfig,
+        "tri_group_config": abi.TriGroupConfig, "tri_image": abi.TriImage,
     }
     lines = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{HEADER}"', "int main(void){"]
     for cname, py in structs.items():

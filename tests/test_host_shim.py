@@ -318,3 +318,62 @@ def test_gpu_shim_skinned_entities(app_mod, oracle):
     a.draw_frame()
     a.draw_frame()
     assert_shim_parity(a, oracle, 1, W, H, min_covered=5000, bones=palette)
+
+
+@pytest.mark.gpu
+def test_gpu_shim_shared_geometry_and_viewport_texture(app_mod, oracle):
+    """The Scene and Game viewports reference ONE device copy of the concatenated geometry
+    (Renderer.cpp:1965-2116 binds one vertex/index buffer for every viewport); GetViewportTexture hands
+    out an image handle whose device memory is the viewport's frame."""
+    from trident_raster import abi, raster, scenes
+
+    a = app_mod.TridentApp()
+    a.set_camera("editor", (0, 1, 6))
+    a.set_camera("runtime", (2, 2, 5), (-10, 20, 0), fov=50.0, ready=True)
+    a.set_viewport(1, 320, 240)
+    a.set_viewport(2, 200, 150)
+    v, i = scenes.uv_sphere_mesh(20, 28, 1.0)
+    m = a.append_mesh(v, i, base_color=(0.7, 0.8, 0.9, 1), metallic=0.3, roughness=0.5)
+    a.add_mesh_entity("none", m, position=(0, 0.5, 0))
+    a.add_mesh_entity("quad", position=(1.5, 0, 0))
+    a.draw_frame()
+    a.draw_frame()
+    assert a.geometry_uploads() == 1  # one upload, two viewports (the quad was created before it)
+    assert_shim_parity(a, oracle, 1, 320, 240, min_covered=3000)
+    assert_shim_parity(a, oracle, 2, 200, 150, min_covered=500)
+    for vp, (w, h) in ((1, (320, 240)), (2, (200, 150))):
+        img = a.viewport_texture(vp)
+        assert (img.width, img.height, img.pitch_bytes, img.format) == (w, h, 4 * w, abi.TRI_FORMAT_B8G8R8A8_UNORM)
+        bgra = raster.copy_device_to_host(img.device_ptr, h * img.pitch_bytes, img.device).reshape(h, w, 4)
+        rgba, _ = a.read_pixels(vp, w, h)
+        assert np.array_equal(bgra[..., [2, 1, 0, 3]], rgba)
+    a.add_mesh_entity("cube", position=(-1.5, 0, 0))  # a new primitive mesh: one more shared upload
+    a.draw_frame()
+    a.draw_frame()
+    assert a.geometry_uploads() == 2
+    assert_shim_parity(a, oracle, 1, 320, 240, min_covered=3000)
+    a.close()
+
+
+@pytest.mark.gpu
+def test_gpu_contexts_share_one_geometry(oracle):
+    from trident_raster import raster, scenes
+
+    s = sc.primitives_row(oracle, 320, 240)
+    g = raster.TriGeometry(0)
+    g.upload(s.vertices, s.indices, s.meshes)
+    outs = []
+    for band in (None, (0, 120), (120, 240)):
+        with raster.TriRaster(s.width, s.height, band=band, device=0) as r:
+            r.bind_geometry(g)
+            r.upload_materials(s.materials)
+            r.upload_skybox(s.skybox)
+            r.set_frame(s.ubo, s.clear)
+            r.set_draws(s.draws)
+            r.render_frame()
+            outs.append(r.readback())
+    g.close()
+    oc, od, _ = oracle.render(s)
+    assert np.array_equal(outs[0][1], od)
+    assert np.array_equal(np.concatenate([outs[1][0], outs[2][0]]), outs[0][0])
+    assert int(np.abs(outs[0][0].astype(np.int16) - oc.astype(np.int16)).max()) <= 1
