@@ -357,7 +357,8 @@ def test_gpu_shim_shared_geometry_and_viewport_texture(app_mod, oracle):
 
 @pytest.mark.gpu
 def test_gpu_contexts_share_one_geometry(oracle):
-    from trident_raster import raster, scenes
+    import scene_cases as sc
+    from trident_raster import raster
 
     s = sc.primitives_row(oracle, 320, 240)
     g = raster.TriGeometry(0)
