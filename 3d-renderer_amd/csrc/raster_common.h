@@ -109,7 +109,7 @@ struct __attribute__((aligned(16))) TriDrawDev {
 
 // Cluster culling (row bands): a mesh's primitives in runs of TRI_CLUSTER_PRIMS, each with the object-
 // space box of the vertices it references and their mesh-local index range, computed once at upload.
-// Per frame k_cull marks the (draw, cluster) pairs whose projected box can reach the context's rows;
+// Per frame the k_vertex waves mark the (draw, cluster) pairs whose projected box can reach the rows;
 // k_setup skips primitives of unmarked clusters before their index fetch, and k_vertex skips each 256-
 // slot vertex block none of whose referencing clusters is marked (TriVertexBlock interval).
 #define TRI_CLUSTER_PRIMS 512
@@ -196,7 +196,7 @@ struct TriFrameParams {
     tri_material_record mat0;
     TriShadeConst sc;
     TriDrawDev draw0;  // the draw when one_draw (its vertex and primitive slots start at 0)
-    // cluster culling (row bands): k_cull over ncl_total (draw, cluster) pairs; cull_vertex also lets
+    // cluster culling (row bands): k_vertex marks ncl_total (draw, cluster) pairs; cull_vertex also lets
     // k_vertex skip vertex blocks (off while the shadow pre-pass needs every caster)
     uint32_t cull_on, cull_vertex, ncl_total, pad_c;
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins

@@ -122,6 +122,11 @@ __device__ __forceinline__ void shadow_vertex(const TriFrameParams& fp, const Tr
     b.lsnap[slot] = sn;
 }
 
+// Lanes of mask m below this lane (v_mbcnt).
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 __device__ __forceinline__ void reset_counters(TriCounters* c) {
     c->ovf_records = 0; c->ovf_verts = 0; c->tris_setup = 0; c->tris_clipped = 0;
     c->bin_entries = 0;  // `flags` / `bin_max` are sticky (cleared by the host)
@@ -199,83 +204,87 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
     if (fp.shadow_on) shadow_vertex(fp, b, slot, world);
 }
 
-// Cluster culling: is the 256-slot vertex block holding draw-local slot `local` referenced by a
-// (draw, cluster) pair k_cull marked? (The block's interval covers every cluster whose index range
-// meets it, so a vertex of any visible primitive is always transformed.)
-__device__ __forceinline__ bool vertex_needed(const TriDeviceBuffers& b, const TriDrawDev& dr, uint32_t cbase,
-                                              uint32_t local) {
-    const uint2 iv = b.vblk[dr.vblk_first + (local / TRI_VBLOCK)];
-    for (uint32_t c = iv.x; c <= iv.y; ++c)
-        if (b.cvis[cbase + c]) return true;
-    return false;
+// Cluster culling (row bands). A cluster's object-space box goes through (P * V) * M; when every corner
+// is in front of the eye (w > 0 over the whole box, w being affine) the box's image is bounded by its
+// corners' images, and a cluster whose bound misses the context's rows or columns (2-pixel margin), or
+// lies wholly before z = 0 or beyond z = w, has no fragment here: k_setup skips its primitives (exactly
+// what their set-up would conclude). Skinned draws move their vertices off the boxes and are kept.
+__device__ __forceinline__ bool cluster_visible(const TriFrameParams& fp, const TriDrawDev& dr, const TriCluster& c) {
+    if (c.lo[0] > c.hi[0]) return false;  // no valid vertex: every primitive of the cluster is dropped anyway
+    if (dr.bone_count > 0) return true;
+    float m[16];  // (P * V) * M, column-major
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            m[4 * j + r] = fp.pv[r] * dr.model[4 * j] + fp.pv[4 + r] * dr.model[4 * j + 1] +
+                           fp.pv[8 + r] * dr.model[4 * j + 2] + fp.pv[12 + r] * dr.model[4 * j + 3];
+    float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY, z0 = INFINITY, z1 = -INFINITY;
+    bool front = true;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const float px = (k & 1) ? c.hi[0] : c.lo[0], py = (k & 2) ? c.hi[1] : c.lo[1], pz = (k & 4) ? c.hi[2] : c.lo[2];
+        const float cx = m[0] * px + m[4] * py + m[8] * pz + m[12];
+        const float cy = m[1] * px + m[5] * py + m[9] * pz + m[13];
+        const float cz = m[2] * px + m[6] * py + m[10] * pz + m[14];
+        const float cw = m[3] * px + m[7] * py + m[11] * pz + m[15];
+        front = front && cw > 1e-4f;
+        const float iw = 1.0f / cw;
+        x0 = fminf(x0, cx * iw); x1 = fmaxf(x1, cx * iw);
+        y0 = fminf(y0, cy * iw); y1 = fmaxf(y1, cy * iw);
+        z0 = fminf(z0, cz * iw); z1 = fmaxf(z1, cz * iw);
+    }
+    if (!front) return true;
+    const float wx0 = x0 * fp.hw + fp.hw, wx1 = x1 * fp.hw + fp.hw;
+    const float wy0 = y0 * fp.hh + fp.hh, wy1 = y1 * fp.hh + fp.hh;
+    return !(wy1 < (float)fp.y0 - 2.0f || wy0 > (float)fp.y1 + 2.0f || wx1 < -2.0f || wx0 > (float)fp.W + 2.0f ||
+             z1 < 0.0f || z0 > 1.0f);
 }
 
+// One lane per vertex slot. With cluster culling on, each wave first evaluates, lane-parallel, the
+// clusters whose index range meets its 256-slot vertex block(s) (per-mesh interval table), stores their
+// visibility for k_setup (waves sharing a cluster store the same flag) and, unless the shadow pre-pass
+// needs every caster, skips a block that no visible cluster references: the vertex of any visible
+// primitive is always transformed, since its cluster's range contains it.
 __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
     const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
     if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
-    if (slot >= fp.nslots) return;
-    if (fp.one_draw) {  // the draw's constants are kernel arguments: scalar loads, no dependent fetch
-        if (fp.cull_vertex && !vertex_needed(b, fp.draw0, 0u, slot)) return;
-        vertex_slot(fp, b, slot, fp.draw0, 0u);
-    } else {
-        const int d = find_range(b.draw_vbase, (int)fp.ndraws, slot);
-        const TriDrawDev& dr = b.draws[d];
-        if (fp.cull_vertex && !vertex_needed(b, dr, b.draw_cbase[d], slot - b.draw_vbase[d])) return;
-        vertex_slot(fp, b, slot, dr, b.draw_vbase[d]);
+    const bool valid = slot < fp.nslots;
+    int d = 0;
+    uint32_t vbase = 0;
+    if (valid && !fp.one_draw) {
+        d = find_range(b.draw_vbase, (int)fp.ndraws, slot);
+        vbase = b.draw_vbase[d];
     }
-}
-
-// Cluster culling (row bands): one lane per (draw, cluster) pair. The cluster's object-space box goes
-// through (P * V) * M; when every corner is in front of the eye (w > 0 over the whole box, w being
-// affine) the box's image is bounded by its corners' images, and a cluster whose bound misses the
-// context's rows or columns (2-pixel margin), or lies wholly before z = 0 or beyond z = w, has no
-// fragment here: its primitives are skipped by k_setup (exactly what their set-up would conclude).
-// Skinned draws move their vertices off the boxes and are always kept.
-__global__ __launch_bounds__(TRI_BLOCK) void k_cull(TriFrameParams fp, TriDeviceBuffers b) {
-    const uint32_t i = blockIdx.x * TRI_BLOCK + threadIdx.x;
-    if (i >= fp.ncl_total) return;
-    const TriDrawDev* dr = &fp.draw0;
-    uint32_t cb = 0;
-    if (!fp.one_draw) {
-        const int d = find_range(b.draw_cbase, (int)fp.ndraws, i);
-        dr = &b.draws[d];
-        cb = b.draw_cbase[d];
-    }
-    const TriCluster c = b.clusters[dr->cl_first + (i - cb)];
-    bool vis = true;
-    if (c.lo[0] > c.hi[0]) {  // no valid vertex: every primitive of the cluster is dropped anyway
-        vis = false;
-    } else if (dr->bone_count <= 0) {
-        float m[16];  // (P * V) * M, column-major
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                m[4 * j + r] = fp.pv[r] * dr->model[4 * j] + fp.pv[4 + r] * dr->model[4 * j + 1] +
-                               fp.pv[8 + r] * dr->model[4 * j + 2] + fp.pv[12 + r] * dr->model[4 * j + 3];
-        float x0 = INFINITY, x1 = -INFINITY, y0 = INFINITY, y1 = -INFINITY, z0 = INFINITY, z1 = -INFINITY;
-        bool front = true;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const float px = (k & 1) ? c.hi[0] : c.lo[0], py = (k & 2) ? c.hi[1] : c.lo[1], pz = (k & 4) ? c.hi[2] : c.lo[2];
-            const float cx = m[0] * px + m[4] * py + m[8] * pz + m[12];
-            const float cy = m[1] * px + m[5] * py + m[9] * pz + m[13];
-            const float cz = m[2] * px + m[6] * py + m[10] * pz + m[14];
-            const float cw = m[3] * px + m[7] * py + m[11] * pz + m[15];
-            front = front && cw > 1e-4f;
-            const float iw = 1.0f / cw;
-            x0 = fminf(x0, cx * iw); x1 = fmaxf(x1, cx * iw);
-            y0 = fminf(y0, cy * iw); y1 = fmaxf(y1, cy * iw);
-            z0 = fminf(z0, cz * iw); z1 = fmaxf(z1, cz * iw);
-        }
-        if (front) {
-            const float wx0 = x0 * fp.hw + fp.hw, wx1 = x1 * fp.hw + fp.hw;
-            const float wy0 = y0 * fp.hh + fp.hh, wy1 = y1 * fp.hh + fp.hh;
-            vis = !(wy1 < (float)fp.y0 - 2.0f || wy0 > (float)fp.y1 + 2.0f || wx1 < -2.0f || wx0 > (float)fp.W + 2.0f ||
-                    z1 < 0.0f || z0 > 1.0f);
+    bool needed = true;
+    if (fp.cull_on) {  // uniform
+        const uint32_t lane = lanes_below(~0ull);
+        const uint32_t blk = (slot - vbase) / TRI_VBLOCK;
+        uint64_t pending = __ballot(valid);
+        while (pending) {  // the wave's distinct (draw, block) groups, usually one
+            const int l = __builtin_ctzll(pending);
+            const int gd = __builtin_amdgcn_readlane(d, l);
+            const uint32_t gb = (uint32_t)__builtin_amdgcn_readlane((int)blk, l);
+            const bool mine = valid && d == gd && blk == gb;
+            pending &= ~__ballot(mine);
+            const TriDrawDev& dr = fp.one_draw ? fp.draw0 : b.draws[gd];
+            const uint32_t cb = fp.one_draw ? 0u : b.draw_cbase[gd];
+            const uint2 iv = b.vblk[dr.vblk_first + gb];
+            bool any = false;
+            for (uint32_t c0 = iv.x; iv.x <= iv.y && c0 <= iv.y; c0 += 64) {
+                const uint32_t c = c0 + lane;
+                bool v = false;
+                if (c <= iv.y) {
+                    v = cluster_visible(fp, dr, b.clusters[dr.cl_first + c]);
+                    b.cvis[cb + c] = v ? 1u : 0u;
+                }
+                any = any || __ballot(v) != 0;
+            }
+            if (mine) needed = any;
         }
     }
-    b.cvis[i] = vis ? 1u : 0u;
+    if (!valid || (fp.cull_vertex && !needed)) return;
+    vertex_slot(fp, b, slot, fp.one_draw ? fp.draw0 : b.draws[d], vbase);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -368,9 +377,6 @@ __device__ __forceinline__ void note_bin_overflow(const TriDeviceBuffers& b, uin
 // wave that target the same bin form a group; each group's leader issues ONE atomicAdd for the whole
 // group (all leaders at once, one round trip), and members take consecutive slots after it. Must be
 // reached by the whole wave (uniform control flow).
-__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
-    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
 
 // Reservation plan (ALU and ballots only): each wanting lane learns its group's leader lane and its
 // rank in the group; a leader learns its group's size.
@@ -1866,8 +1872,6 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         }
     };
     rec(kStageVertex);
-    if (fp.cull_on && fp.ncl_total > 0)
-        hipLaunchKernelGGL(k_cull, dim3((fp.ncl_total + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
     if (fp.nslots > 0)
         hipLaunchKernelGGL(k_vertex, dim3((fp.nslots + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
     else

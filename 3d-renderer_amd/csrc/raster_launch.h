@@ -33,7 +33,7 @@ struct TriDeviceBuffers {
     const TriCluster* clusters;  // all meshes' clusters
     const uint2* vblk;           // per mesh vertex block: [first, last] referencing cluster (mesh-local)
     const uint32_t* draw_cbase;  // ndraws+1: first (draw, cluster) pair of each draw
-    uint32_t* cvis;              // ncl_total visibility flags, written by k_cull each frame
+    uint32_t* cvis;              // ncl_total visibility flags, written by k_vertex each frame
     // shadow-map pre-pass (only when TriFrameParams::shadow_on)
     float4* lpos;                // nslots + ovf_vert_cap: light-NDC position per vertex slot (xyz, 0)
     TriSnap* lsnap;              // nslots: the light-NDC position snapped to the map ({X | outcode << 24, Y, z, 1})

@@ -146,17 +146,38 @@ class BandRenderer:
         self.stream = torch.cuda.Stream(self.dev)
         self.r.set_stream(self.stream.cuda_stream)
         scenes.load_scene(self.r, scene)
+        # the per-frame calls with their ctypes arguments built once (a frame at N = 8 is ~60 us of GPU
+        # work, so Python-side marshalling per call would show up in the frame rate)
+        import ctypes as C
+        from trident_raster import abi
+
+        self._lib, self._ctx = raster.load_library(), self.r._ctx
+        self._ubo = C.byref(scene.ubo)
+        self._clear = C.byref((C.c_float * 4)(*scene.clear))
+        self._draws, self._ndraws = abi.draws_array(scene.draws)
+        self._band_ptrs = {b.data_ptr(): C.c_void_p(b.data_ptr()) for b in self.ring.bands}
+        self._depth_ptr = C.c_void_p(self.depth.data_ptr())
+        self._raster = raster
+
+    def _frame(self):
+        lib, ctx = self._lib, self._ctx
+        band = self.ring.acquire()
+        rc = (lib.tri_bind_output(ctx, self._band_ptrs[band.data_ptr()], self._depth_ptr) or
+              lib.tri_set_frame(ctx, self._ubo, self._clear) or   # per-frame uniform update
+              lib.tri_set_draws(ctx, self._draws, self._ndraws) or  # per-frame draw list (push constants)
+              lib.tri_render(ctx))
+        if rc:
+            self._raster._check(rc)
+        self.ring.publish()
 
     def step(self):
+        if self.world == 1:  # no collective: nothing needs the render stream to be torch's current one
+            self._frame()
+            return
         import torch
 
-        s = self.scene
         with torch.cuda.stream(self.stream):
-            self.r.bind_output(self.ring.acquire().data_ptr(), self.depth.data_ptr())
-            self.r.set_frame(s.ubo, s.clear)  # per-frame uniform update
-            self.r.set_draws(s.draws)         # per-frame draw list (push constants)
-            self.r.render()
-            self.ring.publish()
+            self._frame()
 
     def drain(self):
         import torch
