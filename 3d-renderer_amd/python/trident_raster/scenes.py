@@ -463,9 +463,13 @@ def scene_c5_textured(width=3840, height=2160, n=708, tex_size=2048, shadow_size
     return s
 
 
-def load_scene(rast, scene):
-    """Upload a Scene into a TriRaster or TriGroup (UploadMesh + materials + textures + frame + draws)."""
-    rast.upload_geometry(scene.vertices, scene.indices, scene.meshes)
+def load_scene(rast, scene, geometry=None):
+    """Upload a Scene into a TriRaster or TriGroup (UploadMesh + materials + textures + frame + draws).
+    geometry: a raster.TriGeometry already holding the scene's meshes, bound instead of uploading."""
+    if geometry is not None:
+        rast.bind_geometry(geometry)
+    else:
+        rast.upload_geometry(scene.vertices, scene.indices, scene.meshes)
     rast.upload_materials(scene.materials)
     for slot, tex in scene.textures:
         rast.upload_texture(slot, tex)

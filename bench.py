@@ -85,9 +85,9 @@ class GatherRing:
     render stream waits for frame k's gather (work.wait() is a stream wait; the host does not
     block). Throughput is then max(render, gather) per frame instead of their sum."""
 
-    def __init__(self, world, band_elems, frame_elems, make, mode="gather", rank=0, dst=0):
+    def __init__(self, world, band_elems, frame_elems, make, mode="gather", rank=0, dst=0, nbuf=None):
         self.world, self.mode, self.rank, self.dst = world, mode, rank, dst
-        self.nbuf = 2 if world > 1 else 1
+        self.nbuf = nbuf if nbuf else (2 if world > 1 else 1)
         self.bands = [make(band_elems) for _ in range(self.nbuf)]
         keeps_frame = world > 1 and (mode == "allgather" or rank == dst)
         self.frames = [make(frame_elems) for _ in range(self.nbuf)] if keeps_frame else self.bands
@@ -123,46 +123,58 @@ class GatherRing:
 
 class BandRenderer:
     """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers, assembled
-    by a GatherRing."""
+    by a GatherRing. `inflight` contexts take frames in turn, each on its own stream with its own work
+    buffers and one shared copy of the geometry (tri_geometry), so frame k+1's front end (vertex, set-up)
+    runs while frame k rasterises — the reference also keeps several frames in flight
+    (Renderer::DrawFrame waits on the fence of the frame in flight two frames back, Renderer.cpp:752-772)."""
 
-    def __init__(self, scene, rank, world, device_index, band_world=None, assembly="gather"):
+    def __init__(self, scene, rank, world, device_index, band_world=None, assembly="gather", inflight=1):
+        import ctypes as C
+
         import torch
-        from trident_raster import raster, scenes
+        from trident_raster import abi, raster, scenes
 
         H, W = scene.height, scene.width
         self.band = band_rows(H, band_world or world, rank)
         rows = self.band[1] - self.band[0]
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
         self.dev = torch.device("cuda", device_index)
+        self.inflight = max(1, inflight)
         self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
-                               mode=assembly, rank=rank)
-        self.depth = torch.empty(rows * W, dtype=torch.float32, device=self.dev)
-        self.r = raster.TriRaster(W, H, band=self.band, device=device_index)
-        # A dedicated render stream (a non-zero handle) that is torch's current stream while a frame is
-        # enqueued and published: RCCL's all-gather then waits on the stream k_raster wrote the band on,
-        # and work.wait() in GatherRing.acquire orders that same stream behind the gather that read the
-        # slot. (Torch's default stream is handle 0, which tri_set_stream takes as "the context's own
-        # non-blocking stream" — unordered with the collective.)
-        self.stream = torch.cuda.Stream(self.dev)
-        self.r.set_stream(self.stream.cuda_stream)
-        scenes.load_scene(self.r, scene)
+                               mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1))
+        self.depth = [torch.empty(rows * W, dtype=torch.float32, device=self.dev) for _ in range(self.inflight)]
+        self.geometry = raster.TriGeometry(device_index)
+        self.geometry.upload(scene.vertices, scene.indices, scene.meshes)
+        # Each context renders on a dedicated torch stream (a non-zero handle) that is torch's current
+        # stream while its frame is enqueued and published: the collective then waits on the stream
+        # k_raster wrote the band on, and work.wait() in GatherRing.acquire orders that same stream behind
+        # the gather that read the slot. (Torch's default stream is handle 0, which tri_set_stream takes
+        # as "the context's own non-blocking stream" — unordered with the collective.)
+        self.rs, self.streams = [], []
+        for _ in range(self.inflight):
+            r = raster.TriRaster(W, H, band=self.band, device=device_index)
+            st = torch.cuda.Stream(self.dev)
+            r.set_stream(st.cuda_stream)
+            scenes.load_scene(r, scene, geometry=self.geometry)
+            self.rs.append(r)
+            self.streams.append(st)
+        self.r = self.rs[0]
         # the per-frame calls with their ctypes arguments built once (a frame at N = 8 is ~60 us of GPU
         # work, so Python-side marshalling per call would show up in the frame rate)
-        import ctypes as C
-        from trident_raster import abi
-
-        self._lib, self._ctx = raster.load_library(), self.r._ctx
+        self._lib = raster.load_library()
+        self._ctxs = [r._ctx for r in self.rs]
         self._ubo = C.byref(scene.ubo)
         self._clear = C.byref((C.c_float * 4)(*scene.clear))
         self._draws, self._ndraws = abi.draws_array(scene.draws)
         self._band_ptrs = {b.data_ptr(): C.c_void_p(b.data_ptr()) for b in self.ring.bands}
-        self._depth_ptr = C.c_void_p(self.depth.data_ptr())
+        self._depth_ptrs = [C.c_void_p(d.data_ptr()) for d in self.depth]
         self._raster = raster
+        self.frames = 0
 
-    def _frame(self):
-        lib, ctx = self._lib, self._ctx
+    def _frame(self, i):
+        lib, ctx = self._lib, self._ctxs[i]
         band = self.ring.acquire()
-        rc = (lib.tri_bind_output(ctx, self._band_ptrs[band.data_ptr()], self._depth_ptr) or
+        rc = (lib.tri_bind_output(ctx, self._band_ptrs[band.data_ptr()], self._depth_ptrs[i]) or
               lib.tri_set_frame(ctx, self._ubo, self._clear) or   # per-frame uniform update
               lib.tri_set_draws(ctx, self._draws, self._ndraws) or  # per-frame draw list (push constants)
               lib.tri_render(ctx))
@@ -170,19 +182,36 @@ class BandRenderer:
             self._raster._check(rc)
         self.ring.publish()
 
-    def step(self):
-        if self.world == 1:  # no collective: nothing needs the render stream to be torch's current one
-            self._frame()
+    def step(self, first_only=False):
+        """One frame, on the next context in turn (first_only: always context 0, no overlap)."""
+        i = 0 if first_only else self.frames % self.inflight
+        self.frames += 1
+        if self.world == 1 and self.inflight == 1:  # no collective, one stream: no torch stream context needed
+            self._frame(i)
             return
         import torch
 
-        with torch.cuda.stream(self.stream):
-            self._frame()
+        with torch.cuda.stream(self.streams[i]):
+            self._frame(i)
+
+    def warm(self):
+        """One synchronous frame per context (sizes the internal queues; re-renders after TRI_E_OVERFLOW)."""
+        for r in self.rs:
+            r.render_frame()
+
+    def synchronize(self):
+        for r in self.rs:
+            r.synchronize()
+
+    def close(self):
+        for r in self.rs:
+            r.close()
+        self.geometry.close()
 
     def drain(self):
         import torch
 
-        with torch.cuda.stream(self.stream):
+        with torch.cuda.stream(self.streams[0]):
             self.ring.drain()
 
     def latency_ms(self, frames=20):
@@ -209,11 +238,11 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256):
     short timed run would leave."""
     import torch
 
-    br.r.render_frame()  # first frame sizes the internal queues (re-renders after TRI_E_OVERFLOW)
+    br.warm()  # first frame per context sizes the internal queues (re-renders after TRI_E_OVERFLOW)
     for _ in range(warmup):
         br.step()
     br.drain()
-    br.r.synchronize()
+    br.synchronize()
     torch.cuda.synchronize(br.dev)
     if dist_on:
         import torch.distributed as dist
@@ -227,12 +256,12 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256):
     if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
-    br.r.synchronize()  # surfaces TRI_E_OVERFLOW if any timed frame overflowed
+    br.synchronize()  # surfaces TRI_E_OVERFLOW if any timed frame overflowed
     timing = None
-    if stage_timing:
+    if stage_timing:  # per-kernel durations: context 0 alone, frames back to back without overlap
         br.r.set_timing(True, 1)
         for _ in range(event_frames):
-            br.step()
+            br.step(first_only=True)
         br.drain()
         timing = br.r.timing()
         br.r.set_timing(False)
@@ -327,6 +356,8 @@ def main():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostics (1 GPU, no collective): render only band --sim-rank of an N-way split")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="frames in flight per rank (contexts taking frames in turn, one stream each)")
     ap.add_argument("--assembly", choices=("gather", "allgather"), default="gather",
                     help="N > 1: bands gathered onto the display rank 0 (default) or all-gathered onto every rank")
     ap.add_argument("--no-stage-timing", action="store_true",
@@ -349,9 +380,9 @@ def main():
 
     scene = build_scene(args.config)
     if args.sim_world and world == 1:
-        br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world)
+        br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=args.inflight)
     else:
-        br = BandRenderer(scene, rank, world, local, assembly=args.assembly)
+        br = BandRenderer(scene, rank, world, local, assembly=args.assembly, inflight=args.inflight)
     dt, timing = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing)
     fps = args.steps / dt
     W, H = scene.width, scene.height
@@ -374,7 +405,7 @@ def main():
     if not args.no_secondary and args.config == "c3":
         for key in ("c2", "c5"):  # the other BASELINE.json GPU configs, same timing protocol
             s2 = build_scene(key)
-            br2 = BandRenderer(s2, rank, world, local, assembly=args.assembly)
+            br2 = BandRenderer(s2, rank, world, local, assembly=args.assembly, inflight=args.inflight)
             n2 = max(args.steps, 50) if key == "c2" else max(args.steps // 2, 20)
             dt2, t2 = timed_run(br2, n2, args.warmup, dist_on)
             fps2 = n2 / dt2
@@ -387,7 +418,7 @@ def main():
             if s2.textures:
                 entry["textures"] = f"{len(s2.textures)} x {s2.textures[0][1].shape[0]}^2 sRGB, bilinear REPEAT"
             secondary[s2.name] = entry
-            br2.r.close()
+            br2.close()
             del br2
 
     cpu = None
@@ -410,7 +441,7 @@ def main():
             "data": "synthetic (procedural PCG32-seeded scene; reference Assimp assets absent)",
             "config": {"workload": scene.name, "width": W, "height": H, "triangles": scene.triangles,
                        "vertices": int(scene.vertices.shape[0]), "bin": stats["bin_size"],
-                       "skybox": skybox_name(scene),
+                       "skybox": skybox_name(scene), "frames_in_flight": args.inflight,
                        "parallelism": (f"row-band x{world} + RCCL {'gather to rank 0' if args.assembly == 'gather' else 'all-gather'}"
                                        if world > 1 else "single GPU")},
             "mpix_per_s": fps * W * H / 1e6,
@@ -430,7 +461,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
-    br.r.close()
+    br.close()
     if dist_on:
         import torch.distributed as dist
 

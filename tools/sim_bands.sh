@@ -4,7 +4,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for spec in "1 0" "2 0" "4 0" "4 2" "8 0" "8 4" "8 7"; do
   set -- $spec
-  timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary --sim-world $1 --sim-rank $2 \
+  timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary --sim-world $1 --sim-rank $2 --inflight ${INFLIGHT:-2} \
     > gpurun_out/sim_$1_$2.log 2>&1 || { echo "sim $spec failed"; tail -3 gpurun_out/sim_$1_$2.log; exit 1; }
   python3 -c "
 import json; d=json.loads(open('gpurun_out/sim_$1_$2.log').read().strip().splitlines()[-1])
