@@ -580,22 +580,74 @@ __device__ __forceinline__ void note_shadow_bin_overflow(const TriDeviceBuffers&
 #ifndef TRI_SETUP_WAVES
 #define TRI_SETUP_WAVES 7  // k_setup occupancy target (waves per SIMD)
 #endif
-// SHADOW = the shadow pre-pass's set-up (oracle shadow_raster_triangle): the light-NDC snaps, no
-// culling, no clipping (guard-band violators are dropped), bins of the s_size^2 map's own queues.
-// LPOS (main pass with the pre-pass on): clipped polygon vertices also get light-space positions
-// (a separate instantiation keeps that code, and its registers, out of frames without shadows).
-template <bool SHADOW, bool LPOS>
+
+// The lane's bin-queue entries, one per round: triangle 0's bbox bins, then triangle 1's. A batch of
+// kResBatch rounds is planned with ballots and its reservations (one returning atomic per (wave, bin))
+// are all issued before any result is used, so a wave waits for one atomic round trip per batch instead
+// of one per round. Must be reached by the whole wave. Diagnostics: TRI_ABLATE=8 waits per round.
+template <bool SHADOW_QUEUES>
+__device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bool ok1, uint2 br0, uint2 br1, uint32_t p0,
+                                         uint32_t p1, uint32_t nbx, uint32_t* bin_count, uint32_t* bin_list, uint32_t cap,
+                                         uint32_t lane, uint32_t& nentries) {
+    bool has = (ok0 || ok1) && !(kAblate & 4);  // diagnostics: 4 = setup without binning
+    bool second = !ok0;
+    uint2 cur = second ? br1 : br0;
+    uint32_t bx = cur.x & 0xFFFFu, by = cur.x >> 16;
+    uint32_t bx0 = bx, bx1 = cur.y & 0xFFFFu, by1 = cur.y >> 16;
+    const int batch = (kAblate & 8) ? 1 : kResBatch;
+    while (__ballot(has)) {
+        uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch], rent[kResBatch];
+        bool rwant[kResBatch];
+#pragma unroll
+        for (int r = 0; r < kResBatch; ++r) {
+            rwant[r] = has && r < batch;
+            rbin[r] = by * nbx + bx;
+            rent[r] = second ? p1 : p0;
+            if (rwant[r]) {
+                if (bx < bx1) {
+                    ++bx;
+                } else if (by < by1) {
+                    bx = bx0;
+                    ++by;
+                } else if (!second && ok1) {
+                    second = true;
+                    bx = bx0 = br1.x & 0xFFFFu; by = br1.x >> 16;
+                    bx1 = br1.y & 0xFFFFu; by1 = br1.y >> 16;
+                } else {
+                    has = false;
+                }
+            }
+            uint32_t cnt;
+            wave_reserve_plan(rbin[r], rwant[r], rlead[r], rrank[r], cnt);
+            rbase[r] = 0;
+            if (rwant[r] && lane == rlead[r] && !(kAblate & 16))  // diagnostics: 16 = no atomics
+                rbase[r] = atomicAdd(&bin_count[rbin[r]], cnt);
+        }
+#pragma unroll
+        for (int r = 0; r < kResBatch; ++r) {
+            const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
+            if (rwant[r]) {
+                if (kAblate & 32) continue;  // diagnostics: 32 = no queue stores
+                if (pos < cap) bin_list[(size_t)rbin[r] * cap + pos] = rent[r];
+                else if (SHADOW_QUEUES) note_shadow_bin_overflow(b, pos + 1);
+                else note_bin_overflow(b, pos + 1);
+                ++nentries;
+            }
+        }
+    }
+}
+
+// WITH_SHADOW (frames with the shadow pre-pass): the same index fetch also sets up every primitive
+// for the map (oracle shadow_raster_triangle: light-NDC snaps, no culling, no clipping, guard-band
+// violators dropped) and bins it into the map's own queues; clipped polygon vertices get light-space
+// positions. A separate instantiation keeps that code, and its registers, out of other frames.
+template <bool WITH_SHADOW>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t red[2];
-    __shared__ float clip_poly[SHADOW ? 1 : kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
+    __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
     __syncthreads();
-    uint32_t nsetup = 0, nentries = 0;
-    const uint32_t cap = SHADOW ? fp.s_bin_cap : fp.bin_cap;
-    const uint32_t nbx = SHADOW ? fp.s_nbx : (uint32_t)fp.nbx;
-    uint32_t* const bin_count = SHADOW ? b.sbin_count : b.bin_count;
-    uint32_t* const bin_list = SHADOW ? b.sbin_list : b.bin_list;
-    const TriSnap* const snp = SHADOW ? b.lsnap : b.snap;
+    uint32_t nsetup = 0, nentries = 0, sentries = 0;
     const uint32_t lane = lanes_below(~0ull);
     // Spread concurrently running workgroups over the primitive stream: meshes are usually
     // index-ordered in screen space, and neighbouring chunks hammering the same bin counters
@@ -607,14 +659,15 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     // batch), so a wave's dependent latencies are paid once for two primitives.
     for (int k = 0; k < fp.ppt; k += 2) {  // uniform trip count: the reservations need the whole wave
         uint32_t p[2], sl0[2], sl1[2], sl2[2];
-        bool ok[2], needs_clip[2];
-        uint2 br[2];
+        bool ok[2], needs_clip[2], sok[2];
+        uint2 br[2], sbr[2];
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             p[t] = chunk0 + (k + t) * TRI_BLOCK + threadIdx.x;
-            ok[t] = false; needs_clip[t] = false;
+            ok[t] = false; needs_clip[t] = false; sok[t] = false;
             sl0[t] = sl1[t] = sl2[t] = 0;
             br[t] = make_uint2(0u, 0u);
+            sbr[t] = make_uint2(0u, 0u);
             bool culled = false;
             int d = 0;
             const uint32_t* ip = nullptr;
@@ -623,47 +676,53 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 if (fp.one_draw) {  // kernel-argument constants: the index fetch starts at once
                     ip = b.indices + fp.draw0.first_index + 3u * p[t];
                     vb = 0u - fp.draw0.min_index;
-                    if (!SHADOW && fp.cull_on) culled = !b.cvis[p[t] / TRI_CLUSTER_PRIMS];
+                    if (fp.cull_on) culled = !b.cvis[p[t] / TRI_CLUSTER_PRIMS];
                 } else {
                     d = find_range(b.draw_pbase, (int)fp.ndraws, p[t]);
                     const TriDrawDev& dr = b.draws[d];
                     const uint32_t lp = p[t] - b.draw_pbase[d];
                     ip = b.indices + dr.first_index + 3u * lp;
                     vb = b.draw_vbase[d] - dr.min_index;
-                    if (!SHADOW && fp.cull_on) culled = !b.cvis[b.draw_cbase[d] + lp / TRI_CLUSTER_PRIMS];
+                    if (fp.cull_on) culled = !b.cvis[b.draw_cbase[d] + lp / TRI_CLUSTER_PRIMS];
                 }
             }
-            if (p[t] < fp.nprims && !culled) {
+            // a primitive culled for the context's rows may still cast a shadow into the map
+            if (p[t] < fp.nprims && (!culled || WITH_SHADOW)) {
                 sl0[t] = vb + ip[0]; sl1[t] = vb + ip[1]; sl2[t] = vb + ip[2];
-                const TriSnap a0 = snp[sl0[t]], a1 = snp[sl1[t]], a2 = snp[sl2[t]];
-                const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
-                // invalid vertex, or trivial reject: all three vertices outside one clip half-space
-                if constexpr (SHADOW) {
-                    if (!((oc0 | oc1 | oc2) & (TRI_OC_BAD | TRI_OC_CLIP)) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
-                        const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
-                        const int32_t Y[3] = {a0.y, a1.y, a2.y};
-                        ok[t] = shadow_bins(fp, X, Y, br[t]);
-                        if (ok[t]) b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d);
-                    }
-                } else if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
-                    if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
-                        b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | TRI_PRIM_CLIPPED);
-                        needs_clip[t] = true;
-                    } else {
-                        const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
-                        const int32_t Y[3] = {a0.y, a1.y, a2.y};
-                        const float z[3] = {a0.z, a1.z, a2.z};
-                        const float iw[3] = {a0.iw, a1.iw, a2.iw};
-                        TriRec r;
-                        ok[t] = setup_snapped(fp, X, Y, z, iw, sl0[t], sl1[t], sl2[t], p[t] << 3, r, br[t]);
-                        if (ok[t]) b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d);
+                if (!culled) {
+                    const TriSnap a0 = b.snap[sl0[t]], a1 = b.snap[sl1[t]], a2 = b.snap[sl2[t]];
+                    const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
+                    // invalid vertex, or trivial reject: all three vertices outside one clip half-space
+                    if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
+                        if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
+                            needs_clip[t] = true;
+                        } else {
+                            const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
+                            const int32_t Y[3] = {a0.y, a1.y, a2.y};
+                            const float z[3] = {a0.z, a1.z, a2.z};
+                            const float iw[3] = {a0.iw, a1.iw, a2.iw};
+                            TriRec r;
+                            ok[t] = setup_snapped(fp, X, Y, z, iw, sl0[t], sl1[t], sl2[t], p[t] << 3, r, br[t]);
+                        }
                     }
                 }
+                if constexpr (WITH_SHADOW) {
+                    const TriSnap l0 = b.lsnap[sl0[t]], l1 = b.lsnap[sl1[t]], l2 = b.lsnap[sl2[t]];
+                    const uint32_t oc0 = (uint32_t)l0.xo >> 24, oc1 = (uint32_t)l1.xo >> 24, oc2 = (uint32_t)l2.xo >> 24;
+                    if (!((oc0 | oc1 | oc2) & (TRI_OC_BAD | TRI_OC_CLIP)) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
+                        const int32_t X[3] = {(l0.xo << 8) >> 8, (l1.xo << 8) >> 8, (l2.xo << 8) >> 8};
+                        const int32_t Y[3] = {l0.y, l1.y, l2.y};
+                        sok[t] = shadow_bins(fp, X, Y, sbr[t]);
+                    }
+                }
+                // k_raster's (and k_shadow_raster's) route from the primitive to its vertex slots
+                if (ok[t] || needs_clip[t] || sok[t])
+                    b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | (needs_clip[t] ? TRI_PRIM_CLIPPED : 0u));
             }
             nsetup += ok[t] ? 1u : 0u;
         }
 #pragma unroll
-        for (int t = 0; t < 2 && !SHADOW; ++t) {
+        for (int t = 0; t < 2; ++t) {
             uint64_t cm = __ballot(needs_clip[t]);  // rare: the wave clips its primitives one at a time
             if (cm) {
                 if (lane == 0) atomicAdd(&b.counters->tris_clipped, (uint32_t)__builtin_popcountll(cm));
@@ -671,73 +730,25 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 while (cm) {
                     const int src = __builtin_ctzll(cm);
                     cm &= cm - 1;
-                    clip_prim_wave<LPOS>(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
-                                   (uint32_t)__builtin_amdgcn_readlane((int)sl0[t], src),
-                                   (uint32_t)__builtin_amdgcn_readlane((int)sl1[t], src),
-                                   (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src), nsetup, nentries);
+                    clip_prim_wave<WITH_SHADOW>(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
+                                                (uint32_t)__builtin_amdgcn_readlane((int)sl0[t], src),
+                                                (uint32_t)__builtin_amdgcn_readlane((int)sl1[t], src),
+                                                (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src), nsetup, nentries);
                 }
             }
         }
-        // The lane's bins, one per round: triangle 0's bbox, then triangle 1's.
-        bool has = (ok[0] || ok[1]) && !(kAblate & 4);  // diagnostics: 4 = setup without binning
-        bool second = !ok[0];
-        uint2 cur = second ? br[1] : br[0];
-        uint32_t bx = cur.x & 0xFFFFu, by = cur.x >> 16;
-        uint32_t bx0 = bx, bx1 = cur.y & 0xFFFFu, by1 = cur.y >> 16;
-        // A batch of kResBatch rounds is planned with ballots and its reservations (one returning
-        // atomic per (wave, bin)) are all issued before any result is used, so a wave waits for one
-        // atomic round trip per batch instead of one per round. Diagnostics: TRI_ABLATE=8 waits per
-        // round (batches of one).
-        const int batch = (kAblate & 8) ? 1 : kResBatch;
-        while (__ballot(has)) {
-            uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch], rent[kResBatch];
-            bool rwant[kResBatch];
-#pragma unroll
-            for (int r = 0; r < kResBatch; ++r) {
-                rwant[r] = has && r < batch;
-                rbin[r] = by * nbx + bx;
-                rent[r] = second ? p[1] : p[0];
-                if (rwant[r]) {
-                    if (bx < bx1) {
-                        ++bx;
-                    } else if (by < by1) {
-                        bx = bx0;
-                        ++by;
-                    } else if (!second && ok[1]) {
-                        second = true;
-                        bx = bx0 = br[1].x & 0xFFFFu; by = br[1].x >> 16;
-                        bx1 = br[1].y & 0xFFFFu; by1 = br[1].y >> 16;
-                    } else {
-                        has = false;
-                    }
-                }
-                uint32_t cnt;
-                wave_reserve_plan(rbin[r], rwant[r], rlead[r], rrank[r], cnt);
-                rbase[r] = 0;
-                if (rwant[r] && lane == rlead[r] && !(kAblate & 16))  // diagnostics: 16 = no atomics
-                    rbase[r] = atomicAdd(&bin_count[rbin[r]], cnt);
-            }
-#pragma unroll
-            for (int r = 0; r < kResBatch; ++r) {
-                const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
-                if (rwant[r]) {
-                    if (kAblate & 32) continue;  // diagnostics: 32 = no queue stores
-                    if (pos < cap) bin_list[(size_t)rbin[r] * cap + pos] = rent[r];
-                    else if (SHADOW) note_shadow_bin_overflow(b, pos + 1);
-                    else note_bin_overflow(b, pos + 1);
-                    ++nentries;
-                }
-            }
-        }
+        bin_pair<false>(b, ok[0], ok[1], br[0], br[1], p[0], p[1], (uint32_t)fp.nbx, b.bin_count, b.bin_list,
+                        fp.bin_cap, lane, nentries);
+        if constexpr (WITH_SHADOW)
+            bin_pair<true>(b, sok[0], sok[1], sbr[0], sbr[1], p[0], p[1], fp.s_nbx, b.sbin_count, b.sbin_list,
+                           fp.s_bin_cap, lane, sentries);
     }
-    if constexpr (!SHADOW) {
-        if (nsetup) atomicAdd(&red[0], nsetup);
-        if (nentries) atomicAdd(&red[1], nentries);
-        __syncthreads();
-        // Statistics go to a per-workgroup slot with a plain store: same-address global atomics from
-        // every workgroup serialise across the XCDs (measured: +34 us per frame at 4K/1M).
-        if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(red[0], red[1]);
-    }
+    if (nsetup) atomicAdd(&red[0], nsetup);
+    if (nentries) atomicAdd(&red[1], nentries);
+    __syncthreads();
+    // Statistics go to a per-workgroup slot with a plain store: same-address global atomics from
+    // every workgroup serialise across the XCDs (measured: +34 us per frame at 4K/1M).
+    if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(red[0], red[1]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1863,7 +1874,7 @@ static void launch_raster(const TriFrameParams& fp, const TriDeviceBuffers& b, h
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* ev) {
     static const bool debug_sync = getenv("TRI_DEBUG_SYNC") != nullptr;
-    static const char* names[] = {"vertex", "shadow", "setup", "raster", "end"};
+    static const char* names[] = {"vertex", "shadow raster", "setup", "raster", "end"};
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], stream);
         if (debug_sync) {
@@ -1876,15 +1887,14 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         hipLaunchKernelGGL(k_vertex, dim3((fp.nslots + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
     else
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
-    if (fp.shadow_on) {  // shadow pre-pass: set-up + binning into the map's queues, then the depth raster
-        rec(kStageShadow);
-        if (fp.nchunks > 0) hipLaunchKernelGGL((k_setup<true, false>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
-        hipLaunchKernelGGL(k_shadow_raster, dim3(fp.s_nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
-    }
     rec(kStageSetup);
-    if (fp.nchunks > 0) {
-        if (fp.shadow_on) hipLaunchKernelGGL((k_setup<false, true>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_setup<false, false>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
+    if (fp.nchunks > 0) {  // with the pre-pass, one set-up pass bins each primitive for the frame and the map
+        if (fp.shadow_on) hipLaunchKernelGGL((k_setup<true>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_setup<false>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
+    }
+    if (fp.shadow_on) {  // the map's depth raster, before the frame's raster samples it
+        rec(kStageShadow);
+        hipLaunchKernelGGL(k_shadow_raster, dim3(fp.s_nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
     }
     rec(kStageRaster);
     if (fp.bin_log2 == 5) {

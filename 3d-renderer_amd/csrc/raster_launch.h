@@ -42,7 +42,8 @@ struct TriDeviceBuffers {
     uint32_t* shadow_map;        // s_size * s_size float32 depth bits
 };
 
-// Event stamps of one frame: [vertex | shadow pre-pass (when on) | setup + binning + clip | raster].
+// Event stamps of one frame, in launch order: vertex, setup (+ clip, + the shadow map binning), shadow-map
+// raster (only with the pre-pass), raster, end.
 enum TriStage { kStageVertex = 0, kStageShadow, kStageSetup, kStageRaster, kStageCount };
 
 hipError_t tri_kernels_init();

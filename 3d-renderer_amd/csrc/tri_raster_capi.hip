@@ -511,10 +511,10 @@ int collect_timing(tri_ctx* c) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     for (TimingSet& t : c->pending) {
         float ms[kStageCount] = {}, tot;
-        // the shadow stamp exists only for frames that ran the pre-pass
-        HIP_TRY(hipEventElapsedTime(&ms[kStageVertex], t.ev[kStageVertex], t.ev[t.shadow ? kStageShadow : kStageSetup]));
-        if (t.shadow) HIP_TRY(hipEventElapsedTime(&ms[kStageShadow], t.ev[kStageShadow], t.ev[kStageSetup]));
-        HIP_TRY(hipEventElapsedTime(&ms[kStageSetup], t.ev[kStageSetup], t.ev[kStageRaster]));
+        // stamps: vertex | setup (+ the map's binning) | shadow-map raster (only with the pre-pass) | raster
+        HIP_TRY(hipEventElapsedTime(&ms[kStageVertex], t.ev[kStageVertex], t.ev[kStageSetup]));
+        HIP_TRY(hipEventElapsedTime(&ms[kStageSetup], t.ev[kStageSetup], t.ev[t.shadow ? kStageShadow : kStageRaster]));
+        if (t.shadow) HIP_TRY(hipEventElapsedTime(&ms[kStageShadow], t.ev[kStageShadow], t.ev[kStageRaster]));
         HIP_TRY(hipEventElapsedTime(&ms[kStageRaster], t.ev[kStageRaster], t.ev[kStageCount]));
         HIP_TRY(hipEventElapsedTime(&tot, t.ev[0], t.ev[kStageCount]));
         c->acc.ms_vertex += ms[kStageVertex];

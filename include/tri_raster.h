@@ -143,7 +143,8 @@ typedef struct tri_timing {
     uint64_t frames;        /* frames timed since the last reset                  */
     double ms_vertex;       /* vs_transform (+ per-vertex divide / viewport / snap) */
     double ms_setup;        /* tri_setup_bin (setup + cull + per-bin queues)       */
-    double ms_shadow;       /* shadow-map pre-pass (0 without it; clipping is in ms_setup) */
+    double ms_shadow;       /* shadow-map depth raster (0 without the pre-pass; its set-up/binning  *
+                             * shares the set-up pass and is in ms_setup, as is clipping)             */
     double ms_raster;       /* tile_raster_shade (coverage + early-Z + PBR + store) */
     double ms_frame;        /* first kernel start to last kernel end              */
     double reserved;
