@@ -1412,8 +1412,21 @@ __device__ __forceinline__ uint32_t sky_bgra_persp(const TriFrameParams& fp, con
 #ifndef TRI_RASTER_WAVES
 #define TRI_RASTER_WAVES 6  // k_raster occupancy target at 32x32 bins (waves per SIMD)
 #endif
+#ifndef TRI_RASTER_WAVES_SHADOW
+#define TRI_RASTER_WAVES_SHADOW 5  // with the shadow lookup (6 spilled: C5 raster 207 us at 5 vs 213 at 6)
+#endif
 
-constexpr int kBigArea = 96;  // bbox∩bin pixels above which a triangle is rasterized cooperatively
+// bbox∩bin pixels above which a triangle is rasterized by the whole workgroup (cooperatively):
+// 32x32 bins 96 (64: C3 raster 119 -> 143 us; 160: unchanged), 16x16 bins 160 (96 -> 160: C2 raster
+// 41.8 -> 35.7 us, C2 28.4k -> 33.3k fps)
+#ifndef TRI_BIG_AREA
+#define TRI_BIG_AREA 96
+#endif
+#ifndef TRI_BIG_AREA16
+#define TRI_BIG_AREA16 160
+#endif
+template <int BL>
+constexpr int big_area() { return BL == 4 ? TRI_BIG_AREA16 : TRI_BIG_AREA; }
 constexpr int kBigQueue = 1024;
 
 // Bijective XCD-aware block -> bin remap (cdna_hip_programming.md §5 "XCD swizzle must be
@@ -1473,7 +1486,7 @@ __device__ __forceinline__ void cov_row(const CovEntry& c, uint32_t r, uint64_t*
 template <bool EXACT, int BL, bool SHADOW>
 // 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
 // a little); 64x64 bins are LDS-limited to 3
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? TRI_RASTER_WAVES_SHADOW : TRI_RASTER_WAVES) : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
@@ -1525,7 +1538,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
             rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
             if (cx0 <= cx1 && cy0 <= cy1) {
                 bool big = false;
-                if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > kBigArea) {
+                if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
                     const uint32_t q = atomicAdd(&nbig, 1u);
                     if (q < kBigQueue / 2) { bigq[q] = ri; big = true; }
                 }
@@ -1593,7 +1606,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
-        if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > kBigArea) {
+        if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
             if (sub != 0) continue;  // the first lane of the group hands it over
             const uint32_t q = atomicAdd(&nbig, 1u);
             if (q < kBigQueue) { bigq[q] = ri; continue; }
@@ -1788,7 +1801,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TriFrameParams fp, 
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
-        if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > kBigArea) {
+        if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<5>()) {
             if (sub != 0) continue;
             const uint32_t q = atomicAdd(&nbig, 1u);
             if (q < kBigQueue) { bigq[q] = ri; continue; }
