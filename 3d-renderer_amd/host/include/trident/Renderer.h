@@ -93,6 +93,13 @@ public:
     // HIP/GL-interop backend can display. nullptr before the viewport's first frame; valid until its next
     // resize or Shutdown.
     void* GetViewportTexture(uint32_t viewportId) const;
+    // Shadow-map pre-pass (BASELINE config 5): the reference reserves LightComponent::m_ShadowCaster
+    // (LightComponent.h:33) without rendering shadows; here, when the directional light UpdateUniformBuffer
+    // picks (the first enabled one) is a shadow caster, every viewport renders a size x size map fitted
+    // to the visible draws' world box (tri_shadow_fit_ortho) first. 0 disables the pass entirely.
+    void SetShadowMapSize(uint32_t size) { m_ShadowMapSize = size; }
+    // The pre-pass configuration DrawFrame uses this frame (false: no shadow-casting sun).
+    bool BuildShadowConfig(tri_shadow_config& out);
     // How many times the concatenated geometry went to the device: once per UploadMeshFromCache
     // generation, shared by every viewport (the reference binds one vertex/index buffer for all).
     uint64_t GetGeometryUploadCount() const { return m_GeometryUploads; }
@@ -140,6 +147,7 @@ private:
         uint32_t m_Width = 0, m_Height = 0;
         uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0, m_SkyboxGeneration = 0;
         std::vector<float> m_BonePalette;  // the palette last uploaded to this viewport's context
+        tri_shadow_config m_Shadow{};      // the pre-pass configuration last set on this context
         tri_image m_Image{};               // GetViewportTexture's handle (after the first frame)
         bool m_HasImage = false;
     };
@@ -173,6 +181,8 @@ private:
     tri_geometry* m_SharedGeometry = nullptr;  // the device copy every viewport context binds
     uint64_t m_SharedGeometryGeneration = 0;
     uint64_t m_GeometryUploads = 0;
+    std::vector<glm::vec3> m_MeshBoundsMin, m_MeshBoundsMax;  // object-space box per cached mesh
+    uint32_t m_ShadowMapSize = 2048;
     std::vector<tri_vertex> m_VertexBuffer;
     std::vector<uint32_t> m_IndexBuffer;
     uint64_t m_GeometryGeneration = 1, m_TextureGeneration = 1, m_MaterialGeneration = 1;

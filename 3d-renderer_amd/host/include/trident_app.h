@@ -46,6 +46,13 @@ int trident_app_set_entity_bones(trident_app* app, uint32_t entity, const float*
 int trident_app_add_light(trident_app* app, int type, const float position[3], const float direction[3],
                           const float color[3], float intensity, float range, int enabled, uint32_t* entity);
 
+/* LightComponent::m_ShadowCaster of a light entity (LightComponent.h:33): a shadow-casting first
+ * directional light turns on the shadow-map pre-pass (Renderer::SetShadowMapSize, default 2048). */
+int trident_app_set_light_shadow_caster(trident_app* app, uint32_t entity, int caster);
+int trident_app_set_shadow_map_size(trident_app* app, uint32_t size);
+/* The pre-pass configuration DrawFrame would use now (*enabled = 0 when there is none). */
+int trident_app_shadow_config(trident_app* app, tri_shadow_config* out, int* enabled);
+
 /* which: 0 editor, 1 runtime. Runtime camera readiness follows `ready`. */
 int trident_app_set_camera(trident_app* app, int which, const float position[3], const float rotation_deg[3],
                            float fov_deg, float near_clip, float far_clip, int ready);

@@ -275,6 +275,8 @@ void Renderer::UploadMeshFromCache() {  // Renderer.cpp:1965-2116
     m_VertexBuffer.clear();
     m_IndexBuffer.clear();
     m_MeshDrawInfo.clear();
+    m_MeshBoundsMin.clear();
+    m_MeshBoundsMax.clear();
     uint32_t firstIndex = 0;
     int32_t baseVertex = 0;
     for (const Geometry::Mesh& mesh : m_GeometryCache) {
@@ -288,6 +290,17 @@ void Renderer::UploadMeshFromCache() {  // Renderer.cpp:1965-2116
         info.m_BaseVertex = baseVertex;
         info.m_MaterialIndex = mesh.MaterialIndex;
         m_MeshDrawInfo.push_back(info);
+        glm::vec3 lo{INFINITY}, hi{-INFINITY};  // box of the referenced vertices (shadow frustum fit)
+        for (uint32_t idx : mesh.Indices) {
+            if (idx >= mesh.Vertices.size()) continue;
+            const glm::vec3& p = mesh.Vertices[idx].Position;
+            for (int a = 0; a < 3; ++a) {
+                lo[a] = std::min(lo[a], p[a]);
+                hi[a] = std::max(hi[a], p[a]);
+            }
+        }
+        m_MeshBoundsMin.push_back(lo);
+        m_MeshBoundsMax.push_back(hi);
         firstIndex += info.m_IndexCount;
         baseVertex += static_cast<int32_t>(mesh.Vertices.size());
     }
@@ -510,6 +523,44 @@ void Renderer::UpdateUniformBuffer(const Camera* camera, tri_global_ubo& g) cons
     // AiBlendConfig stays 0: the AI frame blend is outside the hot path (Renderer.cpp:5916-5925)
 }
 
+bool Renderer::BuildShadowConfig(tri_shadow_config& out) {
+    std::memset(&out, 0, sizeof out);
+    if (!m_Registry || m_ShadowMapSize == 0) return false;
+    const LightComponent* sun = nullptr;  // the directional light UpdateUniformBuffer uses (first enabled)
+    for (ECS::Entity e : m_Registry->GetEntities()) {
+        if (!m_Registry->HasComponent<LightComponent>(e)) continue;
+        const LightComponent& L = m_Registry->GetComponent<LightComponent>(e);
+        if (L.m_Enabled && L.m_Type == LightComponent::Type::Directional) {
+            sun = &L;
+            break;
+        }
+    }
+    if (!sun || !sun->m_ShadowCaster) return false;
+    glm::vec3 lo{INFINITY}, hi{-INFINITY};  // world box of the drawn meshes
+    for (const MeshDrawCommand& cmd : m_MeshDrawCommands) {
+        if (!cmd.m_Component || cmd.m_Component->m_MeshIndex >= m_MeshBoundsMin.size()) continue;
+        const glm::vec3 a = m_MeshBoundsMin[cmd.m_Component->m_MeshIndex], b = m_MeshBoundsMax[cmd.m_Component->m_MeshIndex];
+        if (a.x > b.x) continue;
+        for (int k = 0; k < 8; ++k) {
+            const glm::vec4 c{(k & 1) ? b.x : a.x, (k & 2) ? b.y : a.y, (k & 4) ? b.z : a.z, 1.0f};
+            const glm::vec4 w = cmd.m_ModelMatrix * c;
+            for (int ax = 0; ax < 3; ++ax) {
+                lo[ax] = std::min(lo[ax], w[ax]);
+                hi[ax] = std::max(hi[ax], w[ax]);
+            }
+        }
+    }
+    if (lo.x > hi.x) return false;
+    glm::vec3 dir{-0.5f, -1.0f, -0.3f};
+    if (glm::dot(sun->m_Direction, sun->m_Direction) > 0.0001f) dir = sun->m_Direction;
+    const float d[3] = {dir.x, dir.y, dir.z}, mn[3] = {lo.x, lo.y, lo.z}, mx[3] = {hi.x, hi.y, hi.z};
+    if (tri_shadow_fit_ortho(d, mn, mx, out.light_view_proj) != TRI_OK) return false;
+    out.size = m_ShadowMapSize;
+    out.depth_bias = 0.001f;
+    out.slope_bias = 2.0f;
+    return true;
+}
+
 const Camera* Renderer::GetActiveCamera(const ViewportContext& context) const {  // Renderer.cpp:4545-4574
     const uint32_t id = context.m_Info.ViewportID;
     if (id == 1u) return m_EditorCamera;
@@ -571,6 +622,8 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
         vc.m_Width = w;
         vc.m_Height = h;
         vc.m_GeometryGeneration = vc.m_TextureGeneration = vc.m_MaterialGeneration = vc.m_SkyboxGeneration = 0;
+        vc.m_Shadow = tri_shadow_config{};  // a fresh context starts without the pre-pass and bones
+        vc.m_BonePalette.clear();
     }
     if (vc.m_GeometryGeneration != m_GeometryGeneration) {
         // one device copy of the concatenated buffers per generation, bound by every viewport
@@ -645,11 +698,20 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     PrepareBonePaletteBuffer();
     std::vector<tri_draw> draws;
     BuildDrawList(draws);
+    tri_shadow_config shadow;
+    const bool shadowOn = BuildShadowConfig(shadow);
     const float clear[4] = {m_ClearColor.x, m_ClearColor.y, m_ClearColor.z, m_ClearColor.w};
     std::vector<ViewportContext*> submitted;
     for (auto& it : m_Viewports) {  // RecordCommandBuffer's per-viewport render passes
         ViewportContext& vc = it.second;
         if (!PrepareViewport(vc)) continue;
+        if (std::memcmp(&vc.m_Shadow, &shadow, sizeof shadow) != 0) {  // pre-pass on / off / refitted
+            if (tri_set_shadow(vc.m_Ctx, shadowOn ? &shadow : nullptr) != TRI_OK) {
+                LogError("shadow map", tri_last_error());
+                continue;
+            }
+            vc.m_Shadow = shadow;
+        }
         if (vc.m_BonePalette != m_BonePalette) {  // the bone SSBO (binding 4) of this frame
             if (tri_upload_bone_palette(vc.m_Ctx, m_BonePalette.data(), (uint32_t)(m_BonePalette.size() / 16)) != TRI_OK) {
                 LogError("bone palette", tri_last_error());

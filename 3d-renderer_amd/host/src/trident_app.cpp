@@ -160,6 +160,33 @@ void CopySource(const std::string& src, char* out, uint32_t cap) {
 }
 }  // namespace
 
+int trident_app_set_light_shadow_caster(trident_app* app, uint32_t entity, int caster) {
+    return Guard(app, [&] {
+        if (!app->registry.HasComponent<LightComponent>(entity)) return TRI_E_INVALID;
+        app->registry.GetComponent<LightComponent>(entity).m_ShadowCaster = caster != 0;
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_shadow_map_size(trident_app* app, uint32_t size) {
+    return Guard(app, [&] {
+        if (size > TRI_MAX_DIM) return TRI_E_INVALID;
+        app->renderer.SetShadowMapSize(size);
+        return TRI_OK;
+    });
+}
+
+int trident_app_shadow_config(trident_app* app, tri_shadow_config* out, int* enabled) {
+    return Guard(app, [&] {
+        if (!out || !enabled) return TRI_E_INVALID;
+        tri_global_ubo ubo;
+        std::vector<tri_draw> draws;  // GatherMeshDraws for the current registry state
+        app->renderer.BuildFrameInputs(app->renderer.GetActiveViewportId(), ubo, draws);
+        *enabled = app->renderer.BuildShadowConfig(*out) ? 1 : 0;
+        return TRI_OK;
+    });
+}
+
 int trident_app_viewport_texture(trident_app* app, uint32_t viewport_id, tri_image* out) {
     return Guard(app, [&] {
         if (!out) return TRI_E_INVALID;

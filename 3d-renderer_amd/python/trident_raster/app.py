@@ -31,6 +31,9 @@ _APP_FUNCTIONS = [
     ("trident_app_set_entity_bones", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32]),
     ("trident_app_set_assets_dir", C.c_int, [C.c_void_p, C.c_char_p, C.c_char_p, C.c_uint32]),
     ("trident_app_viewport_texture", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(abi.TriImage)]),
+    ("trident_app_set_light_shadow_caster", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
+    ("trident_app_set_shadow_map_size", C.c_int, [C.c_void_p, C.c_uint32]),
+    ("trident_app_shadow_config", C.c_int, [C.c_void_p, C.POINTER(abi.TriShadowConfig), C.POINTER(C.c_int)]),
     ("trident_app_geometry_uploads", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("trident_load_image", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
                                      C.POINTER(C.c_uint32)]),
@@ -144,6 +147,18 @@ class TridentApp:
         buf = C.create_string_buffer(64)
         _check(self._lib.trident_app_set_assets_dir(self._h, os.fsencode(directory), buf, 64), "set_assets_dir")
         return buf.value.decode()
+
+    def set_light_shadow_caster(self, entity, caster=True):
+        _check(self._lib.trident_app_set_light_shadow_caster(self._h, entity, 1 if caster else 0), "shadow caster")
+
+    def set_shadow_map_size(self, size):
+        _check(self._lib.trident_app_set_shadow_map_size(self._h, size), "shadow map size")
+
+    def shadow_config(self):
+        """The pre-pass configuration DrawFrame would use now (abi.TriShadowConfig), or None."""
+        cfg, on = abi.TriShadowConfig(), C.c_int()
+        _check(self._lib.trident_app_shadow_config(self._h, C.byref(cfg), C.byref(on)), "shadow_config")
+        return cfg if on.value else None
 
     def viewport_texture(self, viewport_id):
         """Renderer::GetViewportTexture: the viewport's abi.TriImage handle."""

@@ -378,3 +378,58 @@ def test_gpu_contexts_share_one_geometry(oracle):
     assert np.array_equal(outs[0][1], od)
     assert np.array_equal(np.concatenate([outs[1][0], outs[2][0]]), outs[0][0])
     assert int(np.abs(outs[0][0].astype(np.int16) - oc.astype(np.int16)).max()) <= 1
+
+
+def shadow_app(app_mod, w=320, h=240):
+    a = app_mod.TridentApp()
+    a.set_camera("editor", (0.0, 4.0, 8.0), (-25.0, 0.0, 0.0))
+    a.set_viewport(1, w, h)
+    a.add_mesh_entity("quad", position=(0.0, 0.0, 0.0), rotation=(-90.0, 0.0, 0.0), scale=(12.0, 12.0, 1.0))
+    a.add_mesh_entity("cube", position=(-1.2, 1.4, 0.5), rotation=(15.0, 30.0, 0.0), scale=(1.2, 1.2, 1.2))
+    a.add_mesh_entity("sphere", position=(1.3, 1.0, -0.4), scale=(1.6, 1.6, 1.6))
+    sun = a.add_light("directional", direction=(-0.45, -1.0, -0.35), intensity=4.0)
+    a.set_shadow_map_size(512)
+    return a, sun
+
+
+def test_shadow_caster_fits_the_light_frustum(app_mod, oracle):
+    """A shadow-casting first directional light (LightComponent::m_ShadowCaster) turns the pre-pass on;
+    its light transform is tri_shadow_fit_ortho over the drawn meshes' world box."""
+    a, sun = shadow_app(app_mod)
+    a.frame_inputs(1)  # lazily created primitives
+    assert a.shadow_config() is None  # not a caster yet
+    a.set_light_shadow_caster(sun, True)
+    cfg = a.shadow_config()
+    assert cfg is not None and cfg.size == 512 and cfg.depth_bias > 0 and cfg.slope_bias > 0
+    m = np.array(cfg.light_view_proj, np.float32).reshape(4, 4)
+    ground = np.array([[x, 0.0, z, 1.0] for x in (-6, 6) for z in (-6, 6)], np.float32)
+    ndc = ground @ m
+    assert np.all(np.abs(ndc[:, :2]) < 1.0) and np.all((ndc[:, 2] > 0) & (ndc[:, 2] < 1))
+    a.set_shadow_map_size(0)
+    assert a.shadow_config() is None
+    a.close()
+
+
+@pytest.mark.gpu
+def test_gpu_shim_shadow_caster(app_mod, oracle):
+    """DrawFrame with a shadow-casting sun renders the pre-pass; the frame equals the oracle given the
+    configuration the shim fitted, and differs visibly from the unshadowed frame."""
+    a, sun = shadow_app(app_mod)
+    a.set_light_shadow_caster(sun, True)
+    a.draw_frame()
+    a.draw_frame()
+    s = shim_scene(a, 1, 320, 240)
+    s.shadow = a.shadow_config()
+    assert s.shadow is not None
+    rgba, depth = a.read_pixels(1, 320, 240)
+    oc, od, _ = oracle.render(s)
+    assert np.array_equal(depth.view(np.uint32), od)
+    ob = oc[..., [2, 1, 0, 3]]
+    assert int(np.abs(rgba.astype(np.int16) - ob.astype(np.int16)).max()) <= 1
+    s.shadow = None
+    plain, _, _ = oracle.render(s)
+    assert int((np.abs(plain.astype(np.int16) - oc.astype(np.int16)).max(-1) > 20).sum()) > 500  # visible shadows
+    a.set_light_shadow_caster(sun, False)  # caster off again: the context drops the pre-pass
+    a.draw_frame()
+    assert_shim_parity(a, oracle, 1, 320, 240, min_covered=1000)
+    a.close()
