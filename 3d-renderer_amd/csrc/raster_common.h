@@ -9,7 +9,8 @@
 //   prim_vs   16 B/prim    {vertex slots 0..2, draw | clipped flag}, written by k_setup for the
 //                          primitives it bins or clips: k_raster's one-load route from a primitive
 //                          id to its vertices (instead of draw search -> index buffer)
-//   bin_list   4 B/entry   primitive ids per bin (order-free: visibility is resolved by a 64-bit key)
+//   bin_list  16 B/entry   primitive id + its vertex slots per bin (order-free: visibility is resolved by a
+//                          64-bit key; the slots spare k_raster the queue -> prim_vs -> snap chain)
 //   TriRec    64 B/record  clipped sub-triangles only: snapped vertices, z, 1/w, prim<<3|sub, slots
 //   colour     4 B/pixel   B8G8R8A8_UNORM;  depth 4 B/pixel D32_SFLOAT bits
 #pragma once

@@ -33,6 +33,16 @@ namespace {
 #endif
 constexpr uint32_t kAblate = TRI_ABLATE;
 
+// Diagnostics builds only (-DTRI_PHASE_TIMING): k_raster's wave 0 of every workgroup stamps s_memtime at
+// its phase boundaries (start, init, coverage, large triangles, shading, end) for tools/phase_times.py.
+#ifdef TRI_PHASE_TIMING
+constexpr int kPhaseSlots = 65536;
+__device__ unsigned long long g_tri_phase[kPhaseSlots][6];
+#define TRI_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < kPhaseSlots) g_tri_phase[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
+#else
+#define TRI_STAMP(k) do { } while (0)
+#endif
+
 constexpr uint64_t kBgKey = (0x3F800000ull << 32) | 0xFFFFFFFFull;  // depth 1.0, lowest priority
 constexpr float kPi = 3.14159265359f;                                  // Default.frag:65
 
@@ -399,7 +409,10 @@ __device__ __forceinline__ void wave_reserve_plan(uint32_t bin, bool want, uint3
 }
 
 // Binning rounds whose queue reservations k_setup keeps in flight together.
-constexpr int kResBatch = 4;
+#ifndef TRI_RES_BATCH
+#define TRI_RES_BATCH 4
+#endif
+constexpr int kResBatch = TRI_RES_BATCH;
 
 // ------------------------------------------------------------------------------------------
 // Homogeneous clipping (oracle clip_polygon: Sutherland-Hodgman against w >= WMIN, z >= 0 and the
@@ -543,7 +556,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
             b.recs[rid] = r;
             for_bins(br, fp.nbx, [&](uint32_t bi) {  // rare path: one global atomic per entry
                 const uint32_t pos = atomicAdd(&b.bin_count[bi], 1u);
-                if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = TRI_ENTRY_CLIPPED | rid;
+                if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = make_uint4(TRI_ENTRY_CLIPPED | rid, 0u, 0u, 0u);
                 else note_bin_overflow(b, pos + 1);
                 ++nentries;
             });
@@ -585,10 +598,16 @@ __device__ __forceinline__ void note_shadow_bin_overflow(const TriDeviceBuffers&
 // kResBatch rounds is planned with ballots and its reservations (one returning atomic per (wave, bin))
 // are all issued before any result is used, so a wave waits for one atomic round trip per batch instead
 // of one per round. Must be reached by the whole wave. Diagnostics: TRI_ABLATE=8 waits per round.
-template <bool SHADOW_QUEUES>
-__device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bool ok1, uint2 br0, uint2 br1, uint32_t p0,
-                                         uint32_t p1, uint32_t nbx, uint32_t* bin_count, uint32_t* bin_list, uint32_t cap,
-                                         uint32_t lane, uint32_t& nentries) {
+// Component-wise selects (a plain `c ? a : b` on uint4 became a dynamically indexed stack array).
+__device__ __forceinline__ uint32_t pick(bool c, uint32_t a, uint32_t b) { return c ? a : b; }
+__device__ __forceinline__ uint4 pick(bool c, uint4 a, uint4 b) {
+    return make_uint4(c ? a.x : b.x, c ? a.y : b.y, c ? a.z : b.z, c ? a.w : b.w);
+}
+
+template <bool SHADOW_QUEUES, typename Q>
+__device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bool ok1, uint2 br0, uint2 br1, Q p0, Q p1,
+                                         uint32_t nbx, uint32_t* bin_count, Q* bin_list, uint32_t cap, uint32_t lane,
+                                         uint32_t& nentries) {
     bool has = (ok0 || ok1) && !(kAblate & 4);  // diagnostics: 4 = setup without binning
     bool second = !ok0;
     uint2 cur = second ? br1 : br0;
@@ -596,13 +615,13 @@ __device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bo
     uint32_t bx0 = bx, bx1 = cur.y & 0xFFFFu, by1 = cur.y >> 16;
     const int batch = (kAblate & 8) ? 1 : kResBatch;
     while (__ballot(has)) {
-        uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch], rent[kResBatch];
-        bool rwant[kResBatch];
+        uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch];
+        bool rwant[kResBatch], rsec[kResBatch];
 #pragma unroll
         for (int r = 0; r < kResBatch; ++r) {
             rwant[r] = has && r < batch;
             rbin[r] = by * nbx + bx;
-            rent[r] = second ? p1 : p0;
+            rsec[r] = second;
             if (rwant[r]) {
                 if (bx < bx1) {
                     ++bx;
@@ -628,7 +647,7 @@ __device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bo
             const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
             if (rwant[r]) {
                 if (kAblate & 32) continue;  // diagnostics: 32 = no queue stores
-                if (pos < cap) bin_list[(size_t)rbin[r] * cap + pos] = rent[r];
+                if (pos < cap) bin_list[(size_t)rbin[r] * cap + pos] = pick(rsec[r], p1, p0);
                 else if (SHADOW_QUEUES) note_shadow_bin_overflow(b, pos + 1);
                 else note_bin_overflow(b, pos + 1);
                 ++nentries;
@@ -737,8 +756,9 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 }
             }
         }
-        bin_pair<false>(b, ok[0], ok[1], br[0], br[1], p[0], p[1], (uint32_t)fp.nbx, b.bin_count, b.bin_list,
-                        fp.bin_cap, lane, nentries);
+        bin_pair<false>(b, ok[0], ok[1], br[0], br[1], make_uint4(p[0], sl0[0], sl1[0], sl2[0]),
+                        make_uint4(p[1], sl0[1], sl1[1], sl2[1]), (uint32_t)fp.nbx, b.bin_count, b.bin_list, fp.bin_cap,
+                        lane, nentries);
         if constexpr (WITH_SHADOW)
             bin_pair<true>(b, sok[0], sok[1], sbr[0], sbr[1], p[0], p[1], fp.s_nbx, b.sbin_count, b.sbin_list,
                            fp.s_bin_cap, lane, sentries);
@@ -818,12 +838,11 @@ __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3
 }
 
 // A bin-queue entry -> its triangle.
-__device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
-    if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
+__device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint4 e) {
+    if (e.x & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e.x & ~TRI_ENTRY_CLIPPED);
     const FetchBufs fb = fetch_bufs(fp, b);
-    const uint4 pv = ld128(fb.prim_vs, e * 16u);
-    const uint32_t sl[3] = {pv.x, pv.y, pv.z};
-    return rec_from_snaps(e, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
+    const uint32_t sl[3] = {e.y, e.z, e.w};
+    return rec_from_snaps(e.x, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
 }
 
 // Fragment depth at pixel centre: plane through the snapped vertices, fixed evaluation order.
@@ -1119,6 +1138,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.gV = NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
     f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
               sc.amb[2] * albedo.z * sc.amb_strength);
+    if (kAblate & 64) return make_float4(c.x, c.y, c.z, 1.0f);  // diagnostics: 64 = no lights
     if (sc.has_sun && f.vis > 0.0f)  // vis = 0 (fully shadowed): the sun adds exactly nothing
         eval_pbr_fast(sc, px, mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]),
                       mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), f.vis, c);
@@ -1142,6 +1162,31 @@ __device__ __forceinline__ float interp_exact(float w0, float w1, float w2, floa
 }
 __device__ __forceinline__ float interp_fast(float w0, float w1, float w2, float x0, float x1, float x2) {
     return __builtin_fmaf(w2, x2, __builtin_fmaf(w1, x1, w0 * x0));
+}
+
+// Fast build's perspective-correct weights: per triangle, the barycentric slopes over pixel offsets from
+// vertex 0 (from the exact integer area), with vertex 1's and 2's scaled by iw_k / iw_0; per pixel two
+// FMAs per weight and one reciprocal. Relative to vertex 0, not to a bin, so every bin, band and code path
+// (LDS table or gathered triangle) gives the same bits.
+struct FastW {
+    float a0, b0, a1, b1, a2, b2;
+};
+__device__ __forceinline__ FastW fast_coefs(const TriRec& r) {
+    const int32_t x1 = r.X[1] - r.X[0], y1 = r.Y[1] - r.Y[0], x2 = r.X[2] - r.X[0], y2 = r.Y[2] - r.Y[0];
+    const float iS = frcp((float)((int64_t)x1 * y2 - (int64_t)y1 * x2));
+    const float i0 = frcp(r.iw[0]);
+    const float s1 = (r.iw[1] * i0) * iS, s2 = (r.iw[2] * i0) * iS;
+    return FastW{(float)(y1 - y2) * iS, (float)(x2 - x1) * iS, (float)y2 * s1, -(float)x2 * s1, -(float)y1 * s2,
+                 (float)x1 * s2};
+}
+__device__ __forceinline__ void fast_weights(const FastW& c, int32_t X0, int32_t Y0, int32_t px, int32_t py, float& w0,
+                                             float& w1, float& w2) {
+    const float dx = (float)(256 * px + 128 - X0), dy = (float)(256 * py + 128 - Y0);
+    const float q0 = __builtin_fmaf(c.b0, dy, __builtin_fmaf(c.a0, dx, 1.0f));
+    const float q1 = __builtin_fmaf(c.b1, dy, c.a1 * dx);
+    const float q2 = __builtin_fmaf(c.b2, dy, c.a2 * dx);
+    const float iq = frcp((q0 + q1) + q2);
+    w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
 }
 
 // Perspective-correct barycentric weights of pixel (px, py) in the oracle's order: exact int64 edge
@@ -1189,6 +1234,42 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
     return l0 + bb * (l1 - l0);
 }
 
+// The varyings of the triangle with vertex slots (v0, v1, v2) and draw d at weights (w0, w1, w2), the
+// draw's texture sample and tint: Frag fields 0..18 through `put`.
+template <bool EXACT, typename Put>
+__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, uint32_t v0, uint32_t v1,
+                                            uint32_t v2, uint32_t d, float w0, float w1, float w2, const float* lut,
+                                            Put&& put) {
+    // plain-float views of the varyings (HIP vector unions defeat SROA in the pixel-pair path)
+    auto ldv = [&](uint32_t slot, uint32_t j) -> V4 {
+        const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);
+        return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
+    };
+    auto ip = [&](float x0, float x1, float x2) {
+        return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
+    };
+    const V4 a0 = ldv(v0, 0), a1 = ldv(v0, 1), a2 = ldv(v0, 2);
+    const V4 b0 = ldv(v1, 0), b1 = ldv(v1, 1), b2 = ldv(v1, 2);
+    const V4 c0 = ldv(v2, 0), c1 = ldv(v2, 1), c2 = ldv(v2, 2);
+    // field-wise stores (a struct-valued f3 store is ABI-coerced to <2 x float> + float, which
+    // keeps the pixel-pair path's fragments from being promoted to registers)
+    put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
+    put(3, ip(a1.x, b1.x, c1.x)); put(4, ip(a1.y, b1.y, c1.y)); put(5, ip(a1.z, b1.z, c1.z));
+    put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
+    const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
+    put(9, u); put(10, v);
+    const uint4 st = ld128(fb.shade, d * 48u), sd = ld128(fb.shade, d * 48u + 16u), ss = ld128(fb.shade, d * 48u + 32u);
+    TriTexDesc td;
+    td.texels = reinterpret_cast<const uint32_t*>(((uint64_t)sd.y << 32) | sd.x);
+    td.w = sd.z; td.h = sd.w;
+    td.solid[0] = __uint_as_float(ss.x); td.solid[1] = __uint_as_float(ss.y);
+    td.solid[2] = __uint_as_float(ss.z); td.solid[3] = __uint_as_float(ss.w);
+    const float4 tx = (kAblate & 128) ? make_float4(u, v, u, 1.0f) : sample_tex(td, u, v, lut);  // 128: no texture
+    const float4 tint = make_float4(__uint_as_float(st.x), __uint_as_float(st.y), __uint_as_float(st.z), __uint_as_float(st.w));
+    put(11, tx.x); put(12, tx.y); put(13, tx.z); put(14, tx.w);
+    put(15, tint.x); put(16, tint.y); put(17, tint.z); put(18, tint.w);
+}
+
 // Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
 // Writes the fragment through `put(field_index, value)` (fields in Frag order), so one body serves
 // the single-pixel Frag and the lane-pair FragP without an intermediate in scratch memory.
@@ -1209,17 +1290,8 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     float w0, w1, w2;
     if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
         exact_weights(r, px, py, w0, w1, w2);
-    } else {  // float edge functions relative to vertex 0 (operands < 2^24: exact conversions)
-        const float dx = (float)(256 * px + 128 - r.X[0]), dy = (float)(256 * py + 128 - r.Y[0]);
-        const float fX1 = (float)(r.X[1] - r.X[0]), fY1 = (float)(r.Y[1] - r.Y[0]);
-        const float fX2 = (float)(r.X[2] - r.X[0]), fY2 = (float)(r.Y[2] - r.Y[0]);
-        const float iS = frcp(fX1 * fY2 - fY1 * fX2);
-        const float l2 = (fX1 * dy - fY1 * dx) * iS;
-        const float l1 = (fY2 * dx - fX2 * dy) * iS;
-        const float l0 = 1.0f - l1 - l2;
-        const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
-        const float iq = frcp((q0 + q1) + q2);
-        w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
+    } else {
+        fast_weights(fast_coefs(r), r.X[0], r.Y[0], px, py, w0, w1, w2);
     }
     float vis = 1.0f;
     if constexpr (SHADOW) {  // light-space position at the pixel with the oracle's weights, then the compare
@@ -1233,34 +1305,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
     }
     put(19, vis);
-    // plain-float views of the varyings (HIP vector unions defeat SROA in the pixel-pair path)
-    auto ldv = [&](uint32_t slot, uint32_t j) -> V4 {
-        const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);
-        return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
-    };
-    auto ip = [&](float x0, float x1, float x2) {
-        return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
-    };
-    const V4 a0 = ldv(r.v[0], 0), a1 = ldv(r.v[0], 1), a2 = ldv(r.v[0], 2);
-    const V4 b0 = ldv(r.v[1], 0), b1 = ldv(r.v[1], 1), b2 = ldv(r.v[1], 2);
-    const V4 c0 = ldv(r.v[2], 0), c1 = ldv(r.v[2], 1), c2 = ldv(r.v[2], 2);
-    // field-wise stores (a struct-valued f3 store is ABI-coerced to <2 x float> + float, which
-    // keeps the pixel-pair path's fragments from being promoted to registers)
-    put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
-    put(3, ip(a1.x, b1.x, c1.x)); put(4, ip(a1.y, b1.y, c1.y)); put(5, ip(a1.z, b1.z, c1.z));
-    put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
-    const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
-    put(9, u); put(10, v);
-    const uint4 st = ld128(fb.shade, d * 48u), sd = ld128(fb.shade, d * 48u + 16u), ss = ld128(fb.shade, d * 48u + 32u);
-    TriTexDesc td;
-    td.texels = reinterpret_cast<const uint32_t*>(((uint64_t)sd.y << 32) | sd.x);
-    td.w = sd.z; td.h = sd.w;
-    td.solid[0] = __uint_as_float(ss.x); td.solid[1] = __uint_as_float(ss.y);
-    td.solid[2] = __uint_as_float(ss.z); td.solid[3] = __uint_as_float(ss.w);
-    const float4 tx = sample_tex(td, u, v, lut);
-    put(11, tx.x); put(12, tx.y); put(13, tx.z); put(14, tx.w);
-    put(15, __uint_as_float(st.x)); put(16, __uint_as_float(st.y)); put(17, __uint_as_float(st.z));
-    put(18, __uint_as_float(st.w));
+    fetch_attrs<EXACT>(fp, fb, r.v[0], r.v[1], r.v[2], d, w0, w1, w2, lut, put);
 }
 
 template <bool EXACT, bool SHADOW>
@@ -1490,7 +1535,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
-    __shared__ uint32_t bigq[kBalanced ? kBigQueue / 2 : kBigQueue];
+    constexpr int kBigN = kBalanced ? kBigQueue / 2 : kBigQueue;
+    __shared__ uint32_t bigq[kBigN];  // queue positions of the large triangles
     __shared__ float lut[512];
     constexpr int kJobWords = (kBalanced && kCovJobs > BIN * BIN ? kCovJobs : BIN * BIN);
     __shared__ uint16_t skyq[kJobWords];  // the coverage pass's row jobs, then the skybox queue
@@ -1498,6 +1544,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     __shared__ uint32_t wsum[TRI_BLOCK / 64];
     __shared__ uint32_t nbig, nentries, nsky;
     const int tid = threadIdx.x;
+    TRI_STAMP(0);
     const int bin = xcd_bin(blockIdx.x, fp.nbins);
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
     const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
@@ -1514,7 +1561,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         nentries = min(cnt, fp.bin_cap);
     }
     __syncthreads();
-    const uint32_t* queue = b.bin_list + (size_t)bin * fp.bin_cap;
+    TRI_STAMP(1);
+    const uint4* queue = b.bin_list + (size_t)bin * fp.bin_cap;
     uint32_t s0 = 0, s1 = nentries;
     if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
@@ -1533,14 +1581,13 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         TriRec r;
         int32_t cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
         if (tid < kCovPass && i < s1) {
-            const uint32_t ri = queue[i];
-            r = load_entry(fp, b, ri);
+            r = load_entry(fp, b, queue[i]);
             rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
             if (cx0 <= cx1 && cy0 <= cy1) {
                 bool big = false;
                 if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
                     const uint32_t q = atomicAdd(&nbig, 1u);
-                    if (q < kBigQueue / 2) { bigq[q] = ri; big = true; }
+                    if (q < (uint32_t)kBigN) { bigq[q] = i; big = true; }
                 }
                 if (!big) {
                     EdgeSetup e;
@@ -1601,15 +1648,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     const int share = TRI_COV_SHARE > 1 && (s1 - s0) <= TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
     const int sub = tid % share;
     for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) {
-        const uint32_t ri = queue[i];
-        const TriRec r = load_entry(fp, b, ri);
+        const TriRec r = load_entry(fp, b, queue[i]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
         if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
             if (sub != 0) continue;  // the first lane of the group hands it over
             const uint32_t q = atomicAdd(&nbig, 1u);
-            if (q < kBigQueue) { bigq[q] = ri; continue; }
+            if (q < (uint32_t)kBigN) { bigq[q] = i; continue; }
             raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);  // queue full: this lane walks it all
             continue;
         }
@@ -1617,9 +1663,10 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     }
     __syncthreads();
   }
-    const uint32_t nb = min(nbig, (uint32_t)(kBalanced ? kBigQueue / 2 : kBigQueue));
+    TRI_STAMP(2);
+    const uint32_t nb = min(nbig, (uint32_t)kBigN);
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        const TriRec r = load_entry(fp, b, bigq[q]);
+        const TriRec r = load_entry(fp, b, queue[bigq[q]]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         EdgeSetup e;
@@ -1646,6 +1693,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         }
     }
     __syncthreads();
+    TRI_STAMP(3);
     // shade + store: each wave covers whole BIN-pixel row pieces -> coalesced colour/depth stores.
     // Background pixels go to an LDS queue for the skybox pass below (lane-dense, and its registers
     // are not live during shading).
@@ -1684,7 +1732,12 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         } else {
             z = __uint_as_float((uint32_t)(key >> 32));
             Frag f;
-            fetch_fragment<EXACT, SHADOW>(fp, b, key, px, py, lut, f);
+            if (kAblate & 256) {  // diagnostics: 256 = no varyings fetch (a fragment made from the key)
+                const float k0 = __uint_as_float(((uint32_t)key & 0x7FFFFFu) | 0x3F000000u);
+                for (int q = 0; q < 20; ++q) (&f.wx)[q] = k0 + 0.01f * q;
+            } else {
+                fetch_fragment<EXACT, SHADOW>(fp, b, key, px, py, lut, f);
+            }
             const float4 c = EXACT ? fs_exact(fp, f) : fs_fast(fp.sc, f);
             out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
         }
@@ -1692,6 +1745,11 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         b.color[o] = out;
         if (fp.write_depth) b.depth[o] = z;
     }
+#ifdef TRI_PHASE_TIMING
+    __syncthreads();
+    TRI_STAMP(4);
+    if (!sky_queue) { TRI_STAMP(5); return; }
+#endif
     if (!sky_queue) return;
     __syncthreads();
     const uint32_t ns = nsky;
@@ -1702,6 +1760,10 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         b.color[(size_t)(py - fp.y0) * fp.W + px] =
             persp ? sky_bgra_persp(fp, b, px, py, lut) : sky_bgra(fp, b, px, py, lut);
     }
+#ifdef TRI_PHASE_TIMING
+    __syncthreads();
+    TRI_STAMP(5);
+#endif
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1931,3 +1993,10 @@ hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* 
     hipLaunchKernelGGL(k_blit, g, dim3(TRI_BLOCK), 0, stream, src, w, h, dst, dw, dh, sx, sy, unorm_lut);
     return hipGetLastError();
 }
+
+#ifdef TRI_PHASE_TIMING
+extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {
+    const size_t n = (size_t)(nslots < kPhaseSlots ? nslots : kPhaseSlots) * 6 * sizeof(unsigned long long);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
