@@ -615,7 +615,7 @@ __device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bo
     uint32_t bx0 = bx, bx1 = cur.y & 0xFFFFu, by1 = cur.y >> 16;
     const int batch = (kAblate & 8) ? 1 : kResBatch;
     while (__ballot(has)) {
-        uint32_t rbin[kResBatch], rlead[kResBatch], rrank[kResBatch], rbase[kResBatch];
+        uint32_t rbin[kResBatch], rlr[kResBatch], rbase[kResBatch];  // rlr: group leader lane | rank << 8
         bool rwant[kResBatch], rsec[kResBatch];
 #pragma unroll
         for (int r = 0; r < kResBatch; ++r) {
@@ -636,15 +636,16 @@ __device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bo
                     has = false;
                 }
             }
-            uint32_t cnt;
-            wave_reserve_plan(rbin[r], rwant[r], rlead[r], rrank[r], cnt);
+            uint32_t cnt, lead, rank;
+            wave_reserve_plan(rbin[r], rwant[r], lead, rank, cnt);
+            rlr[r] = lead | (rank << 8);
             rbase[r] = 0;
-            if (rwant[r] && lane == rlead[r] && !(kAblate & 16))  // diagnostics: 16 = no atomics
+            if (rwant[r] && lane == lead && !(kAblate & 16))  // diagnostics: 16 = no atomics
                 rbase[r] = atomicAdd(&bin_count[rbin[r]], cnt);
         }
 #pragma unroll
         for (int r = 0; r < kResBatch; ++r) {
-            const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)rlead[r]) + rrank[r];
+            const uint32_t pos = (uint32_t)__shfl((int)rbase[r], (int)(rlr[r] & 0xFFu)) + (rlr[r] >> 8);
             if (rwant[r]) {
                 if (kAblate & 32) continue;  // diagnostics: 32 = no queue stores
                 if (pos < cap) bin_list[(size_t)rbin[r] * cap + pos] = pick(rsec[r], p1, p0);

@@ -451,7 +451,8 @@ def main():
                          "kernel": "k_raster",
                          "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]) if timing else 0,
                          "algorithmic_bytes": raster_bytes},
-            "roofline_valu": valu_roofline(pmc, raster_ms),
+            # the PMC count is of a whole frame: no VALU roofline for a band
+            "roofline_valu": valu_roofline(pmc if br.rows == H else None, raster_ms),
             "frame_roofline": {"algorithmic_bytes": frame_bytes, "ms_per_frame": frame_ms,
                                "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9 if frame_ms > 0 else None,
                                "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if frame_ms > 0 else None},

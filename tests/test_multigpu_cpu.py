@@ -1,5 +1,6 @@
 """N > 1 path on the CPU: world-size-2 (and 4) gloo process groups run bench.py's band partition,
-band all-gather and max-over-ranks timing. Each rank renders its row band with the oracle (the
+band gather / all-gather and max-over-ranks timing, with and without cluster culling (a restatement
+of k_vertex's cluster test drops the culled clusters' triangles from a band's render). Each rank renders its row band with the oracle (the
 CPU stand-in for its GPU's k_raster band), and the gathered frame must equal a full-frame render.
 Sort-first bands are exact: a pixel depends only on the triangles covering it.
 """
@@ -19,6 +20,61 @@ def _free_port():
         return s.getsockname()[1]
 
 
+CLUSTER_PRIMS = 512  # raster_common.h TRI_CLUSTER_PRIMS
+
+
+def cluster_visible(scene, draw, lo, hi, y0, y1):
+    """Restatement of k_vertex's cluster_visible (raster_kernels.hip): the object-space box through
+    (P V) M; a box wholly in front of the eye whose image misses rows [y0, y1) or the frame's columns (2 px
+    margin), or lies before z = 0 or beyond z = w, has no fragment in the band."""
+    if (lo > hi).any():
+        return False
+    if draw.pc.bone_count > 0:
+        return True
+    u = scene.ubo
+    view = np.array(u.view, np.float32).reshape(4, 4).T
+    proj = np.array(u.projection, np.float32).reshape(4, 4).T
+    model = np.array(draw.pc.model, np.float32).reshape(4, 4).T
+    m = (proj @ view) @ model
+    corners = np.array([[hi[0] if k & 1 else lo[0], hi[1] if k & 2 else lo[1], hi[2] if k & 4 else lo[2], 1.0]
+                        for k in range(8)], np.float32)
+    c = corners @ m.T
+    if not (c[:, 3] > 1e-4).all():
+        return True
+    ndc = c[:, :3] / c[:, 3:4]
+    hw, hh = scene.width / 2.0, scene.height / 2.0
+    wx, wy = ndc[:, 0] * hw + hw, ndc[:, 1] * hh + hh
+    return not (wy.max() < y0 - 2 or wy.min() > y1 + 2 or wx.max() < -2 or wx.min() > scene.width + 2 or
+                ndc[:, 2].max() < 0 or ndc[:, 2].min() > 1)
+
+
+def cull_clusters(scene, y0, y1):
+    """The scene with every triangle of a cluster culled for rows [y0, y1) made degenerate (zero area:
+    no fragment, primitive order unchanged); returns it and the number of culled clusters."""
+    import copy
+
+    s = copy.copy(scene)
+    idx = scene.indices.copy()
+    culled = 0
+    for d in scene.draws:
+        m = scene.meshes[d.mesh_index]
+        f, n, bv = int(m["first_index"]), int(m["index_count"]), int(m["base_vertex"])
+        assert sum(1 for e in scene.draws if e.mesh_index == d.mesh_index) == 1, "one draw per mesh"
+        tris = idx[f:f + n - n % 3].reshape(-1, 3)
+        for c0 in range(0, len(tris), CLUSTER_PRIMS):
+            t = tris[c0:c0 + CLUSTER_PRIMS].astype(np.int64) + bv
+            ok = t[(t >= 0) & (t < len(scene.vertices))]
+            pos = scene.vertices["position"][ok].astype(np.float32)
+            lo = pos.min(0) if len(pos) else np.full(3, np.inf, np.float32)
+            hi = pos.max(0) if len(pos) else np.full(3, -np.inf, np.float32)
+            if not cluster_visible(scene, d, lo, hi, y0, y1):
+                culled += 1
+                tris[c0:c0 + CLUSTER_PRIMS] = tris[c0:c0 + CLUSTER_PRIMS, :1]
+        idx[f:f + len(tris) * 3] = tris.reshape(-1)
+    s.indices = idx
+    return s, culled
+
+
 def _worker(rank, world, port, scene_name, out_dir, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, ROOT)
@@ -35,6 +91,10 @@ def _worker(rank, world, port, scene_name, out_dir, mode):
     scene = getattr(sc, scene_name)()
     W, H = scene.width, scene.height
     y0, y1 = bench.band_rows(H, world, rank)
+    if mode.endswith("+cull"):  # the band renders only the triangles of its visible clusters
+        mode = mode[:-5]
+        scene, culled = cull_clusters(scene, y0, y1)
+        np.save(os.path.join(out_dir, f"culled{rank}.npy"), np.array([culled]))
     col, dep, _ = oracle_py.render(scene, band=(y0, y1), threads=2)
     band = torch.from_numpy(np.ascontiguousarray(col).view(np.int32).reshape(-1).copy())
     dband = torch.from_numpy(np.ascontiguousarray(dep).view(np.int32).reshape(-1).copy())
@@ -52,7 +112,9 @@ def _worker(rank, world, port, scene_name, out_dir, mode):
 
 
 @pytest.mark.parametrize("world,scene_name,mode", [(2, "c1_cube", "gather"), (4, "textured_grid", "gather"),
-                                                   (2, "textured_grid", "allgather")])
+                                                   (2, "textured_grid", "allgather"),
+                                                   (2, "textured_grid", "gather+cull"),
+                                                   (4, "textured_grid", "gather+cull")])
 def test_row_band_assembly_equals_full_frame(world, scene_name, mode, oracle, tmp_path):
     import torch.multiprocessing as mp
 
@@ -63,6 +125,9 @@ def test_row_band_assembly_equals_full_frame(world, scene_name, mode, oracle, tm
                        start_method="spawn")
     scene = getattr(sc, scene_name)()
     col, dep, _ = oracle.render(scene, threads=4)
+    if mode.endswith("+cull"):  # the partition with cluster culling: some band culled something
+        mode = mode[:-5]
+        assert sum(int(np.load(tmp_path / f"culled{r}.npy")[0]) for r in range(world)) > 0
     full = np.ascontiguousarray(col).view(np.int32).reshape(-1)
     dfull = np.ascontiguousarray(dep).view(np.int32).reshape(-1)
     for r in range(world):

@@ -220,3 +220,43 @@ def test_group_bands_on_one_device_assemble_in_place(oracle, nbands, display):
     assert int(np.abs(col.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL
     assert np.array_equal(col, col2)
     assert ptr and dev == 0
+
+
+def test_external_stream_orders_output():
+    """tri_set_stream with a torch stream: the frame is enqueued on THAT stream, so a reader on another
+    stream ordered behind it (wait_stream, no device-wide sync) sees the finished band — what the bench's
+    collectives rely on (a default-stream handle of 0 used to mean the context's own
+    unordered stream)."""
+    import torch
+    from trident_raster import scenes
+
+    s = sc.grid_c3(1920, 1080, 300)
+    W, H = s.width, s.height
+    color = torch.zeros(W * H, dtype=torch.int32, device="cuda")
+    depth = torch.zeros(W * H, dtype=torch.float32, device="cuda")
+    st, reader = torch.cuda.Stream(), torch.cuda.Stream()
+    with raster_ctx(W, H) as r:
+        scenes.load_scene(r, s)
+        r.render_frame()  # sizes the queues
+        ref_c, _ = r.readback()
+        r.set_stream(st.cuda_stream)
+        r.bind_output(color.data_ptr(), depth.data_ptr())
+        for _ in range(3):
+            torch.cuda.synchronize()
+            color.zero_()
+            torch.cuda.synchronize()
+            with torch.cuda.stream(st):
+                r.render()
+            reader.wait_stream(st)
+            with torch.cuda.stream(reader):
+                snap = color.clone()
+            reader.synchronize()
+            got = snap.cpu().numpy().view(np.uint8).reshape(H, W, 4)
+            assert np.array_equal(got, ref_c.reshape(H, W, 4))
+        r.synchronize()
+
+
+def raster_ctx(W, H):
+    from trident_raster import raster
+
+    return raster.TriRaster(W, H)
