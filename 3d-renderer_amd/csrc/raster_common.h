@@ -7,10 +7,10 @@
 //   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, z_ndc, 1/w}
 //   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
 //   prim_vs   16 B/prim    {vertex slots 0..2, draw | clipped flag}, written by k_setup for the
-//                          primitives it bins or clips: k_raster's one-load route from a primitive
-//                          id to its vertices (instead of draw search -> index buffer)
-//   bin_list  16 B/entry   primitive id + its vertex slots per bin (order-free: visibility is resolved by a
-//                          64-bit key; the slots spare k_raster the queue -> prim_vs -> snap chain)
+//                          primitives it bins or clips on frames with several draws: k_raster's one-load
+//                          route from a primitive id to its vertices and draw (instead of a draw search);
+//                          a single-draw frame reads the 12 index bytes instead and writes none
+//   bin_list   4 B/entry   primitive ids per bin (order-free: visibility is resolved by a 64-bit key)
 //   TriRec    64 B/record  clipped sub-triangles only: snapped vertices, z, 1/w, prim<<3|sub, slots
 //   colour     4 B/pixel   B8G8R8A8_UNORM;  depth 4 B/pixel D32_SFLOAT bits
 #pragma once
@@ -29,10 +29,11 @@
 #define TRI_MAX_CLIP_VERTS 12
 // Clipping a triangle by 6 planes yields at most 3 + 6 = 9 vertices; a numerically non-convex
 // polygon can come out longer and is cut to its first 9 (oracle clip_polygon does the same). The fan
-// then has at most 7 sub-triangles, whose index fits the 3-bit `sub` field of a visibility key with
-// sub = 7 left unused, so no key of primitive 0 can equal the background key (depth 1, low 0xFFFFFFFF).
+// then has at most 7 sub-triangles k = 1..7, stored in the 3-bit `sub` field of a visibility key as k
+// (sub = 0: the primitive was not clipped). The background key has depth bits just above 1.0, which no
+// fragment reaches (the [0, 1] clamp), so it never equals a fragment's key.
 #define TRI_MAX_CLIP_POLY 9
-static_assert(TRI_MAX_CLIP_POLY - 2 <= 7, "clipped sub-triangle index must fit 3 bits without reaching 7");
+static_assert(TRI_MAX_CLIP_POLY - 2 <= 7, "clipped sub-triangle number k = 1..nsub must fit 3 bits");
 static_assert(TRI_MAX_CLIP_POLY <= TRI_MAX_CLIP_VERTS, "clip polygon buffers");
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f

@@ -43,7 +43,7 @@ __device__ unsigned long long g_tri_phase[kPhaseSlots][6];
 #define TRI_STAMP(k) do { } while (0)
 #endif
 
-constexpr uint64_t kBgKey = (0x3F800000ull << 32) | 0xFFFFFFFFull;  // depth 1.0, lowest priority
+constexpr uint64_t kBgKey = 0x3F800001ull << 32;  // above every fragment key (depth bits <= 1.0 after the clamp)
 constexpr float kPi = 3.14159265359f;                                  // Default.frag:65
 
 struct VsOut {
@@ -77,11 +77,10 @@ __device__ __forceinline__ uint4 ld128(Rsrc r, uint32_t off) {
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
 struct FetchBufs {  // k_raster's gather sources
-    Rsrc prim_vs, snap, vary, shade;
+    Rsrc snap, vary, shade;
 };
 __device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const TriDeviceBuffers& b) {
     FetchBufs f;
-    f.prim_vs = make_rsrc(b.prim_vs, 16ull * fp.nprims);
     f.snap = make_rsrc(b.snap, 16ull * fp.nslots);
     f.vary = make_rsrc(b.vary, 48ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
     f.shade = make_rsrc(b.draw_shade, (uint64_t)sizeof(TriDrawShade) * fp.ndraws);
@@ -542,12 +541,12 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
                                                (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, 0.0f);
         }
     }
-    if (lane == 0) b.clip_slot[prim] = rbase;  // k_raster's fragment fetch finds sub-triangle `sub` here
+    if (lane == 0) b.clip_slot[prim] = rbase;  // k_raster's fragment fetch finds sub-triangle `sub` at + sub - 1
     if (lane < nsub) {  // fan sub-triangle k = lane + 1: (v0, vk, vk+1)
         const uint32_t k = lane + 1;
         TriRec r;
         uint2 br;
-        const uint32_t ps = (prim << 3) | (k - 1);
+        const uint32_t ps = (prim << 3) | k;  // sub = k >= 1 marks a clipped primitive's sub-triangle
         const uint32_t rid = rbase + k - 1;
         const float4 c0 = cv_load(src).c, ck = cv_load(src + k * kClipStride).c,
                      ck1 = cv_load(src + (k + 1) * kClipStride).c;
@@ -556,7 +555,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
             b.recs[rid] = r;
             for_bins(br, fp.nbx, [&](uint32_t bi) {  // rare path: one global atomic per entry
                 const uint32_t pos = atomicAdd(&b.bin_count[bi], 1u);
-                if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = make_uint4(TRI_ENTRY_CLIPPED | rid, 0u, 0u, 0u);
+                if (pos < fp.bin_cap) b.bin_list[(size_t)bi * fp.bin_cap + pos] = TRI_ENTRY_CLIPPED | rid;
                 else note_bin_overflow(b, pos + 1);
                 ++nentries;
             });
@@ -735,8 +734,9 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                         sok[t] = shadow_bins(fp, X, Y, sbr[t]);
                     }
                 }
-                // k_raster's (and k_shadow_raster's) route from the primitive to its vertex slots
-                if (ok[t] || needs_clip[t] || sok[t])
+                // k_raster's (and k_shadow_raster's) route from the primitive to its vertex slots and draw; a
+                // single-draw frame finds the slots in the index buffer instead (prim_slots)
+                if (!fp.one_draw && (ok[t] || needs_clip[t] || sok[t]))
                     b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | (needs_clip[t] ? TRI_PRIM_CLIPPED : 0u));
             }
             nsetup += ok[t] ? 1u : 0u;
@@ -757,9 +757,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 }
             }
         }
-        bin_pair<false>(b, ok[0], ok[1], br[0], br[1], make_uint4(p[0], sl0[0], sl1[0], sl2[0]),
-                        make_uint4(p[1], sl0[1], sl1[1], sl2[1]), (uint32_t)fp.nbx, b.bin_count, b.bin_list, fp.bin_cap,
-                        lane, nentries);
+        bin_pair<false>(b, ok[0], ok[1], br[0], br[1], p[0], p[1], (uint32_t)fp.nbx, b.bin_count, b.bin_list,
+                        fp.bin_cap, lane, nentries);
         if constexpr (WITH_SHADOW)
             bin_pair<true>(b, sok[0], sok[1], sbr[0], sbr[1], p[0], p[1], fp.s_nbx, b.sbin_count, b.sbin_list,
                            fp.s_bin_cap, lane, sentries);
@@ -838,12 +837,29 @@ __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3
     return r;
 }
 
+// The vertex slots and draw of primitive p: on a single-draw frame straight from the index buffer (slot =
+// index - min_index, as k_setup computed them; k_setup writes no prim_vs then), else its prim_vs record.
+__device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t p,
+                                           uint32_t sl[3], uint32_t& d) {
+    if (fp.one_draw) {
+        const Rsrc ir = make_rsrc(b.indices + fp.draw0.first_index, 12ull * fp.nprims);
+        const auto q = __builtin_amdgcn_raw_buffer_load_b96(ir, p * 12u, 0, 0);
+        sl[0] = q[0] - fp.draw0.min_index; sl[1] = q[1] - fp.draw0.min_index; sl[2] = q[2] - fp.draw0.min_index;
+        d = 0;
+    } else {
+        const uint4 pv = ld128(make_rsrc(b.prim_vs, 16ull * fp.nprims), p * 16u);
+        sl[0] = pv.x; sl[1] = pv.y; sl[2] = pv.z;
+        d = pv.w & ~TRI_PRIM_CLIPPED;
+    }
+}
+
 // A bin-queue entry -> its triangle.
-__device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint4 e) {
-    if (e.x & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e.x & ~TRI_ENTRY_CLIPPED);
+__device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
+    if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
     const FetchBufs fb = fetch_bufs(fp, b);
-    const uint32_t sl[3] = {e.y, e.z, e.w};
-    return rec_from_snaps(e.x, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
+    uint32_t sl[3], d;
+    prim_slots(fp, b, e, sl, d);
+    return rec_from_snaps(e, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
 }
 
 // Fragment depth at pixel centre: plane through the snapped vertices, fixed evaluation order.
@@ -1174,11 +1190,11 @@ struct FastW {
 };
 __device__ __forceinline__ FastW fast_coefs(const TriRec& r) {
     const int32_t x1 = r.X[1] - r.X[0], y1 = r.Y[1] - r.Y[0], x2 = r.X[2] - r.X[0], y2 = r.Y[2] - r.Y[0];
-    const float iS = frcp((float)((int64_t)x1 * y2 - (int64_t)y1 * x2));
+    const float fx1 = (float)x1, fy1 = (float)y1, fx2 = (float)x2, fy2 = (float)y2;
+    const float iS = frcp((float)((int64_t)x1 * y2 - (int64_t)y1 * x2));  // the exact area, rounded once
     const float i0 = frcp(r.iw[0]);
     const float s1 = (r.iw[1] * i0) * iS, s2 = (r.iw[2] * i0) * iS;
-    return FastW{(float)(y1 - y2) * iS, (float)(x2 - x1) * iS, (float)y2 * s1, -(float)x2 * s1, -(float)y1 * s2,
-                 (float)x1 * s2};
+    return FastW{(float)(y1 - y2) * iS, (float)(x2 - x1) * iS, fy2 * s1, -fx2 * s1, -fy1 * s2, fx1 * s2};
 }
 __device__ __forceinline__ void fast_weights(const FastW& c, int32_t X0, int32_t Y0, int32_t px, int32_t py, float& w0,
                                              float& w1, float& w2) {
@@ -1279,13 +1295,13 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
                                                   int32_t px, int32_t py, const float* lut, Put&& put) {
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
+    const uint32_t sub = low & 7u;  // >= 1: sub-triangle `sub` of a clipped primitive
     const FetchBufs fb = fetch_bufs(fp, b);
-    const uint4 pv = ld128(fb.prim_vs, prim * 16u);
-    const uint32_t sl[3] = {pv.x, pv.y, pv.z};
-    const uint32_t d = pv.w & ~TRI_PRIM_CLIPPED;
+    uint32_t sl[3], d;
+    prim_slots(fp, b, prim, sl, d);
     TriRec r;
-    if (pv.w & TRI_PRIM_CLIPPED)
-        r = load_rec(b.recs, b.clip_slot[prim] + (low & 7u));
+    if (sub)
+        r = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
     else
         r = rec_from_snaps(prim, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
     float w0, w1, w2;
@@ -1537,7 +1553,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     __shared__ uint64_t keys[BIN * BIN];
     constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
     constexpr int kBigN = kBalanced ? kBigQueue / 2 : kBigQueue;
-    __shared__ uint32_t bigq[kBigN];  // queue positions of the large triangles
+    __shared__ uint32_t bigq[kBigN];  // queue entries of the large triangles
     __shared__ float lut[512];
     constexpr int kJobWords = (kBalanced && kCovJobs > BIN * BIN ? kCovJobs : BIN * BIN);
     __shared__ uint16_t skyq[kJobWords];  // the coverage pass's row jobs, then the skybox queue
@@ -1563,7 +1579,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     }
     __syncthreads();
     TRI_STAMP(1);
-    const uint4* queue = b.bin_list + (size_t)bin * fp.bin_cap;
+    const uint32_t* queue = b.bin_list + (size_t)bin * fp.bin_cap;
     uint32_t s0 = 0, s1 = nentries;
     if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
@@ -1582,13 +1598,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
         TriRec r;
         int32_t cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
         if (tid < kCovPass && i < s1) {
-            r = load_entry(fp, b, queue[i]);
+            const uint32_t ri = queue[i];
+            r = load_entry(fp, b, ri);
             rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
             if (cx0 <= cx1 && cy0 <= cy1) {
                 bool big = false;
                 if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
                     const uint32_t q = atomicAdd(&nbig, 1u);
-                    if (q < (uint32_t)kBigN) { bigq[q] = i; big = true; }
+                    if (q < (uint32_t)kBigN) { bigq[q] = ri; big = true; }
                 }
                 if (!big) {
                     EdgeSetup e;
@@ -1649,14 +1666,15 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     const int share = TRI_COV_SHARE > 1 && (s1 - s0) <= TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
     const int sub = tid % share;
     for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) {
-        const TriRec r = load_entry(fp, b, queue[i]);
+        const uint32_t ri = queue[i];
+        const TriRec r = load_entry(fp, b, ri);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
         if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
             if (sub != 0) continue;  // the first lane of the group hands it over
             const uint32_t q = atomicAdd(&nbig, 1u);
-            if (q < (uint32_t)kBigN) { bigq[q] = i; continue; }
+            if (q < (uint32_t)kBigN) { bigq[q] = ri; continue; }
             raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);  // queue full: this lane walks it all
             continue;
         }
@@ -1667,7 +1685,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     TRI_STAMP(2);
     const uint32_t nb = min(nbig, (uint32_t)kBigN);
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        const TriRec r = load_entry(fp, b, queue[bigq[q]]);
+        const TriRec r = load_entry(fp, b, bigq[q]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         EdgeSetup e;
@@ -1771,13 +1789,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
 // shadow pre-pass raster (oracle shadow_raster_triangle): one workgroup per 32x32 bin of the s_size^2
 // map, the bin's depth tile in LDS (min over covering fragments of the [0, 1]-clamped plane depth, as
 // uint32 bits: order-free), then one coalesced store of the tile. The triangle of a queue entry is
-// rebuilt from its three map snaps (prim_vs -> lsnap), oriented like the set-up (v1 <-> v2 swapped when
+// rebuilt from its three map snaps (prim_slots -> lsnap), oriented like the set-up (v1 <-> v2 swapped when
 // S < 0, kept when S > 0: no culling).
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ TriRec load_shadow_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
-    const Rsrc pvr = make_rsrc(b.prim_vs, 16ull * fp.nprims), snr = make_rsrc(b.lsnap, 16ull * fp.nslots);
-    const uint4 pv = ld128(pvr, e * 16u);
-    const uint4 q0 = ld128(snr, pv.x * 16u), q1 = ld128(snr, pv.y * 16u), q2 = ld128(snr, pv.z * 16u);
+    const Rsrc snr = make_rsrc(b.lsnap, 16ull * fp.nslots);
+    uint32_t sl[3], d;
+    prim_slots(fp, b, e, sl, d);
+    const uint4 q0 = ld128(snr, sl[0] * 16u), q1 = ld128(snr, sl[1] * 16u), q2 = ld128(snr, sl[2] * 16u);
     const int32_t X0 = ((int32_t)q0.x << 8) >> 8, X1 = ((int32_t)q1.x << 8) >> 8, X2 = ((int32_t)q2.x << 8) >> 8;
     const int32_t Y0 = (int32_t)q0.y, Y1 = (int32_t)q1.y, Y2 = (int32_t)q2.y;
     const int64_t S = (int64_t)(X1 - X0) * (int64_t)(Y2 - Y0) - (int64_t)(Y1 - Y0) * (int64_t)(X2 - X0);

@@ -24,8 +24,7 @@ struct TriDeviceBuffers {
     uint4* prim_vs;              // nprims: {vertex slot 0, 1, 2, draw | TRI_PRIM_CLIPPED} of every
                                  // primitive k_setup passed on (visible or clipped)
     uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
-    uint4* bin_list;             // nbins * bin_cap entries (fixed-capacity queue per bin): {primitive, its
-                                 // vertex slots 0, 1, 2} or {TRI_ENTRY_CLIPPED | record, 0, 0, 0}
+    uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)
     TriCounters* counters;
     uint2* setup_stats;          // nchunks {triangles set up, bin entries} per k_setup workgroup
     uint32_t* color;             // band rows * W

@@ -148,7 +148,7 @@ struct tri_ctx {
     uint2* d_setup_stats = nullptr; size_t cap_setup_stats = 0;
     uint32_t last_nchunks = 0;
     uint32_t* d_bin_count = nullptr; size_t cap_bin_count = 0;
-    uint4* d_bin_list = nullptr; size_t cap_bin_list = 0;
+    uint32_t* d_bin_list = nullptr; size_t cap_bin_list = 0;
     TriCounters* d_ctr = nullptr;
     uint32_t ovf_rec_cap = 1u << 16, ovf_vert_cap = 1u << 17;
     uint32_t bin_cap = 0;
@@ -469,7 +469,7 @@ int ensure_work_buffers(tri_ctx* c) {
     c->bin_cap = std::max<uint32_t>(c->bin_cap, (uint32_t)std::min<uint64_t>(((8 * mean + 64 + 63) / 64) * 64, 1u << 30));
     c->bin_cap = std::max<uint32_t>(c->bin_cap, 256u);
     const size_t nlist = (size_t)c->nbins * c->bin_cap;
-    if (nlist * 16 > (16ull << 30)) return fail(TRI_E_OOM, "bin queues would need %zu MB", nlist * 16 >> 20);
+    if (nlist * 4 > (8ull << 30)) return fail(TRI_E_OOM, "bin queues would need %zu MB", nlist * 4 >> 20);
     // k_raster gathers varyings, snapped vertices and prim_vs records through raw buffer loads with
     // 32-bit byte offsets
     if (nvary * 16 > 0xFFFFFFFFull || (uint64_t)c->nprims * 16 > 0xFFFFFFFFull)

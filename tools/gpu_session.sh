@@ -16,7 +16,7 @@ if [ "$what" = bench ] || [ "$what" = all ]; then
 fi
 if [ "$what" = prof ] || [ "$what" = all ]; then
   PROF_OUT=gpurun_out/prof_c3 bash tools/profile.sh > gpurun_out/prof_c3.log 2>&1 || { tail -5 gpurun_out/prof_c3.log; exit 1; }
-  PROF_OUT=gpurun_out/prof_c5 BENCH_ARGS="--config c5 --steps 50 --warmup 5 --no-cpu-baseline --no-secondary" \
+  PROF_OUT=gpurun_out/prof_c5 BENCH_ARGS="--config c5 --steps 50 --warmup 5 --no-cpu-baseline --no-secondary --inflight 1" \
     bash tools/profile.sh > gpurun_out/prof_c5.log 2>&1 || { tail -5 gpurun_out/prof_c5.log; exit 1; }
   echo prof ok
 fi

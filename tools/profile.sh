@@ -4,7 +4,9 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${PROF_OUT:-gpurun_out/prof}
 mkdir -p $OUT
-ARGS="${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline --no-secondary}"
+# one frame in flight: overlapping kernels of two contexts would stretch every traced duration (and
+# mix the PMC attribution), while the bench times its kernels in a separate single-context event pass
+ARGS="${BENCH_ARGS:---steps 50 --warmup 5 --no-cpu-baseline --no-secondary --inflight 1}"
 run() {  # name, rocprofv3 options...
     local name=$1; shift
     timeout -k 10 300 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 bench.py $ARGS > $OUT/$name.log 2>&1
