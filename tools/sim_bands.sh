@@ -1,8 +1,10 @@
 #!/bin/bash
 # Per-rank render cost of the N-way row-band split, measured on one GPU without the collective.
+# SPECS="8 4,1 0" (comma-separated "world rank" pairs) limits the runs; TRI_RASTER_LIB picks a library.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for spec in "1 0" "2 0" "4 0" "4 2" "8 0" "8 4" "8 7"; do
+IFS=, read -ra SPECLIST <<< "${SPECS:-1 0,2 0,4 0,4 2,8 0,8 4,8 7}"
+for spec in "${SPECLIST[@]}"; do
   set -- $spec
   timeout -k 10 200 python bench.py --steps 200 --warmup 20 --no-cpu-baseline --no-secondary --sim-world $1 --sim-rank $2 --inflight ${INFLIGHT:-2} \
     > gpurun_out/sim_$1_$2.log 2>&1 || { echo "sim $spec failed"; tail -3 gpurun_out/sim_$1_$2.log; exit 1; }
