@@ -250,11 +250,11 @@ __device__ __forceinline__ bool cluster_visible(const TriFrameParams& fp, const 
              z1 < 0.0f || z0 > 1.0f);
 }
 
-// One lane per vertex slot. With cluster culling on, each wave first evaluates, lane-parallel, the
-// clusters whose index range meets its 256-slot vertex block(s) (per-mesh interval table), stores their
-// visibility for k_setup (waves sharing a cluster store the same flag) and, unless the shadow pre-pass
-// needs every caster, skips a block that no visible cluster references: the vertex of any visible
-// primitive is always transformed, since its cluster's range contains it.
+// One lane per vertex slot. With cluster culling on: lanes 0 .. ncl_total-1 of the grid (the first few
+// waves) test one (draw, cluster) box each and store its flag for k_setup; every wave then tests the union
+// box of its 256-slot vertex block (the clusters referencing it, precomputed at upload: one load) and,
+// unless the shadow pre-pass needs every caster, skips a block whose box misses the rows. A vertex of any
+// visible primitive is always transformed: its cluster's box lies inside the block's union box.
 __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
     const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
     if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
@@ -267,7 +267,12 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
     }
     bool needed = true;
     if (fp.cull_on) {  // uniform
-        const uint32_t lane = lanes_below(~0ull);
+        if (slot < fp.ncl_total) {  // this lane's (draw, cluster) flag
+            const int cd = fp.one_draw ? 0 : find_range(b.draw_cbase, (int)fp.ndraws, slot);
+            const TriDrawDev& dr = fp.one_draw ? fp.draw0 : b.draws[cd];
+            const uint32_t lc = slot - (fp.one_draw ? 0u : b.draw_cbase[cd]);
+            b.cvis[slot] = cluster_visible(fp, dr, b.clusters[dr.cl_first + lc]) ? 1u : 0u;
+        }
         const uint32_t blk = (slot - vbase) / TRI_VBLOCK;
         uint64_t pending = __ballot(valid);
         while (pending) {  // the wave's distinct (draw, block) groups, usually one
@@ -277,18 +282,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
             const bool mine = valid && d == gd && blk == gb;
             pending &= ~__ballot(mine);
             const TriDrawDev& dr = fp.one_draw ? fp.draw0 : b.draws[gd];
-            const uint32_t cb = fp.one_draw ? 0u : b.draw_cbase[gd];
-            const uint2 iv = b.vblk[dr.vblk_first + gb];
-            bool any = false;
-            for (uint32_t c0 = iv.x; iv.x <= iv.y && c0 <= iv.y; c0 += 64) {
-                const uint32_t c = c0 + lane;
-                bool v = false;
-                if (c <= iv.y) {
-                    v = cluster_visible(fp, dr, b.clusters[dr.cl_first + c]);
-                    b.cvis[cb + c] = v ? 1u : 0u;
-                }
-                any = any || __ballot(v) != 0;
-            }
+            const bool any = cluster_visible(fp, dr, b.vbox[dr.vblk_first + gb]);
             if (mine) needed = any;
         }
     }
@@ -689,12 +683,15 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             sbr[t] = make_uint2(0u, 0u);
             bool culled = false;
             int d = 0;
-            const uint32_t* ip = nullptr;
-            uint32_t vb = 0;
+            uint32_t vb = 0, i0 = 0, i1 = 0, i2 = 0;
             if (p[t] < fp.nprims) {
+                // the indices are fetched together with the cluster flag, not after it: a band's
+                // visible primitives skip one dependent load (a culled one wastes 12 bytes)
+                const uint32_t* ip;
                 if (fp.one_draw) {  // kernel-argument constants: the index fetch starts at once
                     ip = b.indices + fp.draw0.first_index + 3u * p[t];
                     vb = 0u - fp.draw0.min_index;
+                    i0 = ip[0]; i1 = ip[1]; i2 = ip[2];
                     if (fp.cull_on) culled = !b.cvis[p[t] / TRI_CLUSTER_PRIMS];
                 } else {
                     d = find_range(b.draw_pbase, (int)fp.ndraws, p[t]);
@@ -702,12 +699,13 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                     const uint32_t lp = p[t] - b.draw_pbase[d];
                     ip = b.indices + dr.first_index + 3u * lp;
                     vb = b.draw_vbase[d] - dr.min_index;
+                    i0 = ip[0]; i1 = ip[1]; i2 = ip[2];
                     if (fp.cull_on) culled = !b.cvis[b.draw_cbase[d] + lp / TRI_CLUSTER_PRIMS];
                 }
             }
             // a primitive culled for the context's rows may still cast a shadow into the map
             if (p[t] < fp.nprims && (!culled || WITH_SHADOW)) {
-                sl0[t] = vb + ip[0]; sl1[t] = vb + ip[1]; sl2[t] = vb + ip[2];
+                sl0[t] = vb + i0; sl1[t] = vb + i1; sl2[t] = vb + i2;
                 if (!culled) {
                     const TriSnap a0 = b.snap[sl0[t]], a1 = b.snap[sl1[t]], a2 = b.snap[sl2[t]];
                     const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
@@ -1979,7 +1977,9 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
     };
     rec(kStageVertex);
     if (fp.nslots > 0)
-        hipLaunchKernelGGL(k_vertex, dim3((fp.nslots + TRI_BLOCK - 1) / TRI_BLOCK), dim3(TRI_BLOCK), 0, stream, fp, b);
+        // with cluster culling every (draw, cluster) flag needs a lane, even when a mesh has fewer vertices
+        hipLaunchKernelGGL(k_vertex, dim3(((fp.cull_on && fp.ncl_total > fp.nslots ? fp.ncl_total : fp.nslots) + TRI_BLOCK - 1) / TRI_BLOCK),
+                           dim3(TRI_BLOCK), 0, stream, fp, b);
     else
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
     rec(kStageSetup);

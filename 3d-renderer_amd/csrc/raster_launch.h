@@ -31,7 +31,7 @@ struct TriDeviceBuffers {
     float* depth;                // band rows * W (may be null)
     // cluster culling (only when TriFrameParams::cull_on)
     const TriCluster* clusters;  // all meshes' clusters
-    const uint2* vblk;           // per mesh vertex block: [first, last] referencing cluster (mesh-local)
+    const TriCluster* vbox;      // per mesh vertex block: the union box of the clusters referencing it
     const uint32_t* draw_cbase;  // ndraws+1: first (draw, cluster) pair of each draw
     uint32_t* cvis;              // ncl_total visibility flags, written by k_vertex each frame
     // shadow-map pre-pass (only when TriFrameParams::shadow_on)

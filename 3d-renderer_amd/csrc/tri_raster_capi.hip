@@ -83,7 +83,7 @@ struct tri_geometry {
     std::vector<uint32_t> mesh_min, mesh_max;
     std::vector<uint32_t> mesh_cl_first, mesh_ncl, mesh_vblk_first;  // cluster culling tables per mesh
     TriCluster* d_clusters = nullptr; size_t cap_clusters = 0;
-    uint2* d_vblk = nullptr; size_t cap_vblk = 0;
+    TriCluster* d_vbox = nullptr; size_t cap_vbox = 0;  // per vertex block: union box of its clusters
     bool geometry_set = false;
 };
 
@@ -649,6 +649,7 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
     // boxes and index ranges; per 256-slot vertex block the interval of clusters whose range meets it
     std::vector<TriCluster> cl;
     std::vector<uint2> vblk;
+    std::vector<TriCluster> vbox;  // parallel to vblk
     g->mesh_cl_first.assign(nm, 0);
     g->mesh_ncl.assign(nm, 0);
     g->mesh_vblk_first.assign(nm, 0);
@@ -688,11 +689,23 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
             }
             cl.push_back(t);
         }
+        // per vertex block: the union of the boxes of every cluster whose index range meets it (empty when
+        // none does): k_vertex keeps the block iff that box can reach the rows, one load and one test per wave
+        for (uint32_t bk = 0; bk < nblk; ++bk) {
+            TriCluster u;
+            for (int a = 0; a < 3; ++a) { u.lo[a] = INFINITY; u.hi[a] = -INFINITY; }
+            u.vmin = u.vmax = 0;
+            for (uint32_t k = iv[bk].x; iv[bk].x <= iv[bk].y && k <= iv[bk].y; ++k) {
+                const TriCluster& t = cl[g->mesh_cl_first[m] + k];
+                for (int a = 0; a < 3; ++a) { u.lo[a] = std::fmin(u.lo[a], t.lo[a]); u.hi[a] = std::fmax(u.hi[a], t.hi[a]); }
+            }
+            vbox.push_back(u);
+        }
     }
     if ((rc = grow(g->d_clusters, g->cap_clusters, std::max<size_t>(cl.size(), 1)))) return rc;
     if (!cl.empty()) HIP_TRY(hipMemcpy(g->d_clusters, cl.data(), cl.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
-    if ((rc = grow(g->d_vblk, g->cap_vblk, std::max<size_t>(vblk.size(), 1)))) return rc;
-    if (!vblk.empty()) HIP_TRY(hipMemcpy(g->d_vblk, vblk.data(), vblk.size() * sizeof(uint2), hipMemcpyHostToDevice));
+    if ((rc = grow(g->d_vbox, g->cap_vbox, std::max<size_t>(vbox.size(), 1)))) return rc;
+    if (!vbox.empty()) HIP_TRY(hipMemcpy(g->d_vbox, vbox.data(), vbox.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
     g->geometry_set = true;
     ++g->version;
     return TRI_OK;
@@ -700,8 +713,8 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
 
 void free_geometry(tri_geometry& g) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(g.d_vin); f(g.d_skin); f(g.d_idx); f(g.d_clusters); f(g.d_vblk);
-    g.d_vin = nullptr; g.d_skin = nullptr; g.d_idx = nullptr; g.d_clusters = nullptr; g.d_vblk = nullptr;
+    f(g.d_vin); f(g.d_skin); f(g.d_idx); f(g.d_clusters); f(g.d_vbox);
+    g.d_vin = nullptr; g.d_skin = nullptr; g.d_idx = nullptr; g.d_clusters = nullptr; g.d_vbox = nullptr;
 }
 
 }  // namespace
@@ -1114,7 +1127,7 @@ int tri_render(tri_ctx* c) {
     b.color = c->d_color;
     b.depth = c->d_depth;
     b.clusters = c->geom->d_clusters;
-    b.vblk = c->geom->d_vblk;
+    b.vbox = c->geom->d_vbox;
     b.draw_cbase = c->d_cbase;
     b.cvis = c->d_cvis;
     b.lpos = c->d_lpos;

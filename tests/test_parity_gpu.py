@@ -180,7 +180,7 @@ def test_bin_overflow_grows_and_recovers():
     assert ref[0].shape == (720, 1280, 4)
 
 
-@pytest.mark.parametrize("case", ["grid_turned", "primitives", "invalid", "skinned", "near_clip"])
+@pytest.mark.parametrize("case", ["grid_turned", "primitives", "invalid", "skinned", "near_clip", "dense"])
 def test_cluster_cull_is_exact(oracle, case):
     """TRI_FLAG_CLUSTER_CULL on a whole frame (row bands always cull): frames bit-identical to the
     unculled path and to the oracle, with geometry partly off screen, several draws, invalid vertices,
@@ -191,6 +191,11 @@ def test_cluster_cull_is_exact(oracle, case):
         s = sc.grid_c3(640, 360, 120)
         view, proj = scenes.editor_camera((1.5, 0.5, 0.0), (8.0, 35.0, 0.0), 60.0, (640, 360))
         s.ubo = scenes.pack_ubo(view, proj, (1.5, 0.5, 0.0), [{"type": "directional"}])
+    elif case == "dense":  # 47 clusters over 24 vertex slots: every cluster flag still gets a k_vertex lane
+        s = scenes.scene_c1_cube(1, 320, 240)
+        s.indices = np.tile(s.indices, 2000)
+        s.meshes = s.meshes.copy()
+        s.meshes[0]["index_count"] = s.indices.size
     else:
         s = {"primitives": lambda: sc.primitives_row(oracle), "invalid": lambda: sc.invalid_inputs(oracle),
              "skinned": lambda: sc.skinned_quad(oracle), "near_clip": lambda: sc.near_clip_grid()}[case]()
@@ -199,6 +204,11 @@ def test_cluster_cull_is_exact(oracle, case):
     assert np.array_equal(cull_c, plain_c) and np.array_equal(cull_d, plain_d)
     assert cull_s["triangles_setup"] == plain_s["triangles_setup"]
     assert_parity(s, oracle, flags=abi.TRI_FLAG_CLUSTER_CULL)
+    if case == "dense":  # and in row bands (which always cull), assembled
+        cuts = np.linspace(0, s.height, 5).astype(int)
+        parts = [render_gpu(s, band=(int(a), int(b))) for a, b in zip(cuts[:-1], cuts[1:])]
+        assert np.array_equal(np.concatenate([q[0] for q in parts]), plain_c)
+        assert np.array_equal(np.concatenate([q[1] for q in parts]), plain_d)
 
 
 @pytest.mark.parametrize("nbands,display", [(1, 0), (3, 1), (8, 5)])
