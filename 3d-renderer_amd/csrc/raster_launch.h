@@ -4,6 +4,9 @@
 #include <hip/hip_runtime.h>
 #include "raster_common.h"
 
+// k_setup workgroups resident per CU (its occupancy: 7 waves per SIMD, 4 waves per workgroup)
+#define TRI_SETUP_WGS_PER_CU 7
+
 struct TriDeviceBuffers {
     const TriVsIn* vin;
     const TriVsSkin* vskin;      // may be null when no draw skins

@@ -91,6 +91,7 @@ struct tri_ctx {
     tri_config cfg{};
     int device = 0;
     int32_t W = 0, H = 0, y0 = 0, y1 = 0, nbx = 0, nby = 0, nbins = 0;
+    int cu_count = 256;  // compute units of the device (k_setup's grid sizing)
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
 
@@ -757,6 +758,9 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
     int rc = make_current(c);
     if (rc) return bail(rc);
     if (tri_kernels_init() != hipSuccess) return bail(fail(TRI_E_HIP, "tri_create: kernel attribute setup failed"));
+    if (hipDeviceGetAttribute(&c->cu_count, hipDeviceAttributeMultiprocessorCount, c->device) != hipSuccess ||
+        c->cu_count <= 0)
+        c->cu_count = 256;
     if (hipStreamCreateWithFlags(&c->own_stream, hipStreamNonBlocking) != hipSuccess)
         return bail(fail(TRI_E_HIP, "tri_create: stream creation failed"));
     c->stream = c->own_stream;
@@ -1043,7 +1047,13 @@ int tri_render(tri_ctx* c) {
     fp.W = c->W; fp.H = c->H; fp.y0 = c->y0; fp.y1 = c->y1;
     fp.nbx = c->nbx; fp.nby = c->nby; fp.nbins = c->nbins;
     fp.bin_log2 = c->bin_log2;
-    const uint32_t target_chunks = 4096;  // >= 16 binning workgroups per CU
+    // k_setup grid: a whole frame takes at most one resident round of workgroups (7 per CU at its
+    // occupancy): a workgroup's fetch -> set-up -> reservation -> store chain is latency, and a partial
+    // second round doubles the kernel (C3: 1953 chunks of 512 -> 977 of 1024, set-up 33 -> 30 us). A band
+    // (cluster culling) keeps 512-primitive chunks: most of them exit at once, and the visible ones keep
+    // one chain each.
+    const bool culling = (c->y0 != 0 || c->y1 != c->H || (c->cfg.flags & TRI_FLAG_CLUSTER_CULL)) && c->ncl_total > 0;
+    const uint32_t target_chunks = culling ? 4096u : (uint32_t)c->cu_count * TRI_SETUP_WGS_PER_CU;
     uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
     ppt = std::min<uint32_t>(std::max<uint32_t>((ppt + 1) & ~1u, 2), TRI_MAX_PPT);  // k_setup takes pairs
     fp.ppt = (int32_t)ppt;
@@ -1082,7 +1092,7 @@ int tri_render(tri_ctx* c) {
     }
     for (int t = 0; t < TRI_MAX_TEXTURE_SLOTS && !fp.need_lut; ++t)
         fp.need_lut = c->d_tex[t] && (c->tex_w[t] != 1 || c->tex_h[t] != 1);
-    fp.cull_on = (c->y0 != 0 || c->y1 != c->H || (c->cfg.flags & TRI_FLAG_CLUSTER_CULL)) && c->ncl_total > 0 ? 1u : 0u;
+    fp.cull_on = culling ? 1u : 0u;
     fp.cull_vertex = fp.cull_on && !c->shadow.size ? 1u : 0u;  // the pre-pass needs every caster
     fp.ncl_total = c->ncl_total;
     if (c->shadow.size) {
