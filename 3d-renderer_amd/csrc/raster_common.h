@@ -168,7 +168,7 @@ struct TriFrameParams {
     int32_t W, H, y0, y1;
     int32_t nbx, nby, nbins, ppt;
     int32_t bin_log2;
-    uint32_t pad_a;
+    uint32_t sky_lut;   // the skybox pass samples the cubemap: workgroups with sky pixels stage the sRGB LUT
     uint32_t chunk_stride;  // k_setup visits chunks in the order (blockIdx * stride) mod nchunks
     int32_t pad_b2;
     float hw, hh, gx, gy;
@@ -187,7 +187,7 @@ struct TriFrameParams {
     //                  equal taps returns that texel, so the sky is the constant sky_bgra
     uint32_t sky_mode;
     uint32_t sky_bgra;
-    uint32_t need_lut;  // some texture larger than 1x1 or a sampled skybox: k_raster stages the sRGB LUT
+    uint32_t need_lut;  // some texture larger than 1x1: every k_raster workgroup stages the sRGB LUT
     uint32_t one_draw;  // exactly one draw: draw0 / vbase0 / pbase0 carry it (kernel arguments, scalar loads)
     float sky_far[16];  // inverse(Projection) applied to (xn, yn, 1, 1): rows {x, y, z, w} as (a, b, c, 0)
     float pv[16];

@@ -1770,6 +1770,10 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     if (!sky_queue) return;
     __syncthreads();
     const uint32_t ns = nsky;
+    if (fp.sky_lut && !fp.need_lut && ns > 0) {  // uniform: only bins showing sky stage the LUT
+        for (int i = tid; i < 512; i += TRI_BLOCK) lut[i] = b.srgb_lut[i];
+        __syncthreads();
+    }
     const bool persp = !EXACT && fp.sky_mode == TRI_SKY_PERSP;
     for (uint32_t i = tid; i < ns; i += TRI_BLOCK) {  // skybox pass over the queued background pixels
         const uint32_t li = skyq[i];

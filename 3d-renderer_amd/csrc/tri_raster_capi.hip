@@ -1083,7 +1083,7 @@ int tri_render(tri_ctx* c) {
         const bool persp = fp.sky_pw[3] == 0.0f;
         fp.sky_mode = !persp ? TRI_SKY_RAY : (c->sky_uniform ? TRI_SKY_UNIFORM : TRI_SKY_PERSP);
         fp.sky_bgra = c->sky_uniform_bgra;
-        fp.need_lut = fp.sky_mode != TRI_SKY_UNIFORM || fp.exact_shading;
+        fp.sky_lut = fp.sky_mode != TRI_SKY_UNIFORM || fp.exact_shading ? 1u : 0u;
         for (int r = 0; r < 4; ++r) {  // inverse(P) * (xn, yn, 1, 1), row r
             fp.sky_far[4 * r + 0] = fp.sky_ip[0 * 4 + r];
             fp.sky_far[4 * r + 1] = fp.sky_ip[1 * 4 + r];
