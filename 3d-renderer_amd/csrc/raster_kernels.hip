@@ -1249,23 +1249,29 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
     return l0 + bb * (l1 - l0);
 }
 
-// The varyings of the triangle with vertex slots (v0, v1, v2) and draw d at weights (w0, w1, w2), the
-// draw's texture sample and tint: Frag fields 0..18 through `put`.
-template <bool EXACT, typename Put>
-__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, uint32_t v0, uint32_t v1,
-                                            uint32_t v2, uint32_t d, float w0, float w1, float w2, const float* lut,
-                                            Put&& put) {
-    // plain-float views of the varyings (HIP vector unions defeat SROA in the pixel-pair path)
-    auto ldv = [&](uint32_t slot, uint32_t j) -> V4 {
+// The varyings of the triangle's three vertex slots: nine 16-B gathers, issued before the weights are
+// computed (their addresses need only the slots, the weights need the snapped vertices too).
+struct Taps {
+    V4 a0, a1, a2, b0, b1, b2, c0, c1, c2;
+};
+__device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint32_t v1, uint32_t v2) {
+    auto ldv = [&](uint32_t slot, uint32_t j) -> V4 {  // plain-float views (HIP vector unions defeat SROA)
         const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);
         return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
     };
+    return Taps{ldv(v0, 0), ldv(v0, 1), ldv(v0, 2), ldv(v1, 0), ldv(v1, 1), ldv(v1, 2),
+                ldv(v2, 0), ldv(v2, 1), ldv(v2, 2)};
+}
+
+// The varyings at weights (w0, w1, w2), the draw d's texture sample and tint: Frag fields 0..18 through
+// `put`.
+template <bool EXACT, typename Put>
+__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, const Taps& t, uint32_t d,
+                                            float w0, float w1, float w2, const float* lut, Put&& put) {
     auto ip = [&](float x0, float x1, float x2) {
         return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
     };
-    const V4 a0 = ldv(v0, 0), a1 = ldv(v0, 1), a2 = ldv(v0, 2);
-    const V4 b0 = ldv(v1, 0), b1 = ldv(v1, 1), b2 = ldv(v1, 2);
-    const V4 c0 = ldv(v2, 0), c1 = ldv(v2, 1), c2 = ldv(v2, 2);
+    const V4 &a0 = t.a0, &a1 = t.a1, &a2 = t.a2, &b0 = t.b0, &b1 = t.b1, &b2 = t.b2, &c0 = t.c0, &c1 = t.c1, &c2 = t.c2;
     // field-wise stores (a struct-valued f3 store is ABI-coerced to <2 x float> + float, which
     // keeps the pixel-pair path's fragments from being promoted to registers)
     put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
@@ -1302,6 +1308,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         r = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
     else
         r = rec_from_snaps(prim, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
+    const Taps taps = load_taps(fb, r.v[0], r.v[1], r.v[2]);
     float w0, w1, w2;
     if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
         exact_weights(r, px, py, w0, w1, w2);
@@ -1320,7 +1327,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
     }
     put(19, vis);
-    fetch_attrs<EXACT>(fp, fb, r.v[0], r.v[1], r.v[2], d, w0, w1, w2, lut, put);
+    fetch_attrs<EXACT>(fp, fb, taps, d, w0, w1, w2, lut, put);
 }
 
 template <bool EXACT, bool SHADOW>
