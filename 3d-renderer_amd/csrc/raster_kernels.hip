@@ -39,8 +39,12 @@ constexpr uint32_t kAblate = TRI_ABLATE;
 constexpr int kPhaseSlots = 65536;
 __device__ unsigned long long g_tri_phase[kPhaseSlots][6];
 #define TRI_STAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < kPhaseSlots) g_tri_phase[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
+// k_setup: start, primitives of the first round set up, first round binned, end
+__device__ unsigned long long g_tri_setup_phase[kPhaseSlots][4];
+#define TRI_SSTAMP(k) do { if (threadIdx.x == 0 && blockIdx.x < kPhaseSlots) g_tri_setup_phase[blockIdx.x][k] = __builtin_amdgcn_s_memtime(); } while (0)
 #else
 #define TRI_STAMP(k) do { } while (0)
+#define TRI_SSTAMP(k) do { } while (0)
 #endif
 
 constexpr uint64_t kBgKey = 0x3F800001ull << 32;  // above every fragment key (depth bits <= 1.0 after the clamp)
@@ -658,6 +662,7 @@ template <bool WITH_SHADOW>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
+    TRI_SSTAMP(0);
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
     __syncthreads();
     uint32_t nsetup = 0, nentries = 0, sentries = 0;
@@ -739,6 +744,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             }
             nsetup += ok[t] ? 1u : 0u;
         }
+        if (k == 0) TRI_SSTAMP(1);
 #pragma unroll
         for (int t = 0; t < 2; ++t) {
             uint64_t cm = __ballot(needs_clip[t]);  // rare: the wave clips its primitives one at a time
@@ -760,6 +766,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
         if constexpr (WITH_SHADOW)
             bin_pair<true>(b, sok[0], sok[1], sbr[0], sbr[1], p[0], p[1], fp.s_nbx, b.sbin_count, b.sbin_list,
                            fp.s_bin_cap, lane, sentries);
+        if (k == 0) TRI_SSTAMP(2);
     }
     if (nsetup) atomicAdd(&red[0], nsetup);
     if (nentries) atomicAdd(&red[1], nentries);
@@ -767,6 +774,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     // Statistics go to a per-workgroup slot with a plain store: same-address global atomics from
     // every workgroup serialise across the XCDs (measured: +34 us per frame at 4K/1M).
     if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(red[0], red[1]);
+    TRI_SSTAMP(3);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -962,7 +970,8 @@ __device__ __forceinline__ float sat(float x) { return fminf(fmaxf(x, 0.0f), 1.0
 
 __device__ __forceinline__ uint32_t wrap_repeat(float f, uint32_t n) {  // REPEAT addressing of floor(f)
     const int32_t i = (int32_t)fminf(fmaxf(f, -1.0e9f), 1.0e9f);
-    int32_t r = i % (int32_t)n;
+    if ((n & (n - 1)) == 0) return (uint32_t)i & (n - 1);  // power-of-two size: the mask is the modulo
+    int32_t r = i % (int32_t)n;                             // (two's complement: negative i wraps too)
     if (r < 0) r += (int32_t)n;
     return (uint32_t)r;
 }
@@ -1318,7 +1327,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     float vis = 1.0f;
     if constexpr (SHADOW) {  // light-space position at the pixel with the oracle's weights, then the compare
         float e0 = w0, e1 = w1, e2 = w2;
-        if (!EXACT) exact_weights(r, px, py, e0, e1, e2);
+        if (!EXACT && !(kAblate & 512)) exact_weights(r, px, py, e0, e1, e2);  // 512: fast weights (diagnostics)
         const Rsrc lr = make_rsrc(b.lpos, 16ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
         const uint4 L0 = ld128(lr, r.v[0] * 16u), L1 = ld128(lr, r.v[1] * 16u), L2 = ld128(lr, r.v[2] * 16u);
         auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
@@ -2029,5 +2038,9 @@ hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* 
 extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {
     const size_t n = (size_t)(nslots < kPhaseSlots ? nslots : kPhaseSlots) * 6 * sizeof(unsigned long long);
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int tri_debug_setup_times(unsigned long long* out, int nslots) {
+    const size_t n = (size_t)(nslots < kPhaseSlots ? nslots : kPhaseSlots) * 4 * sizeof(unsigned long long);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_setup_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
