@@ -58,6 +58,17 @@ struct VsOut {
     float cr, cg, cb;
 };
 
+constexpr int kLdsDraws = 64;  // k_setup stages up to this many draws' lookup data in LDS
+
+__device__ __forceinline__ int find_range_lds(const uint32_t* base, int n, uint32_t x) {  // base in LDS
+    int lo = 0, hi = n - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (base[mid] <= x) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+
 __device__ __forceinline__ int find_range(const uint32_t* base, int n, uint32_t x) {
     int lo = 0, hi = n - 1;
     while (lo < hi) {
@@ -662,8 +673,21 @@ template <bool WITH_SHADOW>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
+    // Frames with a few draws: each draw's primitive base, first index, slot offset and cluster base
+    // staged in LDS once per workgroup, so a primitive finds its draw and index row without the global
+    // binary search -> draw record chain in front of its index fetch.
+    __shared__ uint32_t dpb[kLdsDraws + 1], dfi[kLdsDraws], dvb[kLdsDraws], dcb[kLdsDraws];
+    const bool lds_draws = !fp.one_draw && fp.ndraws <= (uint32_t)kLdsDraws;
     TRI_SSTAMP(0);
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
+    if (lds_draws) {
+        for (uint32_t i = threadIdx.x; i <= fp.ndraws; i += TRI_BLOCK) dpb[i] = b.draw_pbase[i];
+        for (uint32_t i = threadIdx.x; i < fp.ndraws; i += TRI_BLOCK) {
+            dfi[i] = (uint32_t)b.draws[i].first_index;
+            dvb[i] = b.draw_vbase[i] - b.draws[i].min_index;
+            dcb[i] = fp.cull_on ? b.draw_cbase[i] : 0u;
+        }
+    }
     __syncthreads();
     uint32_t nsetup = 0, nentries = 0, sentries = 0;
     const uint32_t lane = lanes_below(~0ull);
@@ -698,6 +722,13 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                     vb = 0u - fp.draw0.min_index;
                     i0 = ip[0]; i1 = ip[1]; i2 = ip[2];
                     if (fp.cull_on) culled = !b.cvis[p[t] / TRI_CLUSTER_PRIMS];
+                } else if (lds_draws) {
+                    d = find_range_lds(dpb, (int)fp.ndraws, p[t]);
+                    const uint32_t lp = p[t] - dpb[d];
+                    ip = b.indices + dfi[d] + 3u * lp;
+                    vb = dvb[d];
+                    i0 = ip[0]; i1 = ip[1]; i2 = ip[2];
+                    if (fp.cull_on) culled = !b.cvis[dcb[d] + lp / TRI_CLUSTER_PRIMS];
                 } else {
                     d = find_range(b.draw_pbase, (int)fp.ndraws, p[t]);
                     const TriDrawDev& dr = b.draws[d];

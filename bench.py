@@ -268,6 +268,24 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256):
     return max_over_ranks(dt, br.dev, dist_on), timing
 
 
+def device_copy_gbs(device, nbytes=1 << 29, reps=10):
+    """Measured HBM bandwidth of a device-to-device copy (read + write bytes per second), the practical
+    ceiling next to the 8 TB/s spec peak."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device=device)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        b.copy_(a)
+    torch.cuda.synchronize(device)
+    dt = time.perf_counter() - t0
+    del a, b
+    return 2.0 * nbytes * reps / dt / 1e9
+
+
 def cpu_baseline(scene, seconds):
     """The CPU oracle (a multithreaded C++ port of the same pipeline) on this host's cores, over a
     bounded sample of whole frames of the same workload (lavapipe is absent on this image)."""
@@ -421,6 +439,7 @@ def main():
             br2.close()
             del br2
 
+    copy_gbs = device_copy_gbs(br.dev) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(scene, args.cpu_seconds)
@@ -448,6 +467,7 @@ def main():
             "latency_ms": latency,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                         "measured_copy_GBs": copy_gbs,
                          "kernel": "k_raster",
                          "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]) if timing else 0,
                          "algorithmic_bytes": raster_bytes},
