@@ -1248,20 +1248,34 @@ __device__ __forceinline__ void fast_weights(const FastW& c, int32_t X0, int32_t
 // functions at the pixel centre, IEEE divides (the EXACT build's interpolation; the shadow lookup uses
 // them in both builds so its compare sees the oracle's light-space depth bit for bit).
 __device__ __forceinline__ void exact_weights(const TriRec& r, int32_t px, int32_t py, float& w0, float& w1, float& w2) {
-    const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
-    int64_t e[3];
+    // The edge functions and the area are exact integers converted to float once (round to nearest):
+    // a triangle under 125 px on a side (the common case) has every product below 2^30, so 32-bit
+    // arithmetic gives the same integers, and so the same floats, as the 64-bit form.
+    float fe[3], fS;
+    const int32_t xmin = min(r.X[0], min(r.X[1], r.X[2])), xmax = max(r.X[0], max(r.X[1], r.X[2]));
+    const int32_t ymin = min(r.Y[0], min(r.Y[1], r.Y[2])), ymax = max(r.Y[0], max(r.Y[1], r.Y[2]));
+    if (xmax - xmin < 32000 && ymax - ymin < 32000) {  // |a|, |b|, |pixel - vertex| < 2^15 for a covered pixel
+        const int32_t Xp = 256 * px + 128, Yp = 256 * py + 128;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const int i = k, j = (k + 1) % 3;
-        const int64_t a = (int64_t)r.Y[i] - r.Y[j];
-        const int64_t bb = (int64_t)r.X[j] - r.X[i];
-        const int64_t c = -(a * r.X[i] + bb * r.Y[i]);
-        e[k] = a * Xp + bb * Yp + c;
+        for (int k = 0; k < 3; ++k) {
+            const int i = k, j = (k + 1) % 3;
+            fe[k] = (float)((r.Y[i] - r.Y[j]) * (Xp - r.X[i]) + (r.X[j] - r.X[i]) * (Yp - r.Y[i]));
+        }
+        fS = (float)((r.X[1] - r.X[0]) * (r.Y[2] - r.Y[0]) - (r.Y[1] - r.Y[0]) * (r.X[2] - r.X[0]));
+    } else {
+        const int64_t Xp = 256 * (int64_t)px + 128, Yp = 256 * (int64_t)py + 128;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const int i = k, j = (k + 1) % 3;
+            const int64_t a = (int64_t)r.Y[i] - r.Y[j];
+            const int64_t bb = (int64_t)r.X[j] - r.X[i];
+            const int64_t c = -(a * r.X[i] + bb * r.Y[i]);
+            fe[k] = (float)(a * Xp + bb * Yp + c);
+        }
+        fS = (float)((int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
+                     (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]));
     }
-    const int64_t S = (int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
-                      (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]);
-    const float fS = (float)S;
-    const float l0 = (float)e[1] / fS, l1 = (float)e[2] / fS, l2 = (float)e[0] / fS;
+    const float l0 = fe[1] / fS, l1 = fe[2] / fS, l2 = fe[0] / fS;
     const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
     const float qs = (q0 + q1) + q2;
     w0 = q0 / qs; w1 = q1 / qs; w2 = q2 / qs;
