@@ -598,11 +598,9 @@ __device__ __forceinline__ void note_shadow_bin_overflow(const TriDeviceBuffers&
 // written for a visible triangle: k_raster rebuilds it from `snap`. Triangles needing homogeneous
 // clipping are clipped right here by their wave (clip_prim_wave). Entry order inside a bin is free:
 // k_raster resolves visibility with (depth, primitive order) keys.
-#ifndef TRI_SETUP_WAVES
-#define TRI_SETUP_WAVES 7  // k_setup occupancy target (waves per SIMD)
-#endif
 
-// The lane's bin-queue entries, one per round: triangle 0's bbox bins, then triangle 1's. A batch of
+// Per-wave binning (the shadow and frame rounds whose workgroup bin box is too large for bin_pair_box's
+// LDS grid): the lane's bin-queue entries, one per round: triangle 0's bbox bins, then triangle 1's. A batch of
 // kResBatch rounds is planned with ballots and its reservations (one returning atomic per (wave, bin))
 // are all issued before any result is used, so a wave waits for one atomic round trip per batch instead
 // of one per round. Must be reached by the whole wave. Diagnostics: TRI_ABLATE=8 waits per round.
@@ -665,6 +663,102 @@ __device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bo
     }
 }
 
+// Workgroup-aggregated binning: a round's entries (two primitives per lane) are counted per bin in an
+// LDS grid over the workgroup's union bin box (a wave min-reduction + one LDS atomicMin per wave and
+// corner), one returning global atomic per (workgroup, bin) reserves the bin's run, and each entry takes
+// its position in the run from a returning LDS atomic. The counts return to zero as positions are handed
+// out, so the grid is never cleared. A round whose box exceeds kBinGrid cells bins with the per-wave
+// reservations above (a uniform choice: every wave reads the same box). Must be reached by the whole
+// workgroup. Rejected alternative: an LDS hash table keyed by bin (CAS probing): C3 set-up +2 us.
+constexpr uint32_t kBinGrid = 1024;
+struct BinBox {
+    uint32_t cnt[kBinGrid];
+    uint32_t base[kBinGrid];
+    uint32_t box[2][2][4];  // per queue set and round parity: min bx, min by, ~max bx, ~max by (LDS atomicMin)
+};
+
+__device__ __forceinline__ uint32_t wave_min(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+#ifndef TRI_SETUP_GROUP
+#define TRI_SETUP_GROUP 2
+#endif
+constexpr int kSetupGroup = TRI_SETUP_GROUP;  // primitives per lane set up, then binned, together
+static_assert(kSetupGroup == 2 || kSetupGroup == 4, "k_setup groups are one or two primitive pairs");
+
+template <bool SHADOW_QUEUES>
+__device__ __forceinline__ void bin_pair_box(const TriDeviceBuffers& b, BinBox& g, uint32_t round,
+                                             const bool (&ok)[kSetupGroup], const uint2 (&br)[kSetupGroup],
+                                             const uint32_t (&p)[kSetupGroup], uint32_t nbx, uint32_t* bin_count,
+                                             uint32_t* bin_list, uint32_t cap, uint32_t lane, uint32_t& nentries) {
+    if (kAblate & 4) return;  // diagnostics: 4 = setup without binning
+    const uint32_t q = round & 1u;
+    uint32_t (&box)[2][4] = g.box[SHADOW_QUEUES ? 1 : 0];
+    uint32_t m[4] = {~0u, ~0u, ~0u, ~0u};
+#pragma unroll
+    for (int t = 0; t < kSetupGroup; ++t)
+        if (ok[t]) {
+            m[0] = min(m[0], br[t].x & 0xFFFFu); m[1] = min(m[1], br[t].x >> 16);
+            m[2] = min(m[2], ~(br[t].y & 0xFFFFu)); m[3] = min(m[3], ~(br[t].y >> 16));
+        }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        m[i] = wave_min(m[i]);
+        if (lane == 0 && m[i] != ~0u) atomicMin(&box[q][i], m[i]);
+    }
+    __syncthreads();
+    const uint32_t ox = box[q][0], oy = box[q][1], ex = ~box[q][2], ey = ~box[q][3];
+    // the other parity's box was last read before this barrier; the next round accumulates into it only
+    // after one more barrier (below, or on the early paths)
+    if (threadIdx.x < 4) box[q ^ 1u][threadIdx.x] = ~0u;
+    if (ox == ~0u) {  // no entry in the workgroup this round
+        __syncthreads();
+        return;
+    }
+    const uint32_t w = ex - ox + 1u, cells = w * (ey - oy + 1u);
+    if (cells > kBinGrid) {
+        __syncthreads();
+#pragma unroll
+        for (int t = 0; t < kSetupGroup; t += 2)
+            bin_pair<SHADOW_QUEUES>(b, ok[t], ok[t + 1], br[t], br[t + 1], p[t], p[t + 1], nbx, bin_count, bin_list,
+                                    cap, lane, nentries);
+        return;
+    }
+#pragma unroll
+    for (int t = 0; t < kSetupGroup; ++t)
+        if (ok[t])
+            for (uint32_t by = br[t].x >> 16; by <= (br[t].y >> 16); ++by)
+                for (uint32_t bx = br[t].x & 0xFFFFu; bx <= (br[t].y & 0xFFFFu); ++bx)
+                    atomicAdd(&g.cnt[(by - oy) * w + bx - ox], 1u);
+    __syncthreads();
+    for (uint32_t c = threadIdx.x; c < cells; c += TRI_BLOCK) {
+        const uint32_t n = g.cnt[c];
+        if (n) {
+            const uint32_t cy = c / w;
+            const uint32_t base = atomicAdd(&bin_count[(oy + cy) * nbx + ox + (c - cy * w)], n);
+            g.base[c] = base;
+            if (base + n > cap) {
+                if (SHADOW_QUEUES) note_shadow_bin_overflow(b, base + n);
+                else note_bin_overflow(b, base + n);
+            }
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < kSetupGroup; ++t)
+        if (ok[t])
+            for (uint32_t by = br[t].x >> 16; by <= (br[t].y >> 16); ++by)
+                for (uint32_t bx = br[t].x & 0xFFFFu; bx <= (br[t].y & 0xFFFFu); ++bx) {
+                    const uint32_t c = (by - oy) * w + bx - ox;
+                    const uint32_t pos = g.base[c] + atomicSub(&g.cnt[c], 1u) - 1u;
+                    if (pos < cap) bin_list[(size_t)(by * nbx + bx) * cap + pos] = p[t];
+                    ++nentries;
+                }
+}
+
 // WITH_SHADOW (frames with the shadow pre-pass): the same index fetch also sets up every primitive
 // for the map (oracle shadow_raster_triangle: light-NDC snaps, no culling, no clipping, guard-band
 // violators dropped) and bins it into the map's own queues; clipped polygon vertices get light-space
@@ -678,6 +772,9 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     // binary search -> draw record chain in front of its index fetch.
     __shared__ uint32_t dpb[kLdsDraws + 1], dfi[kLdsDraws], dvb[kLdsDraws], dcb[kLdsDraws];
     const bool lds_draws = !fp.one_draw && fp.ndraws <= (uint32_t)kLdsDraws;
+    __shared__ BinBox bin_box;
+    for (uint32_t s = threadIdx.x; s < kBinGrid; s += TRI_BLOCK) bin_box.cnt[s] = 0;
+    if (threadIdx.x < 16) bin_box.box[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3] = ~0u;
     TRI_SSTAMP(0);
     if (threadIdx.x < 2) red[threadIdx.x] = 0;
     if (lds_draws) {
@@ -699,13 +796,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     // Two primitives per lane, set up and binned together: both index/vertex fetch chains are in
     // flight at once, and the queue reservations of both are batched (one atomic round trip per
     // batch), so a wave's dependent latencies are paid once for two primitives.
-    for (int k = 0; k < fp.ppt; k += 2) {  // uniform trip count: the reservations need the whole wave
-        uint32_t p[2], sl0[2], sl1[2], sl2[2];
-        bool ok[2], needs_clip[2], sok[2];
-        uint2 br[2], sbr[2];
+    for (int k = 0; k < fp.ppt; k += kSetupGroup) {  // uniform trip count: binning needs the whole workgroup
+        uint32_t p[kSetupGroup], sl0[kSetupGroup], sl1[kSetupGroup], sl2[kSetupGroup];
+        bool ok[kSetupGroup], needs_clip[kSetupGroup], sok[kSetupGroup];
+        uint2 br[kSetupGroup], sbr[kSetupGroup];
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
-            p[t] = chunk0 + (k + t) * TRI_BLOCK + threadIdx.x;
+        for (int t = 0; t < kSetupGroup; ++t) {
+            const bool in_chunk = kSetupGroup == 2 || k + t < fp.ppt;  // ppt is even, not always a multiple of 4
+            p[t] = in_chunk ? chunk0 + (k + t) * TRI_BLOCK + threadIdx.x : ~0u;
             ok[t] = false; needs_clip[t] = false; sok[t] = false;
             sl0[t] = sl1[t] = sl2[t] = 0;
             br[t] = make_uint2(0u, 0u);
@@ -777,7 +875,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
         }
         if (k == 0) TRI_SSTAMP(1);
 #pragma unroll
-        for (int t = 0; t < 2; ++t) {
+        for (int t = 0; t < kSetupGroup; ++t) {
             uint64_t cm = __ballot(needs_clip[t]);  // rare: the wave clips its primitives one at a time
             if (cm) {
                 if (lane == 0) atomicAdd(&b.counters->tris_clipped, (uint32_t)__builtin_popcountll(cm));
@@ -792,11 +890,11 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 }
             }
         }
-        bin_pair<false>(b, ok[0], ok[1], br[0], br[1], p[0], p[1], (uint32_t)fp.nbx, b.bin_count, b.bin_list,
-                        fp.bin_cap, lane, nentries);
+        bin_pair_box<false>(b, bin_box, (uint32_t)(k / kSetupGroup), ok, br, p, (uint32_t)fp.nbx, b.bin_count,
+                            b.bin_list, fp.bin_cap, lane, nentries);
         if constexpr (WITH_SHADOW)
-            bin_pair<true>(b, sok[0], sok[1], sbr[0], sbr[1], p[0], p[1], fp.s_nbx, b.sbin_count, b.sbin_list,
-                           fp.s_bin_cap, lane, sentries);
+            bin_pair_box<true>(b, bin_box, (uint32_t)(k / kSetupGroup), sok, sbr, p, fp.s_nbx, b.sbin_count,
+                               b.sbin_list, fp.s_bin_cap, lane, sentries);
         if (k == 0) TRI_SSTAMP(2);
     }
     if (nsetup) atomicAdd(&red[0], nsetup);

@@ -4,8 +4,11 @@
 #include <hip/hip_runtime.h>
 #include "raster_common.h"
 
-// k_setup workgroups resident per CU (its occupancy: 7 waves per SIMD, 4 waves per workgroup)
-#define TRI_SETUP_WGS_PER_CU 7
+// k_setup occupancy target (waves per SIMD); with 4 waves per workgroup, also its workgroups per CU
+#ifndef TRI_SETUP_WAVES
+#define TRI_SETUP_WAVES 6
+#endif
+#define TRI_SETUP_WGS_PER_CU TRI_SETUP_WAVES
 
 struct TriDeviceBuffers {
     const TriVsIn* vin;
