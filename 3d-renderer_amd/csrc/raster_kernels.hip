@@ -802,7 +802,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
         uint2 br[kSetupGroup], sbr[kSetupGroup];
 #pragma unroll
         for (int t = 0; t < kSetupGroup; ++t) {
-            const bool in_chunk = kSetupGroup == 2 || k + t < fp.ppt;  // ppt is even, not always a multiple of 4
+            const bool in_chunk = k + t < fp.ppt;  // ppt need not be a multiple of the group
             p[t] = in_chunk ? chunk0 + (k + t) * TRI_BLOCK + threadIdx.x : ~0u;
             ok[t] = false; needs_clip[t] = false; sok[t] = false;
             sl0[t] = sl1[t] = sl2[t] = 0;
@@ -1702,10 +1702,9 @@ __device__ __forceinline__ void cov_row(const CovEntry& c, uint32_t r, uint64_t*
     }
 }
 
+// One bin: coverage into the LDS key tile, then shading and stores. Reached by the whole workgroup.
 template <bool EXACT, int BL, bool SHADOW>
-// 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
-// a little); 64x64 bins are LDS-limited to 3
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? TRI_RASTER_WAVES_SHADOW : TRI_RASTER_WAVES) : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
+__device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDeviceBuffers& b, const int bin) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
@@ -1719,7 +1718,6 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     __shared__ uint32_t nbig, nentries, nsky;
     const int tid = threadIdx.x;
     TRI_STAMP(0);
-    const int bin = xcd_bin(blockIdx.x, fp.nbins);
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
     const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
     const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);
@@ -1944,6 +1942,16 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     __syncthreads();
     TRI_STAMP(5);
 #endif
+}
+
+// 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
+// a little); 64x64 bins are LDS-limited to 3. One workgroup per bin: a persistent grid (one resident
+// round of workgroups, each walking bins blockIdx + k * gridDim on its XCD) measured 121.5 -> 154 us at C3
+// (13 VGPRs spilled by values hoisted out of the bin loop, and a static bin order that balances worse
+// than the dispatcher's).
+template <bool EXACT, int BL, bool SHADOW>
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? TRI_RASTER_WAVES_SHADOW : TRI_RASTER_WAVES) : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
+    raster_bin<EXACT, BL, SHADOW>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
 
 // ------------------------------------------------------------------------------------------

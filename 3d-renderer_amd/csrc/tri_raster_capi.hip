@@ -1055,7 +1055,10 @@ int tri_render(tri_ctx* c) {
     const bool culling = (c->y0 != 0 || c->y1 != c->H || (c->cfg.flags & TRI_FLAG_CLUSTER_CULL)) && c->ncl_total > 0;
     const uint32_t target_chunks = culling ? 4096u : (uint32_t)c->cu_count * TRI_SETUP_WGS_PER_CU;
     uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
-    ppt = std::min<uint32_t>(std::max<uint32_t>((ppt + 1) & ~1u, 2), TRI_MAX_PPT);  // k_setup takes pairs
+    // k_setup sets up and bins pairs: an odd count leaves half of its last round idle, which costs more
+    // than the extra chunks save (C3: 3 per lane 29.2 us, 4 per lane 28.3 us), except on a frame whose
+    // primitives fit one primitive per lane in one round (C2: 14.2 -> 12.9 us)
+    ppt = ppt <= 1 && !culling ? 1u : std::min<uint32_t>(std::max<uint32_t>((ppt + 1) & ~1u, 2), TRI_MAX_PPT);
     fp.ppt = (int32_t)ppt;
     fp.nchunks = (c->nprims + ppt * TRI_BLOCK - 1) / (ppt * TRI_BLOCK);
     fp.chunk_stride = chunk_stride(fp.nchunks);
