@@ -3,7 +3,8 @@
 //   VsIn      48 B/vertex  {pos.xyz, normal.xyz, color.xyz, uv.xy, pad} (the 44 B of the 100-byte
 //                          Trident Vertex that reach the output; Vertex.h:9-78)
 //   VsSkin    32 B/vertex  {bone indices, bone weights}, only when any draw has BoneCount > 0
-//   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation
+//   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation; written only for
+//                          vertices with an outcode on draws with clip_from_world (the clipper recomputes the rest)
 //   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, z_ndc, 1/w}
 //   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
 //   prim_vs   16 B/prim    {vertex slots 0..2, draw | clipped flag}, written by k_setup for the
@@ -107,7 +108,12 @@ struct __attribute__((aligned(16))) TriDrawDev {
     uint32_t cl_first;   // the mesh's first cluster (TriCluster) and first vertex-block interval
     uint32_t vblk_first;
     uint32_t ncl;        // the mesh's cluster count (0 for an inactive draw)
+    // 1: unskinned with an affine model matrix (last row 0, 0, 0, 1), so world.w == 1 for every finite
+    // vertex and its clip position is pv * (world.xyz, 1): k_vertex stores clip only for vertices with an
+    // outcode, k_setup's clipper recomputes the others from the world position in `vary`
+    uint32_t clip_from_world;
 };
+static_assert(sizeof(TriDrawDev) == 160, "TriDrawDev: 40 words");
 
 // Cluster culling (row bands): a mesh's primitives in runs of TRI_CLUSTER_PRIMS, each with the object-
 // space box of the vertices it references and their mesh-local index range, computed once at upload.

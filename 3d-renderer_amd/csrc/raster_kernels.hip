@@ -211,8 +211,11 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
     const float u = (in.u * dr.tex_scale[0]) * dr.tiling + dr.tex_offset[0];
     const float v = (in.v * dr.tex_scale[1]) * dr.tiling + dr.tex_offset[1];
     const float4 clip = mat_vec_seq(fp.pv, world);
-    b.clip[slot] = clip;
-    const uint32_t oc = outcode(fp, clip);
+    uint32_t oc = outcode(fp, clip);
+    // clip_from_world draws: a vertex without an outcode has world.w == 1 and its clip position is
+    // recomputed by the clipper from `vary`; a non-finite position (w != 1) is marked for clipping
+    if (dr.clip_from_world && oc == 0u && !(world.w == 1.0f)) oc = TRI_OC_CLIP;
+    if (oc != 0u || !dr.clip_from_world) b.clip[slot] = clip;
     TriSnap sn{(int32_t)(oc << 24), 0, 0.0f, 0.0f};
     if (!(oc & TRI_OC_CLIP)) {
         int32_t X, Y;
@@ -474,14 +477,20 @@ __device__ __forceinline__ void wave_lds_sync() {
 // sub-triangle bin it. Must be reached by the whole wave.
 template <bool LPOS>
 __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const TriDeviceBuffers& b, float* poly,
-                                               uint32_t prim, uint32_t sl0, uint32_t sl1, uint32_t sl2,
+                                               uint32_t prim, uint32_t sl0, uint32_t sl1, uint32_t sl2, bool cfw,
                                                uint32_t& nsetup, uint32_t& nentries) {
     const uint32_t lane = lanes_below(~0ull);
     const uint64_t below = (lane == 63) ? 0x7FFFFFFFFFFFFFFFull : ((1ull << lane) - 1ull);
     float* buf[2] = {poly, poly + TRI_MAX_CLIP_VERTS * kClipStride};
     if (lane < 3) {
         ClipVert v;
-        v.c = b.clip[lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2)];
+        const uint32_t sl = lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2);
+        if (cfw && ((uint32_t)b.snap[sl].xo >> 24) == 0u) {  // not stored by k_vertex: world.w == 1
+            const float4 wv = b.vary[3u * sl];
+            v.c = mat_vec_seq(fp.pv, make_float4(wv.x, wv.y, wv.z, 1.0f));
+        } else {
+            v.c = b.clip[sl];
+        }
         v.b0 = lane == 0 ? 1.0f : 0.0f;
         v.b1 = lane == 1 ? 1.0f : 0.0f;
         v.b2 = lane == 2 ? 1.0f : 0.0f;
@@ -799,6 +808,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     for (int k = 0; k < fp.ppt; k += kSetupGroup) {  // uniform trip count: binning needs the whole workgroup
         uint32_t p[kSetupGroup], sl0[kSetupGroup], sl1[kSetupGroup], sl2[kSetupGroup];
         bool ok[kSetupGroup], needs_clip[kSetupGroup], sok[kSetupGroup];
+        int pd[kSetupGroup];  // the primitive's draw
         uint2 br[kSetupGroup], sbr[kSetupGroup];
 #pragma unroll
         for (int t = 0; t < kSetupGroup; ++t) {
@@ -809,7 +819,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             br[t] = make_uint2(0u, 0u);
             sbr[t] = make_uint2(0u, 0u);
             bool culled = false;
-            int d = 0;
+            int& d = pd[t];
+            d = 0;
             uint32_t vb = 0, i0 = 0, i1 = 0, i2 = 0;
             if (p[t] < fp.nprims) {
                 // the indices are fetched together with the cluster flag, not after it: a band's
@@ -886,7 +897,10 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                     clip_prim_wave<WITH_SHADOW>(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl0[t], src),
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl1[t], src),
-                                                (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src), nsetup, nentries);
+                                                (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src),
+                                                fp.one_draw ? fp.draw0.clip_from_world != 0u
+                                                            : b.draws[__builtin_amdgcn_readlane(pd[t], src)].clip_from_world != 0u,
+                                                nsetup, nentries);
                 }
             }
         }

@@ -378,6 +378,8 @@ int resolve_draws(tri_ctx* c) {
         o.tiling = src.pc.tiling_factor;
         o.bone_offset = src.pc.bone_offset;
         o.bone_count = src.pc.bone_count;
+        o.clip_from_world = (o.bone_count <= 0 && o.model[3] == 0.0f && o.model[7] == 0.0f && o.model[11] == 0.0f &&
+                             o.model[15] == 1.0f) ? 1u : 0u;
         vb[d] = (uint32_t)vslots;
         pb[d] = (uint32_t)prims;
         cbase[d] = (uint32_t)ncl;
