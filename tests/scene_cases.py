@@ -100,6 +100,18 @@ def depth_ties(w=256, h=256):
                         materials=[((1, 1, 1, 1), (0.2, 0.5, 1.0, 0.0))])
 
 
+def large_quads(w=1920, h=1080, one_draw=False):
+    """Screen-filling quads over 1920x1080 (2040 bins of 32x32): a set-up round whose bins span more than
+    k_setup's 1024-cell LDS grid, so binning takes the per-wave reservation path."""
+    s = depth_ties(w, h)
+    big = scenes.compose_transform((0.0, 0.0, 0.0), (0, 0, 0), (3.5, 3.5, 1.0))
+    tilted = scenes.compose_transform((0.4, -0.3, 0.5), (25.0, 35.0, 0), (2.5, 2.5, 1.0))
+    s.draws = [abi.make_draw(0, big, tint=(1, 0.3, 0.2, 1))] if one_draw else \
+        [abi.make_draw(0, big, tint=(1, 0.3, 0.2, 1)), abi.make_draw(0, tilted, tint=(0.2, 0.9, 0.4, 1))]
+    s.name = "large_quads_1" if one_draw else "large_quads_2"
+    return s
+
+
 def skinned_quad(oracle, w=256, h=256):
     """GPU skinning branch (Default.vert:64-85): 2-bone palette at an offset, weights per vertex,
     one out-of-range bone index (skipped)."""

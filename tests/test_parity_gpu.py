@@ -66,6 +66,12 @@ def test_c5_four_textured_draws(oracle, flags):
     assert_parity(s, oracle, min_covered=100000, flags=flags)
 
 
+@pytest.mark.parametrize("one_draw", [True, False])
+def test_large_triangles_per_wave_binning(oracle, one_draw):
+    """Triangles spanning more bins than k_setup's workgroup grid: the per-wave reservation fallback."""
+    assert_parity(sc.large_quads(one_draw=one_draw), oracle, min_covered=1920 * 1080 // 2)
+
+
 def test_c2_sphere_1080p(oracle, flags):
     assert_parity(sc.sphere_c2(oracle=oracle), oracle, min_covered=300000, flags=flags)
 
