@@ -5,7 +5,8 @@
 //   VsSkin    32 B/vertex  {bone indices, bone weights}, only when any draw has BoneCount > 0
 //   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation; written only for
 //                          vertices with an outcode on draws with clip_from_world (the clipper recomputes the rest)
-//   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, z_ndc, 1/w}
+//   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, 1/w, z_ndc} (the fragment stage
+//                          loads the first 12 bytes: it needs no depth)
 //   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
 //   prim_vs   16 B/prim    {vertex slots 0..2, draw | clipped flag}, written by k_setup for the
 //                          primitives it bins or clips on frames with several draws: k_raster's one-load
@@ -62,12 +63,12 @@ struct __attribute__((aligned(16))) TriVsSkin {
 };
 
 // Per-vertex window-space record written by k_vertex (the perspective divide + viewport transform
-// + 8-bit snap are done once per vertex): X (signed 24 bits) | outcode << 24, Y, z_ndc, 1/w.
+// + 8-bit snap are done once per vertex): X (signed 24 bits) | outcode << 24, Y, 1/w, z_ndc.
 struct __attribute__((aligned(16))) TriSnap {
     int32_t xo;
     int32_t y;
-    float z;
     float iw;
+    float z;
 };
 // outcode bits: one per Vulkan clip half-space a vertex is outside of, + "needs geometric clip"
 #define TRI_OC_ZNEG 0x01u   /* z < 0     */

@@ -105,6 +105,11 @@ __device__ __forceinline__ TriSnap ld_snap(const FetchBufs& fb, uint32_t slot) {
     const uint4 q = ld128(fb.snap, slot * 16u);
     return TriSnap{(int32_t)q.x, (int32_t)q.y, __uint_as_float(q.z), __uint_as_float(q.w)};
 }
+// The fragment stage's view of a snapped vertex: X, Y and 1/w (12 bytes, one load; z is not needed).
+__device__ __forceinline__ TriSnap ld_snap_xyw(const FetchBufs& fb, uint32_t slot) {
+    const auto q = __builtin_amdgcn_raw_buffer_load_b96(fb.snap, slot * 16u, 0, 0);
+    return TriSnap{(int32_t)q[0], (int32_t)q[1], __uint_as_float(q[2]), 0.0f};
+}
 
 // ((c0*x + c1*y) + c2*z) + c3*w, column-major, no FMA (matches the oracle bit-for-bit)
 __device__ __forceinline__ float4 mat_vec_seq(const float* m, float4 v) {
@@ -137,7 +142,7 @@ __device__ __forceinline__ void shadow_vertex(const TriFrameParams& fp, const Tr
     if (l.y + 1.0f < 0.0f) oc |= TRI_OC_YNEG;
     if (1.0f - l.y < 0.0f) oc |= TRI_OC_YPOS;
     if (l.x < -fp.s_g || l.x > fp.s_g || l.y < -fp.s_g || l.y > fp.s_g) oc |= TRI_OC_CLIP;
-    TriSnap sn{(int32_t)(oc << 24), 0, l.z, 1.0f};
+    TriSnap sn{(int32_t)(oc << 24), 0, 1.0f, l.z};
     if (!(oc & TRI_OC_CLIP)) {
         const int32_t X = (int32_t)rintf((l.x * fp.s_hw + fp.s_hw) * 256.0f);
         sn.xo = (X & 0x00FFFFFF) | (int32_t)(oc << 24);
@@ -1431,8 +1436,17 @@ __device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint
 
 // The varyings at weights (w0, w1, w2), the draw d's texture sample and tint: Frag fields 0..18 through
 // `put`.
+// The draw's 48-B shade record (tint, texture descriptor): its address needs only the draw, so it is
+// loaded together with the varyings.
+struct ShadeRec {
+    uint4 st, sd, ss;
+};
+__device__ __forceinline__ ShadeRec load_shade(const FetchBufs& fb, uint32_t d) {
+    return ShadeRec{ld128(fb.shade, d * 48u), ld128(fb.shade, d * 48u + 16u), ld128(fb.shade, d * 48u + 32u)};
+}
+
 template <bool EXACT, typename Put>
-__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, const Taps& t, uint32_t d,
+__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Taps& t, const ShadeRec& sh,
                                             float w0, float w1, float w2, const float* lut, Put&& put) {
     auto ip = [&](float x0, float x1, float x2) {
         return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
@@ -1445,7 +1459,7 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
     put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
     const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
     put(9, u); put(10, v);
-    const uint4 st = ld128(fb.shade, d * 48u), sd = ld128(fb.shade, d * 48u + 16u), ss = ld128(fb.shade, d * 48u + 32u);
+    const uint4 &st = sh.st, &sd = sh.sd, &ss = sh.ss;
     TriTexDesc td;
     td.texels = reinterpret_cast<const uint32_t*>(((uint64_t)sd.y << 32) | sd.x);
     td.w = sd.z; td.h = sd.w;
@@ -1469,12 +1483,23 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     const FetchBufs fb = fetch_bufs(fp, b);
     uint32_t sl[3], d;
     prim_slots(fp, b, prim, sl, d);
-    TriRec r;
-    if (sub)
-        r = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
-    else
-        r = rec_from_snaps(prim, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
-    const Taps taps = load_taps(fb, r.v[0], r.v[1], r.v[2]);
+    // Every gather that needs only the slots and the draw is issued before the first wait: the snapped
+    // vertices, the nine varyings and the shade record are one round trip after the index fetch (the
+    // snaps are loaded for a clipped primitive too, unused: its sub-triangle's record names its slots).
+    const TriSnap a0 = ld_snap_xyw(fb, sl[0]), a1 = ld_snap_xyw(fb, sl[1]), a2 = ld_snap_xyw(fb, sl[2]);
+    uint32_t v0 = sl[0], v1 = sl[2], v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
+    TriRec rc;
+    if (sub) {
+        rc = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
+        v0 = rc.v[0]; v1 = rc.v[1]; v2 = rc.v[2];
+    }
+    const Taps taps = load_taps(fb, v0, v1, v2);
+    uint4 L0, L1, L2;
+    if constexpr (SHADOW) {
+        const Rsrc lr = make_rsrc(b.lpos, 16ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
+        L0 = ld128(lr, v0 * 16u); L1 = ld128(lr, v1 * 16u); L2 = ld128(lr, v2 * 16u);
+    }
+    const TriRec r = sub ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
     float w0, w1, w2;
     if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
         exact_weights(r, px, py, w0, w1, w2);
@@ -1485,15 +1510,13 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     if constexpr (SHADOW) {  // light-space position at the pixel with the oracle's weights, then the compare
         float e0 = w0, e1 = w1, e2 = w2;
         if (!EXACT && !(kAblate & 512)) exact_weights(r, px, py, e0, e1, e2);  // 512: fast weights (diagnostics)
-        const Rsrc lr = make_rsrc(b.lpos, 16ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
-        const uint4 L0 = ld128(lr, r.v[0] * 16u), L1 = ld128(lr, r.v[1] * 16u), L2 = ld128(lr, r.v[2] * 16u);
         auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
             return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
         };
         vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
     }
     put(19, vis);
-    fetch_attrs<EXACT>(fp, fb, taps, d, w0, w1, w2, lut, put);
+    fetch_attrs<EXACT>(fp, taps, load_shade(fb, d), w0, w1, w2, lut, put);
 }
 
 template <bool EXACT, bool SHADOW>
@@ -1985,9 +2008,9 @@ __device__ __forceinline__ TriRec load_shadow_entry(const TriFrameParams& fp, co
     const int64_t S = (int64_t)(X1 - X0) * (int64_t)(Y2 - Y0) - (int64_t)(Y1 - Y0) * (int64_t)(X2 - X0);
     const bool sw = S < 0;
     TriRec r;
-    r.X[0] = X0; r.Y[0] = Y0; r.z[0] = __uint_as_float(q0.z);
-    r.X[1] = sw ? X2 : X1; r.Y[1] = sw ? Y2 : Y1; r.z[1] = __uint_as_float(sw ? q2.z : q1.z);
-    r.X[2] = sw ? X1 : X2; r.Y[2] = sw ? Y1 : Y2; r.z[2] = __uint_as_float(sw ? q1.z : q2.z);
+    r.X[0] = X0; r.Y[0] = Y0; r.z[0] = __uint_as_float(q0.w);
+    r.X[1] = sw ? X2 : X1; r.Y[1] = sw ? Y2 : Y1; r.z[1] = __uint_as_float(sw ? q2.w : q1.w);
+    r.X[2] = sw ? X1 : X2; r.Y[2] = sw ? Y1 : Y2; r.z[2] = __uint_as_float(sw ? q1.w : q2.w);
     r.iw[0] = r.iw[1] = r.iw[2] = 1.0f;
     r.prim_sub = e << 3;
     r.v[0] = r.v[1] = r.v[2] = 0;

@@ -42,7 +42,7 @@ struct TriDeviceBuffers {
     uint32_t* cvis;              // ncl_total visibility flags, written by k_vertex each frame
     // shadow-map pre-pass (only when TriFrameParams::shadow_on)
     float4* lpos;                // nslots + ovf_vert_cap: light-NDC position per vertex slot (xyz, 0)
-    TriSnap* lsnap;              // nslots: the light-NDC position snapped to the map ({X | outcode << 24, Y, z, 1})
+    TriSnap* lsnap;              // nslots: the light-NDC position snapped to the map ({X | outcode << 24, Y, 1, z})
     uint32_t* sbin_count;        // s_nbins shadow-map bin counters (zeroed by k_shadow_raster)
     uint32_t* sbin_list;         // s_nbins * s_bin_cap primitive ids
     uint32_t* shadow_map;        // s_size * s_size float32 depth bits

@@ -6,16 +6,16 @@ cd "$(dirname "$0")/.."
 name=$1; rev=$2
 src=$(mktemp -d)
 mkdir -p $src/pkg/csrc $src/include 3d-renderer_amd/lib/variants/obj_$name
-for f in raster_kernels.hip tri_raster_capi.hip raster_common.h raster_launch.h; do
+for f in raster_kernels.hip tri_raster_capi.hip tri_group.hip raster_common.h raster_launch.h; do
   git show $rev:3d-renderer_amd/csrc/$f > $src/pkg/csrc/$f
 done
 git show $rev:include/tri_raster.h > $src/include/tri_raster.h
 out=$PWD/3d-renderer_amd/lib/variants
-for s in raster_kernels tri_raster_capi; do
+for s in raster_kernels tri_raster_capi tri_group; do
   (cd $src/pkg && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function \
      -c csrc/$s.hip -o $out/obj_$name/$s.o) &
 done
 wait
-/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o $out/$name.so $out/obj_$name/*.o
+/opt/rocm/bin/hipcc -O3 -fPIC --offload-arch=gfx950 -shared -o $out/$name.so $out/obj_$name/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -rf $src
 echo "built 3d-renderer_amd/lib/variants/$name.so ($rev)"
