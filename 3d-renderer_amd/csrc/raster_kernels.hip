@@ -1263,27 +1263,26 @@ __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag&
 // V and L, |V + L|^2 = 2 + 2 L.V, N.H = (N.V + N.L) / |V + L| and H.V = (1 + L.V) / |V + L|.
 struct PbrPix {
     f3 N, V, F0, omF0, diffK;
-    float NdotVr, NdotV4, gV;  // NdotVr: unclamped N.V
+    float NdotVr, NdotV4, gVa;  // NdotVr: unclamped N.V; gVa = a2 / pi * G_V
 };
 
-__device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const PbrPix& px, f3 L, f3 rad, float scale,
-                                              f3& c) {
+// One light with unclamped N.L and L.V given (the caller forms them without normalising L first).
+__device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const PbrPix& px, float NdotLr, float LdotV,
+                                              f3 rad, float scale, f3& c) {
 #pragma clang fp contract(fast)  // fast build only: FMA contraction is inside the 1-LSB budget
-    const float NdotLr = fdot(px.N, L);
     // N.L <= 0 makes the light's weight 0 and every term finite: c + X * 0 == c exactly, so a wave
     // whose lanes all face away skips the rest (Default.frag evaluates it to the same zero)
     if (!(NdotLr > 0.0f)) return;
-    const float LdotV = fdot(L, px.V);
     const float ih = frsq(fmaxf(__builtin_fmaf(2.0f, LdotV, 2.0f), 1e-30f));
     const float NdotH = fmaxf((px.NdotVr + NdotLr) * ih, 0.0f);
-    const float HdotV = fmaxf(__builtin_fmaf(LdotV, ih, ih), 0.0f);
     const float NdotL = NdotLr;  // > 0 here: max(N.L, 0) is the identity
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
     const float gden = fmaxf(__builtin_fmaf(NdotL, sc.omkg, sc.kg), 1e-4f);
     const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
     // NDF * G_L * G_V / den with NDF = a2 / (pi dd^2), G_L = NdotL / gden
-    const float sp = (sc.a2pi * NdotL) * px.gV * frcp(((dd * dd) * gden) * den);
-    const float q = fmaxf(1.0f - HdotV, 0.0f);
+    const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
+    // 1 - max(H.V, 0), clamped to [0, 1]: one clamped subtract
+    const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
     const float q2 = q * q;
     const float p5 = q2 * q2 * q;
     const float w = NdotL * scale;
@@ -1307,13 +1306,14 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
     px.NdotV4 = 4.0f * NdotV;
-    px.gV = NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
+    px.gVa = sc.a2pi * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
     f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
               sc.amb[2] * albedo.z * sc.amb_strength);
     if (kAblate & 64) return make_float4(c.x, c.y, c.z, 1.0f);  // diagnostics: 64 = no lights
-    if (sc.has_sun && f.vis > 0.0f)  // vis = 0 (fully shadowed): the sun adds exactly nothing
-        eval_pbr_fast(sc, px, mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]),
-                      mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), f.vis, c);
+    if (sc.has_sun && f.vis > 0.0f) {  // vis = 0 (fully shadowed): the sun adds exactly nothing
+        const f3 L = mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]);
+        eval_pbr_fast(sc, px, fdot(px.N, L), fdot(L, px.V), mk(sc.sun_rad[0], sc.sun_rad[1], sc.sun_rad[2]), f.vis, c);
+    }
     const f3 wp = fworld(f);
     for (uint32_t i = 0; i < sc.npt; ++i) {
         const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
@@ -1322,7 +1322,9 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         const float inv = frsq(d2);
         const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
         if (!(att0 > 0.0f)) continue;  // beyond the light's range: (1 - d/r)^2 = 0 adds exactly nothing
-        eval_pbr_fast(sc, px, muls(to, inv), mk(sc.pl_rad[i][0], sc.pl_rad[i][1], sc.pl_rad[i][2]), att0 * att0, c);
+        // L = to / |to| is never formed: N.L and L.V are the dot products with `to`, scaled once
+        eval_pbr_fast(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv,
+                      mk(sc.pl_rad[i][0], sc.pl_rad[i][1], sc.pl_rad[i][2]), att0 * att0, c);
     }
     const float g = 1.0f / 2.2f;
     const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
