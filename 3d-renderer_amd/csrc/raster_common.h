@@ -169,6 +169,9 @@ struct TriShadeConst {
     float pl_rad[TRI_MAX_POINT_LIGHTS][4];  // ColorIntensity.rgb * .w
     // roughness terms of the fast BRDF: a2 - 1, a2 / pi, Schlick-GGX k and 1 - k (a = roughness^2)
     float a2m1, a2pi, kg, omkg;
+    // single-draw frames whose texture slot is 1x1 (TriFrameParams::shade_solid): the draw's decoded texel
+    // and tint, so no fragment gathers its shade record
+    float solid[4], tint[4];
 };
 
 struct TriFrameParams {
@@ -177,7 +180,7 @@ struct TriFrameParams {
     int32_t bin_log2;
     uint32_t sky_lut;   // the skybox pass samples the cubemap: workgroups with sky pixels stage the sRGB LUT
     uint32_t chunk_stride;  // k_setup visits chunks in the order (blockIdx * stride) mod nchunks
-    int32_t pad_b2;
+    uint32_t shade_solid;   // one draw with a 1x1 texture slot: sc.solid / sc.tint replace its shade record
     float hw, hh, gx, gy;
     uint32_t nprims, nslots, ndraws, nchunks;
     uint32_t ovf_rec_cap, ovf_vert_cap, bin_cap, bone_count;

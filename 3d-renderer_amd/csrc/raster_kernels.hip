@@ -1447,8 +1447,9 @@ __device__ __forceinline__ ShadeRec load_shade(const FetchBufs& fb, uint32_t d) 
     return ShadeRec{ld128(fb.shade, d * 48u), ld128(fb.shade, d * 48u + 16u), ld128(fb.shade, d * 48u + 32u)};
 }
 
+
 template <bool EXACT, typename Put>
-__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Taps& t, const ShadeRec& sh,
+__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, const Taps& t, uint32_t d,
                                             float w0, float w1, float w2, const float* lut, Put&& put) {
     auto ip = [&](float x0, float x1, float x2) {
         return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
@@ -1461,6 +1462,12 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Taps
     put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
     const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
     put(9, u); put(10, v);
+    if (fp.shade_solid) {  // uniform: one draw with a 1x1 slot, its texel and tint are kernel arguments
+        for (int i = 0; i < 4; ++i) put(11 + i, fp.sc.solid[i]);
+        for (int i = 0; i < 4; ++i) put(15 + i, fp.sc.tint[i]);
+        return;
+    }
+    const ShadeRec sh = load_shade(fb, d);
     const uint4 &st = sh.st, &sd = sh.sd, &ss = sh.ss;
     TriTexDesc td;
     td.texels = reinterpret_cast<const uint32_t*>(((uint64_t)sd.y << 32) | sd.x);
@@ -1518,7 +1525,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
     }
     put(19, vis);
-    fetch_attrs<EXACT>(fp, taps, load_shade(fb, d), w0, w1, w2, lut, put);
+    fetch_attrs<EXACT>(fp, fb, taps, d, w0, w1, w2, lut, put);
 }
 
 template <bool EXACT, bool SHADOW>

@@ -127,6 +127,7 @@ struct tri_ctx {
     // resolved draws
     TriDrawDev* d_draws = nullptr; size_t cap_draws = 0;
     TriDrawShade* d_draw_shade = nullptr; size_t cap_draw_shade = 0;
+    TriDrawShade shade0{};  // the shade record of a single-draw frame
     uint32_t* d_vbase = nullptr; size_t cap_vbase = 0;
     uint32_t* d_pbase = nullptr; size_t cap_pbase = 0;
     uint32_t* d_cbase = nullptr; size_t cap_cbase = 0;
@@ -439,7 +440,10 @@ int resolve_draws(tri_ctx* c) {
     if (!c->stage_free) HIP_TRY(hipEventCreateWithFlags(&c->stage_free, hipEventDisableTiming));
     HIP_TRY(hipEventRecord(c->stage_free, c->stream));
     c->ndraws = n;
-    if (n == 1) c->draw0 = dd[0];
+    if (n == 1) {
+        c->draw0 = dd[0];
+        c->shade0 = ds[0];
+    }
     c->nslots = (uint32_t)vslots;
     c->nprims = (uint32_t)prims;
     c->ncl_total = (uint32_t)ncl;
@@ -1074,6 +1078,7 @@ int tri_render(tri_ctx* c) {
     fp.ndraws = c->ndraws;
     fp.one_draw = c->ndraws == 1 ? 1u : 0u;
     if (fp.one_draw) fp.draw0 = c->draw0;
+    fp.shade_solid = (fp.one_draw && c->shade0.tex.w == 1 && c->shade0.tex.h == 1) ? 1u : 0u;
     fp.ovf_rec_cap = c->ovf_rec_cap;
     fp.ovf_vert_cap = c->ovf_vert_cap;
     fp.bin_cap = c->bin_cap;
@@ -1116,6 +1121,10 @@ int tri_render(tri_ctx* c) {
     fp.ubo = c->ubo;
     fp.mat0 = c->mat0;
     shade_constants(c->ubo, c->mat0, fp.sc);
+    if (fp.shade_solid) {  // (after shade_constants, which clears fp.sc)
+        std::memcpy(fp.sc.solid, c->shade0.tex.solid, 16);
+        std::memcpy(fp.sc.tint, c->shade0.tint, 16);
+    }
 
     TriDeviceBuffers b;
     b.vin = c->geom->d_vin;
