@@ -161,7 +161,9 @@ __device__ __forceinline__ void reset_counters(TriCounters* c) {
     c->bin_entries = 0;  // `flags` / `bin_max` are sticky (cleared by the host)
 }
 
+#ifndef TRI_RASTER_PLAIN_TU
 __global__ void k_reset(TriDeviceBuffers b) { reset_counters(b.counters); }
+#endif  // TRI_RASTER_PLAIN_TU
 
 // Default.vert for vertex slot `slot` of draw `dr` (whose first slot is `vbase`).
 __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
@@ -278,6 +280,7 @@ __device__ __forceinline__ bool cluster_visible(const TriFrameParams& fp, const 
 // box of its 256-slot vertex block (the clusters referencing it, precomputed at upload: one load) and,
 // unless the shadow pre-pass needs every caster, skips a block whose box misses the rows. A vertex of any
 // visible primitive is always transformed: its cluster's box lies inside the block's union box.
+#ifndef TRI_RASTER_PLAIN_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
     const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
     if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
@@ -312,6 +315,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
     if (!valid || (fp.cull_vertex && !needed)) return;
     vertex_slot(fp, b, slot, fp.one_draw ? fp.draw0 : b.draws[d], vbase);
 }
+#endif  // TRI_RASTER_PLAIN_TU
 
 // ------------------------------------------------------------------------------------------
 // tri_setup_bin
@@ -1422,24 +1426,34 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
     return l0 + bb * (l1 - l0);
 }
 
-// The varyings of the triangle's three vertex slots: nine 16-B gathers, issued before the weights are
-// computed (their addresses need only the slots, the weights need the snapped vertices too).
+// The varyings of the triangle's three vertex slots: 16-B gathers, issued before the weights are
+// computed (their addresses need only the slots, the weights need the snapped vertices too). With
+// TRI_COLOUR_LATE (k_raster_plain) the three colour gathers are issued once the weights are done and the
+// snapped vertices' registers are free: the peak register count falls enough for 7 waves/SIMD.
+#ifndef TRI_COLOUR_LATE
+#ifdef TRI_RASTER_PLAIN_TU
+#define TRI_COLOUR_LATE 1
+#else
+#define TRI_COLOUR_LATE 0
+#endif
+#endif
 struct Taps {
     V4 a0, a1, a2, b0, b1, b2, c0, c1, c2;
 };
+__device__ __forceinline__ V4 ld_vary(const FetchBufs& fb, uint32_t slot, uint32_t j) {
+    const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);  // plain-float views (HIP vector unions defeat SROA)
+    return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
+}
 __device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint32_t v1, uint32_t v2) {
-    auto ldv = [&](uint32_t slot, uint32_t j) -> V4 {  // plain-float views (HIP vector unions defeat SROA)
-        const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);
-        return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
-    };
-    return Taps{ldv(v0, 0), ldv(v0, 1), ldv(v0, 2), ldv(v1, 0), ldv(v1, 1), ldv(v1, 2),
-                ldv(v2, 0), ldv(v2, 1), ldv(v2, 2)};
+    Taps t;
+    t.a0 = ld_vary(fb, v0, 0); t.a1 = ld_vary(fb, v0, 1);
+    t.b0 = ld_vary(fb, v1, 0); t.b1 = ld_vary(fb, v1, 1);
+    t.c0 = ld_vary(fb, v2, 0); t.c1 = ld_vary(fb, v2, 1);
+    if (!TRI_COLOUR_LATE) { t.a2 = ld_vary(fb, v0, 2); t.b2 = ld_vary(fb, v1, 2); t.c2 = ld_vary(fb, v2, 2); }
+    return t;
 }
 
-// The varyings at weights (w0, w1, w2), the draw d's texture sample and tint: Frag fields 0..18 through
-// `put`.
-// The draw's 48-B shade record (tint, texture descriptor): its address needs only the draw, so it is
-// loaded together with the varyings.
+// The draw's 48-B shade record (tint, texture descriptor).
 struct ShadeRec {
     uint4 st, sd, ss;
 };
@@ -1448,6 +1462,8 @@ __device__ __forceinline__ ShadeRec load_shade(const FetchBufs& fb, uint32_t d) 
 }
 
 
+// The varyings at weights (w0, w1, w2), the draw d's texture sample and tint: Frag fields 0..18 through
+// `put`.
 template <bool EXACT, typename Put>
 __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, const Taps& t, uint32_t d,
                                             float w0, float w1, float w2, const float* lut, Put&& put) {
@@ -1492,9 +1508,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     const FetchBufs fb = fetch_bufs(fp, b);
     uint32_t sl[3], d;
     prim_slots(fp, b, prim, sl, d);
-    // Every gather that needs only the slots and the draw is issued before the first wait: the snapped
-    // vertices, the nine varyings and the shade record are one round trip after the index fetch (the
-    // snaps are loaded for a clipped primitive too, unused: its sub-triangle's record names its slots).
+    // Every gather that needs only the slots is issued before the first wait: the snapped vertices and
+    // the varyings are one round trip after the index fetch (the snaps are loaded for a clipped primitive
+    // too, unused: its sub-triangle's record names its slots).
     const TriSnap a0 = ld_snap_xyw(fb, sl[0]), a1 = ld_snap_xyw(fb, sl[1]), a2 = ld_snap_xyw(fb, sl[2]);
     uint32_t v0 = sl[0], v1 = sl[2], v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
     TriRec rc;
@@ -1502,7 +1518,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         rc = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
         v0 = rc.v[0]; v1 = rc.v[1]; v2 = rc.v[2];
     }
-    const Taps taps = load_taps(fb, v0, v1, v2);
+    Taps taps = load_taps(fb, v0, v1, v2);
     uint4 L0, L1, L2;
     if constexpr (SHADOW) {
         const Rsrc lr = make_rsrc(b.lpos, 16ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
@@ -1514,6 +1530,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         exact_weights(r, px, py, w0, w1, w2);
     } else {
         fast_weights(fast_coefs(r), r.X[0], r.Y[0], px, py, w0, w1, w2);
+    }
+    if (TRI_COLOUR_LATE) {
+        taps.a2 = ld_vary(fb, v0, 2); taps.b2 = ld_vary(fb, v1, 2); taps.c2 = ld_vary(fb, v2, 2);
     }
     float vis = 1.0f;
     if constexpr (SHADOW) {  // light-space position at the pixel with the oracle's weights, then the compare
@@ -1676,6 +1695,9 @@ __device__ __forceinline__ uint32_t sky_bgra_persp(const TriFrameParams& fp, con
 
 #ifndef TRI_RASTER_WAVES
 #define TRI_RASTER_WAVES 6  // k_raster occupancy target at 32x32 bins (waves per SIMD)
+#endif
+#ifndef TRI_RASTER_WAVES_PLAIN
+#define TRI_RASTER_WAVES_PLAIN 7  // k_raster_plain (raster_plain.hip, no SLP): 69 VGPRs, no spill
 #endif
 #ifndef TRI_RASTER_WAVES_SHADOW
 #define TRI_RASTER_WAVES_SHADOW 5  // with the shadow lookup (6 spilled: C5 raster 207 us at 5 vs 213 at 6)
@@ -1999,6 +2021,14 @@ template <bool EXACT, int BL, bool SHADOW>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? TRI_RASTER_WAVES_SHADOW : TRI_RASTER_WAVES) : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
     raster_bin<EXACT, BL, SHADOW>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
+// Frames without the shadow pre-pass: this instantiation lives in its own translation unit
+// (raster_plain.hip), compiled without SLP vectorisation: packed-FP32 pairs need their uniform operands
+// copied into VGPR pairs, and without them the fast build fits 7 waves/SIMD with no spill (C3 k_raster
+// 117 -> 112 us). Frames with the pre-pass keep k_raster<.., true> (5 waves, SLP: faster there).
+template <bool EXACT, int BL>
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES_PLAIN : 3))) void k_raster_plain(TriFrameParams fp, TriDeviceBuffers b) {
+    raster_bin<EXACT, BL, false>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
+}
 
 // ------------------------------------------------------------------------------------------
 // shadow pre-pass raster (oracle shadow_raster_triangle): one workgroup per 32x32 bin of the s_size^2
@@ -2069,6 +2099,7 @@ __device__ __forceinline__ void shadow_serial(const TriFrameParams& fp, const Tr
     }
 }
 
+#ifndef TRI_RASTER_PLAIN_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TriFrameParams fp, TriDeviceBuffers b) {
     constexpr int BIN = 32;
     __shared__ uint32_t dep[BIN * BIN];
@@ -2136,6 +2167,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TriFrameParams fp, 
         if (lx < bw && ly < bh) b.shadow_map[(size_t)(oy + ly) * S + ox + lx] = dep[i];
     }
 }
+#endif  // TRI_RASTER_PLAIN_TU
 
 // ------------------------------------------------------------------------------------------
 // presentation blit (Renderer.cpp:5346-5361, vkCmdBlitImage with VK_FILTER_LINEAR): one lane per
@@ -2143,6 +2175,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TriFrameParams fp, 
 // bilinearly over clamp-to-edge taps on UNORM values (b / 255), rounded to UNORM8. Same float
 // operation order as the oracle's blit_linear (bit-exact). Rows are coalesced per wave.
 // ------------------------------------------------------------------------------------------
+#ifndef TRI_RASTER_PLAIN_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__ src, int32_t w, int32_t h,
                                                     uint32_t* __restrict__ dst, int32_t dw, int32_t dh, float sx,
                                                     float sy, const float* __restrict__ lut) {
@@ -2169,16 +2202,40 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__
     }
     dst[(size_t)y * dw + x] = out;
 }
+#endif  // TRI_RASTER_PLAIN_TU
 
 }  // namespace
 
+#ifdef TRI_RASTER_PLAIN_TU
+hipError_t tri_launch_raster_plain(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream) {
+    const dim3 g(fp.nbins), t(TRI_BLOCK);
+    const bool ex = fp.exact_shading != 0;
+    if (fp.bin_log2 == 5) {
+        if (ex) hipLaunchKernelGGL((k_raster_plain<true, 5>), g, t, 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_raster_plain<false, 5>), g, t, 0, stream, fp, b);
+    } else if (fp.bin_log2 == 4) {
+        if (ex) hipLaunchKernelGGL((k_raster_plain<true, 4>), g, t, 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_raster_plain<false, 4>), g, t, 0, stream, fp, b);
+    } else {
+        if (ex) hipLaunchKernelGGL((k_raster_plain<true, 6>), g, t, 0, stream, fp, b);
+        else hipLaunchKernelGGL((k_raster_plain<false, 6>), g, t, 0, stream, fp, b);
+    }
+    return hipGetLastError();
+}
+#ifdef TRI_PHASE_TIMING
+extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {  // k_raster_plain's stamps
+    const size_t n = (size_t)(nslots < kPhaseSlots ? nslots : kPhaseSlots) * 6 * sizeof(unsigned long long);
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
+#else  // the main translation unit
 hipError_t tri_kernels_init() { return hipSuccess; }
 
 template <bool EXACT, int BL>
 static void launch_raster(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream) {
     const dim3 g(fp.nbins), t(TRI_BLOCK);
     if (fp.shadow_on) hipLaunchKernelGGL((k_raster<EXACT, BL, true>), g, t, 0, stream, fp, b);
-    else hipLaunchKernelGGL((k_raster<EXACT, BL, false>), g, t, 0, stream, fp, b);
+    else (void)tri_launch_raster_plain(fp, b, stream);  // raster_plain.hip (errors surface in hipGetLastError)
 }
 
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
@@ -2232,12 +2289,9 @@ hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* 
 }
 
 #ifdef TRI_PHASE_TIMING
-extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {
-    const size_t n = (size_t)(nslots < kPhaseSlots ? nslots : kPhaseSlots) * 6 * sizeof(unsigned long long);
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
 extern "C" int tri_debug_setup_times(unsigned long long* out, int nslots) {
     const size_t n = (size_t)(nslots < kPhaseSlots ? nslots : kPhaseSlots) * 4 * sizeof(unsigned long long);
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_setup_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
+#endif  // TRI_RASTER_PLAIN_TU

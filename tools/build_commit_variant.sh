@@ -5,14 +5,20 @@ set -e
 cd "$(dirname "$0")/.."
 name=$1; rev=$2
 src=$(mktemp -d)
-mkdir -p $src/pkg/csrc $src/include 3d-renderer_amd/lib/variants/obj_$name
-for f in raster_kernels.hip tri_raster_capi.hip tri_group.hip raster_common.h raster_launch.h; do
-  git show $rev:3d-renderer_amd/csrc/$f > $src/pkg/csrc/$f
+out=$PWD/3d-renderer_amd/lib/variants
+rm -rf $out/obj_$name
+mkdir -p $src/pkg/csrc $src/include $out/obj_$name
+units=""
+for f in raster_kernels.hip raster_plain.hip tri_raster_capi.hip tri_group.hip raster_common.h raster_launch.h; do
+  if git cat-file -e $rev:3d-renderer_amd/csrc/$f 2>/dev/null; then
+    git show $rev:3d-renderer_amd/csrc/$f > $src/pkg/csrc/$f
+    case $f in *.hip) units="$units ${f%.hip}";; esac
+  fi
 done
 git show $rev:include/tri_raster.h > $src/include/tri_raster.h
-out=$PWD/3d-renderer_amd/lib/variants
-for s in raster_kernels tri_raster_capi tri_group; do
-  (cd $src/pkg && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function \
+for s in $units; do
+  extra=""; [ $s = raster_plain ] && extra="-fno-slp-vectorize"
+  (cd $src/pkg && /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function $extra \
      -c csrc/$s.hip -o $out/obj_$name/$s.o) &
 done
 wait
