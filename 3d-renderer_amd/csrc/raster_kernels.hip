@@ -997,9 +997,12 @@ __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3
 
 // The vertex slots and draw of primitive p: on a single-draw frame straight from the index buffer (slot =
 // index - min_index, as k_setup computed them; k_setup writes no prim_vs then), else its prim_vs record.
+// ONE (k_raster_plain's single-draw, 1x1-texture instantiation): fp.one_draw and fp.shade_solid are known
+// to be set, so the other paths and their uniform flags compile away.
+template <bool ONE = false>
 __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t p,
                                            uint32_t sl[3], uint32_t& d) {
-    if (fp.one_draw) {
+    if (ONE || fp.one_draw) {
         const Rsrc ir = make_rsrc(b.indices + fp.draw0.first_index, 12ull * fp.nprims);
         const auto q = __builtin_amdgcn_raw_buffer_load_b96(ir, p * 12u, 0, 0);
         sl[0] = q[0] - fp.draw0.min_index; sl[1] = q[1] - fp.draw0.min_index; sl[2] = q[2] - fp.draw0.min_index;
@@ -1012,11 +1015,12 @@ __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDe
 }
 
 // A bin-queue entry -> its triangle.
+template <bool ONE = false>
 __device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
     if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
     const FetchBufs fb = fetch_bufs(fp, b);
     uint32_t sl[3], d;
-    prim_slots(fp, b, e, sl, d);
+    prim_slots<ONE>(fp, b, e, sl, d);
     return rec_from_snaps(e, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
 }
 
@@ -1464,7 +1468,7 @@ __device__ __forceinline__ ShadeRec load_shade(const FetchBufs& fb, uint32_t d) 
 
 // The varyings at weights (w0, w1, w2), the draw d's texture sample and tint: Frag fields 0..18 through
 // `put`.
-template <bool EXACT, typename Put>
+template <bool EXACT, bool ONE, typename Put>
 __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, const Taps& t, uint32_t d,
                                             float w0, float w1, float w2, const float* lut, Put&& put) {
     auto ip = [&](float x0, float x1, float x2) {
@@ -1478,7 +1482,7 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
     put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
     const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
     put(9, u); put(10, v);
-    if (fp.shade_solid) {  // uniform: one draw with a 1x1 slot, its texel and tint are kernel arguments
+    if (ONE || fp.shade_solid) {  // uniform: one draw with a 1x1 slot, its texel and tint are kernel arguments
         for (int i = 0; i < 4; ++i) put(11 + i, fp.sc.solid[i]);
         for (int i = 0; i < 4; ++i) put(15 + i, fp.sc.tint[i]);
         return;
@@ -1499,7 +1503,7 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
 // Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
 // Writes the fragment through `put(field_index, value)` (fields in Frag order), so one body serves
 // the single-pixel Frag and the lane-pair FragP without an intermediate in scratch memory.
-template <bool EXACT, bool SHADOW, typename Put>
+template <bool EXACT, bool SHADOW, bool ONE, typename Put>
 __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
                                                   int32_t px, int32_t py, const float* lut, Put&& put) {
     const uint32_t low = (uint32_t)key;
@@ -1507,7 +1511,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     const uint32_t sub = low & 7u;  // >= 1: sub-triangle `sub` of a clipped primitive
     const FetchBufs fb = fetch_bufs(fp, b);
     uint32_t sl[3], d;
-    prim_slots(fp, b, prim, sl, d);
+    prim_slots<ONE>(fp, b, prim, sl, d);
     // Every gather that needs only the slots is issued before the first wait: the snapped vertices and
     // the varyings are one round trip after the index fetch (the snaps are loaded for a clipped primitive
     // too, unused: its sub-triangle's record names its slots).
@@ -1544,13 +1548,13 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
     }
     put(19, vis);
-    fetch_attrs<EXACT>(fp, fb, taps, d, w0, w1, w2, lut, put);
+    fetch_attrs<EXACT, ONE>(fp, fb, taps, d, w0, w1, w2, lut, put);
 }
 
-template <bool EXACT, bool SHADOW>
+template <bool EXACT, bool SHADOW, bool ONE>
 __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
                                                int32_t px, int32_t py, const float* lut, Frag& f) {
-    fetch_fragment_to<EXACT, SHADOW>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
+    fetch_fragment_to<EXACT, SHADOW, ONE>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1771,7 +1775,7 @@ __device__ __forceinline__ void cov_row(const CovEntry& c, uint32_t r, uint64_t*
 }
 
 // One bin: coverage into the LDS key tile, then shading and stores. Reached by the whole workgroup.
-template <bool EXACT, int BL, bool SHADOW>
+template <bool EXACT, int BL, bool SHADOW, bool ONE = false>
 __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDeviceBuffers& b, const int bin) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
@@ -1806,7 +1810,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     uint32_t s0 = 0, s1 = nentries;
     if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
-            const TriRec r = load_entry(fp, b, queue[0]);
+            const TriRec r = load_entry<ONE>(fp, b, queue[0]);
             const uint64_t key = (0x3F000000ull << 32) | key_low(r.prim_sub);
             for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = key;
         }
@@ -1822,7 +1826,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
         int32_t cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
         if (tid < kCovPass && i < s1) {
             const uint32_t ri = queue[i];
-            r = load_entry(fp, b, ri);
+            r = load_entry<ONE>(fp, b, ri);
             rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
             if (cx0 <= cx1 && cy0 <= cy1) {
                 bool big = false;
@@ -1890,7 +1894,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     const int sub = tid % share;
     for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) {
         const uint32_t ri = queue[i];
-        const TriRec r = load_entry(fp, b, ri);
+        const TriRec r = load_entry<ONE>(fp, b, ri);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) continue;
@@ -1908,7 +1912,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     TRI_STAMP(2);
     const uint32_t nb = min(nbig, (uint32_t)kBigN);
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        const TriRec r = load_entry(fp, b, bigq[q]);
+        const TriRec r = load_entry<ONE>(fp, b, bigq[q]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         EdgeSetup e;
@@ -1978,7 +1982,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
                 const float k0 = __uint_as_float(((uint32_t)key & 0x7FFFFFu) | 0x3F000000u);
                 for (int q = 0; q < 20; ++q) (&f.wx)[q] = k0 + 0.01f * q;
             } else {
-                fetch_fragment<EXACT, SHADOW>(fp, b, key, px, py, lut, f);
+                fetch_fragment<EXACT, SHADOW, ONE>(fp, b, key, px, py, lut, f);
             }
             const float4 c = EXACT ? fs_exact(fp, f) : fs_fast(fp.sc, f);
             out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
@@ -2025,9 +2029,9 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
 // (raster_plain.hip), compiled without SLP vectorisation: packed-FP32 pairs need their uniform operands
 // copied into VGPR pairs, and without them the fast build fits 7 waves/SIMD with no spill (C3 k_raster
 // 117 -> 112 us). Frames with the pre-pass keep k_raster<.., true> (5 waves, SLP: faster there).
-template <bool EXACT, int BL>
+template <bool EXACT, int BL, bool ONE>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES_PLAIN : 3))) void k_raster_plain(TriFrameParams fp, TriDeviceBuffers b) {
-    raster_bin<EXACT, BL, false>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
+    raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2209,16 +2213,20 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__
 #ifdef TRI_RASTER_PLAIN_TU
 hipError_t tri_launch_raster_plain(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream) {
     const dim3 g(fp.nbins), t(TRI_BLOCK);
-    const bool ex = fp.exact_shading != 0;
-    if (fp.bin_log2 == 5) {
-        if (ex) hipLaunchKernelGGL((k_raster_plain<true, 5>), g, t, 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_raster_plain<false, 5>), g, t, 0, stream, fp, b);
-    } else if (fp.bin_log2 == 4) {
-        if (ex) hipLaunchKernelGGL((k_raster_plain<true, 4>), g, t, 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_raster_plain<false, 4>), g, t, 0, stream, fp, b);
+    // ONE: a single draw over a 1x1 texture slot (the common untextured mesh), the specialised instantiation
+    const bool one = fp.one_draw && fp.shade_solid;
+    auto go = [&](auto kernel) { hipLaunchKernelGGL(kernel, g, t, 0, stream, fp, b); };
+    const int bl = fp.bin_log2 == 5 ? 5 : fp.bin_log2 == 4 ? 4 : 6;
+    const int sel = (fp.exact_shading ? 1 : 0) | (one ? 2 : 0);
+    if (bl == 5) {
+        if (sel == 0) go(k_raster_plain<false, 5, false>); else if (sel == 1) go(k_raster_plain<true, 5, false>);
+        else if (sel == 2) go(k_raster_plain<false, 5, true>); else go(k_raster_plain<true, 5, true>);
+    } else if (bl == 4) {
+        if (sel == 0) go(k_raster_plain<false, 4, false>); else if (sel == 1) go(k_raster_plain<true, 4, false>);
+        else if (sel == 2) go(k_raster_plain<false, 4, true>); else go(k_raster_plain<true, 4, true>);
     } else {
-        if (ex) hipLaunchKernelGGL((k_raster_plain<true, 6>), g, t, 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_raster_plain<false, 6>), g, t, 0, stream, fp, b);
+        if (sel == 0) go(k_raster_plain<false, 6, false>); else if (sel == 1) go(k_raster_plain<true, 6, false>);
+        else if (sel == 2) go(k_raster_plain<false, 6, true>); else go(k_raster_plain<true, 6, true>);
     }
     return hipGetLastError();
 }
