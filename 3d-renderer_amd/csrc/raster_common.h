@@ -172,6 +172,9 @@ struct TriShadeConst {
     // single-draw frames whose texture slot is 1x1 (TriFrameParams::shade_solid): the draw's decoded texel
     // and tint, so no fragment gathers its shade record
     float solid[4], tint[4];
+    // and the fast build's uniform albedo factor of such a draw: ((solid * base) * tint).rgb and the
+    // fragment alpha (base.a * tint.a) * solid.a, in Default.frag's order of operations
+    float sbt[4];
 };
 
 struct TriFrameParams {

@@ -1300,12 +1300,15 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
     c.z = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(px.omF0.z, p5, px.F0.z), sp - px.diffK.z, px.diffK.z), rad.z * w, c.z);
 }
 
+// ONE: the texel, base colour and tint are uniform and their product is a kernel argument (sc.sbt)
+template <bool ONE = false>
 __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f) {
 #pragma clang fp contract(fast)
     PbrPix px;
     px.N = fnorm(fnrm(f));
     px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), fworld(f)));
-    const f3 albedo = mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])), ftint(f)), fvcol(f));
+    const f3 albedo = ONE ? mul(mk(sc.sbt[0], sc.sbt[1], sc.sbt[2]), fvcol(f))
+                          : mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])), ftint(f)), fvcol(f));
     const float m = sc.metallic;
     const float om = 0.04f * (1.0f - m);
     px.F0 = mk(__builtin_fmaf(albedo.x, m, om), __builtin_fmaf(albedo.y, m, om), __builtin_fmaf(albedo.z, m, om));
@@ -1336,7 +1339,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     }
     const float g = 1.0f / 2.2f;
     const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
-    return make_float4(fpow(t.x, g), fpow(t.y, g), fpow(t.z, g), (sc.base[3] * f.tw) * f.sw);
+    return make_float4(fpow(t.x, g), fpow(t.y, g), fpow(t.z, g), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);
 }
 
 __device__ __forceinline__ float interp_exact(float w0, float w1, float w2, float x0, float x1, float x2) {
@@ -1356,7 +1359,9 @@ struct FastW {
 __device__ __forceinline__ FastW fast_coefs(const TriRec& r) {
     const int32_t x1 = r.X[1] - r.X[0], y1 = r.Y[1] - r.Y[0], x2 = r.X[2] - r.X[0], y2 = r.Y[2] - r.Y[0];
     const float fx1 = (float)x1, fy1 = (float)y1, fx2 = (float)x2, fy2 = (float)y2;
-    const float iS = frcp((float)((int64_t)x1 * y2 - (int64_t)y1 * x2));  // the exact area, rounded once
+    // the exact area, rounded once: |x|, |y| < 2^23, so both products and their difference are exact in
+    // double (one v_fma_f64 instead of a 64-bit integer product and its int64 -> float conversion)
+    const float iS = frcp((float)__builtin_fma((double)x1, (double)y2, -((double)y1 * (double)x2)));
     const float i0 = frcp(r.iw[0]);
     const float s1 = (r.iw[1] * i0) * iS, s2 = (r.iw[2] * i0) * iS;
     return FastW{(float)(y1 - y2) * iS, (float)(x2 - x1) * iS, fy2 * s1, -fx2 * s1, -fy1 * s2, fx1 * s2};
@@ -1517,12 +1522,15 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     // too, unused: its sub-triangle's record names its slots).
     const TriSnap a0 = ld_snap_xyw(fb, sl[0]), a1 = ld_snap_xyw(fb, sl[1]), a2 = ld_snap_xyw(fb, sl[2]);
     uint32_t v0 = sl[0], v1 = sl[2], v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
+    // the varyings are gathered before the (rare) clipped branch: its record loads are waited for inside
+    // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
+    Taps taps = load_taps(fb, v0, v1, v2);
     TriRec rc;
-    if (sub) {
+    if (sub) {  // a clipped primitive's sub-triangle: its own slots, its varyings gathered again
         rc = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
         v0 = rc.v[0]; v1 = rc.v[1]; v2 = rc.v[2];
+        taps = load_taps(fb, v0, v1, v2);
     }
-    Taps taps = load_taps(fb, v0, v1, v2);
     uint4 L0, L1, L2;
     if constexpr (SHADOW) {
         const Rsrc lr = make_rsrc(b.lpos, 16ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
@@ -1984,7 +1992,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             } else {
                 fetch_fragment<EXACT, SHADOW, ONE>(fp, b, key, px, py, lut, f);
             }
-            const float4 c = EXACT ? fs_exact(fp, f) : fs_fast(fp.sc, f);
+            const float4 c = EXACT ? fs_exact(fp, f) : fs_fast<ONE>(fp.sc, f);
             out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
         }
         const size_t o = (size_t)(py - fp.y0) * fp.W + px;

@@ -1124,6 +1124,8 @@ int tri_render(tri_ctx* c) {
     if (fp.shade_solid) {  // (after shade_constants, which clears fp.sc)
         std::memcpy(fp.sc.solid, c->shade0.tex.solid, 16);
         std::memcpy(fp.sc.tint, c->shade0.tint, 16);
+        for (int i = 0; i < 3; ++i) fp.sc.sbt[i] = (fp.sc.solid[i] * fp.sc.base[i]) * fp.sc.tint[i];
+        fp.sc.sbt[3] = (fp.sc.base[3] * fp.sc.tint[3]) * fp.sc.solid[3];
     }
 
     TriDeviceBuffers b;
