@@ -13,15 +13,18 @@ from collections import defaultdict
 
 
 def short(name):
-    """Kernel name without namespace / parameter list: k_raster<false, 5, *> -> k_raster (the fast
-    build, the one the bench runs), k_raster<true, 5, *> -> k_raster_exact; k_setup<true, *> (the
+    """Kernel name without namespace / parameter list: k_raster<false, 5, *> and k_raster_plain<false, ..>
+    -> k_raster (the fast build, the one the bench runs), k_raster<true, 5, *> -> k_raster_exact; k_setup<true, *> (the
     shadow pre-pass set-up) -> k_setup_shadow, k_setup<false, *> -> k_setup."""
     m = re.search(r"(k_[a-z_]+)(<([a-z]+)[^>]*>)?\(", name)
     if m:
         first = m.group(3) == "true"
         if m.group(1) == "k_setup":
             return "k_setup_shadow" if first else "k_setup"
-        return m.group(1) + ("_exact" if first else "")
+        # k_raster_plain (frames without the shadow pre-pass) and k_raster<.., true> (with it) are the
+        # frame's raster kernel either way
+        base = "k_raster" if m.group(1) == "k_raster_plain" else m.group(1)
+        return base + ("_exact" if first else "")
     for k in ("copyBuffer", "fillBuffer"):
         if k in name:
             return k
