@@ -781,7 +781,9 @@ __device__ __forceinline__ void bin_pair_box(const TriDeviceBuffers& b, BinBox& 
 // for the map (oracle shadow_raster_triangle: light-NDC snaps, no culling, no clipping, guard-band
 // violators dropped) and bins it into the map's own queues; clipped polygon vertices get light-space
 // positions. A separate instantiation keeps that code, and its registers, out of other frames.
-template <bool WITH_SHADOW>
+// ONE: a single-draw frame (fp.one_draw known set: the draw search, LDS staging and prim_vs records compile
+// away)
+template <bool WITH_SHADOW, bool ONE>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
@@ -789,7 +791,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     // staged in LDS once per workgroup, so a primitive finds its draw and index row without the global
     // binary search -> draw record chain in front of its index fetch.
     __shared__ uint32_t dpb[kLdsDraws + 1], dfi[kLdsDraws], dvb[kLdsDraws], dcb[kLdsDraws];
-    const bool lds_draws = !fp.one_draw && fp.ndraws <= (uint32_t)kLdsDraws;
+    const bool lds_draws = !ONE && !fp.one_draw && fp.ndraws <= (uint32_t)kLdsDraws;
     __shared__ BinBox bin_box;
     for (uint32_t s = threadIdx.x; s < kBinGrid; s += TRI_BLOCK) bin_box.cnt[s] = 0;
     if (threadIdx.x < 16) bin_box.box[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3] = ~0u;
@@ -835,7 +837,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 // the indices are fetched together with the cluster flag, not after it: a band's
                 // visible primitives skip one dependent load (a culled one wastes 12 bytes)
                 const uint32_t* ip;
-                if (fp.one_draw) {  // kernel-argument constants: the index fetch starts at once
+                if (ONE || fp.one_draw) {  // kernel-argument constants: the index fetch starts at once
                     ip = b.indices + fp.draw0.first_index + 3u * p[t];
                     vb = 0u - fp.draw0.min_index;
                     i0 = ip[0]; i1 = ip[1]; i2 = ip[2];
@@ -888,7 +890,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 }
                 // k_raster's (and k_shadow_raster's) route from the primitive to its vertex slots and draw; a
                 // single-draw frame finds the slots in the index buffer instead (prim_slots)
-                if (!fp.one_draw && (ok[t] || needs_clip[t] || sok[t]))
+                if (!ONE && !fp.one_draw && (ok[t] || needs_clip[t] || sok[t]))
                     b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | (needs_clip[t] ? TRI_PRIM_CLIPPED : 0u));
             }
             nsetup += ok[t] ? 1u : 0u;
@@ -907,7 +909,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl0[t], src),
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl1[t], src),
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src),
-                                                fp.one_draw ? fp.draw0.clip_from_world != 0u
+                                                (ONE || fp.one_draw) ? fp.draw0.clip_from_world != 0u
                                                             : b.draws[__builtin_amdgcn_readlane(pd[t], src)].clip_from_world != 0u,
                                                 nsetup, nentries);
                 }
@@ -2320,8 +2322,14 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
     rec(kStageSetup);
     if (fp.nchunks > 0) {  // with the pre-pass, one set-up pass bins each primitive for the frame and the map
-        if (fp.shadow_on) hipLaunchKernelGGL((k_setup<true>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
-        else hipLaunchKernelGGL((k_setup<false>), dim3(fp.nchunks), dim3(TRI_BLOCK), 0, stream, fp, b);
+        const dim3 g(fp.nchunks), t(TRI_BLOCK);
+        if (fp.shadow_on) {
+            if (fp.one_draw) hipLaunchKernelGGL((k_setup<true, true>), g, t, 0, stream, fp, b);
+            else hipLaunchKernelGGL((k_setup<true, false>), g, t, 0, stream, fp, b);
+        } else {
+            if (fp.one_draw) hipLaunchKernelGGL((k_setup<false, true>), g, t, 0, stream, fp, b);
+            else hipLaunchKernelGGL((k_setup<false, false>), g, t, 0, stream, fp, b);
+        }
     }
     if (fp.shadow_on) {  // the map's depth raster, before the frame's raster samples it
         rec(kStageShadow);
