@@ -121,6 +121,26 @@ __device__ __forceinline__ float4 mat_vec_seq(const float* m, float4 v) {
     return r;
 }
 
+// IEEE a / b for several numerators over one denominator. This is the compiler's own f32 division
+// sequence (v_rcp, one Newton step on the reciprocal, two FMA corrections of the quotient: LLVM's
+// LowerFDIV32) without its v_div_scale / v_div_fixup range handling, which changes nothing for finite
+// normal operands whose exponents are far from the format's limits -- exact integers below 2^48, their
+// ratios, depth differences and perspective weights. The refined reciprocal is computed once per
+// denominator, so each further quotient costs a multiply and four FMAs instead of a full division, with
+// the same bits.
+struct RcpRef {
+    float b, y;
+};
+__device__ __forceinline__ RcpRef rcp_ref(float b) {
+    const float y0 = __builtin_amdgcn_rcpf(b);
+    return RcpRef{b, __builtin_fmaf(__builtin_fmaf(-b, y0, 1.0f), y0, y0)};
+}
+__device__ __forceinline__ float div_rn(float a, const RcpRef& r) {
+    const float q0 = a * r.y;
+    const float q1 = __builtin_fmaf(__builtin_fmaf(-r.b, q0, a), r.y, q0);
+    return __builtin_fmaf(__builtin_fmaf(-r.b, q1, a), r.y, q1);
+}
+
 // ------------------------------------------------------------------------------------------
 // vs_transform
 // ------------------------------------------------------------------------------------------
@@ -960,8 +980,9 @@ __device__ __forceinline__ void edge_setup(const TriRec& r, EdgeSetup& e) {
     const float fX2 = (float)(r.X[2] - r.X[0]), fY2 = (float)(r.Y[2] - r.Y[0]);
     const float fS = (float)S;
     const float dz1 = r.z[1] - r.z[0], dz2 = r.z[2] - r.z[0];
-    e.dzdX = (dz1 * fY2 - dz2 * fY1) / fS;
-    e.dzdY = (dz2 * fX1 - dz1 * fX2) / fS;
+    const RcpRef rS = rcp_ref(fS);
+    e.dzdX = div_rn(dz1 * fY2 - dz2 * fY1, rS);
+    e.dzdY = div_rn(dz2 * fX1 - dz1 * fX2, rS);
 }
 
 __device__ __forceinline__ int32_t clamp_edge(int64_t f, bool& reject) {
@@ -1086,8 +1107,9 @@ __device__ __forceinline__ bool edge_start(const TriRec& r, int32_t cx0, int32_t
         const float fS = (float)(__mul24(X1, Y2) - __mul24(Y1, X2));
         const float fX1 = (float)X1, fY1 = (float)Y1, fX2 = (float)X2, fY2 = (float)Y2;
         const float dz1 = r.z[1] - r.z[0], dz2 = r.z[2] - r.z[0];
-        dzdX = (dz1 * fY2 - dz2 * fY1) / fS;
-        dzdY = (dz2 * fX1 - dz1 * fX2) / fS;
+        const RcpRef rS = rcp_ref(fS);
+        dzdX = div_rn(dz1 * fY2 - dz2 * fY1, rS);
+        dzdY = div_rn(dz2 * fX1 - dz1 * fX2, rS);
         return true;
     }
     EdgeSetup e;
@@ -1452,10 +1474,12 @@ __device__ __forceinline__ void exact_weights(const TriRec& r, int32_t px, int32
         fS = (float)((int64_t)(r.X[1] - r.X[0]) * (int64_t)(r.Y[2] - r.Y[0]) -
                      (int64_t)(r.Y[1] - r.Y[0]) * (int64_t)(r.X[2] - r.X[0]));
     }
-    const float l0 = fe[1] / fS, l1 = fe[2] / fS, l2 = fe[0] / fS;
+    const RcpRef rS = rcp_ref(fS);
+    const float l0 = div_rn(fe[1], rS), l1 = div_rn(fe[2], rS), l2 = div_rn(fe[0], rS);
     const float q0 = l0 * r.iw[0], q1 = l1 * r.iw[1], q2 = l2 * r.iw[2];
     const float qs = (q0 + q1) + q2;
-    w0 = q0 / qs; w1 = q1 / qs; w2 = q2 / qs;
+    const RcpRef rq = rcp_ref(qs);
+    w0 = div_rn(q0, rq); w1 = div_rn(q1, rq); w2 = div_rn(q2, rq);
 }
 
 // Shadow lookup (oracle shadow_visibility): the fraction of the 2x2 bilinear depth compare
