@@ -813,6 +813,21 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     __shared__ uint32_t dpb[kLdsDraws + 1], dfi[kLdsDraws], dvb[kLdsDraws], dcb[kLdsDraws];
     const bool lds_draws = !ONE && !fp.one_draw && fp.ndraws <= (uint32_t)kLdsDraws;
     __shared__ BinBox bin_box;
+    if constexpr (ONE && !WITH_SHADOW) {
+        // A row band's chunk whose clusters k_vertex culled (most chunks at N = 8): the whole workgroup
+        // leaves before the LDS set-up and the binning barriers (its cluster flags: a few scalar loads)
+        if (fp.cull_on) {
+            const uint32_t ck = (uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks);
+            const uint32_t p0 = ck * (uint32_t)(TRI_BLOCK * fp.ppt);
+            const uint32_t p1 = min(p0 + (uint32_t)(TRI_BLOCK * fp.ppt), fp.nprims);
+            bool any = false;
+            for (uint32_t c = p0 / TRI_CLUSTER_PRIMS; c <= (p1 - 1) / TRI_CLUSTER_PRIMS && !any; ++c) any = b.cvis[c] != 0u;
+            if (!any) {
+                if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(0u, 0u);
+                return;
+            }
+        }
+    }
     for (uint32_t s = threadIdx.x; s < kBinGrid; s += TRI_BLOCK) bin_box.cnt[s] = 0;
     if (threadIdx.x < 16) bin_box.box[threadIdx.x >> 3][(threadIdx.x >> 2) & 1][threadIdx.x & 3] = ~0u;
     TRI_SSTAMP(0);
