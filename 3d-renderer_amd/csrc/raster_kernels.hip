@@ -1383,9 +1383,102 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
 }
 
 // ONE: the texel, base colour and tint are uniform and their product is a kernel argument (sc.sbt)
+// Packed colour pairs: kept for the shadow instantiation (C5 k_raster 197.4 -> 195.8 us); k_raster_plain is
+// faster with scalar channels (C3 103.9 vs 105.7 us).
+#ifndef TRI_PK_SHADE
+#ifdef TRI_RASTER_PLAIN_TU
+#define TRI_PK_SHADE 0
+#else
+#define TRI_PK_SHADE 1
+#endif
+#endif
+#if TRI_PK_SHADE
+// Colour channels x, y as one packed-FP32 pair (v_pk_fma_f32 / v_pk_mul_f32: two IEEE operations per
+// instruction, the same bits as the scalar form) and z on its own; written out by hand, not left to the SLP
+// vectoriser, so that only these values occupy register pairs (raster_plain.hip is built without SLP).
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pk_fma(f2v a, f2v b, f2v c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ f2v splat(float x) { return f2v{x, x}; }
+struct PbrPixP {
+    f3 N, V;
+    f2v F0xy, omF0xy, diffKxy;
+    float F0z, omF0z, diffKz;
+    float NdotVr, NdotV4, gVa;
+};
+__device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const PbrPixP& px, float NdotLr, float LdotV,
+                                                f2v radxy, float radz, float scale, f2v& cxy, float& cz) {
+#pragma clang fp contract(fast)
+    if (!(NdotLr > 0.0f)) return;  // (see eval_pbr_fast)
+    const float ih = frsq(fmaxf(__builtin_fmaf(2.0f, LdotV, 2.0f), 1e-30f));
+    const float NdotH = fmaxf((px.NdotVr + NdotLr) * ih, 0.0f);
+    const float NdotL = NdotLr;
+    const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
+    const float gden = fmaxf(__builtin_fmaf(NdotL, sc.omkg, sc.kg), 1e-4f);
+    const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
+    const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
+    const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
+    const float q2 = q * q;
+    const float p5 = q2 * q2 * q;
+    const float w = NdotL * scale;
+    cxy = pk_fma(pk_fma(pk_fma(px.omF0xy, splat(p5), px.F0xy), splat(sp) - px.diffKxy, px.diffKxy), radxy * splat(w), cxy);
+    cz = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(px.omF0z, p5, px.F0z), sp - px.diffKz, px.diffKz), radz * w, cz);
+}
+#endif
+
 template <bool ONE = false>
 __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f) {
 #pragma clang fp contract(fast)
+#if TRI_PK_SHADE
+    PbrPixP px;
+    px.N = fnorm(fnrm(f));
+    px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), fworld(f)));
+    f2v albxy;
+    float albz;
+    if (ONE) {
+        albxy = f2v{sc.sbt[0], sc.sbt[1]} * f2v{f.cx, f.cy};
+        albz = sc.sbt[2] * f.cz;
+    } else {
+        albxy = ((f2v{f.sx, f.sy} * f2v{sc.base[0], sc.base[1]}) * f2v{f.tx, f.ty}) * f2v{f.cx, f.cy};
+        albz = ((f.sz * sc.base[2]) * f.tz) * f.cz;
+    }
+    const float m = sc.metallic;
+    const float om = 0.04f * (1.0f - m);
+    px.F0xy = pk_fma(albxy, splat(m), splat(om));
+    px.F0z = __builtin_fmaf(albz, m, om);
+    px.omF0xy = splat(1.0f) - px.F0xy;
+    px.omF0z = 1.0f - px.F0z;
+    const float kd = (1.0f - m) * (1.0f / kPi);
+    px.diffKxy = albxy * splat(kd);
+    px.diffKz = albz * kd;
+    px.NdotVr = fdot(px.N, px.V);
+    const float NdotV = fmaxf(px.NdotVr, 0.0f);
+    px.NdotV4 = 4.0f * NdotV;
+    px.gVa = sc.a2pi * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
+    f2v cxy = (f2v{sc.amb[0], sc.amb[1]} * albxy) * splat(sc.amb_strength);
+    float cz = (sc.amb[2] * albz) * sc.amb_strength;
+    if (kAblate & 64) return make_float4(cxy.x, cxy.y, cz, 1.0f);  // diagnostics: 64 = no lights
+    if (sc.has_sun && f.vis > 0.0f) {  // vis = 0 (fully shadowed): the sun adds exactly nothing
+        const f3 L = mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]);
+        eval_pbr_fast_p(sc, px, fdot(px.N, L), fdot(L, px.V), f2v{sc.sun_rad[0], sc.sun_rad[1]}, sc.sun_rad[2], f.vis,
+                        cxy, cz);
+    }
+    const f3 wp = fworld(f);
+    for (uint32_t i = 0; i < sc.npt; ++i) {
+        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
+        const float d2 = fdot(to, to);
+        if (d2 <= 1e-8f) continue;  // dist <= 1e-4
+        const float inv = frsq(d2);
+        const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
+        if (!(att0 > 0.0f)) continue;  // beyond the light's range: (1 - d/r)^2 = 0 adds exactly nothing
+        eval_pbr_fast_p(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv, f2v{sc.pl_rad[i][0], sc.pl_rad[i][1]},
+                        sc.pl_rad[i][2], att0 * att0, cxy, cz);
+    }
+    const float g = 1.0f / 2.2f;
+    const f2v c1 = cxy + splat(1.0f);
+    const f2v txy = cxy * f2v{frcp(c1.x), frcp(c1.y)};
+    const float tz = cz * frcp(cz + 1.0f);
+    return make_float4(fpow(txy.x, g), fpow(txy.y, g), fpow(tz, g), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);
+#else
     PbrPix px;
     px.N = fnorm(fnrm(f));
     px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), fworld(f)));
@@ -1422,6 +1515,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     const float g = 1.0f / 2.2f;
     const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
     return make_float4(fpow(t.x, g), fpow(t.y, g), fpow(t.z, g), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);
+#endif
 }
 
 __device__ __forceinline__ float interp_exact(float w0, float w1, float w2, float x0, float x1, float x2) {
