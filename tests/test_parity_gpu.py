@@ -161,6 +161,34 @@ def test_repeat_render_is_deterministic():
         assert np.array_equal(c, outs[0][0]) and np.array_equal(d, outs[0][1])
 
 
+def test_texture_upload_switches_specialised_raster(oracle, flags):
+    """One context, one draw: while its texture slot is empty (it aliases the 1x1 white default) the frame
+    takes the single-draw solid instantiation (texel and tint as kernel arguments); uploading the texture
+    must switch it to the sampling path on the next frame, and clearing the tint back to the default
+    slot must switch it back (the shade record a frame uses is refreshed with the slot)."""
+    import copy
+
+    from trident_raster import raster, scenes
+
+    textured = sc.textured_grid()
+    solid = copy.copy(textured)
+    solid.textures = []  # slot 3 empty: the draw samples the default white 1x1 slot
+    with raster.TriRaster(textured.width, textured.height, flags=flags) as r:
+        scenes.load_scene(r, solid)
+        frames = []
+        for scene, upload in ((solid, None), (textured, textured.textures[0]), (solid, None)):
+            if upload is not None:
+                r.upload_texture(*upload)
+            elif scene is solid and frames:  # back to the 1x1 default: a 1x1 white texel in slot 3
+                r.upload_texture(3, np.full((1, 1, 4), 255, np.uint8))
+            r.render_frame()
+            frames.append((scene, *r.readback()))
+    for scene, col, dep in frames:
+        oc, od, _ = oracle.render(scene)
+        assert np.array_equal(dep, od), scene.name
+        assert int(np.abs(col.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL, scene.name
+
+
 def test_bin_overflow_grows_and_recovers():
     """A frame that overflows the bin list reports TRI_E_OVERFLOW, grows, and re-renders correctly."""
     from trident_raster import abi, raster, scenes
