@@ -1466,10 +1466,9 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     for (uint32_t i = 0; i < sc.npt; ++i) {
         const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
         const float d2 = fdot(to, to);
-        if (d2 <= 1e-8f) continue;  // dist <= 1e-4
         const float inv = frsq(d2);
         const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
-        if (!(att0 > 0.0f)) continue;  // beyond the light's range: (1 - d/r)^2 = 0 adds exactly nothing
+        if (!(d2 > 1e-8f && att0 > 0.0f)) continue;  // dist <= 1e-4, or beyond the range (see below)
         eval_pbr_fast_p(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv, f2v{sc.pl_rad[i][0], sc.pl_rad[i][1]},
                         sc.pl_rad[i][2], att0 * att0, cxy, cz);
     }
@@ -1504,10 +1503,11 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     for (uint32_t i = 0; i < sc.npt; ++i) {
         const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
         const float d2 = fdot(to, to);
-        if (d2 <= 1e-8f) continue;  // dist <= 1e-4
         const float inv = frsq(d2);
         const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
-        if (!(att0 > 0.0f)) continue;  // beyond the light's range: (1 - d/r)^2 = 0 adds exactly nothing
+        // dist <= 1e-4 (Default.frag skips it; d2 = 0 gives att0 = 0 here too), or beyond the light's
+        // range: (1 - d/r)^2 = 0 adds exactly nothing. One exact skip instead of two.
+        if (!(d2 > 1e-8f && att0 > 0.0f)) continue;
         // L = to / |to| is never formed: N.L and L.V are the dot products with `to`, scaled once
         eval_pbr_fast(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv,
                       mk(sc.pl_rad[i][0], sc.pl_rad[i][1], sc.pl_rad[i][2]), att0 * att0, c);
