@@ -1929,6 +1929,9 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 #endif
 static_assert((TRI_COV_SHARE & (TRI_COV_SHARE - 1)) == 0 && TRI_BLOCK % TRI_COV_SHARE == 0,
               "TRI_COV_SHARE must be a power of two dividing the workgroup (each lane group owns one entry)");
+#ifndef TRI_COV_PRIO
+#define TRI_COV_PRIO 0
+#endif
 #ifndef TRI_COV_BALANCED
 #define TRI_COV_BALANCED 1
 #endif
@@ -1976,6 +1979,9 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ uint32_t nbig, nentries, nsky;
     const int tid = threadIdx.x;
     TRI_STAMP(0);
+    // 32x32 bins: the latency-bound init and coverage phases issue ahead of other workgroups' shading waves
+    // (C3 k_raster 103.9 -> 102.5 us; at 16x16 bins, C2, it was slower: 32.5 -> 33.5 us)
+    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1);
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
     const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
     const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);
@@ -2129,6 +2135,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     }
     __syncthreads();
     TRI_STAMP(3);
+    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(0);
     // shade + store: each wave covers whole BIN-pixel row pieces -> coalesced colour/depth stores.
     // Background pixels go to an LDS queue for the skybox pass below (lane-dense, and its registers
     // are not live during shading).
