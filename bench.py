@@ -231,16 +231,35 @@ class BandRenderer:
         return ts[len(ts) // 2]
 
 
-def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256):
+def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, warm_seconds=0.1):
     """Time exactly `steps` frames (no per-kernel events inside the timed region), then, outside it,
     a separate pass of `event_frames` frames with HIP events around every kernel of every frame:
     the per-kernel durations (roofline.kernel_ms) rest on that many samples, not on the few frames a
-    short timed run would leave."""
+    short timed run would leave.
+
+    Warm-up: `warmup` frames, and back-to-back frames for at least `warm_seconds` of wall time. The
+    GPU leaves its idle clock state only after several ms of continuous work: after the scene upload
+    (seconds of host work) 5 warm-up frames (0.6 ms) left the first timed frames at low clocks, and a
+    20-frame run measured 0.134-0.140 ms/frame against 0.113-0.118 for the same frames after 50 ms of
+    work (tools/step_timing.py, profiles/round3/step_timing.log). Nothing is removed from the timed
+    region; it only starts at the clock every later frame runs at. Returns (seconds, timing, frames
+    the warm-up ran)."""
     import torch
 
     br.warm()  # first frame per context sizes the internal queues (re-renders after TRI_E_OVERFLOW)
-    for _ in range(warmup):
+    t0 = time.perf_counter()
+    for _ in range(max(warmup, 1)):
         br.step()
+    br.drain()
+    torch.cuda.synchronize(br.dev)
+    el = time.perf_counter() - t0
+    # every rank runs the same number of frames (each one ends in a collective): the extra frames that
+    # fill warm_seconds at the rate just measured, the maximum over ranks
+    extra = 0 if el >= warm_seconds else min(int((warm_seconds - el) / (el / max(warmup, 1))) + 1, 100000)
+    extra = int(max_over_ranks(float(extra), br.dev, dist_on))
+    for _ in range(extra):
+        br.step()
+    n_warm = max(warmup, 1) + extra
     br.drain()
     br.synchronize()
     torch.cuda.synchronize(br.dev)
@@ -265,7 +284,7 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256):
         br.drain()
         timing = br.r.timing()
         br.r.set_timing(False)
-    return max_over_ranks(dt, br.dev, dist_on), timing
+    return max_over_ranks(dt, br.dev, dist_on), timing, n_warm
 
 
 def device_copy_gbs(device, nbytes=1 << 29, reps=10):
@@ -286,17 +305,47 @@ def device_copy_gbs(device, nbytes=1 << 29, reps=10):
     return 2.0 * nbytes * reps / dt / 1e9
 
 
+def effective_cpus(cgroup_root="/sys/fs/cgroup"):
+    """CPUs this process can use at once: min(affinity mask, cgroup v2 cpu.max quota / period,
+    rounded up), falling back to the cgroup v1 cfs files. {"effective", "affinity", "quota"}; quota is
+    None when unlimited or unreadable."""
+    import math
+
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    try:
+        with open(os.path.join(cgroup_root, "cpu.max")) as f:
+            q, period = f.read().split()[:2]
+        if q != "max" and float(period) > 0:
+            quota = math.ceil(float(q) / float(period))
+    except (OSError, ValueError):
+        try:
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_quota_us")) as f:
+                q = float(f.read())
+            with open(os.path.join(cgroup_root, "cpu", "cpu.cfs_period_us")) as f:
+                period = float(f.read())
+            if q > 0 and period > 0:
+                quota = math.ceil(q / period)
+        except (OSError, ValueError):
+            pass
+    eff = max(1, min(affinity, quota) if quota else affinity)
+    return {"effective": eff, "affinity": affinity, "quota": quota}
+
+
 def cpu_baseline(scene, seconds):
     """The CPU oracle (a multithreaded C++ port of the same pipeline) on this host's cores, over a
     bounded sample of whole frames of the same workload (lavapipe is absent on this image)."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle_py
 
-    # every host core (SURVEY §8(d): "all host cores, core count stated"); capped at 256 threads to
-    # stay far inside the GPU box's per-job task limit. A cgroup CPU quota below that (the box's CPU
-    # share) shows up as threads that do not all run at once, which is part of the measurement.
+    # every CPU this process may actually run on (SURVEY §8(d): "all host cores, core count stated"):
+    # os.cpu_count() is the whole machine's, the job's share is its affinity mask and cgroup CPU quota
     host_cpus = os.cpu_count() or 1
-    threads = min(host_cpus, 256)
+    cpus = effective_cpus()
+    threads = cpus["effective"]
     oracle_py.render(scene, threads=threads)  # warm-up frame (page-in, allocator)
     n, t0 = 0, time.perf_counter()
     while True:
@@ -305,12 +354,8 @@ def cpu_baseline(scene, seconds):
         if time.perf_counter() - t0 >= seconds:
             break
     dt = time.perf_counter() - t0
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = host_cpus
     return {"value": n / dt, "unit": "frames/s", "cores": threads, "host_cpus": host_cpus,
-            "affinity_cpus": affinity, "kind": "port",
+            "affinity_cpus": cpus["affinity"], "cgroup_quota_cpus": cpus["quota"], "kind": "port",
             "sample": f"{n} full {scene.width}x{scene.height} frame(s) of {scene.name} "
                       f"({scene.triangles} tris) rendered by oracle/tri_oracle.cpp, {dt:.1f} s"}
 
@@ -369,6 +414,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--warm-seconds", type=float, default=0.1,
+                    help="untimed back-to-back frames before the timed region (at least --warmup frames): the "
+                         "GPU's clock ramp out of idle takes a few ms")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-secondary", action="store_true")
     ap.add_argument("--sim-world", type=int, default=0,
@@ -401,7 +449,8 @@ def main():
         br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=args.inflight)
     else:
         br = BandRenderer(scene, rank, world, local, assembly=args.assembly, inflight=args.inflight)
-    dt, timing = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing)
+    dt, timing, n_warm = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing,
+                                   warm_seconds=args.warm_seconds)
     fps = args.steps / dt
     W, H = scene.width, scene.height
     stats = br.r.frame_stats()
@@ -425,7 +474,7 @@ def main():
             s2 = build_scene(key)
             br2 = BandRenderer(s2, rank, world, local, assembly=args.assembly, inflight=args.inflight)
             n2 = max(args.steps, 50) if key == "c2" else max(args.steps // 2, 20)
-            dt2, t2 = timed_run(br2, n2, args.warmup, dist_on)
+            dt2, t2, _ = timed_run(br2, n2, args.warmup, dist_on, warm_seconds=args.warm_seconds)
             fps2 = n2 / dt2
             st2 = stage_ms(t2)
             entry = {"frames_per_s": fps2, "mpix_per_s": fps2 * s2.width * s2.height / 1e6, "ms_per_frame": 1e3 / fps2,
@@ -452,6 +501,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "warmup_frames_run": n_warm,
             "ms_per_step": dt / args.steps * 1e3,
             "higher_is_better": True,
             "scaling": "strong",
