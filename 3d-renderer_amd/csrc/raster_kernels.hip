@@ -291,8 +291,10 @@ __device__ __forceinline__ bool cluster_visible(const TriFrameParams& fp, const 
     if (!front) return true;
     const float wx0 = x0 * fp.hw + fp.hw, wx1 = x1 * fp.hw + fp.hw;
     const float wy0 = y0 * fp.hh + fp.hh, wy1 = y1 * fp.hh + fp.hh;
+    // the margins (2 px, 1e-4 in depth) cover the rounding difference between the box corners' (P V) M
+    // product and the vertices' P V (M p): the test is never stricter than the vertices' own
     return !(wy1 < (float)fp.y0 - 2.0f || wy0 > (float)fp.y1 + 2.0f || wx1 < -2.0f || wx0 > (float)fp.W + 2.0f ||
-             z1 < 0.0f || z0 > 1.0f);
+             z1 < -1e-4f || z0 > 1.0f + 1e-4f);
 }
 
 // One lane per vertex slot. With cluster culling on: lanes 0 .. ncl_total-1 of the grid (the first few

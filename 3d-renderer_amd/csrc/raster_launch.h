@@ -73,3 +73,6 @@ hipStream_t tri_internal_stream(tri_ctx* ctx);
 int tri_internal_device(tri_ctx* ctx);
 // Record an error message for tri_last_error (returns `code`).
 int tri_internal_fail(int code, const char* msg);
+// The device a geometry object lives on; the UNORM8 decode table (b / 255) on a context's device.
+int tri_internal_geometry_device(const tri_geometry* geometry);
+const float* tri_internal_unorm_lut(tri_ctx* ctx);

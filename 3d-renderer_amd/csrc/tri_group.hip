@@ -7,9 +7,19 @@
 // ncclRecv moves over xGMI — each remote band crosses one link once, all links at the same time (a
 // gather, not an all-gather: (N-1)/N of a frame lands on one GPU instead of on every GPU).
 //
+// Geometry: ONE tri_geometry per distinct device, bound by every band context on it (N bands on one
+// device hold one copy, as the editor's viewports share one vertex/index buffer, Renderer.cpp:1965-2116),
+// or the caller's own per-device geometry objects (tri_group_bind_geometry).
+//
+// Frames in flight: the assembled frame and every remote band buffer are double-buffered. Frame k renders
+// into frame[k & 1]; a remote band's buffer k & 1 is reused by frame k + 2 only after frame k's assembly
+// read it (a device-side wait on that assembly's event); an in-place band of frame k + 2 waits for the
+// consumer's fence on frame k (tri_group_present), so a presenter still reading frame k is never
+// overwritten while frame k + 1 renders into the other buffer.
+//
 // Streams: each band renders on its context's stream; per distinct device the group owns an assembly
 // stream that waits (events) for that device's bands and carries the device's RCCL calls, so every
-// communicator sees one stream. A band's next frame waits for the assembly that read its buffer.
+// communicator sees one stream.
 #include "raster_launch.h"
 
 #include <hip/hip_runtime.h>
@@ -26,13 +36,20 @@ struct tri_group {
     std::vector<tri_ctx*> ctx;       // per band
     std::vector<int32_t> udev;       // distinct devices
     std::vector<int> urank;          // band -> index of its device in udev (its RCCL rank)
+    std::vector<tri_geometry*> geom; // per distinct device: the group's own geometry
     std::vector<ncclComm_t> comm;    // per distinct device (only when there are several)
     std::vector<hipStream_t> astream;  // per distinct device: assembly stream
-    std::vector<hipEvent_t> band_done;   // per band: its render finished
-    std::vector<hipEvent_t> asm_done;    // per distinct device: its part of the assembly finished
-    std::vector<uint32_t*> band_buf;     // per band on a non-display device: its colour band
-    uint32_t* frame = nullptr;           // W*H on the display device
-    bool assembled_once = false;
+    std::vector<hipEvent_t> band_done;   // per band: its render of the current frame finished
+    std::vector<hipEvent_t> asm_done[2]; // per buffer parity, per distinct device: that frame's assembly finished
+    std::vector<uint32_t*> band_buf[2];  // per buffer parity, per band on a non-display device: its colour band
+    uint32_t* frame[2] = {nullptr, nullptr};  // W*H on the display device
+    hipEvent_t present_done[2] = {nullptr, nullptr};  // consumer fence per buffer (tri_group_present)
+    bool present_armed[2] = {false, false};
+    bool asm_recorded[2] = {false, false};  // asm_done[p] holds a recorded assembly
+    uint64_t frames = 0;                    // frames enqueued
+    uint32_t* present = nullptr;            // tri_group_blit_linear's owned target (display device)
+    size_t cap_present = 0;
+    uint32_t present_w = 0, present_h = 0;
 };
 
 namespace {
@@ -68,6 +85,9 @@ int each(tri_group* g, F&& f) {
     return TRI_OK;
 }
 
+// Buffer parity of the most recent frame (the one tri_group_frame / readback / present refer to).
+uint32_t last_parity(const tri_group* g) { return g->frames ? (uint32_t)((g->frames - 1) & 1u) : 0u; }
+
 }  // namespace
 
 extern "C" {
@@ -78,14 +98,16 @@ int tri_group_destroy(tri_group* g) {
         (void)hipSetDevice(g->udev[u]);
         if (g->astream[u]) (void)hipStreamSynchronize(g->astream[u]);
     }
-    for (tri_ctx* c : g->ctx) tri_destroy(c);
+    for (tri_ctx* c : g->ctx) tri_destroy(c);  // before the geometry they bind
+    for (tri_geometry* geo : g->geom) tri_geometry_destroy(geo);
     for (ncclComm_t c : g->comm)
         if (c) (void)ncclCommDestroy(c);
-    for (uint32_t r = 0; r < g->band_buf.size(); ++r)
-        if (g->band_buf[r]) {
-            (void)hipSetDevice(g->dev[r]);
-            (void)hipFree(g->band_buf[r]);
-        }
+    for (int p = 0; p < 2; ++p)
+        for (uint32_t r = 0; r < g->band_buf[p].size(); ++r)
+            if (g->band_buf[p][r]) {
+                (void)hipSetDevice(g->dev[r]);
+                (void)hipFree(g->band_buf[p][r]);
+            }
     for (uint32_t r = 0; r < g->band_done.size(); ++r)
         if (g->band_done[r]) {
             (void)hipSetDevice(g->dev[r]);
@@ -93,12 +115,17 @@ int tri_group_destroy(tri_group* g) {
         }
     for (size_t u = 0; u < g->udev.size(); ++u) {
         (void)hipSetDevice(g->udev[u]);
-        if (u < g->asm_done.size() && g->asm_done[u]) (void)hipEventDestroy(g->asm_done[u]);
+        for (int p = 0; p < 2; ++p)
+            if (u < g->asm_done[p].size() && g->asm_done[p][u]) (void)hipEventDestroy(g->asm_done[p][u]);
         if (u < g->astream.size() && g->astream[u]) (void)hipStreamDestroy(g->astream[u]);
     }
-    if (g->frame) {
+    if (!g->dev.empty()) {
         (void)hipSetDevice(g->dev[g->display]);
-        (void)hipFree(g->frame);
+        for (int p = 0; p < 2; ++p) {
+            if (g->frame[p]) (void)hipFree(g->frame[p]);
+            if (g->present_done[p]) (void)hipEventDestroy(g->present_done[p]);
+        }
+        if (g->present) (void)hipFree(g->present);
     }
     delete g;
     return TRI_OK;
@@ -128,40 +155,47 @@ int tri_group_create(const tri_group_config* cfg, tri_group** out) {
     }
     for (uint32_t r = 0; r < g->n; ++r)
         g->urank.push_back((int)(std::find(g->udev.begin(), g->udev.end(), g->dev[r]) - g->udev.begin()));
+    g->geom.assign(g->udev.size(), nullptr);
+    for (size_t u = 0; u < g->udev.size(); ++u) {
+        const int rc = tri_geometry_create(g->udev[u], &g->geom[u]);
+        if (rc) return bail(rc);
+    }
     const int32_t ddev = g->dev[g->display];
     for (uint32_t r = 0; r < g->n; ++r) {
         tri_config c{g->W, g->H, g->y0[r], g->y1[r], g->dev[r], cfg->flags};
         tri_ctx* ctx = nullptr;
-        const int rc = tri_create(&c, &ctx);
+        int rc = tri_create(&c, &ctx);
         if (rc) return bail(rc);
         g->ctx.push_back(ctx);
+        if ((rc = tri_bind_geometry(ctx, g->geom[g->urank[r]]))) return bail(rc);
     }
-    if (hipSetDevice(ddev) != hipSuccess || hipMalloc(&g->frame, (size_t)g->W * g->H * 4) != hipSuccess)
-        return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: frame allocation failed"));
-    g->band_buf.assign(g->n, nullptr);
+    if (hipSetDevice(ddev) != hipSuccess)
+        return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: hipSetDevice failed"));
+    for (int p = 0; p < 2; ++p) {
+        if (hipMalloc(&g->frame[p], (size_t)g->W * g->H * 4) != hipSuccess)
+            return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: frame allocation failed"));
+        if (hipEventCreateWithFlags(&g->present_done[p], hipEventDisableTiming) != hipSuccess)
+            return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: event creation failed"));
+        g->band_buf[p].assign(g->n, nullptr);
+    }
     g->band_done.assign(g->n, nullptr);
     for (uint32_t r = 0; r < g->n; ++r) {
-        uint32_t* out_ptr;
-        if (g->dev[r] == ddev) {
-            out_ptr = g->frame + (size_t)g->y0[r] * g->W;  // renders in place
-        } else {
-            if (hipSetDevice(g->dev[r]) != hipSuccess ||
-                hipMalloc(&g->band_buf[r], (size_t)(g->y1[r] - g->y0[r]) * g->W * 4) != hipSuccess)
-                return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: band buffer allocation failed"));
-            out_ptr = g->band_buf[r];
-        }
-        int rc = tri_bind_output(g->ctx[r], out_ptr, nullptr);  // depth stays in the band context
-        if (rc) return bail(rc);
-        if (hipSetDevice(g->dev[r]) != hipSuccess ||
-            hipEventCreateWithFlags(&g->band_done[r], hipEventDisableTiming) != hipSuccess)
+        if (hipSetDevice(g->dev[r]) != hipSuccess)
+            return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: hipSetDevice failed"));
+        if (g->dev[r] != ddev)
+            for (int p = 0; p < 2; ++p)
+                if (hipMalloc(&g->band_buf[p][r], (size_t)(g->y1[r] - g->y0[r]) * g->W * 4) != hipSuccess)
+                    return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: band buffer allocation failed"));
+        if (hipEventCreateWithFlags(&g->band_done[r], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: event creation failed"));
     }
     g->astream.assign(g->udev.size(), nullptr);
-    g->asm_done.assign(g->udev.size(), nullptr);
+    for (int p = 0; p < 2; ++p) g->asm_done[p].assign(g->udev.size(), nullptr);
     for (size_t u = 0; u < g->udev.size(); ++u) {
         if (hipSetDevice(g->udev[u]) != hipSuccess ||
             hipStreamCreateWithFlags(&g->astream[u], hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&g->asm_done[u], hipEventDisableTiming) != hipSuccess)
+            hipEventCreateWithFlags(&g->asm_done[0][u], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->asm_done[1][u], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: assembly stream creation failed"));
     }
     if (g->udev.size() > 1) {  // one RCCL communicator per distinct device, in this process
@@ -184,8 +218,31 @@ int tri_group_context(tri_group* g, uint32_t band, tri_ctx** out) {
 
 int tri_group_upload_geometry(tri_group* g, const tri_vertex* v, uint64_t nv, const uint32_t* idx, uint64_t ni,
                               const tri_mesh_range* m, uint32_t nm) {
-    return each(g, [&](tri_ctx* c) { return tri_upload_geometry(c, v, nv, idx, ni, m, nm); });
+    if (!g) return tri_internal_fail(TRI_E_INVALID, "tri_group_upload_geometry: null group");
+    int rc = tri_group_bind_geometry(g, 0, nullptr);  // back to the group's own per-device copies
+    if (rc) return rc;
+    for (tri_geometry* geo : g->geom)  // one upload per distinct device
+        if ((rc = tri_geometry_upload(geo, v, nv, idx, ni, m, nm))) return rc;
+    return TRI_OK;
 }
+
+int tri_group_bind_geometry(tri_group* g, uint32_t count, tri_geometry* const* geometries) {
+    if (!g) return tri_internal_fail(TRI_E_INVALID, "tri_group_bind_geometry: null group");
+    if (count && !geometries) return tri_internal_fail(TRI_E_INVALID, "tri_group_bind_geometry: null geometry list");
+    for (uint32_t r = 0; r < g->n; ++r) {
+        tri_geometry* use = g->geom[g->urank[r]];
+        if (count) {
+            use = nullptr;
+            for (uint32_t i = 0; i < count && !use; ++i)
+                if (geometries[i] && tri_internal_geometry_device(geometries[i]) == g->dev[r]) use = geometries[i];
+            if (!use) return tri_internal_fail(TRI_E_INVALID, "tri_group_bind_geometry: no geometry on a band's device");
+        }
+        const int rc = tri_bind_geometry(g->ctx[r], use);
+        if (rc) return rc;
+    }
+    return TRI_OK;
+}
+
 int tri_group_upload_materials(tri_group* g, const tri_material_record* r, uint32_t n) {
     return each(g, [&](tri_ctx* c) { return tri_upload_materials(c, r, n); });
 }
@@ -211,36 +268,63 @@ int tri_group_set_draws(tri_group* g, const tri_draw* d, uint32_t n) {
 int tri_group_render(tri_group* g) {
     if (!g) return tri_internal_fail(TRI_E_INVALID, "tri_group_render: null group");
     const int32_t ddev = g->dev[g->display];
+    const uint32_t p = (uint32_t)(g->frames & 1u);
     for (uint32_t r = 0; r < g->n; ++r) {
         GH(hipSetDevice(g->dev[r]));
         hipStream_t s = tri_internal_stream(g->ctx[r]);
-        // the previous frame's assembly read this band's buffer: the band waits for it (device-side)
-        if (g->assembled_once && g->dev[r] != ddev) GH(hipStreamWaitEvent(s, g->asm_done[g->urank[r]], 0));
-        const int rc = tri_render(g->ctx[r]);
+        uint32_t* out_ptr;
+        if (g->dev[r] == ddev) {
+            out_ptr = g->frame[p] + (size_t)g->y0[r] * g->W;  // in place
+            // the consumer of frame k - 2 (same buffer) has released it
+            if (g->present_armed[p]) GH(hipStreamWaitEvent(s, g->present_done[p], 0));
+        } else {
+            out_ptr = g->band_buf[p][r];
+            // frame k - 2's assembly read this buffer
+            if (g->asm_recorded[p]) GH(hipStreamWaitEvent(s, g->asm_done[p][g->urank[r]], 0));
+        }
+        int rc = tri_bind_output(g->ctx[r], out_ptr, nullptr);  // depth stays in the band context
         if (rc) return rc;
+        if ((rc = tri_render(g->ctx[r]))) return rc;
         GH(hipEventRecord(g->band_done[r], s));
     }
+    const int disp = g->urank[g->display];
     for (size_t u = 0; u < g->udev.size(); ++u) {  // each device's assembly stream waits for its bands
         GH(hipSetDevice(g->udev[u]));
         for (uint32_t r = 0; r < g->n; ++r)
             if (g->urank[r] == (int)u) GH(hipStreamWaitEvent(g->astream[u], g->band_done[r], 0));
+        // the receives into frame[p] wait for the consumer's fence on frame k - 2 as well
+        if ((int)u == disp && g->present_armed[p]) GH(hipStreamWaitEvent(g->astream[u], g->present_done[p], 0));
     }
     if (!g->comm.empty()) {
-        const int disp = g->urank[g->display];
         GN(ncclGroupStart());
         for (uint32_t r = 0; r < g->n; ++r) {
             if (g->dev[r] == ddev) continue;
             const size_t bytes = (size_t)(g->y1[r] - g->y0[r]) * g->W * 4;
-            GN(ncclSend(g->band_buf[r], bytes, ncclUint8, disp, g->comm[g->urank[r]], g->astream[g->urank[r]]));
-            GN(ncclRecv(g->frame + (size_t)g->y0[r] * g->W, bytes, ncclUint8, g->urank[r], g->comm[disp], g->astream[disp]));
+            GN(ncclSend(g->band_buf[p][r], bytes, ncclUint8, disp, g->comm[g->urank[r]], g->astream[g->urank[r]]));
+            GN(ncclRecv(g->frame[p] + (size_t)g->y0[r] * g->W, bytes, ncclUint8, g->urank[r], g->comm[disp],
+                        g->astream[disp]));
         }
         GN(ncclGroupEnd());
     }
     for (size_t u = 0; u < g->udev.size(); ++u) {
         GH(hipSetDevice(g->udev[u]));
-        GH(hipEventRecord(g->asm_done[u], g->astream[u]));
+        GH(hipEventRecord(g->asm_done[p][u], g->astream[u]));
     }
-    g->assembled_once = true;
+    g->asm_recorded[p] = true;
+    g->present_armed[p] = false;  // waited for; the consumer re-arms it for this frame
+    ++g->frames;
+    return TRI_OK;
+}
+
+int tri_group_present(tri_group* g, void* hip_stream) {
+    if (!g) return tri_internal_fail(TRI_E_INVALID, "tri_group_present: null group");
+    if (!g->frames) return tri_internal_fail(TRI_E_STATE, "tri_group_present: no frame rendered");
+    const uint32_t p = last_parity(g);
+    GH(hipSetDevice(g->dev[g->display]));
+    // host release: stamp it behind the frame's own assembly, so the fence can never precede the frame
+    hipStream_t s = hip_stream ? static_cast<hipStream_t>(hip_stream) : g->astream[g->urank[g->display]];
+    GH(hipEventRecord(g->present_done[p], s));
+    g->present_armed[p] = true;
     return TRI_OK;
 }
 
@@ -264,7 +348,7 @@ int tri_group_readback(tri_group* g, uint8_t* bgra, uint32_t* depth) {
     if (rc) return rc;
     if (bgra) {
         GH(hipSetDevice(g->dev[g->display]));
-        GH(hipMemcpy(bgra, g->frame, (size_t)g->W * g->H * 4, hipMemcpyDeviceToHost));
+        GH(hipMemcpy(bgra, g->frame[last_parity(g)], (size_t)g->W * g->H * 4, hipMemcpyDeviceToHost));
     }
     if (depth)
         for (uint32_t r = 0; r < g->n; ++r)
@@ -274,8 +358,57 @@ int tri_group_readback(tri_group* g, uint8_t* bgra, uint32_t* depth) {
 
 int tri_group_frame(tri_group* g, void** ptr, int32_t* device) {
     if (!g || !ptr || !device) return tri_internal_fail(TRI_E_INVALID, "tri_group_frame: null argument");
-    *ptr = g->frame;
+    *ptr = g->frame[last_parity(g)];
     *device = g->dev[g->display];
+    return TRI_OK;
+}
+
+int tri_group_get_output(tri_group* g, tri_image* out) {
+    if (!g || !out) return tri_internal_fail(TRI_E_INVALID, "tri_group_get_output: null argument");
+    out->device_ptr = g->frame[last_parity(g)];
+    out->width = g->W;
+    out->height = g->H;
+    out->pitch_bytes = g->W * 4u;
+    out->format = TRI_FORMAT_B8G8R8A8_UNORM;
+    out->device = g->dev[g->display];
+    out->reserved = 0;
+    return TRI_OK;
+}
+
+int tri_group_blit_linear(tri_group* g, void* dst, uint32_t width, uint32_t height) {
+    if (!g) return tri_internal_fail(TRI_E_INVALID, "tri_group_blit_linear: null group");
+    if (width == 0 || height == 0 || width > TRI_MAX_DIM || height > TRI_MAX_DIM)
+        return tri_internal_fail(TRI_E_INVALID, "tri_group_blit_linear: destination size out of range");
+    if (!g->frames) return tri_internal_fail(TRI_E_STATE, "tri_group_blit_linear: no frame rendered");
+    const int32_t ddev = g->dev[g->display];
+    GH(hipSetDevice(ddev));
+    hipStream_t s = g->astream[g->urank[g->display]];  // behind the frame's assembly
+    uint32_t* out = static_cast<uint32_t*>(dst);
+    if (!out) {
+        const size_t need = (size_t)width * height;
+        if (need > g->cap_present) {
+            GH(hipStreamSynchronize(s));
+            if (g->present) GH(hipFree(g->present));
+            g->present = nullptr;
+            g->cap_present = 0;
+            GH(hipMalloc(&g->present, need * 4));
+            g->cap_present = need;
+        }
+        out = g->present;
+        g->present_w = width;
+        g->present_h = height;
+    }
+    GH(tri_launch_blit(g->frame[last_parity(g)], (int32_t)g->W, (int32_t)g->H, out, (int32_t)width,
+                       (int32_t)height, tri_internal_unorm_lut(g->ctx[g->display]), s));
+    return TRI_OK;
+}
+
+int tri_group_read_present(tri_group* g, uint8_t* bgra) {
+    if (!g || !bgra) return tri_internal_fail(TRI_E_INVALID, "tri_group_read_present: null argument");
+    if (!g->present || !g->present_w) return tri_internal_fail(TRI_E_STATE, "tri_group_read_present: nothing was blitted");
+    GH(hipSetDevice(g->dev[g->display]));
+    GH(hipStreamSynchronize(g->astream[g->urank[g->display]]));
+    GH(hipMemcpy(bgra, g->present, (size_t)g->present_w * g->present_h * 4, hipMemcpyDeviceToHost));
     return TRI_OK;
 }
 

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cmath>
 #include <cstdio>
@@ -714,7 +715,10 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
     if ((rc = grow(g->d_vbox, g->cap_vbox, std::max<size_t>(vbox.size(), 1)))) return rc;
     if (!vbox.empty()) HIP_TRY(hipMemcpy(g->d_vbox, vbox.data(), vbox.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
     g->geometry_set = true;
-    ++g->version;
+    // versions come from one process-wide counter: a context that switches between geometry objects
+    // (tri_bind_geometry, tri_upload_geometry) can never see an equal version on a different object
+    static std::atomic<uint64_t> g_geometry_version{0};
+    g->version = ++g_geometry_version;
     return TRI_OK;
 }
 
@@ -729,6 +733,8 @@ void free_geometry(tri_geometry& g) {
 hipStream_t tri_internal_stream(tri_ctx* c) { return c->stream; }
 int tri_internal_device(tri_ctx* c) { return c->device; }
 int tri_internal_fail(int code, const char* msg) { return fail(code, "%s", msg); }
+int tri_internal_geometry_device(const tri_geometry* g) { return g->device; }
+const float* tri_internal_unorm_lut(tri_ctx* c) { return c->d_lut + 256; }
 
 extern "C" {
 
@@ -832,6 +838,8 @@ int tri_upload_geometry(tri_ctx* c, const tri_vertex* v, uint64_t nv, const uint
     HIP_TRY(hipStreamSynchronize(c->stream));
     c->geom = &c->own_geom;
     c->own_geom.device = c->device;
+    c->geom_seen = 0;  // re-resolve the draws against the new buffers even if the draw list is unchanged
+    c->draws_dirty = true;
     return geometry_upload(&c->own_geom, v, nv, idx, ni, meshes, nm);
 }
 
@@ -1040,9 +1048,12 @@ int tri_render(tri_ctx* c) {
     if ((rc = resolve_draws(c))) return rc;
     if (c->any_skin && !c->geom->has_skin_data) {
         // a skinned draw over vertices without weights: skin matrix = 0 -> everything collapses
-        // to the origin, exactly like the shader with all-zero weights; give the kernel zeros.
+        // to the origin, exactly like the shader with all-zero weights; give the kernel zeros. The
+        // geometry may be shared with contexts on other streams, so the zeros are in place (device
+        // synchronised) before the shared flag says so.
         if ((rc = grow(c->geom->d_skin, c->geom->cap_skin, std::max<uint64_t>(c->geom->nverts, 1)))) return rc;
-        HIP_TRY(hipMemsetAsync(c->geom->d_skin, 0, std::max<uint64_t>(c->geom->nverts, 1) * sizeof(TriVsSkin), c->stream));
+        HIP_TRY(hipMemset(c->geom->d_skin, 0, std::max<uint64_t>(c->geom->nverts, 1) * sizeof(TriVsSkin)));
+        HIP_TRY(hipDeviceSynchronize());
         c->geom->has_skin_data = true;
     }
     if ((rc = choose_bin_grid(c))) return rc;

@@ -5,6 +5,7 @@
 // become opaque device pointers (GetViewportTexture).
 #pragma once
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <map>
@@ -118,6 +119,14 @@ public:
     bool BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::vector<tri_draw>& draws);
     // Rasterizer flags (TRI_FLAG_*) used for viewports created from now on.
     void SetRasterFlags(uint32_t flags) { m_RasterFlags = flags; }
+    // Multi-device viewports (SURVEY 8(b) tri_config.device_count, 8(e)): with count > 1 every viewport
+    // renders as a tri_group of `count` row bands on `devices` (default 0 .. count-1; an ordinal may
+    // repeat), the frame assembled on the first band's device over RCCL; count <= 1 is one context per
+    // viewport (the default). Existing viewport targets are rebuilt at the next DrawFrame. The geometry
+    // goes to each distinct device once per generation and is shared by every viewport there. Returns
+    // false (and changes nothing) for an invalid device list.
+    bool SetDeviceCount(uint32_t count, const std::vector<int32_t>& devices = {});
+    uint32_t GetDeviceCount() const { return (uint32_t)std::max<size_t>(m_Devices.size(), 1); }
     bool IsShutdown() const { return m_Shutdown; }
     // The concatenated buffers UploadMeshFromCache builds (the device copy of these is what
     // tri_upload_geometry receives).
@@ -143,7 +152,8 @@ private:
     };
     struct ViewportContext {
         ViewportInfo m_Info{};
-        tri_ctx* m_Ctx = nullptr;
+        tri_ctx* m_Ctx = nullptr;      // one-device viewport
+        tri_group* m_Group = nullptr;  // multi-device viewport (SetDeviceCount > 1)
         uint32_t m_Width = 0, m_Height = 0;
         uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0, m_SkyboxGeneration = 0;
         std::vector<float> m_BonePalette;  // the palette last uploaded to this viewport's context
@@ -180,6 +190,11 @@ private:
     bool m_IsUploadingMeshes = false;
     tri_geometry* m_SharedGeometry = nullptr;  // the device copy every viewport context binds
     uint64_t m_SharedGeometryGeneration = 0;
+    std::vector<int32_t> m_Devices;                 // SetDeviceCount's bands (empty: one context per viewport)
+    std::vector<tri_geometry*> m_DeviceGeometry;    // multi-device: one shared copy per distinct device
+    std::vector<uint64_t> m_DeviceGeometryGeneration;
+    bool UploadSharedGeometry(std::vector<tri_geometry*>& out);
+    void DestroyViewportTargets();
     uint64_t m_GeometryUploads = 0;
     std::vector<glm::vec3> m_MeshBoundsMin, m_MeshBoundsMax;  // object-space box per cached mesh
     uint32_t m_ShadowMapSize = 2048;
@@ -202,7 +217,8 @@ private:
     ViewportInfo m_LastViewport{};
     uint32_t m_ActiveViewportId = 0;
     uint32_t m_PresentWidth = 0, m_PresentHeight = 0;
-    tri_ctx* m_PresentSource = nullptr;  // viewport context the last present was blitted from
+    tri_ctx* m_PresentSource = nullptr;    // viewport context the last present was blitted from
+    tri_group* m_PresentGroup = nullptr;   // ... or multi-device viewport
     uint32_t m_RasterFlags = 0;
 
     glm::vec3 m_AmbientColor{0.03f};

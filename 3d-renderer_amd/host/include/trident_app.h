@@ -50,6 +50,9 @@ int trident_app_add_light(trident_app* app, int type, const float position[3], c
  * directional light turns on the shadow-map pre-pass (Renderer::SetShadowMapSize, default 2048). */
 int trident_app_set_light_shadow_caster(trident_app* app, uint32_t entity, int caster);
 int trident_app_set_shadow_map_size(trident_app* app, uint32_t size);
+/* Renderer::SetDeviceCount: with count > 1 every viewport renders as `count` row bands on `devices`
+ * (NULL = 0 .. count-1; ordinals may repeat) assembled on the first band's device (tri_group). */
+int trident_app_set_device_count(trident_app* app, uint32_t count, const int32_t* devices);
 /* The pre-pass configuration DrawFrame would use now (*enabled = 0 when there is none). */
 int trident_app_shadow_config(trident_app* app, tri_shadow_config* out, int* enabled);
 

@@ -136,6 +136,36 @@ void CopyMat(const glm::mat4& m, float* out) {
         for (int r = 0; r < 4; ++r) out[c * 4 + r] = m[c][r];
 }
 
+// A viewport's render target: one context, or a group of row bands on several devices (SetDeviceCount).
+// Every per-context call of the draw path goes to the context or is broadcast to the group's bands.
+struct Target {
+    tri_ctx* c;
+    tri_group* g;
+    int Materials(const tri_material_record* r, uint32_t n) const {
+        return g ? tri_group_upload_materials(g, r, n) : tri_upload_materials(c, r, n);
+    }
+    int Skybox(const uint8_t* f, uint32_t n) const { return g ? tri_group_upload_skybox(g, f, n) : tri_upload_skybox(c, f, n); }
+    int Texture(uint32_t slot, const uint8_t* p, uint32_t w, uint32_t h) const {
+        return g ? tri_group_upload_texture(g, slot, p, w, h) : tri_upload_texture(c, slot, p, w, h);
+    }
+    int Shadow(const tri_shadow_config* s) const { return g ? tri_group_set_shadow(g, s) : tri_set_shadow(c, s); }
+    int Bones(const float* m, uint32_t n) const {
+        return g ? tri_group_upload_bone_palette(g, m, n) : tri_upload_bone_palette(c, m, n);
+    }
+    int Frame(const tri_global_ubo* u, const float* clear) const {
+        return g ? tri_group_set_frame(g, u, clear) : tri_set_frame(c, u, clear);
+    }
+    int Draws(const tri_draw* d, uint32_t n) const { return g ? tri_group_set_draws(g, d, n) : tri_set_draws(c, d, n); }
+    int Render() const { return g ? tri_group_render(g) : tri_render(c); }
+    int Sync() const { return g ? tri_group_synchronize(g) : tri_synchronize(c); }
+    int Output(tri_image* o) const { return g ? tri_group_get_output(g, o) : tri_get_output(c, o); }
+    int Blit(uint32_t w, uint32_t h) const { return g ? tri_group_blit_linear(g, nullptr, w, h) : tri_blit_linear(c, nullptr, w, h); }
+    int ReadPresent(uint8_t* p) const { return g ? tri_group_read_present(g, p) : tri_read_present(c, p); }
+    int Readback(uint8_t* bgra, uint32_t* depth) const {
+        return g ? tri_group_readback(g, bgra, depth) : tri_readback(c, bgra, depth);
+    }
+};
+
 }  // namespace
 
 Renderer::Renderer() = default;
@@ -157,17 +187,86 @@ void Renderer::Init() {
     m_Shutdown = false;
 }
 
-void Renderer::Shutdown() {
+void Renderer::DestroyViewportTargets() {
     for (auto& it : m_Viewports) {
-        tri_destroy(it.second.m_Ctx);
-        it.second.m_Ctx = nullptr;
+        ViewportContext& vc = it.second;
+        tri_destroy(vc.m_Ctx);
+        tri_group_destroy(vc.m_Group);
+        vc.m_Ctx = nullptr;
+        vc.m_Group = nullptr;
+        vc.m_HasImage = false;
+        vc.m_Width = vc.m_Height = 0;
     }
-    m_Viewports.clear();
-    tri_geometry_destroy(m_SharedGeometry);  // after every context that bound it
+    m_PresentSource = nullptr;
+    m_PresentGroup = nullptr;
+    // after every context that bound them
+    tri_geometry_destroy(m_SharedGeometry);
     m_SharedGeometry = nullptr;
     m_SharedGeometryGeneration = 0;
+    for (tri_geometry* g : m_DeviceGeometry) tri_geometry_destroy(g);
+    m_DeviceGeometry.clear();
+    m_DeviceGeometryGeneration.clear();
+}
+
+void Renderer::Shutdown() {
+    DestroyViewportTargets();
+    m_Viewports.clear();
     if (m_Initialised) m_Shutdown = true;
     m_Initialised = false;
+}
+
+bool Renderer::SetDeviceCount(uint32_t count, const std::vector<int32_t>& devices) {
+    std::vector<int32_t> devs;
+    if (count > 1) {
+        if (!devices.empty() && devices.size() != count) {
+            LogError("SetDeviceCount", "device list length differs from the count");
+            return false;
+        }
+        for (uint32_t i = 0; i < count; ++i) {
+            const int32_t d = devices.empty() ? (int32_t)i : devices[i];
+            if (d < 0) {
+                LogError("SetDeviceCount", "negative device ordinal");
+                return false;
+            }
+            devs.push_back(d);
+        }
+    }
+    if (devs == m_Devices) return true;
+    DestroyViewportTargets();  // rebuilt by the next DrawFrame's PrepareViewport
+    m_Devices = devs;
+    return true;
+}
+
+// Multi-device viewports: one copy of the concatenated buffers per distinct device and generation,
+// bound by every viewport's group (tri_group_bind_geometry picks each band's device copy).
+bool Renderer::UploadSharedGeometry(std::vector<tri_geometry*>& out) {
+    std::vector<int32_t> udev;
+    for (int32_t d : m_Devices)
+        if (std::find(udev.begin(), udev.end(), d) == udev.end()) udev.push_back(d);
+    if (m_DeviceGeometry.size() != udev.size()) {
+        for (tri_geometry* g : m_DeviceGeometry) tri_geometry_destroy(g);
+        m_DeviceGeometry.assign(udev.size(), nullptr);
+        m_DeviceGeometryGeneration.assign(udev.size(), 0);
+    }
+    const std::vector<tri_mesh_range> ranges = GetMeshRanges();
+    for (size_t u = 0; u < udev.size(); ++u) {
+        if (!m_DeviceGeometry[u] && tri_geometry_create(udev[u], &m_DeviceGeometry[u]) != TRI_OK) {
+            LogError("UploadMeshFromCache", tri_last_error());
+            m_DeviceGeometry[u] = nullptr;
+            return false;
+        }
+        if (m_DeviceGeometryGeneration[u] != m_GeometryGeneration) {
+            if (tri_geometry_upload(m_DeviceGeometry[u], m_VertexBuffer.data(), m_VertexBuffer.size(), m_IndexBuffer.data(),
+                                    m_IndexBuffer.size(), ranges.data(), (uint32_t)ranges.size()) != TRI_OK) {
+                LogError("UploadMeshFromCache", tri_last_error());
+                return false;
+            }
+            m_DeviceGeometryGeneration[u] = m_GeometryGeneration;
+            ++m_GeometryUploads;
+        }
+    }
+    out = m_DeviceGeometry;
+    return true;
 }
 
 // Renderer.cpp:3818-3927: the discovered cubemap (KTX, Default/ directory, loose px/nx/... PNG faces),
@@ -607,16 +706,28 @@ std::vector<tri_mesh_range> Renderer::GetMeshRanges() const {
 bool Renderer::PrepareViewport(ViewportContext& vc) {
     const uint32_t w = (uint32_t)std::max(vc.m_Info.Size.x, 0.0f), h = (uint32_t)std::max(vc.m_Info.Size.y, 0.0f);
     if (w == 0 || h == 0) return false;
-    if (vc.m_Ctx && (vc.m_Width != w || vc.m_Height != h)) {  // CreateOrResizeOffscreenResources
+    const bool multi = m_Devices.size() > 1;
+    if ((vc.m_Ctx || vc.m_Group) && (vc.m_Width != w || vc.m_Height != h)) {  // CreateOrResizeOffscreenResources
         tri_destroy(vc.m_Ctx);
+        tri_group_destroy(vc.m_Group);
         vc.m_Ctx = nullptr;
+        vc.m_Group = nullptr;
         vc.m_HasImage = false;
     }
-    if (!vc.m_Ctx) {
-        tri_config cfg{w, h, 0, 0, -1, m_RasterFlags};
-        if (tri_create(&cfg, &vc.m_Ctx) != TRI_OK) {
+    if (!vc.m_Ctx && !vc.m_Group) {
+        int rc;
+        if (multi) {  // row bands on m_Devices, assembled on the first band's device
+            if (h < m_Devices.size()) return false;
+            tri_group_config gc{w, h, (uint32_t)m_Devices.size(), 0u, m_Devices.data(), m_RasterFlags, 0u};
+            rc = tri_group_create(&gc, &vc.m_Group);
+        } else {
+            tri_config cfg{w, h, 0, 0, -1, m_RasterFlags};
+            rc = tri_create(&cfg, &vc.m_Ctx);
+        }
+        if (rc != TRI_OK) {
             LogError("viewport target", tri_last_error());
             vc.m_Ctx = nullptr;
+            vc.m_Group = nullptr;
             return false;
         }
         vc.m_Width = w;
@@ -624,6 +735,16 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
         vc.m_GeometryGeneration = vc.m_TextureGeneration = vc.m_MaterialGeneration = vc.m_SkyboxGeneration = 0;
         vc.m_Shadow = tri_shadow_config{};  // a fresh context starts without the pre-pass and bones
         vc.m_BonePalette.clear();
+    }
+    const Target t{vc.m_Ctx, vc.m_Group};
+    if (vc.m_GeometryGeneration != m_GeometryGeneration && multi) {
+        std::vector<tri_geometry*> geos;
+        if (!UploadSharedGeometry(geos)) return false;
+        if (tri_group_bind_geometry(vc.m_Group, (uint32_t)geos.size(), geos.data()) != TRI_OK) {
+            LogError("UploadMeshFromCache", tri_last_error());
+            return false;
+        }
+        vc.m_GeometryGeneration = m_GeometryGeneration;
     }
     if (vc.m_GeometryGeneration != m_GeometryGeneration) {
         // one device copy of the concatenated buffers per generation, bound by every viewport
@@ -652,7 +773,7 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
         for (const Geometry::Material& m : m_Materials)
             recs.push_back({{m.BaseColorFactor.x, m.BaseColorFactor.y, m.BaseColorFactor.z, m.BaseColorFactor.w},
                             {m.MetallicFactor, m.RoughnessFactor, 1.0f, 0.0f}});
-        if (tri_upload_materials(vc.m_Ctx, recs.data(), (uint32_t)recs.size()) != TRI_OK) {
+        if (t.Materials(recs.data(), (uint32_t)recs.size()) != TRI_OK) {
             LogError("material buffer", tri_last_error());
             return false;
         }
@@ -660,8 +781,7 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
     }
     if (vc.m_SkyboxGeneration != m_SkyboxGeneration) {
         const bool ok = m_SkyboxCubemap.IsValid();
-        if (tri_upload_skybox(vc.m_Ctx, ok ? m_SkyboxCubemap.m_PixelData.data() : nullptr,
-                              ok ? m_SkyboxCubemap.m_Width : 0) != TRI_OK) {
+        if (t.Skybox(ok ? m_SkyboxCubemap.m_PixelData.data() : nullptr, ok ? m_SkyboxCubemap.m_Width : 0) != TRI_OK) {
             LogError("skybox cubemap", tri_last_error());
             return false;
         }
@@ -669,9 +789,8 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
     }
     if (vc.m_TextureGeneration != m_TextureGeneration) {
         for (size_t s = 0; s < m_TextureSlots.size(); ++s) {
-            const Loader::TextureData& t = m_TextureSlots[s].m_Data;
-            if (tri_upload_texture(vc.m_Ctx, (uint32_t)s, t.Pixels.data(), (uint32_t)t.Width, (uint32_t)t.Height) !=
-                TRI_OK) {
+            const Loader::TextureData& tex = m_TextureSlots[s].m_Data;
+            if (t.Texture((uint32_t)s, tex.Pixels.data(), (uint32_t)tex.Width, (uint32_t)tex.Height) != TRI_OK) {
                 LogError("texture slot", tri_last_error());
                 return false;
             }
@@ -705,15 +824,16 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     for (auto& it : m_Viewports) {  // RecordCommandBuffer's per-viewport render passes
         ViewportContext& vc = it.second;
         if (!PrepareViewport(vc)) continue;
+        const Target t{vc.m_Ctx, vc.m_Group};
         if (std::memcmp(&vc.m_Shadow, &shadow, sizeof shadow) != 0) {  // pre-pass on / off / refitted
-            if (tri_set_shadow(vc.m_Ctx, shadowOn ? &shadow : nullptr) != TRI_OK) {
+            if (t.Shadow(shadowOn ? &shadow : nullptr) != TRI_OK) {
                 LogError("shadow map", tri_last_error());
                 continue;
             }
             vc.m_Shadow = shadow;
         }
         if (vc.m_BonePalette != m_BonePalette) {  // the bone SSBO (binding 4) of this frame
-            if (tri_upload_bone_palette(vc.m_Ctx, m_BonePalette.data(), (uint32_t)(m_BonePalette.size() / 16)) != TRI_OK) {
+            if (t.Bones(m_BonePalette.data(), (uint32_t)(m_BonePalette.size() / 16)) != TRI_OK) {
                 LogError("bone palette", tri_last_error());
                 continue;
             }
@@ -721,34 +841,40 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
         }
         tri_global_ubo ubo;
         UpdateUniformBuffer(GetActiveCamera(vc), ubo);
-        if (tri_set_frame(vc.m_Ctx, &ubo, clear) != TRI_OK ||
-            tri_set_draws(vc.m_Ctx, draws.data(), (uint32_t)draws.size()) != TRI_OK || tri_render(vc.m_Ctx) != TRI_OK) {
+        if (t.Frame(&ubo, clear) != TRI_OK || t.Draws(draws.data(), (uint32_t)draws.size()) != TRI_OK ||
+            t.Render() != TRI_OK) {
             LogError("DrawFrame", tri_last_error());
             continue;
         }
-        vc.m_HasImage = tri_get_output(vc.m_Ctx, &vc.m_Image) == TRI_OK;
+        vc.m_HasImage = t.Output(&vc.m_Image) == TRI_OK;
         submitted.push_back(&vc);
     }
     // Frame fence (Renderer.cpp:744-760). A frame that outgrew the bin/clip queues has grown them
     // inside tri_synchronize and is re-rendered, so a presented frame is always complete.
     for (ViewportContext* vc : submitted) {
-        int rc = tri_synchronize(vc->m_Ctx);
+        const Target t{vc->m_Ctx, vc->m_Group};
+        int rc = t.Sync();
         for (int retry = 0; rc == TRI_E_OVERFLOW && retry < 3; ++retry) {
-            rc = tri_render(vc->m_Ctx);
-            if (rc == TRI_OK) rc = tri_synchronize(vc->m_Ctx);
+            rc = t.Render();
+            if (rc == TRI_OK) rc = t.Sync();
         }
         if (rc != TRI_OK) LogError("frame fence", tri_last_error());
+        if (rc == TRI_OK) vc->m_HasImage = t.Output(&vc->m_Image) == TRI_OK;  // a re-render moves a group's buffer
     }
     // Primary viewport -> swapchain image, VK_FILTER_LINEAR (Renderer.cpp:5346-5361).
     m_PresentSource = nullptr;
+    m_PresentGroup = nullptr;
     auto active = m_Viewports.find(m_ActiveViewportId);
-    if (m_PresentWidth && m_PresentHeight && active != m_Viewports.end() && active->second.m_Ctx &&
+    if (m_PresentWidth && m_PresentHeight && active != m_Viewports.end() &&
+        (active->second.m_Ctx || active->second.m_Group) &&
         std::find(submitted.begin(), submitted.end(), &active->second) != submitted.end()) {
-        if (tri_blit_linear(active->second.m_Ctx, nullptr, m_PresentWidth, m_PresentHeight) == TRI_OK &&
-            tri_synchronize(active->second.m_Ctx) == TRI_OK)
+        const Target t{active->second.m_Ctx, active->second.m_Group};
+        if (t.Blit(m_PresentWidth, m_PresentHeight) == TRI_OK && t.Sync() == TRI_OK) {
             m_PresentSource = active->second.m_Ctx;
-        else
+            m_PresentGroup = active->second.m_Group;
+        } else {
             LogError("present blit", tri_last_error());
+        }
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     RecordFrameTiming(ms);
@@ -783,18 +909,18 @@ void Renderer::RecordFrameTiming(double ms) {  // Renderer.cpp:6286-6343
 
 void* Renderer::GetViewportTexture(uint32_t viewportId) const {
     auto it = m_Viewports.find(viewportId);
-    if (it == m_Viewports.end() || !it->second.m_Ctx || !it->second.m_HasImage) return nullptr;
+    if (it == m_Viewports.end() || (!it->second.m_Ctx && !it->second.m_Group) || !it->second.m_HasImage) return nullptr;
     return const_cast<tri_image*>(&it->second.m_Image);
 }
 
 bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgba, std::vector<float>* depth) {
     auto it = m_Viewports.find(viewportId);
-    if (it == m_Viewports.end() || !it->second.m_Ctx) return false;
+    if (it == m_Viewports.end() || (!it->second.m_Ctx && !it->second.m_Group)) return false;
     ViewportContext& vc = it->second;
     std::vector<uint8_t> bgra((size_t)vc.m_Width * vc.m_Height * 4);
     std::vector<uint32_t> dbits;
     if (depth) dbits.resize((size_t)vc.m_Width * vc.m_Height);
-    if (tri_readback(vc.m_Ctx, bgra.data(), depth ? dbits.data() : nullptr) != TRI_OK) {
+    if (Target{vc.m_Ctx, vc.m_Group}.Readback(bgra.data(), depth ? dbits.data() : nullptr) != TRI_OK) {
         LogError("readback", tri_last_error());
         return false;
     }
@@ -813,9 +939,9 @@ bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgb
 }
 
 bool Renderer::ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height) {
-    if (!m_PresentSource) return false;
+    if (!m_PresentSource && !m_PresentGroup) return false;
     std::vector<uint8_t> bgra((size_t)m_PresentWidth * m_PresentHeight * 4);
-    if (tri_read_present(m_PresentSource, bgra.data()) != TRI_OK) {
+    if (Target{m_PresentSource, m_PresentGroup}.ReadPresent(bgra.data()) != TRI_OK) {
         LogError("present readback", tri_last_error());
         return false;
     }

@@ -176,6 +176,14 @@ int trident_app_set_shadow_map_size(trident_app* app, uint32_t size) {
     });
 }
 
+int trident_app_set_device_count(trident_app* app, uint32_t count, const int32_t* devices) {
+    return Guard(app, [&] {
+        std::vector<int32_t> devs;
+        if (devices && count > 1) devs.assign(devices, devices + count);
+        return app->renderer.SetDeviceCount(count, devs) ? TRI_OK : TRI_E_INVALID;
+    });
+}
+
 int trident_app_shadow_config(trident_app* app, tri_shadow_config* out, int* enabled) {
     return Guard(app, [&] {
         if (!out || !enabled) return TRI_E_INVALID;

@@ -9,6 +9,8 @@ import ctypes as C
 
 import numpy as np
 
+TRI_RASTER_ABI_VERSION = 2  # include/tri_raster.h
+
 TRI_OK = 0
 TRI_E_INVALID = -1
 TRI_E_HIP = -2
@@ -242,6 +244,11 @@ CABI_FUNCTIONS = [
     ("tri_group_synchronize", C.c_int, [C.c_void_p]),
     ("tri_group_readback", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tri_group_frame", C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_int32)]),
+    ("tri_group_get_output", C.c_int, [C.c_void_p, C.POINTER(TriImage)]),
+    ("tri_group_present", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("tri_group_bind_geometry", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("tri_group_blit_linear", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
+    ("tri_group_read_present", C.c_int, [C.c_void_p, C.c_void_p]),
 ]
 
 

@@ -33,6 +33,7 @@ _APP_FUNCTIONS = [
     ("trident_app_viewport_texture", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(abi.TriImage)]),
     ("trident_app_set_light_shadow_caster", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
     ("trident_app_set_shadow_map_size", C.c_int, [C.c_void_p, C.c_uint32]),
+    ("trident_app_set_device_count", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     ("trident_app_shadow_config", C.c_int, [C.c_void_p, C.POINTER(abi.TriShadowConfig), C.POINTER(C.c_int)]),
     ("trident_app_geometry_uploads", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("trident_load_image", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
@@ -153,6 +154,11 @@ class TridentApp:
 
     def set_shadow_map_size(self, size):
         _check(self._lib.trident_app_set_shadow_map_size(self._h, size), "shadow map size")
+
+    def set_device_count(self, count, devices=None):
+        """Renderer::SetDeviceCount: viewports as `count` row bands on `devices` (tri_group), count <= 1: one context."""
+        arr = (C.c_int32 * len(devices))(*devices) if devices else None
+        _check(self._lib.trident_app_set_device_count(self._h, count, arr), "device count")
 
     def shadow_config(self):
         """The pre-pass configuration DrawFrame would use now (abi.TriShadowConfig), or None."""

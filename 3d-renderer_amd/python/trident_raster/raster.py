@@ -37,8 +37,8 @@ def load_library(path=None):
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    if lib.tri_abi_version() != 1:
-        raise ImportError("tri_raster ABI version mismatch")
+    if lib.tri_abi_version() != abi.TRI_RASTER_ABI_VERSION:
+        raise ImportError(f"tri_raster ABI version {lib.tri_abi_version()}, binding expects {abi.TRI_RASTER_ABI_VERSION}")
     _lib = lib
     return lib
 
@@ -345,3 +345,33 @@ class TriGroup:
         p, d = C.c_void_p(), C.c_int32()
         _check(_lib.tri_group_frame(self._g, C.byref(p), C.byref(d)))
         return p.value, d.value
+
+    def output_image(self):
+        img = abi.TriImage()
+        _check(_lib.tri_group_get_output(self._g, C.byref(img)))
+        return img
+
+    def present(self, stream_ptr=None):
+        """tri_group_present: the consumer fence on the most recent frame (after `stream_ptr`'s work, or now)."""
+        _check(_lib.tri_group_present(self._g, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+    def bind_geometry(self, geometries):
+        """tri_group_bind_geometry: caller-owned TriGeometry objects (one per device); [] = the group's own."""
+        arr = (C.c_void_p * max(len(geometries), 1))(*[g._g.value for g in geometries])
+        _check(_lib.tri_group_bind_geometry(self._g, len(geometries), arr))
+
+    def context(self, band):
+        """The band's tri_ctx handle (tri_group_context)."""
+        c = C.c_void_p()
+        _check(_lib.tri_group_context(self._g, band, C.byref(c)))
+        return c
+
+    def blit(self, width, height, dst_ptr=None):
+        _check(_lib.tri_group_blit_linear(self._g, C.c_void_p(dst_ptr) if dst_ptr else None, width, height))
+        self._present = (width, height)
+
+    def read_present(self):
+        w, h = self._present
+        out = np.empty((h, w, 4), dtype=np.uint8)
+        _check(_lib.tri_group_read_present(self._g, _ptr(out)))
+        return out

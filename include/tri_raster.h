@@ -27,7 +27,7 @@
 extern "C" {
 #endif
 
-#define TRI_RASTER_ABI_VERSION 1
+#define TRI_RASTER_ABI_VERSION 2 /* 2: tri_geometry, tri_image, shadow pre-pass, tri_group fences */
 
 /* ---- status codes ---------------------------------------------------------------------- */
 #define TRI_OK 0
@@ -304,7 +304,11 @@ int tri_get_frame_stats(tri_ctx* ctx, tri_frame_stats* out); /* synchronizes    
  * frame on the display context's device: bands on that device render straight into the frame, bands
  * on other devices are gathered with RCCL grouped ncclSend / ncclRecv over xGMI (one communicator per
  * distinct device, ncclCommInitAll). One host thread drives the whole group, as Renderer::DrawFrame
- * does (the engine's single render thread, Application.cpp:82-134). */
+ * does (the engine's single render thread, Application.cpp:82-134).
+ * The geometry is held once per distinct device (one tri_geometry bound by every band context there).
+ * The assembled frame is double-buffered: frame k lands in buffer k % 2, and frame k + 2 overwrites it
+ * only after the consumer's fence on frame k (tri_group_present), when one was set — the reference keeps
+ * one framebuffer per swapchain image and waits on that image's fence (Renderer.cpp:744-772). */
 typedef struct tri_group tri_group;
 typedef struct tri_group_config {
     uint32_t width;
@@ -340,8 +344,25 @@ int tri_group_synchronize(tri_group* group);
 /* The assembled frame (width*height BGRA8, from the display device) and, optionally, the depth of
  * every band (width*height float32 bits). Synchronous. */
 int tri_group_readback(tri_group* group, uint8_t* bgra8, uint32_t* depth_bits);
-/* The assembled frame in device memory: its pointer on the display device and that device's ordinal. */
+/* The assembled frame in device memory: its pointer on the display device and that device's ordinal
+ * (the buffer of the most recent tri_group_render; complete once its assembly has run). */
 int tri_group_frame(tri_group* group, void** device_bgra8, int32_t* device);
+/* The same buffer as a tri_image (GetViewportTexture's handle for a multi-device viewport). */
+int tri_group_get_output(tri_group* group, tri_image* out);
+/* Consumer fence ("frame k presented"): the caller is done reading the most recent frame once the work
+ * already enqueued on hip_stream (a stream on the display device) has run; NULL = done now. Frame k + 2,
+ * which reuses that buffer, waits for this point on the device before any band or receive writes it.
+ * Without a fence the next-but-one frame overwrites the buffer unconditionally (a caller that reads with
+ * tri_group_readback, which synchronises, needs none). */
+int tri_group_present(tri_group* group, void* hip_stream);
+/* Binds caller-owned geometry objects: for every band, the one of `geometries` on the band's device
+ * (TRI_E_INVALID if a band's device has none). count 0 returns the bands to the group's own per-device
+ * copies, which tri_group_upload_geometry fills. The objects must outlive the binding. */
+int tri_group_bind_geometry(tri_group* group, uint32_t count, tri_geometry* const* geometries);
+/* tri_blit_linear / tri_read_present over the assembled frame (the presentation blit of a multi-device
+ * viewport, on the display device, stream-ordered after the frame's assembly). */
+int tri_group_blit_linear(tri_group* group, void* dst, uint32_t width, uint32_t height);
+int tri_group_read_present(tri_group* group, uint8_t* bgra8);
 
 #ifdef __cplusplus
 } /* extern "C" */

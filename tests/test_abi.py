@@ -61,7 +61,7 @@ def test_library_exports_every_declared_symbol(hiplib):
     exported = set(re.findall(r"\bT (tri_\w+)", out))
     missing = set(header_functions()) - exported
     assert not missing, missing
-    assert hiplib.tri_abi_version() == 1
+    assert hiplib.tri_abi_version() == abi.TRI_RASTER_ABI_VERSION == 2
 
 
 def test_fails_loudly_without_gpu(hiplib):

@@ -1,0 +1,220 @@
+"""C4 readiness on one GPU: the full C3 frame (3840x2160, 999,698 triangles, the reference cubemap) split
+into 8 row bands, as 8 band contexts and as a tri_group of 8 bands, bit-exact against the single-context
+frame and depth bit-exact against the oracle's full frame (BASELINE configs[3]); the group's
+double-buffered frame with its consumer fence; and the Trident::Renderer shim driving a group
+(Renderer::SetDeviceCount, the tri_config.device_count of SURVEY 8(b)).
+
+On a one-GPU box every band sits on device 0 (the stand-in for N devices): the RCCL send/recv branch of
+tri_group runs only on the driver's 8-GPU node. The band split, cluster culling, in-place assembly, the
+per-device geometry, the buffer rotation and the fences are the same code either way.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+
+import scene_cases as sc
+
+pytestmark = pytest.mark.gpu
+
+COLOR_TOL = 1
+
+
+@pytest.fixture(scope="module")
+def c3_full():
+    from trident_raster import scenes
+
+    return scenes.scene_c3_grid()
+
+
+def _render_single(scene, flags):
+    from trident_raster import raster, scenes
+
+    with raster.TriRaster(scene.width, scene.height, flags=flags) as r:
+        scenes.load_scene(r, scene)
+        r.render_frame()
+        return r.readback()
+
+
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+def test_c4_full_frame_eight_bands(oracle, c3_full, mode):
+    """C4 = C3 on 8 GPUs: eight 270-row bands of the full 4K / 1M-triangle frame, rendered (a) as eight
+    band contexts sharing one tri_geometry and (b) as a tri_group over devices [0]*8, assemble to the
+    single-context frame bit for bit; depth is bit-exact against the oracle's full frame."""
+    from trident_raster import abi, raster, scenes
+
+    flags = abi.TRI_FLAG_EXACT_SHADING if mode == "exact" else 0
+    s = c3_full
+    full_c, full_d = _render_single(s, flags)
+    rows = s.height // 8
+    g = raster.TriGeometry(0)
+    g.upload(s.vertices, s.indices, s.meshes)
+    parts = []
+    for r in range(8):
+        with raster.TriRaster(s.width, s.height, band=(r * rows, (r + 1) * rows), device=0, flags=flags) as ctx:
+            scenes.load_scene(ctx, s, geometry=g)
+            ctx.render_frame()
+            parts.append(ctx.readback())
+    g.close()
+    band_c = np.concatenate([p[0] for p in parts])
+    band_d = np.concatenate([p[1] for p in parts])
+    assert np.array_equal(band_d, full_d), int((band_d != full_d).sum())
+    assert np.array_equal(band_c, full_c), int((band_c != full_c).any(-1).sum())
+    with raster.TriGroup(s.width, s.height, [0] * 8, display=0, flags=flags) as grp:
+        scenes.load_scene(grp, s)
+        grp.render_frame()
+        grp_c, grp_d = grp.readback()
+    assert np.array_equal(grp_d, full_d) and np.array_equal(grp_c, full_c)
+    oc, od, _ = oracle.render(s)
+    assert np.array_equal(full_d, od), int((full_d != od).sum())
+    assert int(np.abs(full_c.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL
+
+
+def _copy_frame(ptr, dev, w, h):
+    from trident_raster import raster
+
+    return raster.copy_device_to_host(ptr, w * h * 4, dev).reshape(h, w, 4)
+
+
+def test_group_double_buffer_and_present_fence(oracle):
+    """Frame k lands in buffer k % 2: while frame k + 1 renders into the other buffer, frame k's image
+    stays intact for its presenter; frame k + 2 reuses frame k's buffer after the consumer fence
+    (tri_group_present). Three different camera positions, so every frame differs."""
+    from trident_raster import raster, scenes
+
+    base = sc.primitives_row(oracle, 320, 240)
+    cams = [(0.0, 1.0, 6.0), (0.6, 1.3, 6.5), (-0.7, 0.8, 5.5)]
+    frames = []
+    for cam in cams:
+        s = sc.primitives_row(oracle, 320, 240)
+        view, proj = scenes.editor_camera(cam, (0, 0, 0), 60.0, (320, 240))
+        s.ubo = scenes.pack_ubo(view, proj, cam, [{"type": "directional"}])
+        frames.append(s)
+    with raster.TriGroup(base.width, base.height, [0] * 3, display=1) as g:
+        scenes.load_scene(g, frames[0])
+        g.render_frame()
+        p0, dev = g.frame_pointer()
+        img0 = _copy_frame(p0, dev, 320, 240)
+        g.present()  # the presenter of frame 0 is done with it
+        g.set_frame(frames[1].ubo, frames[1].clear)
+        g.render_frame()
+        p1, _ = g.frame_pointer()
+        assert p1 != p0
+        # frame 0's buffer was not touched by frame 1
+        assert np.array_equal(_copy_frame(p0, dev, 320, 240), img0)
+        img1 = _copy_frame(p1, dev, 320, 240)
+        g.set_frame(frames[2].ubo, frames[2].clear)
+        g.render_frame()  # frame 2 reuses buffer 0 (after the fence)
+        p2, _ = g.frame_pointer()
+        assert p2 == p0
+        assert np.array_equal(_copy_frame(p1, dev, 320, 240), img1)  # frame 1 intact
+        col2, dep2 = g.readback()
+        img = g.output_image()
+        assert img.device_ptr == p2 and (img.width, img.height) == (320, 240)
+    for (col, want) in ((img0, frames[0]), (img1, frames[1]), (col2, frames[2])):
+        oc, od, _ = oracle.render(want)
+        assert int(np.abs(col.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL
+    assert not np.array_equal(img0, img1)
+    _, od2, _ = oracle.render(frames[2])
+    assert np.array_equal(dep2, od2)
+
+
+def test_group_shares_one_geometry_per_device(oracle):
+    """Caller-owned geometry (tri_group_bind_geometry): every band on device 0 binds the one object;
+    the frame equals the oracle's, and binding back to the group's own copy (after its upload) too."""
+    from trident_raster import raster, scenes
+
+    s = sc.primitives_row(oracle, 320, 240)
+    geo = raster.TriGeometry(0)
+    geo.upload(s.vertices, s.indices, s.meshes)
+    oc, od, _ = oracle.render(s)
+    with raster.TriGroup(s.width, s.height, [0] * 4) as g:
+        g.bind_geometry([geo])
+        g.upload_materials(s.materials)
+        g.upload_skybox(s.skybox)
+        g.set_frame(s.ubo, s.clear)
+        g.set_draws(s.draws)
+        g.render_frame()
+        col, dep = g.readback()
+        assert np.array_equal(dep, od)
+        assert int(np.abs(col.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL
+        g.upload_geometry(s.vertices, s.indices, s.meshes)  # back to the group's own per-device copy
+        g.render_frame()
+        col2, dep2 = g.readback()
+    geo.close()
+    assert np.array_equal(dep2, od) and np.array_equal(col2, col)
+
+
+def test_group_blit_matches_single_context():
+    """tri_group_blit_linear over the assembled frame == tri_blit_linear of the single-context frame."""
+    from trident_raster import raster, scenes
+
+    s = sc.grid_c3(640, 360, 80)
+    with raster.TriRaster(s.width, s.height) as r:
+        scenes.load_scene(r, s)
+        r.render_frame()
+        r.blit(500, 281)
+        want = r.read_present()
+    with raster.TriGroup(s.width, s.height, [0] * 3) as g:
+        scenes.load_scene(g, s)
+        g.render_frame()
+        g.blit(500, 281)
+        got = g.read_present()
+    assert np.array_equal(got, want)
+
+
+@pytest.fixture(scope="module")
+def app_mod():
+    from trident_raster import app
+
+    app.load_library()
+    return app
+
+
+def _shim_scene(app_mod, devices):
+    from trident_raster import scenes
+
+    a = app_mod.TridentApp()
+    if devices:
+        a.set_device_count(len(devices), devices)
+    a.set_camera("editor", (0, 1, 6))
+    a.set_camera("runtime", (2, 2, 5), (-10, 20, 0), fov=50.0, ready=True)
+    a.set_viewport(2, 200, 150)
+    a.set_viewport(1, 320, 240)
+    v, i = scenes.uv_sphere_mesh(20, 28, 1.0)
+    m = a.append_mesh(v, i, base_color=(0.7, 0.8, 0.9, 1), metallic=0.3, roughness=0.5)
+    a.add_mesh_entity("none", m, position=(0, 0.5, 0))
+    a.add_mesh_entity("cube", position=(-1.5, 0, 0), rotation=(10, 20, 30))
+    a.add_light("point", position=(0, 2, 2), color=(1, 0.9, 0.8), intensity=8.0, range=6.0)
+    a.set_present_extent(400, 300)
+    a.draw_frame()
+    a.draw_frame()
+    return a
+
+
+def test_gpu_shim_device_group_equals_single_viewport(app_mod):
+    """Renderer::SetDeviceCount(4, [0, 0, 0, 0]): both viewports render as 4-band groups; every frame,
+    the viewport textures and the presented image equal the one-context shim's, and the geometry went
+    to the (single distinct) device once for both viewports."""
+    from trident_raster import abi, raster
+
+    single = _shim_scene(app_mod, None)
+    multi = _shim_scene(app_mod, [0, 0, 0, 0])
+    for vp, (w, h) in ((1, (320, 240)), (2, (200, 150))):
+        sc_, sd = single.read_pixels(vp, w, h)
+        mc, md = multi.read_pixels(vp, w, h)
+        assert np.array_equal(md, sd) and np.array_equal(mc, sc_)
+        img = multi.viewport_texture(vp)
+        assert (img.width, img.height, img.format, img.device) == (w, h, abi.TRI_FORMAT_B8G8R8A8_UNORM, 0)
+        bgra = raster.copy_device_to_host(img.device_ptr, h * img.pitch_bytes, img.device).reshape(h, w, 4)
+        assert np.array_equal(bgra[..., [2, 1, 0, 3]], mc)
+    assert np.array_equal(multi.read_present(400, 300), single.read_present(400, 300))
+    assert multi.geometry_uploads() == 1
+    multi.set_device_count(1)  # back to one context per viewport: the same frame again
+    multi.draw_frame()
+    mc, md = multi.read_pixels(1, 320, 240)
+    sc_, sd = single.read_pixels(1, 320, 240)
+    assert np.array_equal(md, sd) and np.array_equal(mc, sc_)
+    single.close()
+    multi.close()
+    assert C.sizeof(abi.TriImage) == 32
