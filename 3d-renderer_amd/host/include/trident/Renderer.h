@@ -150,6 +150,12 @@ private:
         uint32_t m_BoneCount = 0;
         ECS::Entity m_Entity = 0;
     };
+    struct SpriteDrawCommand {  // Renderer.h SpriteDrawCommand: one visible SpriteComponent per frame
+        glm::mat4 m_ModelMatrix{1.0f};
+        const SpriteComponent* m_Component = nullptr;
+        const TextureComponent* m_TextureComponent = nullptr;
+        ECS::Entity m_Entity = 0;
+    };
     struct ViewportContext {
         ViewportInfo m_Info{};
         tri_ctx* m_Ctx = nullptr;      // one-device viewport
@@ -168,6 +174,8 @@ private:
     size_t CreatePrimitiveMeshInCache(MeshComponent::PrimitiveType primitiveType);
     void ResolveMaterialTextureSlots(const std::vector<std::string>& textures, size_t offset, size_t count);
     void GatherMeshDraws();
+    void GatherSpriteDraws();
+    void GatherDraws();  // GatherMeshDraws + GatherSpriteDraws (adds the sprite quad to the geometry once)
     void PrepareBonePaletteBuffer();
     void UpdateUniformBuffer(const Camera* camera, tri_global_ubo& out) const;
     void BuildDrawList(std::vector<tri_draw>& out) const;
@@ -184,6 +192,12 @@ private:
     std::vector<Geometry::Material> m_Materials;
     std::vector<MeshDrawInfo> m_MeshDrawInfo;
     std::vector<MeshDrawCommand> m_MeshDrawCommands;
+    std::vector<SpriteDrawCommand> m_SpriteDrawList;
+    // The sprite quad (BuildSpriteGeometry, Renderer.cpp:2853-2890): the reference keeps it in its own
+    // vertex/index buffer; here it is one more mesh range after the cached meshes, appended to the
+    // device geometry the first time a sprite is drawn (mesh index m_MeshDrawInfo.size()).
+    bool m_HasSpriteGeometry = false;
+    MeshDrawInfo m_SpriteDrawInfo{};
     static constexpr uint32_t s_MaxBonesPerSkeleton = 128;  // Renderer.h:291
     std::vector<float> m_BonePalette;  // PrepareBonePaletteBuffer's scratch: per-draw palettes, back to back
     size_t m_PrimitiveMeshIndices[3] = {SIZE_MAX, SIZE_MAX, SIZE_MAX};

@@ -115,6 +115,24 @@ struct LightComponent {
     bool m_Reserved1 = false;
 };
 
+// SpriteComponent (ECS/Components/SpriteComponent.h:17-43): a camera-independent unit quad drawn with the
+// Default pipeline after the meshes (Renderer.cpp:2996-3089, :5154-5157). The atlas / animation fields are
+// authoring data the renderer does not read yet (the reference's DrawSprites ignores them too).
+struct SpriteComponent {
+    std::string m_TextureId{};
+    glm::vec4 m_TintColor{1.0f};
+    glm::vec2 m_UVScale{1.0f};
+    glm::vec2 m_UVOffset{0.0f};
+    float m_TilingFactor{1.0f};
+    bool m_Visible{true};
+    bool m_UseMaterialOverride{false};
+    std::string m_MaterialOverrideId{};
+    int32_t m_AtlasTiles[2]{1, 1};
+    int m_AtlasIndex{0};
+    float m_AnimationSpeed{0.0f};
+    float m_SortOffset{0.0f};
+};
+
 // AnimationComponent (ECS/Components/AnimationComponent.h:29-73), the part the renderer reads: the
 // skinning palette the CPU animation system writes each frame (m_BoneMatrices, column-major mat4s).
 // Clip/skeleton bookkeeping stays with the animation system, which is outside the hot path.

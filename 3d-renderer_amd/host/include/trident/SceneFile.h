@@ -2,9 +2,9 @@
 // :288-430 SerializeEntity, :432-961 DeserializeEntity, :963-1081 RebuildMeshAssetsFromComponents)
 // and Forge's model import (ApplicationLayer::ImportDroppedAssets, ApplicationLayer.cpp:815-1031),
 // restricted to the components the draw path reads: Tag, UUID, Transform, Camera, Mesh (with the
-// SourceAsset provenance that rebuilds geometry on load), Texture and Light. Sprite, Animation and
-// Script lines are recognised and skipped (their subsystems are outside the hot path), including an
-// Animation component's trailing AnimationBones line.
+// SourceAsset provenance that rebuilds geometry on load), Sprite (Scene.cpp:343-367, :549-779), Texture
+// and Light. Animation and Script lines are recognised and skipped (their subsystems are outside the hot
+// path), including an Animation component's trailing AnimationBones line.
 #pragma once
 
 #include <cstdint>

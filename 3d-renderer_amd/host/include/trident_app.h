@@ -37,6 +37,15 @@ int trident_app_upload_texture(trident_app* app, const char* path, const uint8_t
 int trident_app_add_mesh_entity(trident_app* app, int primitive, uint32_t mesh_index, const float position[3],
                                 const float rotation_deg[3], const float scale[3], uint32_t* entity);
 int trident_app_set_entity_texture(trident_app* app, uint32_t entity, const char* texture_path);
+/* Entity with Transform + SpriteComponent (tint, UV scale / offset, tiling; NULL = the component's
+ * defaults); drawn after the meshes (GatherSpriteDraws / DrawSprites, Renderer.cpp:2996-3089). A texture
+ * goes on with trident_app_set_entity_texture. */
+int trident_app_add_sprite_entity(trident_app* app, const float position[3], const float rotation_deg[3],
+                                  const float scale[3], const float tint[4], const float uv_scale[2],
+                                  const float uv_offset[2], float tiling, uint32_t* entity);
+int trident_app_set_sprite_visible(trident_app* app, uint32_t entity, int visible);
+/* SpriteComponent of an entity: tint[4], uv_scale[2], uv_offset[2], tiling, visible. */
+int trident_app_entity_sprite(trident_app* app, uint32_t entity, float out[10]);
 int trident_app_set_entity_transform(trident_app* app, uint32_t entity, const float position[3],
                                      const float rotation_deg[3], const float scale[3]);
 int trident_app_set_entity_visible(trident_app* app, uint32_t entity, int visible);

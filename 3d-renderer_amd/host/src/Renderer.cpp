@@ -46,6 +46,31 @@ Geometry::Mesh BuildPrimitiveQuadMesh() {
     return mesh;
 }
 
+// BuildSpriteGeometry (Renderer.cpp:2853-2890): a unit quad facing -Z with indices {0, 2, 1, 0, 3, 2}
+// (the opposite winding of the quad primitive: a sprite seen from +Z is back-facing and culled, as in
+// the reference, whose Default pipeline culls BACK for sprites too).
+Geometry::Mesh BuildSpriteQuadMesh() {
+    Geometry::Mesh mesh;
+    Vertex v[4]{};
+    v[0].Position = {-0.5f, -0.5f, 0.0f};
+    v[1].Position = {0.5f, -0.5f, 0.0f};
+    v[2].Position = {0.5f, 0.5f, 0.0f};
+    v[3].Position = {-0.5f, 0.5f, 0.0f};
+    for (Vertex& it : v) {
+        it.Normal = {0.0f, 0.0f, -1.0f};
+        it.Tangent = {1.0f, 0.0f, 0.0f};
+        it.Bitangent = {0.0f, 1.0f, 0.0f};
+        it.Color = {1.0f, 1.0f, 1.0f};
+    }
+    v[0].TexCoord = {0.0f, 0.0f};
+    v[1].TexCoord = {1.0f, 0.0f};
+    v[2].TexCoord = {1.0f, 1.0f};
+    v[3].TexCoord = {0.0f, 1.0f};
+    mesh.Vertices.assign(v, v + 4);
+    mesh.Indices = {0, 2, 1, 0, 3, 2};
+    return mesh;
+}
+
 Geometry::Mesh BuildPrimitiveCubeMesh() {
     struct Face {
         glm::vec3 n, t, b;
@@ -403,6 +428,17 @@ void Renderer::UploadMeshFromCache() {  // Renderer.cpp:1965-2116
         firstIndex += info.m_IndexCount;
         baseVertex += static_cast<int32_t>(mesh.Vertices.size());
     }
+    if (m_HasSpriteGeometry) {  // after every cached mesh, outside m_MeshDrawInfo (no MeshComponent reaches it)
+        const Geometry::Mesh quad = BuildSpriteQuadMesh();
+        const size_t v0 = m_VertexBuffer.size();
+        m_VertexBuffer.resize(v0 + quad.Vertices.size());
+        std::memcpy(m_VertexBuffer.data() + v0, quad.Vertices.data(), quad.Vertices.size() * sizeof(Vertex));
+        m_IndexBuffer.insert(m_IndexBuffer.end(), quad.Indices.begin(), quad.Indices.end());
+        m_SpriteDrawInfo.m_FirstIndex = firstIndex;
+        m_SpriteDrawInfo.m_IndexCount = static_cast<uint32_t>(quad.Indices.size());
+        m_SpriteDrawInfo.m_BaseVertex = baseVertex;
+        m_SpriteDrawInfo.m_MaterialIndex = -1;
+    }
     m_MeshDrawCommands.clear();
     if (m_Registry) {
         for (ECS::Entity e : m_Registry->GetEntities()) {
@@ -417,7 +453,7 @@ void Renderer::UploadMeshFromCache() {  // Renderer.cpp:1965-2116
         }
     }
     m_ModelCount = m_GeometryCache.size();
-    m_TriangleCount = m_IndexBuffer.size() / 3;
+    m_TriangleCount = firstIndex / 3;  // the cached meshes' triangles (the sprite quad is not a model)
     ++m_GeometryGeneration;
     ++m_MaterialGeneration;
     m_IsUploadingMeshes = false;
@@ -517,6 +553,42 @@ void Renderer::GatherMeshDraws() {  // Renderer.cpp:2910-2994
     }
 }
 
+void Renderer::GatherSpriteDraws() {  // Renderer.cpp:2996-3042
+    m_SpriteDrawList.clear();
+    if (!m_Registry) return;
+    for (ECS::Entity e : m_Registry->GetEntities()) {
+        if (!m_Registry->HasComponent<Transform>(e) || !m_Registry->HasComponent<SpriteComponent>(e)) continue;
+        SpriteComponent& sprite = m_Registry->GetComponent<SpriteComponent>(e);
+        if (!sprite.m_Visible) continue;
+        TextureComponent* tex = nullptr;
+        if (m_Registry->HasComponent<TextureComponent>(e)) {
+            tex = &m_Registry->GetComponent<TextureComponent>(e);
+            if (tex->m_IsDirty || tex->m_TextureSlot < 0) {
+                tex->m_TextureSlot = ResolveTextureSlot(tex->m_TexturePath);
+                tex->m_IsDirty = false;
+            }
+        }
+        SpriteDrawCommand cmd;
+        cmd.m_ModelMatrix = ComposeTransform(m_Registry->GetComponent<Transform>(e));
+        cmd.m_Component = &sprite;
+        cmd.m_TextureComponent = tex;
+        cmd.m_Entity = e;
+        m_SpriteDrawList.push_back(cmd);
+    }
+}
+
+void Renderer::GatherDraws() {
+    GatherMeshDraws();
+    GatherSpriteDraws();
+    if (!m_SpriteDrawList.empty() && !m_HasSpriteGeometry) {
+        // first sprite: the quad joins the device geometry (the reference built its own buffer at Init);
+        // the upload clears the mesh commands, which are gathered again (no texture slot changes)
+        m_HasSpriteGeometry = true;
+        UploadMeshFromCache();
+        GatherMeshDraws();
+    }
+}
+
 // Renderer.cpp:3168-3245: each animated draw gets a slice [offset, offset + count) of one palette
 // (count clamped to s_MaxBonesPerSkeleton); draws without a palette keep offset 0 / count 0.
 void Renderer::PrepareBonePaletteBuffer() {
@@ -562,6 +634,27 @@ void Renderer::BuildDrawList(std::vector<tri_draw>& out) const {  // Renderer.cp
         pc.material_index = info.m_MaterialIndex;
         pc.bone_offset = static_cast<int32_t>(cmd.m_BoneOffset);  // :5145-5146
         pc.bone_count = static_cast<int32_t>(cmd.m_BoneCount);
+        out.push_back(d);
+    }
+    if (!m_HasSpriteGeometry) return;
+    for (const SpriteDrawCommand& cmd : m_SpriteDrawList) {  // DrawSprites, Renderer.cpp:3044-3089
+        if (!cmd.m_Component) continue;
+        const SpriteComponent& sp = *cmd.m_Component;
+        tri_draw d;
+        std::memset(&d, 0, sizeof d);
+        d.mesh_index = static_cast<uint32_t>(m_MeshDrawInfo.size());  // the sprite quad's range
+        tri_push_constant& pc = d.pc;
+        CopyMat(cmd.m_ModelMatrix, pc.model);
+        pc.tint[0] = sp.m_TintColor.x; pc.tint[1] = sp.m_TintColor.y;
+        pc.tint[2] = sp.m_TintColor.z; pc.tint[3] = sp.m_TintColor.w;
+        pc.texture_scale[0] = sp.m_UVScale.x; pc.texture_scale[1] = sp.m_UVScale.y;
+        pc.texture_offset[0] = sp.m_UVOffset.x; pc.texture_offset[1] = sp.m_UVOffset.y;
+        pc.tiling_factor = sp.m_TilingFactor;
+        pc.use_material_override = sp.m_UseMaterialOverride ? 1 : 0;
+        pc.sort_bias = sp.m_SortOffset;
+        pc.texture_slot = (cmd.m_TextureComponent && cmd.m_TextureComponent->m_TextureSlot >= 0)
+                              ? cmd.m_TextureComponent->m_TextureSlot : 0;
+        pc.material_index = -1;  // RenderablePushConstant default (RenderData.h:25)
         out.push_back(d);
     }
 }
@@ -649,6 +742,17 @@ bool Renderer::BuildShadowConfig(tri_shadow_config& out) {
             }
         }
     }
+    for (const SpriteDrawCommand& cmd : m_SpriteDrawList) {  // sprites cast too: their quad's corners
+        if (!m_HasSpriteGeometry) break;
+        for (int k = 0; k < 4; ++k) {
+            const glm::vec4 c{(k & 1) ? 0.5f : -0.5f, (k & 2) ? 0.5f : -0.5f, 0.0f, 1.0f};
+            const glm::vec4 w = cmd.m_ModelMatrix * c;
+            for (int ax = 0; ax < 3; ++ax) {
+                lo[ax] = std::min(lo[ax], w[ax]);
+                hi[ax] = std::max(hi[ax], w[ax]);
+            }
+        }
+    }
     if (lo.x > hi.x) return false;
     glm::vec3 dir{-0.5f, -1.0f, -0.3f};
     if (glm::dot(sun->m_Direction, sun->m_Direction) > 0.0001f) dir = sun->m_Direction;
@@ -700,6 +804,9 @@ std::vector<tri_mesh_range> Renderer::GetMeshRanges() const {
     for (size_t i = 0; i < ranges.size(); ++i)
         ranges[i] = {m_MeshDrawInfo[i].m_FirstIndex, m_MeshDrawInfo[i].m_IndexCount, m_MeshDrawInfo[i].m_BaseVertex,
                      m_MeshDrawInfo[i].m_MaterialIndex};
+    if (m_HasSpriteGeometry)
+        ranges.push_back({m_SpriteDrawInfo.m_FirstIndex, m_SpriteDrawInfo.m_IndexCount, m_SpriteDrawInfo.m_BaseVertex,
+                          m_SpriteDrawInfo.m_MaterialIndex});
     return ranges;
 }
 
@@ -803,7 +910,7 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
 bool Renderer::BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::vector<tri_draw>& draws) {
     auto it = m_Viewports.find(viewportId);
     if (it == m_Viewports.end()) return false;
-    GatherMeshDraws();
+    GatherDraws();
     PrepareBonePaletteBuffer();
     UpdateUniformBuffer(GetActiveCamera(it->second), ubo);
     BuildDrawList(draws);
@@ -813,7 +920,7 @@ bool Renderer::BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::v
 void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     const auto t0 = std::chrono::steady_clock::now();
     if (!m_Initialised || m_Shutdown) return;
-    GatherMeshDraws();
+    GatherDraws();
     PrepareBonePaletteBuffer();
     std::vector<tri_draw> draws;
     BuildDrawList(draws);

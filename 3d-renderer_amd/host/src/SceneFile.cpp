@@ -32,6 +32,62 @@ std::string ExtractQuotedToken(const std::string& line) {
 
 bool StartsWith(const std::string& s, const char* p) { return s.rfind(p, 0) == 0; }
 
+// Scene.cpp:549-779: each "Key=" token runs to the next space; an absent token keeps the default, a
+// malformed one warns and keeps what was parsed before the failure (istream semantics).
+std::string SpriteToken(const std::string& line, const std::string& key) {
+    const size_t k = line.find(key);
+    if (k == std::string::npos) return {};
+    const size_t a = k + key.size();
+    size_t b = line.find(' ', a);
+    if (b == std::string::npos) b = line.size();
+    return line.substr(a, b - a);
+}
+
+template <typename T>
+bool ParseList(const std::string& v, T* out, int n) {  // "x,y[,z,w]"
+    if (v.empty()) return true;
+    std::istringstream ts(v);
+    for (int i = 0; i < n; ++i) {
+        char comma = ',';
+        if (i > 0 && (!(ts >> comma) || comma != ',')) return false;
+        if (!(ts >> out[i])) return false;
+    }
+    return true;
+}
+
+bool ParseBoolToken(const std::string& v, bool& out) {
+    if (v.empty()) return true;
+    std::istringstream ts(v);
+    if (ts >> std::boolalpha >> out) return true;
+    std::istringstream ti(v);
+    int x = 0;
+    if (ti >> x) {
+        out = x != 0;
+        return true;
+    }
+    return false;
+}
+
+SpriteComponent ParseSprite(const std::string& line) {
+    SpriteComponent sp{};
+    sp.m_TextureId = ExtractQuotedToken(line);
+    auto warn = [](const char* what, const std::string& tok) { Warn(std::string("failed to parse sprite ") + what + " token '" + tok + "'"); };
+    std::string t;
+    if (!ParseList(t = SpriteToken(line, "Tint="), &sp.m_TintColor.x, 4)) warn("tint", t);
+    if (!ParseList(t = SpriteToken(line, "UVScale="), &sp.m_UVScale.x, 2)) warn("UVScale", t);
+    if (!ParseList(t = SpriteToken(line, "UVOffset="), &sp.m_UVOffset.x, 2)) warn("UVOffset", t);
+    if (!ParseList(t = SpriteToken(line, "Tiling="), &sp.m_TilingFactor, 1)) warn("tiling", t);
+    if (!ParseBoolToken(t = SpriteToken(line, "Visible="), sp.m_Visible)) warn("visibility", t);
+    if (!ParseBoolToken(t = SpriteToken(line, "UseMaterialOverride="), sp.m_UseMaterialOverride)) warn("material override", t);
+    const size_t m = line.find("Material=");
+    if (m != std::string::npos) sp.m_MaterialOverrideId = ExtractQuotedToken(line.substr(m));
+    if (!ParseList(t = SpriteToken(line, "AtlasTiles="), sp.m_AtlasTiles, 2)) warn("atlas tiles", t);
+    if (!ParseList(t = SpriteToken(line, "AtlasIndex="), &sp.m_AtlasIndex, 1)) warn("atlas index", t);
+    if (!ParseList(t = SpriteToken(line, "AnimationSpeed="), &sp.m_AnimationSpeed, 1)) warn("animation speed", t);
+    if (!ParseList(t = SpriteToken(line, "SortOffset="), &sp.m_SortOffset, 1)) warn("sort offset", t);
+    return sp;
+}
+
 }  // namespace
 
 Scene::Scene(ECS::Registry& registry, Renderer* renderer, std::string name)
@@ -110,6 +166,17 @@ void Scene::SerializeEntity(std::ostream& s, ECS::Entity e) const {  // Scene.cp
             s << ' ' << "SourceAsset=\"" << EscapeString(m.m_SourceAssetPath) << "\"" << ' ' << "SourceMeshIndex="
               << m.m_SourceMeshIndex;
         s << "\n";
+    }
+    if (m_Registry.HasComponent<SpriteComponent>(e)) {  // Scene.cpp:343-367
+        const SpriteComponent& sp = m_Registry.GetComponent<SpriteComponent>(e);
+        s << "Sprite " << "Texture=\"" << EscapeString(sp.m_TextureId) << "\" " << "Tint=" << sp.m_TintColor.x << ','
+          << sp.m_TintColor.y << ',' << sp.m_TintColor.z << ',' << sp.m_TintColor.w << ' ' << "UVScale=" << sp.m_UVScale.x
+          << ',' << sp.m_UVScale.y << ' ' << "UVOffset=" << sp.m_UVOffset.x << ',' << sp.m_UVOffset.y << ' '
+          << "Tiling=" << sp.m_TilingFactor << ' ' << "Visible=" << sp.m_Visible << ' '
+          << "UseMaterialOverride=" << sp.m_UseMaterialOverride << ' ';
+        if (!sp.m_MaterialOverrideId.empty()) s << "Material=\"" << EscapeString(sp.m_MaterialOverrideId) << "\" ";
+        s << "AtlasTiles=" << sp.m_AtlasTiles[0] << ',' << sp.m_AtlasTiles[1] << ' ' << "AtlasIndex=" << sp.m_AtlasIndex
+          << ' ' << "AnimationSpeed=" << sp.m_AnimationSpeed << ' ' << "SortOffset=" << sp.m_SortOffset << "\n";
     }
     if (m_Registry.HasComponent<TextureComponent>(e)) {
         const TextureComponent& t = m_Registry.GetComponent<TextureComponent>(e);
@@ -239,7 +306,11 @@ void Scene::DeserializeEntity(std::istream& s) {  // Scene.cpp:432-961 (ids in t
             if (bones > 0) std::getline(s, line);
             continue;
         }
-        if (StartsWith(line, "Sprite ") || StartsWith(line, "Script ")) continue;  // outside the draw path
+        if (StartsWith(line, "Sprite ")) {
+            m_Registry.AddComponent<SpriteComponent>(e, ParseSprite(line));
+            continue;
+        }
+        if (StartsWith(line, "Script ")) continue;  // outside the draw path
         Warn("unknown token while deserialising entity: '" + line + "'");
     }
 }

@@ -121,6 +121,45 @@ int trident_app_add_mesh_entity(trident_app* app, int primitive, uint32_t mesh_i
     });
 }
 
+int trident_app_add_sprite_entity(trident_app* app, const float position[3], const float rotation_deg[3],
+                                  const float scale[3], const float tint[4], const float uv_scale[2],
+                                  const float uv_offset[2], float tiling, uint32_t* entity) {
+    return Guard(app, [&] {
+        const ECS::Entity e = app->registry.CreateEntity();
+        Transform& t = app->registry.AddComponent<Transform>(e);
+        t.Position = V3(position, glm::vec3{0.0f});
+        t.Rotation = V3(rotation_deg, glm::vec3{0.0f});
+        t.Scale = V3(scale, glm::vec3{1.0f});
+        SpriteComponent& sp = app->registry.AddComponent<SpriteComponent>(e);
+        if (tint) sp.m_TintColor = {tint[0], tint[1], tint[2], tint[3]};
+        if (uv_scale) sp.m_UVScale = {uv_scale[0], uv_scale[1]};
+        if (uv_offset) sp.m_UVOffset = {uv_offset[0], uv_offset[1]};
+        sp.m_TilingFactor = tiling;
+        if (entity) *entity = e;
+        return TRI_OK;
+    });
+}
+
+int trident_app_set_sprite_visible(trident_app* app, uint32_t entity, int visible) {
+    return Guard(app, [&] {
+        if (!app->registry.HasComponent<SpriteComponent>(entity)) return TRI_E_INVALID;
+        app->registry.GetComponent<SpriteComponent>(entity).m_Visible = visible != 0;
+        return TRI_OK;
+    });
+}
+
+int trident_app_entity_sprite(trident_app* app, uint32_t entity, float out[10]) {
+    return Guard(app, [&] {
+        if (!app->registry.HasComponent<SpriteComponent>(entity)) return TRI_E_INVALID;
+        const SpriteComponent& sp = app->registry.GetComponent<SpriteComponent>(entity);
+        const float v[10] = {sp.m_TintColor.x, sp.m_TintColor.y, sp.m_TintColor.z, sp.m_TintColor.w, sp.m_UVScale.x,
+                             sp.m_UVScale.y, sp.m_UVOffset.x, sp.m_UVOffset.y, sp.m_TilingFactor,
+                             sp.m_Visible ? 1.0f : 0.0f};
+        std::memcpy(out, v, sizeof v);
+        return TRI_OK;
+    });
+}
+
 int trident_app_set_entity_texture(trident_app* app, uint32_t entity, const char* texture_path) {
     return Guard(app, [&] {
         TextureComponent& t = app->registry.AddComponent<TextureComponent>(entity);

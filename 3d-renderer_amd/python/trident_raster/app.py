@@ -34,6 +34,10 @@ _APP_FUNCTIONS = [
     ("trident_app_set_light_shadow_caster", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
     ("trident_app_set_shadow_map_size", C.c_int, [C.c_void_p, C.c_uint32]),
     ("trident_app_set_device_count", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    ("trident_app_add_sprite_entity", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                                C.c_void_p, C.c_float, C.POINTER(C.c_uint32)]),
+    ("trident_app_set_sprite_visible", C.c_int, [C.c_void_p, C.c_uint32, C.c_int]),
+    ("trident_app_entity_sprite", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_float * 10)]),
     ("trident_app_shadow_config", C.c_int, [C.c_void_p, C.POINTER(abi.TriShadowConfig), C.POINTER(C.c_int)]),
     ("trident_app_geometry_uploads", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64)]),
     ("trident_load_image", C.c_int, [C.c_char_p, C.c_int, C.c_void_p, C.c_uint64, C.POINTER(C.c_uint32),
@@ -132,6 +136,27 @@ class TridentApp:
         _check(self._lib.trident_app_add_mesh_entity(self._h, PRIMITIVE[primitive], mesh_index, _vec(position),
                                                      _vec(rotation), _vec(scale), C.byref(e)), "add_mesh_entity")
         return e.value
+
+    def add_sprite_entity(self, position=(0, 0, 0), rotation=(0, 0, 0), scale=(1, 1, 1), tint=(1, 1, 1, 1),
+                          uv_scale=(1, 1), uv_offset=(0, 0), tiling=1.0):
+        """Transform + SpriteComponent (drawn after the meshes, Renderer.cpp:2996-3089)."""
+        f = lambda v: (C.c_float * len(v))(*[float(x) for x in v])  # noqa: E731
+        e = C.c_uint32()
+        _check(self._lib.trident_app_add_sprite_entity(self._h, f(position), f(rotation), f(scale), f(tint), f(uv_scale),
+                                                       f(uv_offset), float(tiling), C.byref(e)), "add_sprite_entity")
+        return e.value
+
+    def set_sprite_visible(self, entity, visible):
+        _check(self._lib.trident_app_set_sprite_visible(self._h, entity, 1 if visible else 0), "set_sprite_visible")
+
+    def entity_sprite(self, entity):
+        """SpriteComponent: {tint, uv_scale, uv_offset, tiling, visible}, or None."""
+        out = (C.c_float * 10)()
+        if self._lib.trident_app_entity_sprite(self._h, entity, C.byref(out)) != 0:
+            return None
+        v = list(out)
+        return {"tint": tuple(v[0:4]), "uv_scale": tuple(v[4:6]), "uv_offset": tuple(v[6:8]), "tiling": v[8],
+                "visible": bool(v[9])}
 
     def set_entity_texture(self, entity, path):
         _check(self._lib.trident_app_set_entity_texture(self._h, entity, path.encode()), "set_entity_texture")

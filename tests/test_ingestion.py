@@ -268,7 +268,8 @@ def test_scene_save_load_round_trip(app_mod, tmp_path):
 
 def test_scene_reference_text_format(app_mod, tmp_path):
     """A file in the reference's own layout (Scene.cpp:288-430), with component lines this path
-    does not own (Sprite, Animation + AnimationBones, Script) that must be skipped cleanly."""
+    does not own (Animation + AnimationBones, Script) that must be skipped cleanly, and a Sprite line
+    (Scene.cpp:549-779) that is parsed and drawn after the meshes."""
     (tmp_path / "tri.obj").write_text("v -1 0 0\nv 1 0 0\nv 0 1 0\nf 1 2 3\n")
     text = f"""# Trident Scene
 Scene "Imported"
@@ -312,7 +313,10 @@ EndEntity
     assert ubo.light_counts[1] == 1  # the enabled point light
     assert ubo.light_counts[0] == 0  # the sun is disabled; a point light exists, so no fallback (:5908)
     _, draws = a.frame_inputs(2)
-    assert sorted(d.mesh_index for d in draws) == [0, 1]
+    # the two meshes, then entity 9's sprite over the sprite quad (the mesh range after the cached meshes)
+    assert [d.mesh_index for d in draws] == [0, 1, 2]
+    assert a.entity_sprite(1) == {"tint": (1, 1, 1, 1), "uv_scale": (1, 1), "uv_offset": (0, 0), "tiling": 1.0,
+                                  "visible": True}
 
 
 # ---- GPU: imported scenes render like the oracle on the shim's inputs --------------------------
