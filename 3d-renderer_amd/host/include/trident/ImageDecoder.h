@@ -1,4 +1,4 @@
-// ImageDecoder.h — PNG decoding with stb_image's observable semantics, for the texture and skybox
+// ImageDecoder.h — PNG (and JPEG, JpegDecoder.cpp) decoding with stb_image's observable semantics, for the texture and skybox
 // loaders (TextureLoader.cpp:290-304 loads 2D textures with stbi_load(..., STBI_rgb_alpha) after
 // stbi_set_flip_vertically_on_load(true); LoadFromFileList, :773-830, loads cube faces unflipped).
 // stb is an un-vendored submodule of the reference, so its PNG path is restated here on zlib:
@@ -25,6 +25,13 @@ bool DecodePng(const std::string& bytes, int& width, int& height, std::vector<ui
 
 // True when `bytes` starts with the PNG signature.
 bool IsPng(const std::string& bytes);
+
+// Decodes a baseline or progressive JPEG (JpegDecoder.cpp: stb_image's JPEG path restated) into
+// top-to-bottom RGBA8 rows. Returns false (with `error` set) on malformed or unsupported input.
+bool DecodeJpeg(const std::string& bytes, int& width, int& height, std::vector<uint8_t>& rgba, std::string& error);
+
+// True when `bytes` starts with an SOI marker followed by another marker.
+bool IsJpeg(const std::string& bytes);
 
 void FlipRowsVertically(std::vector<uint8_t>& rgba, int width, int height);
 

@@ -704,7 +704,7 @@ ModelData ModelLoader::Load(const std::string& filePath) {
 }
 
 namespace {
-// One image file -> top-to-bottom RGBA8 rows (PNG or PPM/PAM), unflipped. Width 0 on failure.
+// One image file -> top-to-bottom RGBA8 rows (PNG, JPEG or PPM/PAM), unflipped. Width 0 on failure.
 TextureData DecodeImageFile(const std::string& filePath) {
     TextureData t;
     std::string s;
@@ -716,6 +716,15 @@ TextureData DecodeImageFile(const std::string& filePath) {
         std::string err;
         if (!DecodePng(s, t.Width, t.Height, t.Pixels, err)) {
             LogError(("PNG decode failed: " + err).c_str(), filePath);
+            return TextureData{};
+        }
+        t.Channels = 4;
+        return t;
+    }
+    if (IsJpeg(s)) {
+        std::string err;
+        if (!DecodeJpeg(s, t.Width, t.Height, t.Pixels, err)) {
+            LogError(("JPEG decode failed: " + err).c_str(), filePath);
             return TextureData{};
         }
         t.Channels = 4;
