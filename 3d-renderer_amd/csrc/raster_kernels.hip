@@ -2214,311 +2214,6 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
 #endif
 }
 
-// ------------------------------------------------------------------------------------------
-// Attribute planes (fast build, single-draw solid frames at 32x32 bins: k_raster_plain<false, 5, true>).
-// After coverage, every queue entry's triangle is set up ONCE into a bin-local table in LDS: the
-// perspective denominator Q = q0 + q1 + q2 and, for each of the 9 varyings the fragment shader reads
-// (world xyz, normal xyz, vertex colour), the numerator N = q0 v0 + q1 v1 + q2 v2, both as planes in the
-// pixel-centre offsets (dx, dy) from the triangle's vertex 0 -- the offsets and barycentric numerators
-// q_k of the fast build's fast_weights, so a pixel's attribute N / Q is the same perspective-correct
-// interpolation, re-associated: two FMAs per plane and one reciprocal per pixel instead of the per-pixel
-// index -> snapped-vertex -> varying gathers, triangle set-up and three-weight interpolation. The planes
-// depend on the triangle only (not on the bin), so every bin, row band and chunk gives a pixel the same bits.
-// A pixel finds its entry through an LDS hash of its visibility key's primitive bits (inserted by each
-// entry's coverage lane), resolved once per pixel into a register while the key tile is live; the table
-// then overwrites the key tile. A bin with more entries than the table holds is shaded in chunks of
-// kPlaneCap entries, each wave compacting the pixels of the current chunk into a lane-dense list.
-// ------------------------------------------------------------------------------------------
-#ifndef TRI_PLANES
-#define TRI_PLANES 1
-#endif
-#ifndef TRI_PLANE_CAP
-#define TRI_PLANE_CAP 128
-#endif
-constexpr int kPlaneCap = TRI_PLANE_CAP;  // table rows (queue entries) per chunk
-static_assert(kPlaneCap <= 128, "chunk-local rows must fit the 7 bits of a pixel-list entry");
-constexpr int kPlaneHash = 1024;          // hash slots (a bin beyond kPlaneHashMax entries shades per pixel)
-constexpr uint32_t kPlaneHashMax = 896;
-constexpr int kPlaneF4 = 8;               // float4 per table row
-constexpr int kPlaneBigQ = 256;           // large-triangle queue (more: the lane walks it itself)
-struct PlaneCovLds {
-    uint64_t keys[1024];
-    unsigned long long hkv[kPlaneHash];  // {key low word, entry}, ~0 = empty
-};
-union PlaneLds {
-    PlaneCovLds cov;                     // coverage: key tile + primitive -> entry hash
-    float4 table[kPlaneCap * kPlaneF4];  // shading: attribute planes of one chunk of entries
-    float lut[512];                      // skybox pass: the sRGB decode table
-};
-
-__device__ __forceinline__ uint32_t plane_hash(uint32_t low) { return (low * 2654435761u) >> (32 - 10); }
-
-// Table row of queue entry e: {X0, Y0, Qx, Qy}, then per varying {v0, Nx, Ny} (9 of them) in the order
-// world xyz, normal xyz, colour rgb; Q(dx, dy) = 1 + Qx dx + Qy dy, N(dx, dy) = v0 + Nx dx + Ny dy.
-__device__ __forceinline__ void plane_row(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e, float4* row) {
-#pragma clang fp contract(fast)
-    const FetchBufs fb = fetch_bufs(fp, b);
-    TriRec r;
-    uint32_t v0, v1, v2;
-    if (e & TRI_ENTRY_CLIPPED) {
-        r = load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
-        v0 = r.v[0]; v1 = r.v[1]; v2 = r.v[2];
-    } else {
-        uint32_t sl[3], d;
-        prim_slots<true>(fp, b, e, sl, d);
-        const TriSnap a0 = ld_snap_xyw(fb, sl[0]), a1 = ld_snap_xyw(fb, sl[1]), a2 = ld_snap_xyw(fb, sl[2]);
-        r = rec_from_snaps(e, sl, a0, a1, a2);
-        v0 = sl[0]; v1 = sl[2]; v2 = sl[1];
-    }
-    const V4 p0 = ld_vary(fb, v0, 0), n0 = ld_vary(fb, v0, 1), c0 = ld_vary(fb, v0, 2);
-    const V4 p1 = ld_vary(fb, v1, 0), n1 = ld_vary(fb, v1, 1), c1 = ld_vary(fb, v1, 2);
-    const V4 p2 = ld_vary(fb, v2, 0), n2 = ld_vary(fb, v2, 1), c2 = ld_vary(fb, v2, 2);
-    const FastW c = fast_coefs(r);
-    auto sx = [&](float a, float bb, float cc) { return __builtin_fmaf(c.a2, cc, __builtin_fmaf(c.a1, bb, c.a0 * a)); };
-    auto sy = [&](float a, float bb, float cc) { return __builtin_fmaf(c.b2, cc, __builtin_fmaf(c.b1, bb, c.b0 * a)); };
-    row[0] = make_float4(__int_as_float(r.X[0]), __int_as_float(r.Y[0]), (c.a0 + c.a1) + c.a2, (c.b0 + c.b1) + c.b2);
-    row[1] = make_float4(p0.x, sx(p0.x, p1.x, p2.x), sy(p0.x, p1.x, p2.x), p0.y);
-    row[2] = make_float4(sx(p0.y, p1.y, p2.y), sy(p0.y, p1.y, p2.y), p0.z, sx(p0.z, p1.z, p2.z));
-    row[3] = make_float4(sy(p0.z, p1.z, p2.z), n0.x, sx(n0.x, n1.x, n2.x), sy(n0.x, n1.x, n2.x));
-    row[4] = make_float4(n0.y, sx(n0.y, n1.y, n2.y), sy(n0.y, n1.y, n2.y), n0.z);
-    row[5] = make_float4(sx(n0.z, n1.z, n2.z), sy(n0.z, n1.z, n2.z), c0.x, sx(c0.x, c1.x, c2.x));
-    row[6] = make_float4(sy(c0.x, c1.x, c2.x), c0.y, sx(c0.y, c1.y, c2.y), sy(c0.y, c1.y, c2.y));
-    row[7] = make_float4(c0.z, sx(c0.z, c1.z, c2.z), sy(c0.z, c1.z, c2.z), 0.0f);
-}
-
-// Shade pixel (px, py) from its table row t: the fragment of Default.frag, BGRA8 out.
-template <typename Row>
-__device__ __forceinline__ uint32_t plane_shade(const TriFrameParams& fp, const Row& t, int32_t px, int32_t py) {
-#pragma clang fp contract(fast)
-    const float4 t0 = t[0], t1 = t[1], t2 = t[2], t3 = t[3], t4 = t[4], t5 = t[5], t6 = t[6], t7 = t[7];
-    const float dx = (float)(256 * px + 128 - __float_as_int(t0.x)), dy = (float)(256 * py + 128 - __float_as_int(t0.y));
-    auto ev = [&](float v, float nx, float ny) { return __builtin_fmaf(ny, dy, __builtin_fmaf(nx, dx, v)); };
-    const float iq = frcp(ev(1.0f, t0.z, t0.w));
-    Frag f;
-    f.wx = ev(t1.x, t1.y, t1.z) * iq;
-    f.wy = ev(t1.w, t2.x, t2.y) * iq;
-    f.wz = ev(t2.z, t2.w, t3.x) * iq;
-    f.nx = ev(t3.y, t3.z, t3.w) * iq;
-    f.ny = ev(t4.x, t4.y, t4.z) * iq;
-    f.nz = ev(t4.w, t5.x, t5.y) * iq;
-    f.cx = ev(t5.z, t5.w, t6.x) * iq;
-    f.cy = ev(t6.y, t6.z, t6.w) * iq;
-    f.cz = ev(t7.x, t7.y, t7.z) * iq;
-    f.u = 0.0f; f.v = 0.0f;
-    f.sx = fp.sc.solid[0]; f.sy = fp.sc.solid[1]; f.sz = fp.sc.solid[2]; f.sw = fp.sc.solid[3];
-    f.tx = fp.sc.tint[0]; f.ty = fp.sc.tint[1]; f.tz = fp.sc.tint[2]; f.tw = fp.sc.tint[3];
-    f.vis = 1.0f;
-    const float4 c = fs_fast<true>(fp.sc, f);
-    return unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
-}
-
-// One bin of a single-draw solid frame (fast build, 32x32 bins) through the attribute-plane table.
-// Coverage, the large-triangle pass and the sky pass are raster_bin's; see the block comment above.
-__device__ __forceinline__ void raster_bin_planes(const TriFrameParams& fp, const TriDeviceBuffers& b, const int bin) {
-    constexpr int BL = 5, BIN = 32, kIter = BIN * BIN / TRI_BLOCK;  // pixels per lane
-    __shared__ PlaneLds u;
-    __shared__ uint16_t plist[TRI_BLOCK / 64][64 * kIter];  // per wave: the current chunk's pixels
-    __shared__ uint16_t skyq[BIN * BIN];
-    __shared__ uint32_t bigq[kPlaneBigQ];
-    __shared__ uint32_t nbig, nentries, nsky;
-    uint64_t* keys = u.cov.keys;
-    const int tid = threadIdx.x;
-    TRI_STAMP(0);
-    const int bx = bin % fp.nbx, by = bin / fp.nbx;
-    const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
-    const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);
-    for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = kBgKey;
-    for (int i = tid; i < kPlaneHash; i += TRI_BLOCK) u.cov.hkv[i] = ~0ull;  // (no key's low word is all ones)
-    if (tid == 0) {
-        nbig = 0;
-        nsky = 0;
-        const uint32_t cnt = b.bin_count[bin];
-        b.bin_count[bin] = 0;  // queue consumed: ready for the next frame
-        if (cnt > fp.bin_cap) note_bin_overflow(b, cnt);
-        nentries = min(cnt, fp.bin_cap);
-    }
-    __syncthreads();
-    TRI_STAMP(1);
-    const uint32_t* queue = b.bin_list + (size_t)bin * fp.bin_cap;
-    const uint32_t n = nentries;
-    const bool hashed = n <= kPlaneHashMax;  // uniform; else every pixel rebuilds its entry's row itself
-    auto insert = [&](uint32_t low, uint32_t i) {  // one 64-bit slot: low word = key bits, high = entry
-        uint32_t h = plane_hash(low);
-        const unsigned long long kv = ((unsigned long long)i << 32) | low;
-        for (int probe = 0; probe < kPlaneHash; ++probe, h = (h + 1) & (kPlaneHash - 1))
-            if (atomicCAS(&u.cov.hkv[h], ~0ull, kv) == ~0ull) return;
-    };
-    // coverage: raster_bin's per-lane walk (two lanes per entry in bins of <= 128 entries)
-    auto cover = [&](uint32_t i, int32_t sub, int32_t step) {
-        const uint32_t ri = queue[i];
-        const TriRec r = load_entry<true>(fp, b, ri);
-        int32_t cx0, cx1, cy0, cy1;
-        rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
-        if (cx0 > cx1 || cy0 > cy1) return;
-        if (hashed && sub == 0) insert(key_low(r.prim_sub), i);
-        if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
-            if (sub != 0) return;
-            const uint32_t q = atomicAdd(&nbig, 1u);
-            if (q < (uint32_t)kPlaneBigQ) { bigq[q] = ri; return; }
-            raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);
-            return;
-        }
-        raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys, sub, step);
-    };
-    const int share = TRI_COV_SHARE > 1 && n <= (uint32_t)TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
-    for (uint32_t i = tid / share; i < n; i += TRI_BLOCK / share) cover(i, tid % share, share);
-    __syncthreads();
-    const uint32_t nb = min(nbig, (uint32_t)kPlaneBigQ);
-    for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        const TriRec r = load_entry<true>(fp, b, bigq[q]);
-        int32_t cx0, cx1, cy0, cy1;
-        rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
-        EdgeSetup e;
-        edge_setup(r, e);
-        bool rej = false;
-        int32_t F[3];
-#pragma unroll
-        for (int k = 0; k < 3; ++k) F[k] = clamp_edge((int64_t)e.A[k] * cx0 + (int64_t)e.B[k] * cy0 + e.D[k], rej);
-        if (rej) continue;  // uniform across the workgroup
-        const bool far_clip = (r.z[0] > 1.0f) || (r.z[1] > 1.0f) || (r.z[2] > 1.0f);
-        const uint32_t low = key_low(r.prim_sub);
-        const int32_t rw = cx1 - cx0 + 1, rh = cy1 - cy0 + 1;
-        for (int j = tid; j < rw * rh; j += TRI_BLOCK) {
-            const int32_t dy = j / rw, dx = j - dy * rw;
-            const int32_t f0 = F[0] + e.A[0] * dx + e.B[0] * dy;
-            const int32_t f1 = F[1] + e.A[1] * dx + e.B[1] * dy;
-            const int32_t f2 = F[2] + e.A[2] * dx + e.B[2] * dy;
-            if ((f0 | f1 | f2) >= 0) {
-                const int32_t px = cx0 + dx, py = cy0 + dy;
-                uint64_t key;
-                if (depth_key(frag_depth(r, e, px, py), far_clip, low, key))
-                    atomicMin(&keys[((py - oy) << BL) + (px - ox)], key);
-            }
-        }
-    }
-    __syncthreads();
-    TRI_STAMP(2);
-    const int lx = tid & (BIN - 1), ly0 = tid >> BL;
-    const bool sky_on = fp.sky_size != 0;
-    const bool sky_const = sky_on && fp.sky_mode == TRI_SKY_UNIFORM;
-    const bool sky_queue = sky_on && !sky_const;
-    const uint32_t bg_bgra = sky_const ? fp.sky_bgra : fp.clear_bgra;
-    // resolve: per pixel its depth and background colour (stored now) and its queue entry (kept in a
-    // register, two 16-bit slots per register: the lane that resolves a pixel is the one that shades it, or
-    // that lists it for its chunk). A bin beyond the hash shades each pixel here from its own rebuilt row.
-    static_assert(kIter == 4, "four 16-bit slots in two registers");
-    uint32_t slo = 0, shi = 0;  // shifted in: after the loop slo = s0 | s1 << 16, shi = s2 | s3 << 16
-#pragma unroll
-    for (int j = 0; j < kIter; ++j) {
-        const int ly = ly0 + j * (TRI_BLOCK / BIN);
-        uint32_t sl = 0xFFFFu;
-        const bool in = lx < bw && ly < bh;
-        const int p = (ly << BL) + lx;
-        const uint64_t key = in ? keys[p] : 0ull;
-        const bool bg = in && key == kBgKey;
-        if (sky_queue) {  // wave-aggregated append (uniform control flow here)
-            const uint64_t m = __ballot(bg);
-            if (m) {
-                const uint32_t lane = lanes_below(~0ull);
-                const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&nsky, (uint32_t)__builtin_popcountll(m));
-                base = (uint32_t)__shfl((int)base, (int)leader);
-                if (bg) skyq[base + lanes_below(m)] = (uint16_t)p;
-            }
-        }
-        if (in) {
-            const size_t o = (size_t)(oy + ly - fp.y0) * fp.W + ox + lx;
-            if (fp.write_depth) b.depth[o] = bg ? 1.0f : __uint_as_float((uint32_t)(key >> 32));
-            if (bg) {
-                if (!sky_queue) b.color[o] = bg_bgra;
-            } else if (hashed) {
-                const uint32_t low = (uint32_t)key;
-                uint32_t h = plane_hash(low);
-                unsigned long long kv = u.cov.hkv[h];
-                for (int probe = 0; probe < kPlaneHash && (uint32_t)kv != low; ++probe) {
-                    h = (h + 1) & (kPlaneHash - 1);
-                    kv = u.cov.hkv[h];
-                }
-                sl = (uint32_t)(kv >> 32);
-            } else {  // the key names the entry: a primitive, or a clipped primitive's sub-triangle record
-                const uint32_t low = (uint32_t)key, prim = TRI_PRIM_MAX - (low >> 3), sub = low & 7u;
-                const uint32_t e = sub ? (TRI_ENTRY_CLIPPED | (b.clip_slot[prim] + sub - 1u)) : prim;
-                float4 row[kPlaneF4];
-                plane_row(fp, b, e, row);
-                b.color[o] = plane_shade(fp, row, ox + lx, oy + ly);
-            }
-        }
-        slo = (slo >> 16) | (shi << 16);
-        shi = (shi >> 16) | (sl << 16);
-    }
-    // shading, one chunk of kPlaneCap entries at a time (one chunk for most bins)
-    const uint32_t nchunks = hashed ? (n + kPlaneCap - 1) / kPlaneCap : 0u;
-    const uint32_t wave = (uint32_t)tid >> 6, lane = lanes_below(~0ull);
-    auto slot_of = [&](int j) { return ((j < 2 ? slo : shi) >> (16 * (j & 1))) & 0xFFFFu; };
-    for (uint32_t k = 0; k < nchunks; ++k) {
-        const uint32_t e0 = k * kPlaneCap;
-        __syncthreads();  // the key tile / the previous chunk's rows are no longer read
-        if (k == 0) TRI_STAMP(3);
-        for (uint32_t i = tid; i < (uint32_t)kPlaneCap && e0 + i < n; i += TRI_BLOCK) {
-            float4 row[kPlaneF4];
-            plane_row(fp, b, queue[e0 + i], row);
-#pragma unroll
-            for (int q = 0; q < kPlaneF4; ++q) u.table[i * kPlaneF4 + q] = row[q];
-        }
-        __syncthreads();
-        if (k == 0) TRI_STAMP(4);
-        if (nchunks == 1) {  // every pixel of the bin in place: whole-row, coalesced stores
-#pragma unroll 1
-            for (int j = 0; j < kIter; ++j) {
-                const uint32_t sl = slot_of(j);
-                if (sl == 0xFFFFu) continue;
-                const int32_t px = ox + lx, py = oy + ly0 + j * (TRI_BLOCK / BIN);
-                b.color[(size_t)(py - fp.y0) * fp.W + px] = plane_shade(fp, u.table + sl * kPlaneF4, px, py);
-            }
-            continue;
-        }
-        // several chunks: the wave lists its pixels of this chunk ((chunk row << 8) | (j << 6) | lane), then
-        // shades the list lane-dense
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int j = 0; j < kIter; ++j) {
-            const uint32_t rrow = slot_of(j) - e0;  // (0xFFFF - e0 >= kPlaneCap: e0 + kPlaneCap <= 1024)
-            const bool mine = rrow < (uint32_t)kPlaneCap;
-            const uint64_t m = __ballot(mine);
-            if (mine) plist[wave][cnt + lanes_below(m)] = (uint16_t)((rrow << 8) | ((uint32_t)j << 6) | lane);
-            cnt += (uint32_t)__builtin_popcountll(m);
-        }
-        wave_lds_sync();
-        for (uint32_t t = lane; t < cnt; t += 64) {
-            const uint32_t le = plist[wave][t];
-            const uint32_t src = le & 63u, j = (le >> 6) & 3u;
-            const int32_t px = ox + (int32_t)((wave * 64 + src) & (BIN - 1));
-            const int32_t py = oy + (int32_t)(((wave * 64 + src) >> BL) + j * (TRI_BLOCK / BIN));
-            b.color[(size_t)(py - fp.y0) * fp.W + px] = plane_shade(fp, u.table + (le >> 8) * kPlaneF4, px, py);
-        }
-    }
-    if (!sky_queue) {
-        TRI_STAMP(5);
-        return;
-    }
-    __syncthreads();
-    const uint32_t ns = nsky;
-    if (ns == 0) {  // uniform
-        TRI_STAMP(5);
-        return;
-    }
-    for (int i = tid; i < 512; i += TRI_BLOCK) u.lut[i] = b.srgb_lut[i];  // the table / keys are dead
-    __syncthreads();
-    const bool persp = fp.sky_mode == TRI_SKY_PERSP;
-    for (uint32_t i = tid; i < ns; i += TRI_BLOCK) {
-        const uint32_t li = skyq[i];
-        const int32_t px = ox + (int32_t)(li & (BIN - 1)), py = oy + (int32_t)(li >> BL);
-        b.color[(size_t)(py - fp.y0) * fp.W + px] = persp ? sky_bgra_persp(fp, b, px, py, u.lut) : sky_bgra(fp, b, px, py, u.lut);
-    }
-    TRI_STAMP(5);
-}
-
 // 6 waves/SIMD at 32x32 bins: the fast build fits 80 VGPRs without spilling (the exact build spills
 // a little); 64x64 bins are LDS-limited to 3. One workgroup per bin: a persistent grid (one resident
 // round of workgroups, each walking bins blockIdx + k * gridDim on its XCD) measured 121.5 -> 154 us at C3
@@ -2534,10 +2229,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
 // 117 -> 112 us). Frames with the pre-pass keep k_raster<.., true> (5 waves, SLP: faster there).
 template <bool EXACT, int BL, bool ONE>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES_PLAIN : 3))) void k_raster_plain(TriFrameParams fp, TriDeviceBuffers b) {
-    if constexpr (TRI_PLANES && ONE && !EXACT && BL == 5)
-        raster_bin_planes(fp, b, xcd_bin(blockIdx.x, fp.nbins));
-    else
-        raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
+    raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
 
 // ------------------------------------------------------------------------------------------

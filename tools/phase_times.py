@@ -52,8 +52,7 @@ def main(which="c3", band=None):
     a = np.frombuffer(buf, dtype=np.uint64).reshape(n, 6).astype(np.int64)
     nb = int((a[:, 0] != 0).sum())
     a = a[:nb]
-    names = (["init", "coverage+big", "resolve", "fill", "shade+sky"] if os.environ.get("TRI_PHASES_PLANES")
-             else ["init", "coverage", "big", "shade", "sky"])
+    names = ["init", "coverage", "big", "shade", "sky"]
     d = np.diff(a, axis=1)
     tot = a[:, 5] - a[:, 0]
     print(f"{which}: {nb} workgroups; cycles per workgroup (s_memtime ticks)")
