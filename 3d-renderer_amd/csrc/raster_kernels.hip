@@ -1369,7 +1369,9 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
     const float NdotH = fmaxf((px.NdotVr + NdotLr) * ih, 0.0f);
     const float NdotL = NdotLr;  // > 0 here: max(N.L, 0) is the identity
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
-    const float gden = fmaxf(__builtin_fmaf(NdotL, sc.omkg, sc.kg), 1e-4f);
+    // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
+    // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
+    const float gden = __builtin_fmaf(NdotL, sc.omkg, sc.kg);
     const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
     // NDF * G_L * G_V / den with NDF = a2 / (pi dd^2), G_L = NdotL / gden
     const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
@@ -1415,7 +1417,9 @@ __device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const P
     const float NdotH = fmaxf((px.NdotVr + NdotLr) * ih, 0.0f);
     const float NdotL = NdotLr;
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
-    const float gden = fmaxf(__builtin_fmaf(NdotL, sc.omkg, sc.kg), 1e-4f);
+    // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
+    // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
+    const float gden = __builtin_fmaf(NdotL, sc.omkg, sc.kg);
     const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
     const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
     const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
@@ -1527,29 +1531,23 @@ __device__ __forceinline__ float interp_fast(float w0, float w1, float w2, float
     return __builtin_fmaf(w2, x2, __builtin_fmaf(w1, x1, w0 * x0));
 }
 
-// Fast build's perspective-correct weights: per triangle, the barycentric slopes over pixel offsets from
-// vertex 0 (from the exact integer area), with vertex 1's and 2's scaled by iw_k / iw_0; per pixel two
-// FMAs per weight and one reciprocal. Relative to vertex 0, not to a bin, so every bin, band and code path
-// (LDS table or gathered triangle) gives the same bits.
-struct FastW {
-    float a0, b0, a1, b1, a2, b2;
-};
-__device__ __forceinline__ FastW fast_coefs(const TriRec& r) {
+// Fast build's perspective-correct weights from the pixel-centre offsets (dx, dy) to vertex 0: the three
+// edge functions at the pixel, e0 = S + (y1 - y2) dx + (x2 - x1) dy, e1 = y2 dx - x2 dy, e2 = x1 dy - y1 dx
+// (S the exact doubled area, so e0 + e1 + e2 = S), weighted by 1/w: q_k = e_k iw_k, w_k = q_k / (q0 + q1 + q2).
+// This is the barycentric form scaled by S iw0, which cancels in the normalisation, so the only reciprocal is
+// that of the sum (no 1/S, no 1/iw0). Relative to vertex 0, not to a bin: every bin, band and code path
+// gives a pixel the same bits.
+__device__ __forceinline__ void fast_weights(const TriRec& r, int32_t px, int32_t py, float& w0, float& w1, float& w2) {
     const int32_t x1 = r.X[1] - r.X[0], y1 = r.Y[1] - r.Y[0], x2 = r.X[2] - r.X[0], y2 = r.Y[2] - r.Y[0];
     const float fx1 = (float)x1, fy1 = (float)y1, fx2 = (float)x2, fy2 = (float)y2;
     // the exact area, rounded once: |x|, |y| < 2^23, so both products and their difference are exact in
     // double (one v_fma_f64 instead of a 64-bit integer product and its int64 -> float conversion)
-    const float iS = frcp((float)__builtin_fma((double)x1, (double)y2, -((double)y1 * (double)x2)));
-    const float i0 = frcp(r.iw[0]);
-    const float s1 = (r.iw[1] * i0) * iS, s2 = (r.iw[2] * i0) * iS;
-    return FastW{(float)(y1 - y2) * iS, (float)(x2 - x1) * iS, fy2 * s1, -fx2 * s1, -fy1 * s2, fx1 * s2};
-}
-__device__ __forceinline__ void fast_weights(const FastW& c, int32_t X0, int32_t Y0, int32_t px, int32_t py, float& w0,
-                                             float& w1, float& w2) {
-    const float dx = (float)(256 * px + 128 - X0), dy = (float)(256 * py + 128 - Y0);
-    const float q0 = __builtin_fmaf(c.b0, dy, __builtin_fmaf(c.a0, dx, 1.0f));
-    const float q1 = __builtin_fmaf(c.b1, dy, c.a1 * dx);
-    const float q2 = __builtin_fmaf(c.b2, dy, c.a2 * dx);
+    const float fS = (float)__builtin_fma((double)x1, (double)y2, -((double)y1 * (double)x2));
+    const float dx = (float)(256 * px + 128 - r.X[0]), dy = (float)(256 * py + 128 - r.Y[0]);
+    const float e0 = __builtin_fmaf((float)(x2 - x1), dy, __builtin_fmaf((float)(y1 - y2), dx, fS));
+    const float e1 = __builtin_fmaf(-fx2, dy, fy2 * dx);
+    const float e2 = __builtin_fmaf(fx1, dy, -fy1 * dx);
+    const float q0 = e0 * r.iw[0], q1 = e1 * r.iw[1], q2 = e2 * r.iw[2];
     const float iq = frcp((q0 + q1) + q2);
     w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
 }
@@ -1721,7 +1719,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
         exact_weights(r, px, py, w0, w1, w2);
     } else {
-        fast_weights(fast_coefs(r), r.X[0], r.Y[0], px, py, w0, w1, w2);
+        fast_weights(r, px, py, w0, w1, w2);
     }
     if (TRI_COLOUR_LATE) {
         taps.a2 = ld_vary(fb, v0, 2); taps.b2 = ld_vary(fb, v1, 2); taps.c2 = ld_vary(fb, v2, 2);
@@ -1931,8 +1929,11 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 #endif
 static_assert((TRI_COV_SHARE & (TRI_COV_SHARE - 1)) == 0 && TRI_BLOCK % TRI_COV_SHARE == 0,
               "TRI_COV_SHARE must be a power of two dividing the workgroup (each lane group owns one entry)");
+// Raised wave priority (s_setprio 1) from a 32x32 bin's start to the end of its coverage: the latency-bound
+// init and coverage phases issue ahead of other workgroups' shading waves (C3 k_raster 101.7 -> 99.6 us,
+// round 3 A/B; at 16x16 bins it was slower, so BL == 5 only). Scheduling only: output unchanged.
 #ifndef TRI_COV_PRIO
-#define TRI_COV_PRIO 0
+#define TRI_COV_PRIO 1
 #endif
 #ifndef TRI_COV_BALANCED
 #define TRI_COV_BALANCED 1
@@ -1981,9 +1982,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ uint32_t nbig, nentries, nsky;
     const int tid = threadIdx.x;
     TRI_STAMP(0);
-    // 32x32 bins: the latency-bound init and coverage phases issue ahead of other workgroups' shading waves
-    // (C3 k_raster 103.9 -> 102.5 us; at 16x16 bins, C2, it was slower: 32.5 -> 33.5 us)
-    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1);
+    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1);  // (TRI_COV_PRIO above)
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
     const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
     const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);

@@ -224,12 +224,14 @@ def test_gpu_shadow_off_again_matches_plain(oracle):
 
 
 @pytest.mark.gpu
-def test_gpu_c5_full_4k_textures_and_shadow(oracle):
+@pytest.mark.parametrize("mode", ["fast", "exact"])
+def test_gpu_c5_full_4k_textures_and_shadow(oracle, mode):
     """BASELINE C5 at full size: 3840x2160, 1M triangles in 4 draws with four 2048^2 sRGB textures and
-    the 2048^2 shadow pre-pass. Map and depth bit-exact, colour within 1 LSB."""
-    from trident_raster import scenes
+    the 2048^2 shadow pre-pass, in both shading builds. Map and depth bit-exact, colour within 1 LSB."""
+    from trident_raster import abi, scenes
 
     s = scenes.scene_c5_textured()
     assert s.shadow is not None and s.shadow.size == 2048
-    om = assert_shadow_parity(s, oracle, 0, min_covered=3840 * 2160 // 2)
+    flags = abi.TRI_FLAG_EXACT_SHADING if mode == "exact" else 0
+    om = assert_shadow_parity(s, oracle, flags, min_covered=3840 * 2160 // 2)
     assert (om != 0x3F800000).sum() > 100000
