@@ -497,6 +497,14 @@ __device__ __forceinline__ ClipVert cv_load(const float* p) {
     v.b0 = p[4]; v.b1 = p[5]; v.b2 = p[6];
     return v;
 }
+// Workgroup barrier ordering LDS only (s_waitcnt lgkmcnt(0) + s_barrier): global loads issued before it stay
+// in flight (__syncthreads' fence would wait for them too).
+__device__ __forceinline__ void lds_barrier() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // LDS traffic between lanes of one wave: DS instructions of a wave execute in order, so a
 // compiler barrier is all that is needed between a lane's store and another lane's load.
 __device__ __forceinline__ void wave_lds_sync() {
@@ -1979,28 +1987,40 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ uint16_t skyq[kJobWords];  // the coverage pass's row jobs, then the skybox queue
     __shared__ CovEntry cov[kBalanced ? kCovPass : 1];
     __shared__ uint32_t wsum[TRI_BLOCK / 64];
-    __shared__ uint32_t nbig, nentries, nsky;
+    __shared__ uint32_t nbig, nsky;
     const int tid = threadIdx.x;
     TRI_STAMP(0);
     if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1);  // (TRI_COV_PRIO above)
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
     const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
     const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);
+    // Every lane loads the bin's entry count with a vector (buffer) load issued before the key-tile clear:
+    // the barrier below fences LDS only, so the load stays in flight across it instead of being waited for
+    // in front of it (a scalar or a lane-0 load would sit on the barrier's critical path).
+    const uint32_t cnt_v = __builtin_amdgcn_raw_buffer_load_b32(make_rsrc(b.bin_count, 4ull * fp.nbins), (uint32_t)bin * 4u, 0, 0);
+#ifndef TRI_QUEUE_PREFETCH
+#define TRI_QUEUE_PREFETCH 1  // round-3 A/B: C3 k_raster 98.9 -> 98.0 us, C5 195.6 -> 193.3 us
+#endif
+    // the lane's first queue entry for either lane split of the per-lane walk, in flight likewise (entries
+    // past the count are loaded and ignored: the queue holds bin_cap >= 256 slots)
+    uint32_t pre1 = 0, pre2 = 0;
+    if constexpr (TRI_QUEUE_PREFETCH && !(TRI_COV_BALANCED && BL == 4)) {
+        const Rsrc qr = make_rsrc(b.bin_list + (size_t)bin * fp.bin_cap, 4ull * fp.bin_cap);
+        pre1 = __builtin_amdgcn_raw_buffer_load_b32(qr, (uint32_t)tid * 4u, 0, 0);
+        pre2 = __builtin_amdgcn_raw_buffer_load_b32(qr, (uint32_t)(tid / TRI_COV_SHARE) * 4u, 0, 0);
+    }
     for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = kBgKey;
     if (fp.need_lut)
         for (int i = tid; i < 512; i += TRI_BLOCK) lut[i] = b.srgb_lut[i];
     if (tid == 0) {
         nbig = 0;
         nsky = 0;
-        const uint32_t cnt = b.bin_count[bin];
-        b.bin_count[bin] = 0;  // queue consumed: ready for the next frame
-        if (cnt > fp.bin_cap) note_bin_overflow(b, cnt);
-        nentries = min(cnt, fp.bin_cap);
     }
-    __syncthreads();
+    lds_barrier();
     TRI_STAMP(1);
+    const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt_v);
     const uint32_t* queue = b.bin_list + (size_t)bin * fp.bin_cap;
-    uint32_t s0 = 0, s1 = nentries;
+    uint32_t s0 = 0, s1 = min(cnt, fp.bin_cap);
     if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
             const TriRec r = load_entry<ONE>(fp, b, queue[0]);
@@ -2083,8 +2103,8 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
   } else {
     // `share` lanes per triangle when the bin has few entries (lanes would idle otherwise); each takes
     // every share-th row of its bbox. Uniform per workgroup.
-    auto cover = [&](uint32_t i, int32_t sub, int32_t step) {
-        const uint32_t ri = queue[i];
+    auto cover = [&](uint32_t i, int32_t sub, int32_t step, bool first) {
+        const uint32_t ri = (TRI_QUEUE_PREFETCH && first) ? (step > 1 ? pre2 : pre1) : queue[i];
         const TriRec r = load_entry<ONE>(fp, b, ri);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
@@ -2102,7 +2122,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     // every lane works, measured slower: 105.5 -> 109.8 us at C3. The duplicated fetch and set-up of a
     // pair costs issue slots the CU's other workgroups would use; a wave with no entry costs none.)
     const int share = TRI_COV_SHARE > 1 && (s1 - s0) <= (uint32_t)TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
-    for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) cover(i, tid % share, share);
+    for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) cover(i, tid % share, share, i < (uint32_t)(TRI_BLOCK / share));
     __syncthreads();
   }
     TRI_STAMP(2);
@@ -2136,6 +2156,12 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     }
     __syncthreads();
     TRI_STAMP(3);
+    // queue consumed (every wave's count load has completed: each waited for it, and the barrier's fence
+    // covers this workgroup's global accesses): ready for the next frame
+    if (tid == 0) {
+        b.bin_count[bin] = 0;
+        if (cnt > fp.bin_cap) note_bin_overflow(b, cnt);
+    }
     if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(0);
     // shade + store: each wave covers whole BIN-pixel row pieces -> coalesced colour/depth stores.
     // Background pixels go to an LDS queue for the skybox pass below (lane-dense, and its registers

@@ -231,13 +231,14 @@ class BandRenderer:
         return ts[len(ts) // 2]
 
 
-def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, warm_seconds=0.1):
+def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, warm_seconds=0.25):
     """Time exactly `steps` frames (no per-kernel events inside the timed region), then, outside it,
     a separate pass of `event_frames` frames with HIP events around every kernel of every frame:
     the per-kernel durations (roofline.kernel_ms) rest on that many samples, not on the few frames a
     short timed run would leave.
 
-    Warm-up: `warmup` frames, and back-to-back frames for at least `warm_seconds` of wall time. The
+    Warm-up: `warmup` frames, back-to-back frames for at least `warm_seconds` of wall time, then batches
+    of `steps` frames until two consecutive batches agree within 2 % (at most 8). The
     GPU leaves its idle clock state only after several ms of continuous work: after the scene upload
     (seconds of host work) 5 warm-up frames (0.6 ms) left the first timed frames at low clocks, and a
     20-frame run measured 0.134-0.140 ms/frame against 0.113-0.118 for the same frames after 50 ms of
@@ -259,6 +260,22 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, w
     extra = int(max_over_ranks(float(extra), br.dev, dist_on))
     for _ in range(extra):
         br.step()
+    # then batches of `steps` frames until two consecutive batches agree within 2 % (at most 8 batches):
+    # the clock has settled at the rate the timed frames will run at
+    batch, prev = max(steps, 20), None
+    for _ in range(8):
+        br.drain()
+        torch.cuda.synchronize(br.dev)
+        tb = time.perf_counter()
+        for _ in range(batch):
+            br.step()
+        br.drain()
+        torch.cuda.synchronize(br.dev)
+        cur = max_over_ranks(time.perf_counter() - tb, br.dev, dist_on)
+        extra += batch
+        if prev is not None and abs(cur - prev) <= 0.02 * prev:
+            break
+        prev = cur
     n_warm = max(warmup, 1) + extra
     br.drain()
     br.synchronize()
@@ -414,7 +431,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--config", default="c3")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--warm-seconds", type=float, default=0.1,
+    ap.add_argument("--warm-seconds", type=float, default=0.25,
                     help="untimed back-to-back frames before the timed region (at least --warmup frames): the "
                          "GPU's clock ramp out of idle takes a few ms")
     ap.add_argument("--no-cpu-baseline", action="store_true")
