@@ -537,7 +537,12 @@ def main():
                          "measured_copy_GBs": copy_gbs,
                          "kernel": "k_raster",
                          "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]) if timing else 0,
-                         "algorithmic_bytes": raster_bytes},
+                         "algorithmic_bytes": raster_bytes,
+                         "traffic_source": (None if traffic is None else
+                                            f"profiles/pmc_summary.json k_raster: {pmc.get('hbm_read_method', '2 x FETCH_SIZE')}"
+                                            " reads + WRITE_SIZE, per launch; the read counters are calibrated against"
+                                            " known bytes for k_raster's 12-B / 16-B gather shapes in"
+                                            " profiles/round3/fetch_calib.json (tools/fetch_calib.sh)")},
             # the PMC count is of a whole frame: no VALU roofline for a band
             "roofline_valu": valu_roofline(pmc if br.rows == H else None, raster_ms),
             "frame_roofline": {"algorithmic_bytes": frame_bytes, "ms_per_frame": frame_ms,

@@ -16,6 +16,8 @@ rocprofv3 -L > $OUT/counters_list.txt 2>&1 || true
 run trace --kernel-trace --stats || exit $?
 run pmc_fetch --pmc FETCH_SIZE || exit $?
 run pmc_write --pmc WRITE_SIZE || exit $?
+# sized L2->fabric read requests: the byte count the FETCH_SIZE calibration validates (tools/fetch_calib.sh)
+run pmc_sized --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_128B_sum || exit $?
 run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY || exit $?
 run pmc_sq2 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE || exit $?
 run pmc_tcc --pmc TCC_HIT_sum TCC_MISS_sum || exit $?
