@@ -214,14 +214,20 @@ def test_bin_overflow_grows_and_recovers():
     assert ref[0].shape == (720, 1280, 4)
 
 
-@pytest.mark.parametrize("case", ["grid_turned", "primitives", "invalid", "skinned", "near_clip", "dense"])
+@pytest.mark.parametrize("case", ["grid_turned", "primitives", "invalid", "skinned", "near_clip", "dense",
+                                  "near_far_planes"])
 def test_cluster_cull_is_exact(oracle, case):
     """TRI_FLAG_CLUSTER_CULL on a whole frame (row bands always cull): frames bit-identical to the
     unculled path and to the oracle, with geometry partly off screen, several draws, invalid vertices,
-    skinned draws (never culled) and clipped primitives."""
+    skinned draws (never culled), clipped primitives, and clusters cut by both the near and the far plane
+    (the cull's depth margin, raster_kernels.hip cluster_visible)."""
     from trident_raster import abi, scenes
 
-    if case == "grid_turned":
+    if case == "near_far_planes":  # the displaced grid spans z in [-5.9, -4.1]: both planes cut its clusters
+        s = sc.grid_c3(640, 360, 120)
+        view, proj = scenes.editor_camera((0.0, 0.0, 0.0), (0, 0, 0), 60.0, (640, 360), 4.6, 5.3)
+        s.ubo = scenes.pack_ubo(view, proj, (0.0, 0.0, 0.0), [{"type": "directional"}])
+    elif case == "grid_turned":
         s = sc.grid_c3(640, 360, 120)
         view, proj = scenes.editor_camera((1.5, 0.5, 0.0), (8.0, 35.0, 0.0), 60.0, (640, 360))
         s.ubo = scenes.pack_ubo(view, proj, (1.5, 0.5, 0.0), [{"type": "directional"}])
@@ -238,7 +244,7 @@ def test_cluster_cull_is_exact(oracle, case):
     assert np.array_equal(cull_c, plain_c) and np.array_equal(cull_d, plain_d)
     assert cull_s["triangles_setup"] == plain_s["triangles_setup"]
     assert_parity(s, oracle, flags=abi.TRI_FLAG_CLUSTER_CULL)
-    if case == "dense":  # and in row bands (which always cull), assembled
+    if case in ("dense", "near_far_planes"):  # and in row bands (which always cull), assembled
         cuts = np.linspace(0, s.height, 5).astype(int)
         parts = [render_gpu(s, band=(int(a), int(b))) for a, b in zip(cuts[:-1], cuts[1:])]
         assert np.array_equal(np.concatenate([q[0] for q in parts]), plain_c)
@@ -304,3 +310,28 @@ def raster_ctx(W, H):
     from trident_raster import raster
 
     return raster.TriRaster(W, H)
+
+
+def test_own_geometry_after_a_shared_one(oracle):
+    """A context that rendered a shared tri_geometry, then uploads geometry of its own with an unchanged
+    draw list, resolves its draws against the new buffers (per-object geometry versions could
+    collide): both frames match the oracle."""
+    from trident_raster import raster, scenes
+
+    s1, s2 = sc.grid_c3(320, 240, 24), sc.grid_c3(320, 240, 37)
+    g = raster.TriGeometry(0)
+    g.upload(s1.vertices, s1.indices, s1.meshes)
+    with raster.TriRaster(320, 240, device=0) as r:
+        scenes.load_scene(r, s1, geometry=g)
+        r.render_frame()
+        got1 = r.readback()
+        r.upload_geometry(s2.vertices, s2.indices, s2.meshes)  # own geometry; same draws
+        r.set_draws(s2.draws)
+        r.render_frame()
+        got2 = r.readback()
+    g.close()
+    for (gc, gd), s in ((got1, s1), (got2, s2)):
+        oc, od, _ = oracle.render(s)
+        assert np.array_equal(gd, od)
+        assert int(np.abs(gc.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL
+    assert not np.array_equal(got1[1], got2[1])
