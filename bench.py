@@ -47,11 +47,49 @@ def band_rows(height, world, rank):
     return rank * rows, (rank + 1) * rows
 
 
-def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=0):
-    """Assemble the full frame from the per-rank BGRA8 bands; band r lands at rows [r*rows, (r+1)*rows).
-    mode "gather" (default): onto the display rank `dst` only (RCCL grouped send/recv over xGMI: each
-    rank sends its 1/N of the frame once, the display rank receives N-1 bands over N-1 links at once);
-    "allgather": onto every rank (all_gather_into_tensor: (N-1)/N of the frame into every GPU).
+def band_split(height, world, display_rows=None):
+    """Every rank's row band [y0, y1), top to bottom. Default: equal bands (any remainder one row at a
+    time). With display_rows, the display rank 0 takes that many rows and the others share the rest
+    (sizes within one row): the display rank's band never crosses a link, so when the gather is the
+    bottleneck a larger display band shortens every remote band's transfer (sort-first load balancing;
+    autotune_split picks the size on the hardware)."""
+    if world == 1:
+        return [(0, height)]
+    if display_rows is None:
+        base, rem = divmod(height, world)
+        sizes = [base + (1 if r < rem else 0) for r in range(world)]
+    else:
+        d = int(display_rows)
+        if d < 1 or height - d < world - 1:
+            raise ValueError(f"display band of {d} rows leaves no rows for {world - 1} other ranks of {height}")
+        base, rem = divmod(height - d, world - 1)
+        sizes = [d] + [base + (1 if r < rem else 0) for r in range(world - 1)]
+    bands, y = [], 0
+    for n in sizes:
+        bands.append((y, y + n))
+        y += n
+    return bands
+
+
+class _Works:
+    """The requests of one grouped send/recv as one handle (wait() = a stream wait on each)."""
+
+    def __init__(self, works):
+        self.works = works
+
+    def wait(self):
+        for w in self.works:
+            w.wait()
+
+
+def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=0, spans=None):
+    """Assemble the full frame from the per-rank BGRA8 bands; band r lands at elements
+    [spans[r][0], spans[r][0] + spans[r][1]) of the frame (default: equal bands, r * n).
+    mode "gather" (default): onto the display rank `dst` only, as one grouped point-to-point exchange
+    (RCCL ncclSend/ncclRecv over xGMI: each rank sends its band once, the display rank receives N-1 bands
+    over N-1 links at once; bands may differ in size). The display rank's own band is copied in unless it
+    already is the frame's view (BandRenderer renders it in place). "allgather": onto every rank
+    (all_gather_into_tensor, equal bands only: (N-1)/N of the frame into every GPU).
     Returns the work handle (None for world 1) with async_op, else the assembled frame (None on a
     non-display rank in gather mode). gloo backs the same calls in the CPU tests."""
     if world == 1:
@@ -61,10 +99,21 @@ def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=
     if mode == "allgather":
         work = dist.all_gather_into_tensor(frame, band, async_op=async_op)
         return work if async_op else frame
-    n = band.numel()
-    parts = [frame.narrow(0, r * n, n) for r in range(world)] if rank == dst else None
-    work = dist.gather(band, gather_list=parts, dst=dst, async_op=async_op)
-    return work if async_op else (frame if rank == dst else None)
+    if spans is None:
+        n = band.numel()
+        spans = [(r * n, n) for r in range(world)]
+    if rank == dst:
+        own = frame.narrow(0, *spans[dst])
+        if own.data_ptr() != band.data_ptr():
+            own.copy_(band)
+        ops = [dist.P2POp(dist.irecv, frame.narrow(0, *spans[r]), r) for r in range(world) if r != dst]
+    else:
+        ops = [dist.P2POp(dist.isend, band, dst)]
+    work = _Works(dist.batch_isend_irecv(ops))
+    if async_op:
+        return work
+    work.wait()
+    return frame if rank == dst else None
 
 
 def max_over_ranks(value, device, dist_on):
@@ -85,12 +134,18 @@ class GatherRing:
     render stream waits for frame k's gather (work.wait() is a stream wait; the host does not
     block). Throughput is then max(render, gather) per frame instead of their sum."""
 
-    def __init__(self, world, band_elems, frame_elems, make, mode="gather", rank=0, dst=0, nbuf=None):
-        self.world, self.mode, self.rank, self.dst = world, mode, rank, dst
+    def __init__(self, world, band_elems, frame_elems, make, mode="gather", rank=0, dst=0, nbuf=None, spans=None):
+        self.world, self.mode, self.rank, self.dst, self.spans = world, mode, rank, dst, spans
         self.nbuf = nbuf if nbuf else (2 if world > 1 else 1)
-        self.bands = [make(band_elems) for _ in range(self.nbuf)]
         keeps_frame = world > 1 and (mode == "allgather" or rank == dst)
-        self.frames = [make(frame_elems) for _ in range(self.nbuf)] if keeps_frame else self.bands
+        if keeps_frame and mode == "gather":
+            # the display rank renders its band straight into the frame (no copy, no transfer)
+            self.frames = [make(frame_elems) for _ in range(self.nbuf)]
+            off, n = spans[dst] if spans else (dst * band_elems, band_elems)
+            self.bands = [f.narrow(0, off, n) for f in self.frames]
+        else:
+            self.bands = [make(band_elems) for _ in range(self.nbuf)]
+            self.frames = [make(frame_elems) for _ in range(self.nbuf)] if keeps_frame else self.bands
         self.pending = [None] * self.nbuf
         self.k = 0
 
@@ -106,7 +161,7 @@ class GatherRing:
         """Start frame k's gather of the band returned by acquire()."""
         i = self.k % self.nbuf
         self.pending[i] = gather_bands(self.frames[i], self.bands[i], self.world, async_op=True, mode=self.mode,
-                                       rank=self.rank, dst=self.dst)
+                                       rank=self.rank, dst=self.dst, spans=self.spans)
         self.k += 1
 
     def drain(self):
@@ -128,20 +183,26 @@ class BandRenderer:
     runs while frame k rasterises — the reference also keeps several frames in flight
     (Renderer::DrawFrame waits on the fence of the frame in flight two frames back, Renderer.cpp:752-772)."""
 
-    def __init__(self, scene, rank, world, device_index, band_world=None, assembly="gather", inflight=1):
+    def __init__(self, scene, rank, world, device_index, band_world=None, assembly="gather", inflight=1,
+                 display_rows=None):
         import ctypes as C
 
         import torch
         from trident_raster import abi, raster, scenes
 
         H, W = scene.height, scene.width
-        self.band = band_rows(H, band_world or world, rank)
+        if band_world or assembly == "allgather":  # equal bands (the all-gather needs equal sizes)
+            self.bands = [band_rows(H, band_world or world, r) for r in range(band_world or world)]
+        else:
+            self.bands = band_split(H, world, display_rows)
+        self.band = self.bands[rank]
         rows = self.band[1] - self.band[0]
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
         self.dev = torch.device("cuda", device_index)
         self.inflight = max(1, inflight)
+        spans = [(y0 * W, (y1 - y0) * W) for y0, y1 in self.bands] if world > 1 else None
         self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
-                               mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1))
+                               mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1), spans=spans)
         self.depth = [torch.empty(rows * W, dtype=torch.float32, device=self.dev) for _ in range(self.inflight)]
         self.geometry = raster.TriGeometry(device_index)
         self.geometry.upload(scene.vertices, scene.indices, scene.meshes)
@@ -229,6 +290,71 @@ class BandRenderer:
             ts.append((time.perf_counter() - t0) * 1e3)
         ts.sort()
         return ts[len(ts) // 2]
+
+
+def split_candidates(height, world, min_rows=32):
+    """Display-band sizes autotune_split tries: the equal split and display bands up to 3x it, as long
+    as every other rank keeps at least `min_rows` rows (one bin row)."""
+    base = height / world
+    out = []
+    for m in (1.0, 1.25, 1.5, 1.75, 2.0, 2.5, 3.0):
+        d = int(round(base * m))
+        if height - d >= (world - 1) * min_rows and d not in out:
+            out.append(d)
+    return out
+
+
+def measure_fps(br, frames, dist_on):
+    """Whole-job frames/s of `frames` back-to-back frames (render + gather), the slowest rank's clock."""
+    import torch
+
+    def sync():
+        if br.dev.type == "cuda":
+            torch.cuda.synchronize(br.dev)
+
+    br.drain()
+    sync()
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(frames):
+        br.step()
+    br.drain()
+    sync()
+    if dist_on:
+        dist.barrier()
+    return frames / max_over_ranks(time.perf_counter() - t0, br.dev, dist_on)
+
+
+def autotune_split(make, height, world, dist_on, frames=80, rounds=2, warm_seconds=0.25, candidates=None):
+    """Sort-first load balancing on the hardware: every candidate display-band size (split_candidates) is
+    built (make(display_rows) -> BandRenderer) and timed over `rounds` interleaved rounds of `frames`
+    frames (the best round counts, so a clock ramp or a noisy round does not decide); the fastest wins,
+    ties going to the more even split. Every rank computes the same max-over-ranks rates, so every rank
+    picks the same split without a broadcast. Returns (display_rows, [(display_rows, frames/s), ...])."""
+    cands = candidates or split_candidates(height, world)
+    brs = []
+    for d in cands:
+        br = make(d)
+        br.warm()
+        brs.append(br)
+    t_end = time.perf_counter() + warm_seconds  # the GPU's clock ramp out of idle, before any measurement
+    while True:
+        for _ in range(20):
+            brs[0].step()
+        brs[0].drain()
+        if max_over_ranks(t_end - time.perf_counter(), brs[0].dev, dist_on) <= 0:
+            break
+    best = [0.0] * len(cands)
+    for _ in range(rounds):
+        for i, br in enumerate(brs):
+            best[i] = max(best[i], measure_fps(br, frames, dist_on))
+    for br in brs:
+        br.close()
+    pick = max(range(len(cands)), key=lambda i: (best[i], -cands[i]))
+    return cands[pick], list(zip(cands, best))
 
 
 def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, warm_seconds=0.25):
@@ -443,6 +569,9 @@ def main():
                     help="frames in flight per rank (contexts taking frames in turn, one stream each)")
     ap.add_argument("--assembly", choices=("gather", "allgather"), default="gather",
                     help="N > 1: bands gathered onto the display rank 0 (default) or all-gathered onto every rank")
+    ap.add_argument("--split", default="auto",
+                    help="N > 1 gather: 'auto' (time candidate display-band sizes on the hardware, keep the fastest), "
+                         "'equal', or the display rank's row count")
     ap.add_argument("--no-stage-timing", action="store_true",
                     help="diagnostics: no per-kernel HIP events in the timed loop (roofline fields become null)")
     args = ap.parse_args()
@@ -462,10 +591,26 @@ def main():
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     scene = build_scene(args.config)
+
+    def make_renderer(sc, display_rows=None):
+        return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=args.inflight,
+                            display_rows=display_rows)
+
+    def choose_split(sc):
+        """(display_rows or None, the autotune log) for a config at this world size."""
+        if world == 1 or args.assembly != "gather" or args.split == "equal":
+            return None, None
+        if args.split != "auto":
+            return int(args.split), None
+        return autotune_split(lambda d: make_renderer(sc, d), sc.height, world, dist_on,
+                              warm_seconds=args.warm_seconds)
+
+    split_log = None
     if args.sim_world and world == 1:
         br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=args.inflight)
     else:
-        br = BandRenderer(scene, rank, world, local, assembly=args.assembly, inflight=args.inflight)
+        display_rows, split_log = choose_split(scene)
+        br = make_renderer(scene, display_rows)
     dt, timing, n_warm = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing,
                                    warm_seconds=args.warm_seconds)
     fps = args.steps / dt
@@ -489,7 +634,8 @@ def main():
     if not args.no_secondary and args.config == "c3":
         for key in ("c2", "c5"):  # the other BASELINE.json GPU configs, same timing protocol
             s2 = build_scene(key)
-            br2 = BandRenderer(s2, rank, world, local, assembly=args.assembly, inflight=args.inflight)
+            d2, log2 = choose_split(s2)
+            br2 = make_renderer(s2, d2)
             n2 = max(args.steps, 50) if key == "c2" else max(args.steps // 2, 20)
             dt2, t2, _ = timed_run(br2, n2, args.warmup, dist_on, warm_seconds=args.warm_seconds)
             fps2 = n2 / dt2
@@ -497,6 +643,9 @@ def main():
             entry = {"frames_per_s": fps2, "mpix_per_s": fps2 * s2.width * s2.height / 1e6, "ms_per_frame": 1e3 / fps2,
                      "stage_ms": st2, "kernel_samples": int(t2["frames"]) if t2 else 0, "triangles": s2.triangles,
                      "algorithmic_bytes": s2.algorithmic_bytes(rows=br2.rows)}
+            if world > 1:
+                entry["bands"] = [y1 - y0 for y0, y1 in br2.bands]
+                entry["split_autotune"] = log2
             if s2.shadow is not None:
                 entry["shadow_map"] = f"{s2.shadow.size}^2 D32 pre-pass for the sun (tri_set_shadow, DESIGN.md 5d)"
             if s2.textures:
@@ -529,7 +678,9 @@ def main():
                        "vertices": int(scene.vertices.shape[0]), "bin": stats["bin_size"],
                        "skybox": skybox_name(scene), "frames_in_flight": args.inflight,
                        "parallelism": (f"row-band x{world} + RCCL {'gather to rank 0' if args.assembly == 'gather' else 'all-gather'}"
-                                       if world > 1 else "single GPU")},
+                                       if world > 1 else "single GPU"),
+                       "bands": [y1 - y0 for y0, y1 in br.bands] if world > 1 else None,
+                       "split_autotune": split_log},
             "mpix_per_s": fps * W * H / 1e6,
             "latency_ms": latency,
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

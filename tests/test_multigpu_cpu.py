@@ -198,3 +198,149 @@ def test_band_rows_partition():
         assert len({b[1] - b[0] for b in bands}) == 1
     with pytest.raises(ValueError):
         bench.band_rows(1081, 2, 0)
+
+
+def test_band_split_partition():
+    """bench.band_split: contiguous bands covering [0, H) top to bottom; equal by default (within one row,
+    any height); with display_rows, rank 0 takes exactly that many and the others within one row of each
+    other."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    for H, N, d in [(2160, 1, None), (2160, 2, None), (2161, 3, None), (2160, 8, None), (2160, 2, 1400),
+                    (2160, 8, 540), (1080, 8, 300), (480, 4, 121)]:
+        bands = bench.band_split(H, N, d)
+        assert len(bands) == N and bands[0][0] == 0 and bands[-1][1] == H
+        assert all(bands[i][1] == bands[i + 1][0] for i in range(N - 1))
+        sizes = [b - a for a, b in bands]
+        rest = sizes if d is None else sizes[1:]
+        if rest:
+            assert max(rest) - min(rest) <= 1
+        if d is not None and N > 1:
+            assert sizes[0] == d
+    with pytest.raises(ValueError):
+        bench.band_split(100, 4, 98)
+    assert bench.split_candidates(2160, 8)[0] == 270
+    assert all(2160 - d >= 7 * 32 for d in bench.split_candidates(2160, 8))
+    assert bench.split_candidates(2160, 2)[-1] <= 2160 - 32
+
+
+def _uneven_worker(rank, world, port, scene_name, out_dir, display_rows, ring):
+    """Uneven sort-first bands (a larger display band) rendered by the oracle per rank and assembled by
+    bench.gather_bands (one grouped point-to-point exchange) or by a GatherRing whose display band is a
+    view of the frame (rendered in place)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "3d-renderer_amd", "python"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import oracle_py
+    import scene_cases as sc
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scene = getattr(sc, scene_name)()
+    W, H = scene.width, scene.height
+    bands = bench.band_split(H, world, display_rows)
+    spans = [(a * W, (b - a) * W) for a, b in bands]
+    col, _, _ = oracle_py.render(scene, band=bands[rank], threads=2)
+    mine = torch.from_numpy(np.ascontiguousarray(col).view(np.int32).reshape(-1).copy())
+    if ring:
+        r = bench.GatherRing(world, spans[rank][1], H * W, lambda n: torch.zeros(n, dtype=torch.int32), rank=rank,
+                             spans=spans)
+        for k in range(3):  # three frames through the double buffer; the last one is checked
+            band = r.acquire()
+            if rank == 0:
+                assert band.data_ptr() == r.frames[k % 2].data_ptr()  # the display band is the frame's view
+            band.copy_(mine if k == 2 else torch.full_like(mine, k))
+            r.publish()
+        r.drain()
+        out = r.frame if rank == 0 else None
+    else:
+        out = bench.gather_bands(torch.empty(H * W, dtype=torch.int32), mine, world, rank=rank, spans=spans)
+    if out is not None:
+        np.save(os.path.join(out_dir, "frame.npy"), out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,display_rows,ring", [(2, 230, False), (3, 200, True), (4, 150, False),
+                                                     (4, 90, True)])
+def test_uneven_bands_assemble_to_full_frame(world, display_rows, ring, oracle, tmp_path):
+    import torch.multiprocessing as mp
+
+    import scene_cases as sc
+
+    mp.start_processes(_uneven_worker, args=(world, _free_port(), "textured_grid", str(tmp_path), display_rows, ring),
+                       nprocs=world, join=True, start_method="spawn")
+    col, _, _ = oracle.render(sc.textured_grid(), threads=4)
+    assert np.array_equal(np.load(tmp_path / "frame.npy"), np.ascontiguousarray(col).view(np.int32).reshape(-1))
+
+
+class _FakeBand:
+    """A stand-in BandRenderer for the autotune logic: step() costs a model time that depends on the
+    display-band size and the rank (remote ranks: transfer-bound when their band is large)."""
+
+    def __init__(self, d, rank, H, world):
+        import torch
+
+        self.d, self.rank, self.dev = d, rank, torch.device("cpu")
+        rows = d if rank == 0 else (H - d) / (world - 1)
+        self.cost = 2e-5 * rows * (1.0 if rank == 0 else 3.0)  # remote: transfer 3x slower per row
+        self.closed = False
+
+    def warm(self):
+        pass
+
+    def step(self):
+        t = time.perf_counter() + self.cost
+        while time.perf_counter() < t:
+            pass
+
+    def drain(self):
+        pass
+
+    def close(self):
+        self.closed = True
+
+
+import time  # noqa: E402
+
+
+def _autotune_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    H = 1000
+    made = []
+
+    def make(d):
+        made.append(_FakeBand(d, rank, H, world))
+        return made[-1]
+
+    d, log = bench.autotune_split(make, H, world, True, frames=12, rounds=2, warm_seconds=0.01)
+    assert all(b.closed for b in made)
+    np.save(os.path.join(out_dir, f"pick{rank}.npy"), np.array([d] + [x for x, _ in log]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_autotune_split_picks_the_balanced_display_band(tmp_path):
+    """Model: rank 0 costs d rows, each remote rank (H - d) rows at 3x per row (a slow link). The best
+    candidate balances them (d = 0.75 H at world 2); every rank picks the same split (max-over-ranks rates)."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    mp.start_processes(_autotune_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    picks = [np.load(tmp_path / f"pick{r}.npy") for r in range(world)]
+    assert np.array_equal(picks[0], picks[1])
+    d, cands = int(picks[0][0]), [int(x) for x in picks[0][1:]]
+    assert cands == [500, 625, 750, 875]
+    assert d == 750, (d, cands)  # 1.5 x the equal band: the balance point
