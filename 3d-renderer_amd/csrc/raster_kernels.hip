@@ -1543,16 +1543,16 @@ __device__ __forceinline__ float interp_fast(float w0, float w1, float w2, float
 // edge functions at the pixel, e0 = S + (y1 - y2) dx + (x2 - x1) dy, e1 = y2 dx - x2 dy, e2 = x1 dy - y1 dx
 // (S the exact doubled area, so e0 + e1 + e2 = S), weighted by 1/w: q_k = e_k iw_k, w_k = q_k / (q0 + q1 + q2).
 // This is the barycentric form scaled by S iw0, which cancels in the normalisation, so the only reciprocal is
-// that of the sum (no 1/S, no 1/iw0). Relative to vertex 0, not to a bin: every bin, band and code path
-// gives a pixel the same bits.
+// that of the sum (no 1/S, no 1/iw0). e0 is formed about vertex 1, e0 = (x2 - x1)(dy - y1) - (y2 - y1)(dx - x1)
+// (the same function: its constant term is S), so no area product is needed. Every offset is an exact
+// integer below 2^24 inside the guard band, converted once. Relative to the triangle's own vertices, not to a
+// bin: every bin, band and code path gives a pixel the same bits.
 __device__ __forceinline__ void fast_weights(const TriRec& r, int32_t px, int32_t py, float& w0, float& w1, float& w2) {
     const int32_t x1 = r.X[1] - r.X[0], y1 = r.Y[1] - r.Y[0], x2 = r.X[2] - r.X[0], y2 = r.Y[2] - r.Y[0];
     const float fx1 = (float)x1, fy1 = (float)y1, fx2 = (float)x2, fy2 = (float)y2;
-    // the exact area, rounded once: |x|, |y| < 2^23, so both products and their difference are exact in
-    // double (one v_fma_f64 instead of a 64-bit integer product and its int64 -> float conversion)
-    const float fS = (float)__builtin_fma((double)x1, (double)y2, -((double)y1 * (double)x2));
-    const float dx = (float)(256 * px + 128 - r.X[0]), dy = (float)(256 * py + 128 - r.Y[0]);
-    const float e0 = __builtin_fmaf((float)(x2 - x1), dy, __builtin_fmaf((float)(y1 - y2), dx, fS));
+    const int32_t idx = 256 * px + 128 - r.X[0], idy = 256 * py + 128 - r.Y[0];
+    const float dx = (float)idx, dy = (float)idy;
+    const float e0 = __builtin_fmaf((float)(x2 - x1), (float)(idy - y1), -((float)(y2 - y1) * (float)(idx - x1)));
     const float e1 = __builtin_fmaf(-fx2, dy, fy2 * dx);
     const float e2 = __builtin_fmaf(fx1, dy, -fy1 * dx);
     const float q0 = e0 * r.iw[0], q1 = e1 * r.iw[1], q2 = e2 * r.iw[2];

@@ -191,10 +191,10 @@ class BandRenderer:
         from trident_raster import abi, raster, scenes
 
         H, W = scene.height, scene.width
-        if band_world or assembly == "allgather":  # equal bands (the all-gather needs equal sizes)
-            self.bands = [band_rows(H, band_world or world, r) for r in range(band_world or world)]
-        else:
-            self.bands = band_split(H, world, display_rows)
+        if assembly == "allgather" and not band_world:  # equal bands (the all-gather needs equal sizes)
+            self.bands = [band_rows(H, world, r) for r in range(world)]
+        else:  # band_world: one band of an N-way split rendered alone (diagnostics, no collective)
+            self.bands = band_split(H, band_world or world, display_rows)
         self.band = self.bands[rank]
         rows = self.band[1] - self.band[0]
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
@@ -292,16 +292,18 @@ class BandRenderer:
         return ts[len(ts) // 2]
 
 
-def split_candidates(height, world, min_rows=32):
-    """Display-band sizes autotune_split tries: the equal split and display bands up to 3x it, as long
-    as every other rank keeps at least `min_rows` rows (one bin row)."""
+def split_candidates(height, world, min_rows=32, inflights=(2,)):
+    """(display rows, frames in flight) pairs autotune_split tries: the equal split and display bands up to
+    2.5x it, as long as every other rank keeps at least `min_rows` rows (one bin row), at each frame count
+    in `inflights` (a band's kernels are short at large N, and a third frame in flight keeps more of the
+    GPU busy: N = 8 rank 4 on one GPU 33.4k frames/s with 2, 39.0k with 3, 33.1k with 4)."""
     base = height / world
-    out = []
-    for m in (1.0, 1.25, 1.5, 1.75, 2.0, 2.5, 3.0):
+    ds = []
+    for m in (1.0, 1.25, 1.5, 2.0, 2.5):
         d = int(round(base * m))
-        if height - d >= (world - 1) * min_rows and d not in out:
-            out.append(d)
-    return out
+        if height - d >= (world - 1) * min_rows and d not in ds:
+            ds.append(d)
+    return [(d, k) for k in inflights for d in ds]
 
 
 def measure_fps(br, frames, dist_on):
@@ -328,16 +330,18 @@ def measure_fps(br, frames, dist_on):
     return frames / max_over_ranks(time.perf_counter() - t0, br.dev, dist_on)
 
 
-def autotune_split(make, height, world, dist_on, frames=80, rounds=2, warm_seconds=0.25, candidates=None):
-    """Sort-first load balancing on the hardware: every candidate display-band size (split_candidates) is
-    built (make(display_rows) -> BandRenderer) and timed over `rounds` interleaved rounds of `frames`
-    frames (the best round counts, so a clock ramp or a noisy round does not decide); the fastest wins,
-    ties going to the more even split. Every rank computes the same max-over-ranks rates, so every rank
-    picks the same split without a broadcast. Returns (display_rows, [(display_rows, frames/s), ...])."""
-    cands = candidates or split_candidates(height, world)
+def autotune_split(make, height, world, dist_on, frames=80, rounds=2, warm_seconds=0.25, candidates=None,
+                   inflights=(2, 3)):
+    """Sort-first load balancing on the hardware: every candidate (display-band size, frames in flight)
+    (split_candidates) is built (make(display_rows, inflight) -> BandRenderer) and timed over `rounds`
+    interleaved rounds of `frames` frames (the best round counts, so a clock ramp or a noisy round does not
+    decide); the fastest wins, ties going to the more even split and fewer frames in flight. Every rank
+    computes the same max-over-ranks rates, so every rank picks the same candidate without a broadcast.
+    Returns ((display_rows, inflight), [(display_rows, inflight, frames/s), ...])."""
+    cands = candidates or split_candidates(height, world, inflights=inflights)
     brs = []
-    for d in cands:
-        br = make(d)
+    for d, k in cands:
+        br = make(d, k)
         br.warm()
         brs.append(br)
     t_end = time.perf_counter() + warm_seconds  # the GPU's clock ramp out of idle, before any measurement
@@ -353,8 +357,8 @@ def autotune_split(make, height, world, dist_on, frames=80, rounds=2, warm_secon
             best[i] = max(best[i], measure_fps(br, frames, dist_on))
     for br in brs:
         br.close()
-    pick = max(range(len(cands)), key=lambda i: (best[i], -cands[i]))
-    return cands[pick], list(zip(cands, best))
+    pick = max(range(len(cands)), key=lambda i: (best[i], -cands[i][0], -cands[i][1]))
+    return cands[pick], [(d, k, f) for (d, k), f in zip(cands, best)]
 
 
 def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, warm_seconds=0.25):
@@ -565,6 +569,8 @@ def main():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostics (1 GPU, no collective): render only band --sim-rank of an N-way split")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--sim-display-rows", type=int, default=None,
+                    help="diagnostics: the simulated split's display band (rank 0) size, the others sharing the rest")
     ap.add_argument("--inflight", type=int, default=2,
                     help="frames in flight per rank (contexts taking frames in turn, one stream each)")
     ap.add_argument("--assembly", choices=("gather", "allgather"), default="gather",
@@ -572,6 +578,8 @@ def main():
     ap.add_argument("--split", default="auto",
                     help="N > 1 gather: 'auto' (time candidate display-band sizes on the hardware, keep the fastest), "
                          "'equal', or the display rank's row count")
+    ap.add_argument("--inflight-candidates", default="2,3",
+                    help="N > 1 with --split auto: the frames-in-flight counts the autotune tries")
     ap.add_argument("--no-stage-timing", action="store_true",
                     help="diagnostics: no per-kernel HIP events in the timed loop (roofline fields become null)")
     args = ap.parse_args()
@@ -592,25 +600,28 @@ def main():
 
     scene = build_scene(args.config)
 
-    def make_renderer(sc, display_rows=None):
-        return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=args.inflight,
+    def make_renderer(sc, display_rows=None, inflight=None):
+        return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=inflight or args.inflight,
                             display_rows=display_rows)
 
     def choose_split(sc):
-        """(display_rows or None, the autotune log) for a config at this world size."""
+        """((display_rows or None, frames in flight), the autotune log) for a config at this world size."""
         if world == 1 or args.assembly != "gather" or args.split == "equal":
-            return None, None
+            return (None, args.inflight), None
         if args.split != "auto":
-            return int(args.split), None
-        return autotune_split(lambda d: make_renderer(sc, d), sc.height, world, dist_on,
-                              warm_seconds=args.warm_seconds)
+            return (int(args.split), args.inflight), None
+        return autotune_split(lambda d, k: make_renderer(sc, d, k), sc.height, world, dist_on,
+                              warm_seconds=args.warm_seconds,
+                              inflights=tuple(int(k) for k in args.inflight_candidates.split(",")))
 
     split_log = None
+    inflight = args.inflight
     if args.sim_world and world == 1:
-        br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=args.inflight)
+        br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=args.inflight,
+                          display_rows=args.sim_display_rows)
     else:
-        display_rows, split_log = choose_split(scene)
-        br = make_renderer(scene, display_rows)
+        (display_rows, inflight), split_log = choose_split(scene)
+        br = make_renderer(scene, display_rows, inflight)
     dt, timing, n_warm = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing,
                                    warm_seconds=args.warm_seconds)
     fps = args.steps / dt
@@ -634,8 +645,8 @@ def main():
     if not args.no_secondary and args.config == "c3":
         for key in ("c2", "c5"):  # the other BASELINE.json GPU configs, same timing protocol
             s2 = build_scene(key)
-            d2, log2 = choose_split(s2)
-            br2 = make_renderer(s2, d2)
+            (d2, k2), log2 = choose_split(s2)
+            br2 = make_renderer(s2, d2, k2)
             n2 = max(args.steps, 50) if key == "c2" else max(args.steps // 2, 20)
             dt2, t2, _ = timed_run(br2, n2, args.warmup, dist_on, warm_seconds=args.warm_seconds)
             fps2 = n2 / dt2
@@ -645,6 +656,7 @@ def main():
                      "algorithmic_bytes": s2.algorithmic_bytes(rows=br2.rows)}
             if world > 1:
                 entry["bands"] = [y1 - y0 for y0, y1 in br2.bands]
+                entry["frames_in_flight"] = k2
                 entry["split_autotune"] = log2
             if s2.shadow is not None:
                 entry["shadow_map"] = f"{s2.shadow.size}^2 D32 pre-pass for the sun (tri_set_shadow, DESIGN.md 5d)"
@@ -676,7 +688,7 @@ def main():
             "data": "synthetic (procedural PCG32-seeded scene; reference Assimp assets absent)",
             "config": {"workload": scene.name, "width": W, "height": H, "triangles": scene.triangles,
                        "vertices": int(scene.vertices.shape[0]), "bin": stats["bin_size"],
-                       "skybox": skybox_name(scene), "frames_in_flight": args.inflight,
+                       "skybox": skybox_name(scene), "frames_in_flight": inflight,
                        "parallelism": (f"row-band x{world} + RCCL {'gather to rank 0' if args.assembly == 'gather' else 'all-gather'}"
                                        if world > 1 else "single GPU"),
                        "bands": [y1 - y0 for y0, y1 in br.bands] if world > 1 else None,

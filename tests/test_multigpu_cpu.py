@@ -220,9 +220,10 @@ def test_band_split_partition():
             assert sizes[0] == d
     with pytest.raises(ValueError):
         bench.band_split(100, 4, 98)
-    assert bench.split_candidates(2160, 8)[0] == 270
-    assert all(2160 - d >= 7 * 32 for d in bench.split_candidates(2160, 8))
-    assert bench.split_candidates(2160, 2)[-1] <= 2160 - 32
+    assert bench.split_candidates(2160, 8)[0] == (270, 2)
+    assert all(2160 - d >= 7 * 32 for d, _ in bench.split_candidates(2160, 8, inflights=(2, 3)))
+    assert bench.split_candidates(2160, 2)[-1][0] <= 2160 - 32
+    assert {k for _, k in bench.split_candidates(2160, 4, inflights=(2, 3))} == {2, 3}
 
 
 def _uneven_worker(rank, world, port, scene_name, out_dir, display_rows, ring):
@@ -283,12 +284,14 @@ class _FakeBand:
     """A stand-in BandRenderer for the autotune logic: step() costs a model time that depends on the
     display-band size and the rank (remote ranks: transfer-bound when their band is large)."""
 
-    def __init__(self, d, rank, H, world):
+    def __init__(self, d, rank, H, world, inflight):
         import torch
 
         self.d, self.rank, self.dev = d, rank, torch.device("cpu")
         rows = d if rank == 0 else (H - d) / (world - 1)
         self.cost = 2e-5 * rows * (1.0 if rank == 0 else 3.0)  # remote: transfer 3x slower per row
+        if inflight == 3:  # the model's third frame in flight hides a tenth of the work
+            self.cost *= 0.9
         self.closed = False
 
     def warm(self):
@@ -320,13 +323,13 @@ def _autotune_worker(rank, world, port, out_dir):
     H = 1000
     made = []
 
-    def make(d):
-        made.append(_FakeBand(d, rank, H, world))
+    def make(d, k):
+        made.append(_FakeBand(d, rank, H, world, k))
         return made[-1]
 
-    d, log = bench.autotune_split(make, H, world, True, frames=12, rounds=2, warm_seconds=0.01)
-    assert all(b.closed for b in made)
-    np.save(os.path.join(out_dir, f"pick{rank}.npy"), np.array([d] + [x for x, _ in log]))
+    (d, k), log = bench.autotune_split(make, H, world, True, frames=12, rounds=2, warm_seconds=0.01)
+    assert all(b.closed for b in made) and len(made) == len(log)
+    np.save(os.path.join(out_dir, f"pick{rank}.npy"), np.array([d, k] + [x for x, _, _ in log]))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -341,6 +344,6 @@ def test_autotune_split_picks_the_balanced_display_band(tmp_path):
                        start_method="spawn")
     picks = [np.load(tmp_path / f"pick{r}.npy") for r in range(world)]
     assert np.array_equal(picks[0], picks[1])
-    d, cands = int(picks[0][0]), [int(x) for x in picks[0][1:]]
-    assert cands == [500, 625, 750, 875]
-    assert d == 750, (d, cands)  # 1.5 x the equal band: the balance point
+    d, k, cands = int(picks[0][0]), int(picks[0][1]), [int(x) for x in picks[0][2:]]
+    assert cands == [500, 625, 750] * 2
+    assert (d, k) == (750, 3), (d, k, cands)  # 1.5 x the equal band: the balance point
