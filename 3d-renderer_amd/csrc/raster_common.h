@@ -212,8 +212,9 @@ struct TriFrameParams {
     TriShadeConst sc;
     TriDrawDev draw0;  // the draw when one_draw (its vertex and primitive slots start at 0)
     // cluster culling (row bands): k_vertex marks ncl_total (draw, cluster) pairs; cull_vertex also lets
-    // k_vertex skip vertex blocks (off while the shadow pre-pass needs every caster)
-    uint32_t cull_on, cull_vertex, ncl_total, pad_c;
+    // k_vertex skip vertex blocks (off while the shadow pre-pass needs every caster); setup_multi: k_setup
+    // runs a quarter of the chunks' workgroups, four strided chunks each (single-draw bands, no pre-pass)
+    uint32_t cull_on, cull_vertex, ncl_total, setup_multi;
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
     uint32_t shadow_on, s_size, s_nbx, s_nbins;
     uint32_t s_bin_cap;

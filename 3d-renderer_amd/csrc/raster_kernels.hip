@@ -337,6 +337,33 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
     if (!valid || (fp.cull_vertex && !needed)) return;
     vertex_slot(fp, b, slot, fp.one_draw ? fp.draw0 : b.draws[d], vbase);
 }
+
+// Row bands of single-draw frames (cull_vertex && one_draw): a quarter of k_vertex's workgroups, each owning
+// the four 256-slot vertex blocks blockIdx.x + i * gridDim.x (i = 0..3). Wave i tests block i's union box
+// (the four tests run side by side instead of four waves repeating one), the flags meet in LDS, and the
+// whole workgroup transforms the visible blocks one after another. A band's visible blocks are contiguous
+// in slot order (its rows' clusters), so the stride spreads them over different workgroups: at N = 8 a
+// workgroup holds at most one, and 3/4 of the launch's dispatches (all empty) are gone. The cluster flags
+// for k_setup are the same lanes' work as in k_vertex, grid-strided.
+__global__ __launch_bounds__(TRI_BLOCK) void k_vertex_band(TriFrameParams fp, TriDeviceBuffers b) {
+    __shared__ uint32_t blk_vis[TRI_BLOCK / 64];
+    const uint32_t tid = threadIdx.x, G = gridDim.x;
+    if (blockIdx.x == 0 && tid == 0) reset_counters(b.counters);
+    const TriDrawDev& dr = fp.draw0;
+    for (uint32_t c = blockIdx.x * TRI_BLOCK + tid; c < fp.ncl_total; c += G * TRI_BLOCK)
+        b.cvis[c] = cluster_visible(fp, dr, b.clusters[dr.cl_first + c]) ? 1u : 0u;
+    const uint32_t nblk = (fp.nslots + TRI_VBLOCK - 1) / TRI_VBLOCK;
+    const uint32_t w = tid / 64u, blk = blockIdx.x + w * G;
+    const bool vis = blk < nblk && cluster_visible(fp, dr, b.vbox[dr.vblk_first + blk]);
+    if ((tid & 63u) == 0) blk_vis[w] = vis ? 1u : 0u;
+    __syncthreads();
+#pragma unroll
+    for (uint32_t i = 0; i < TRI_BLOCK / 64; ++i) {
+        if (!blk_vis[i]) continue;  // uniform
+        const uint32_t slot = (blockIdx.x + i * G) * TRI_VBLOCK + tid;
+        if (slot < fp.nslots) vertex_slot(fp, b, slot, dr, 0u);
+    }
+}
 #endif  // TRI_RASTER_PLAIN_TU
 
 // ------------------------------------------------------------------------------------------
@@ -823,16 +850,36 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     __shared__ uint32_t dpb[kLdsDraws + 1], dfi[kLdsDraws], dvb[kLdsDraws], dcb[kLdsDraws];
     const bool lds_draws = !ONE && !fp.one_draw && fp.ndraws <= (uint32_t)kLdsDraws;
     __shared__ BinBox bin_box;
+    // Row bands of single-draw frames (fp.setup_multi): a quarter of the chunks' workgroups, each owning the
+    // four chunks blockIdx.x + i * gridDim.x. Wave i reads chunk i's cluster flags, and the workgroup sets up
+    // and bins the visible ones in turn (a band's visible chunks are contiguous, so the stride gives each
+    // workgroup at most one at N = 8, and 3/4 of the launch's mostly empty dispatches are gone).
+    __shared__ uint32_t chunk_vis[TRI_BLOCK / 64];
+    const bool multi = ONE && !WITH_SHADOW && fp.cull_on && fp.setup_multi;
+    const auto chunk_visible = [&](uint32_t ck) {
+        const uint32_t p0 = ck * (uint32_t)(TRI_BLOCK * fp.ppt);
+        const uint32_t p1 = min(p0 + (uint32_t)(TRI_BLOCK * fp.ppt), fp.nprims);
+        bool any = false;
+        for (uint32_t c = p0 / TRI_CLUSTER_PRIMS; c <= (p1 - 1) / TRI_CLUSTER_PRIMS && !any; ++c) any = b.cvis[c] != 0u;
+        return any;
+    };
     if constexpr (ONE && !WITH_SHADOW) {
-        // A row band's chunk whose clusters k_vertex culled (most chunks at N = 8): the whole workgroup
-        // leaves before the LDS set-up and the binning barriers (its cluster flags: a few scalar loads)
-        if (fp.cull_on) {
-            const uint32_t ck = (uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks);
-            const uint32_t p0 = ck * (uint32_t)(TRI_BLOCK * fp.ppt);
-            const uint32_t p1 = min(p0 + (uint32_t)(TRI_BLOCK * fp.ppt), fp.nprims);
+        if (multi) {
+            const uint32_t w = threadIdx.x / 64u, ck = blockIdx.x + w * gridDim.x;
+            const bool vis = ck < fp.nchunks && chunk_visible(ck);
+            if ((threadIdx.x & 63u) == 0) chunk_vis[w] = vis ? 1u : 0u;
+            __syncthreads();
             bool any = false;
-            for (uint32_t c = p0 / TRI_CLUSTER_PRIMS; c <= (p1 - 1) / TRI_CLUSTER_PRIMS && !any; ++c) any = b.cvis[c] != 0u;
+#pragma unroll
+            for (int i = 0; i < TRI_BLOCK / 64; ++i) any = any || chunk_vis[i] != 0u;
             if (!any) {
+                if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(0u, 0u);
+                return;
+            }
+        } else if (fp.cull_on) {
+            // A row band's chunk whose clusters k_vertex culled (most chunks at N = 8): the whole workgroup
+            // leaves before the LDS set-up and the binning barriers (its cluster flags: a few scalar loads)
+            if (!chunk_visible((uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks))) {
                 if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(0u, 0u);
                 return;
             }
@@ -853,10 +900,13 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     __syncthreads();
     uint32_t nsetup = 0, nentries = 0, sentries = 0;
     const uint32_t lane = lanes_below(~0ull);
+    uint32_t round_base = 0;  // binning rounds so far (the bin box alternates its two halves per round)
+    for (uint32_t ci = 0; ci < (multi ? (uint32_t)(TRI_BLOCK / 64) : 1u); ++ci) {
+    if (multi && !chunk_vis[ci]) continue;  // uniform
     // Spread concurrently running workgroups over the primitive stream: meshes are usually
     // index-ordered in screen space, and neighbouring chunks hammering the same bin counters
     // serialise their atomics. The stride is coprime to nchunks, so the remap is a bijection.
-    const uint32_t chunk = (uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks);
+    const uint32_t chunk = multi ? blockIdx.x + ci * gridDim.x : (uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks);
     const uint32_t chunk0 = chunk * (uint32_t)(TRI_BLOCK * fp.ppt);
     // Two primitives per lane, set up and binned together: both index/vertex fetch chains are in
     // flight at once, and the queue reservations of both are batched (one atomic round trip per
@@ -960,12 +1010,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 }
             }
         }
-        bin_pair_box<false>(b, bin_box, (uint32_t)(k / kSetupGroup), ok, br, p, (uint32_t)fp.nbx, b.bin_count,
-                            b.bin_list, fp.bin_cap, lane, nentries);
+        bin_pair_box<false>(b, bin_box, round_base + (uint32_t)(k / kSetupGroup), ok, br, p, (uint32_t)fp.nbx,
+                            b.bin_count, b.bin_list, fp.bin_cap, lane, nentries);
         if constexpr (WITH_SHADOW)
-            bin_pair_box<true>(b, bin_box, (uint32_t)(k / kSetupGroup), sok, sbr, p, fp.s_nbx, b.sbin_count,
-                               b.sbin_list, fp.s_bin_cap, lane, sentries);
+            bin_pair_box<true>(b, bin_box, round_base + (uint32_t)(k / kSetupGroup), sok, sbr, p, fp.s_nbx,
+                               b.sbin_count, b.sbin_list, fp.s_bin_cap, lane, sentries);
         if (k == 0) TRI_SSTAMP(2);
+    }
+    round_base += (uint32_t)((fp.ppt + kSetupGroup - 1) / kSetupGroup);
     }
     if (nsetup) atomicAdd(&red[0], nsetup);
     if (nentries) atomicAdd(&red[1], nentries);
@@ -2469,6 +2521,15 @@ static void launch_raster(const TriFrameParams& fp, const TriDeviceBuffers& b, h
     else (void)tri_launch_raster_plain(fp, b, stream);  // raster_plain.hip (errors surface in hipGetLastError)
 }
 
+// TRI_BAND_VERTEX=0: row bands of single-draw frames take k_vertex instead of k_vertex_band (A/B only)
+static bool band_vertex_off() {
+    static const bool off = [] {
+        const char* e = getenv("TRI_BAND_VERTEX");
+        return e && e[0] == '0';
+    }();
+    return off;
+}
+
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* ev) {
     static const bool debug_sync = getenv("TRI_DEBUG_SYNC") != nullptr;
@@ -2481,7 +2542,11 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         }
     };
     rec(kStageVertex);
-    if (fp.nslots > 0)
+    if (fp.nslots > 0 && fp.cull_vertex && fp.one_draw && !band_vertex_off())
+        // one workgroup per four vertex blocks (TRI_VBLOCK == TRI_BLOCK slots each)
+        hipLaunchKernelGGL(k_vertex_band, dim3((fp.nslots + 4u * TRI_VBLOCK - 1) / (4u * TRI_VBLOCK)), dim3(TRI_BLOCK), 0,
+                           stream, fp, b);
+    else if (fp.nslots > 0)
         // with cluster culling every (draw, cluster) flag needs a lane, even when a mesh has fewer vertices
         hipLaunchKernelGGL(k_vertex, dim3(((fp.cull_on && fp.ncl_total > fp.nslots ? fp.ncl_total : fp.nslots) + TRI_BLOCK - 1) / TRI_BLOCK),
                            dim3(TRI_BLOCK), 0, stream, fp, b);
@@ -2489,7 +2554,7 @@ hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b,
         hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
     rec(kStageSetup);
     if (fp.nchunks > 0) {  // with the pre-pass, one set-up pass bins each primitive for the frame and the map
-        const dim3 g(fp.nchunks), t(TRI_BLOCK);
+        const dim3 g(fp.setup_multi ? (fp.nchunks + 3u) / 4u : fp.nchunks), t(TRI_BLOCK);
         if (fp.shadow_on) {
             if (fp.one_draw) hipLaunchKernelGGL((k_setup<true, true>), g, t, 0, stream, fp, b);
             else hipLaunchKernelGGL((k_setup<true, false>), g, t, 0, stream, fp, b);

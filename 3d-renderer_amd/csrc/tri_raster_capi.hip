@@ -1116,6 +1116,14 @@ int tri_render(tri_ctx* c) {
     fp.cull_on = culling ? 1u : 0u;
     fp.cull_vertex = fp.cull_on && !c->shadow.size ? 1u : 0u;  // the pre-pass needs every caster
     fp.ncl_total = c->ncl_total;
+    {
+        static const bool multi_off = [] {  // TRI_BAND_SETUP=0: one chunk per k_setup workgroup (A/B only)
+            const char* e = getenv("TRI_BAND_SETUP");
+            return e && e[0] == '0';
+        }();
+        fp.setup_multi = fp.cull_on && fp.one_draw && !c->shadow.size && !multi_off ? 1u : 0u;
+        if (fp.setup_multi) c->last_nchunks = (fp.nchunks + 3u) / 4u;  // the launch's statistics slots
+    }
     if (c->shadow.size) {
         fp.shadow_on = 1u;
         fp.s_size = c->shadow.size;
