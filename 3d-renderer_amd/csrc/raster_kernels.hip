@@ -1244,6 +1244,79 @@ __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int3
     }
 }
 
+// Span walk (the per-lane path of 32x32 bins, triangles under 64 px on a side): each row's covered pixels
+// are the integer x with f_k(x) = F_k + A_k (x - cx0) >= 0 for k = 0..2, an interval [L, R] found from the
+// three crossings v_k = -F_k / A_k instead of testing every bbox pixel (the bbox of a C3 triangle is ~3x
+// its area). Exact: with |A_k| < 2^14, |F_k| < 2^21 (converted to float exactly) and v_rcp's 1-ulp
+// reciprocal, t = fma(-F, 1/A, -/+delta) lies within 2^-16 of v -/+ delta for |v| <= 64, and a
+// non-integer v is at least 1/|A| > 2^-14 from every integer, so with delta = 2^-15 ceil(t) = ceil(v) on
+// the left (A > 0) and floor(t) = floor(v) on the right (A < 0), integer v included; crossings further
+// than 64 px lie outside the 32-px bin either way. A horizontal edge (A = 0) empties the row when F < 0
+// (scale 2^100 on the left side). Then the same keys as raster_serial over [L, R] only.
+template <int BL>
+__device__ __forceinline__ void raster_span(const TriRec& r, int32_t cx0, int32_t cx1, int32_t cy0, int32_t cy1,
+                                            int32_t ox, int32_t oy, uint64_t* keys, int32_t sub = 0,
+                                            int32_t step = 1) {
+    const int32_t xmin = min(r.X[0], min(r.X[1], r.X[2])), xmax = max(r.X[0], max(r.X[1], r.X[2]));
+    const int32_t ymin = min(r.Y[0], min(r.Y[1], r.Y[2])), ymax = max(r.Y[0], max(r.Y[1], r.Y[2]));
+    if (!(xmax - xmin < 16384 && ymax - ymin < 16384)) {
+        raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys, sub, step);
+        return;
+    }
+    int32_t A[3], B[3], F[3];
+    float dzdX, dzdY;
+    edge_start(r, cx0, cy0, A, B, F, dzdX, dzdY);  // the 32-bit form: never rejects
+    constexpr float kDelta = 0x1p-15f;
+    float nrl[3], dl[3], nrr[3], dr[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const float rc = -__builtin_amdgcn_rcpf((float)A[k]);
+        nrl[k] = A[k] > 0 ? rc : (A[k] == 0 ? -0x1p100f : 0.0f);
+        dl[k] = A[k] >= 0 ? -kDelta : -INFINITY;
+        nrr[k] = A[k] < 0 ? rc : 0.0f;
+        dr[k] = A[k] < 0 ? kDelta : INFINITY;
+    }
+    const bool far_clip = (r.z[0] > 1.0f) || (r.z[1] > 1.0f) || (r.z[2] > 1.0f);
+    const uint32_t low = key_low(r.prim_sub);
+    const float wmax = (float)(cx1 - cx0);
+    const int32_t fx0 = 256 * cx0 + 128 - r.X[0];
+    float fdy = (float)(256 * (cy0 + sub) + 128 - r.Y[0]);
+    uint32_t row = (uint32_t)(((cy0 + sub - oy) << BL) + (cx0 - ox));
+#pragma unroll
+    for (int k = 0; k < 3; ++k) F[k] += B[k] * sub;
+    for (int32_t py = cy0 + sub; py <= cy1; py += step) {
+        const float f0 = (float)F[0], f1 = (float)F[1], f2 = (float)F[2];
+        const float tl = fmaxf(fmaxf(__builtin_fmaf(f0, nrl[0], dl[0]), __builtin_fmaf(f1, nrl[1], dl[1])),
+                               __builtin_fmaf(f2, nrl[2], dl[2]));
+        const float tr = fminf(fminf(__builtin_fmaf(f0, nrr[0], dr[0]), __builtin_fmaf(f1, nrr[1], dr[1])),
+                               __builtin_fmaf(f2, nrr[2], dr[2]));
+        const float Lf = fmaxf(ceilf(tl), 0.0f), Rf = fminf(floorf(tr), wmax);
+        if (Lf <= Rf) {  // both in [0, wmax] here: the conversions are exact
+            const int32_t L = (int32_t)Lf, R = (int32_t)Rf;
+            const float t2 = dzdY * fdy;
+            float fdx = (float)(fx0 + 256 * L);
+            const uint32_t rend = row + (uint32_t)R;
+            if (!far_clip) {  // (nearly every triangle: no per-pixel far-plane test)
+                for (uint32_t a = row + (uint32_t)L; a <= rend; ++a) {
+                    uint64_t key;
+                    depth_key((r.z[0] + dzdX * fdx) + t2, false, low, key);
+                    atomicMin(&keys[a], key);
+                    fdx += 256.0f;
+                }
+            } else {
+                for (uint32_t a = row + (uint32_t)L; a <= rend; ++a) {
+                    uint64_t key;
+                    if (depth_key((r.z[0] + dzdX * fdx) + t2, true, low, key)) atomicMin(&keys[a], key);
+                    fdx += 256.0f;
+                }
+            }
+        }
+        F[0] += B[0] * step; F[1] += B[1] * step; F[2] += B[2] * step;
+        fdy += 256.0f * (float)step;
+        row += (uint32_t)step << BL;
+    }
+}
+
 // ------------------------------------------------------------------------------------------
 // tile_raster_shade: Default.frag
 // ------------------------------------------------------------------------------------------
@@ -1982,10 +2055,17 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 // exactly like raster_serial (integer edge functions, float depth offsets in steps of 256: exact), so
 // the keys are bit-identical.
 #ifndef TRI_COV_SHARE
-#define TRI_COV_SHARE 2  // 32x32 bins: lanes per triangle when the bin has at most TRI_COV_SHARE_MAX entries
+// 32x32 bins: lanes per triangle when the bin has at most TRI_COV_SHARE_MAX entries. Two lanes per triangle
+// paid with the per-pixel bbox walk (round 2); with the span walk one lane per triangle is faster (C3 k_raster
+// 95.3 -> 94.0 us; four lanes 94.5)
+#define TRI_COV_SHARE 1
 #endif
 #ifndef TRI_COV_SHARE_MAX
 #define TRI_COV_SHARE_MAX (TRI_BLOCK / TRI_COV_SHARE)  // one entry per lane group
+#endif
+// the shadow pre-pass's per-pixel walk (shadow_serial) keeps two lanes per triangle
+#ifndef TRI_SHADOW_SHARE
+#define TRI_SHADOW_SHARE 2
 #endif
 static_assert((TRI_COV_SHARE & (TRI_COV_SHARE - 1)) == 0 && TRI_BLOCK % TRI_COV_SHARE == 0,
               "TRI_COV_SHARE must be a power of two dividing the workgroup (each lane group owns one entry)");
@@ -1997,6 +2077,10 @@ static_assert((TRI_COV_SHARE & (TRI_COV_SHARE - 1)) == 0 && TRI_BLOCK % TRI_COV_
 #endif
 #ifndef TRI_COV_BALANCED
 #define TRI_COV_BALANCED 1
+#endif
+// 32x32 bins: the per-lane walk visits each row's covered span only (raster_span)
+#ifndef TRI_SPAN_WALK
+#define TRI_SPAN_WALK 1
 #endif
 constexpr int kCovPass = 160;   // entries per pass (LDS: 64 B each)
 constexpr int kCovJobs = 1024;  // row jobs per pass (u16: entry << 6 | row); rows beyond stay with their lane
@@ -2041,6 +2125,12 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ uint32_t wsum[TRI_BLOCK / 64];
     __shared__ uint32_t nbig, nsky;
     const int tid = threadIdx.x;
+#if TRI_STAGGER
+    // experiment: half the first round's workgroups start late, so a CU's workgroups are not all in the
+    // same phase (coverage: latency-bound; shading: VALU-bound) at once
+    if (blockIdx.x < 2048 && ((blockIdx.x >> 8) & 1))
+        for (int s = 0; s < TRI_STAGGER; s += 8128) __builtin_amdgcn_s_sleep(127);
+#endif
     TRI_STAMP(0);
     if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1);  // (TRI_COV_PRIO above)
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
@@ -2059,7 +2149,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     if constexpr (TRI_QUEUE_PREFETCH && !(TRI_COV_BALANCED && BL == 4)) {
         const Rsrc qr = make_rsrc(b.bin_list + (size_t)bin * fp.bin_cap, 4ull * fp.bin_cap);
         pre1 = __builtin_amdgcn_raw_buffer_load_b32(qr, (uint32_t)tid * 4u, 0, 0);
-        pre2 = __builtin_amdgcn_raw_buffer_load_b32(qr, (uint32_t)(tid / TRI_COV_SHARE) * 4u, 0, 0);
+        pre2 = TRI_COV_SHARE > 1 ? __builtin_amdgcn_raw_buffer_load_b32(qr, (uint32_t)(tid / TRI_COV_SHARE) * 4u, 0, 0) : pre1;
     }
     for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = kBgKey;
     if (fp.need_lut)
@@ -2168,7 +2258,11 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);  // queue full: this lane walks it all
             return;
         }
+#if TRI_SPAN_WALK
+        raster_span<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys, sub, step);
+#else
         raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys, sub, step);
+#endif
     };
     // (Pairing only as many entries as there are spare lanes when the bin holds 129..256 entries, so that
     // every lane works, measured slower: 105.5 -> 109.8 us at C3. The duplicated fetch and set-up of a
@@ -2400,7 +2494,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TriFrameParams fp, 
     __syncthreads();
     const uint32_t* queue = b.sbin_list + (size_t)bin * fp.s_bin_cap;
     const uint32_t n = nentries;
-    const int share = TRI_COV_SHARE > 1 && n <= (uint32_t)TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
+    const int share = n <= (uint32_t)(TRI_BLOCK / TRI_SHADOW_SHARE) ? TRI_SHADOW_SHARE : 1;
     const int sub = tid % share;
     for (uint32_t i = tid / share; i < n; i += TRI_BLOCK / share) {
         const uint32_t ri = queue[i];
