@@ -175,6 +175,9 @@ struct TriShadeConst {
     // and the fast build's uniform albedo factor of such a draw: ((solid * base) * tint).rgb and the
     // fragment alpha (base.a * tint.a) * solid.a, in Default.frag's order of operations
     float sbt[4];
+    // G_L's denominator divided through by 1 - k (the fast build's per-light v_fma becomes one add):
+    // k / (1 - k) and a2 / pi / (1 - k), so NDF * G_L * G_V keeps its value
+    float kgo, a2pio, pad3[2];
 };
 
 struct TriFrameParams {

@@ -1382,6 +1382,25 @@ __device__ __forceinline__ uint32_t unorm8(float c) {
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
 }
 
+// Fast build's tone curve output (Default.frag:185-189 then the UNORM8 store). TRI_SHADE_TRIM: the channel
+// comes back already scaled by 255 — 255 t^(1/2.2) as one exp2 with log2(255) folded into its argument
+// (t = c / (c + 1) lies in [0, 1), so no clamp is needed). Either form is within a small fraction of an LSB
+// of the IEEE value before rounding, so the stored byte stays within the 1-LSB bar. (v_cvt_rpi_i32_f32 would
+// fold the + 0.5 too, but only inline asm reaches it, and the compiler does not guard inline asm against
+// the trans-result hazard: a v_cvt reading a v_exp result in the next slot read a stale register.)
+#ifndef TRI_SHADE_TRIM
+#define TRI_SHADE_TRIM 7  // bits: 1 = G_L denominator, 2 = tone curve, 4 = e0 from the area
+#endif
+__device__ __forceinline__ float tone_out(float t) {
+    constexpr float g = 1.0f / 2.2f;
+    if (TRI_SHADE_TRIM & 2) return __builtin_amdgcn_exp2f(__builtin_fmaf(g, __builtin_amdgcn_logf(t), 7.99435343685886f));
+    return fpow(t, g);
+}
+__device__ __forceinline__ uint32_t fast_u8(float v) {  // v: tone_out's value, in [0, 255]
+    if (!(TRI_SHADE_TRIM & 2)) return unorm8(v);
+    return (uint32_t)(int)(v + 0.5f);
+}
+
 struct __attribute__((aligned(16))) V4 {
     float x, y, z, w;
 };
@@ -1504,7 +1523,7 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
     // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
     // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
-    const float gden = __builtin_fmaf(NdotL, sc.omkg, sc.kg);
+    const float gden = (TRI_SHADE_TRIM & 1) ? NdotL + sc.kgo : __builtin_fmaf(NdotL, sc.omkg, sc.kg);
     const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
     // NDF * G_L * G_V / den with NDF = a2 / (pi dd^2), G_L = NdotL / gden
     const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
@@ -1552,7 +1571,7 @@ __device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const P
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
     // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
     // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
-    const float gden = __builtin_fmaf(NdotL, sc.omkg, sc.kg);
+    const float gden = (TRI_SHADE_TRIM & 1) ? NdotL + sc.kgo : __builtin_fmaf(NdotL, sc.omkg, sc.kg);
     const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
     const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
     const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
@@ -1592,7 +1611,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
     px.NdotV4 = 4.0f * NdotV;
-    px.gVa = sc.a2pi * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
+    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
     f2v cxy = (f2v{sc.amb[0], sc.amb[1]} * albxy) * splat(sc.amb_strength);
     float cz = (sc.amb[2] * albz) * sc.amb_strength;
     if (kAblate & 64) return make_float4(cxy.x, cxy.y, cz, 1.0f);  // diagnostics: 64 = no lights
@@ -1611,11 +1630,10 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         eval_pbr_fast_p(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv, f2v{sc.pl_rad[i][0], sc.pl_rad[i][1]},
                         sc.pl_rad[i][2], att0 * att0, cxy, cz);
     }
-    const float g = 1.0f / 2.2f;
     const f2v c1 = cxy + splat(1.0f);
     const f2v txy = cxy * f2v{frcp(c1.x), frcp(c1.y)};
     const float tz = cz * frcp(cz + 1.0f);
-    return make_float4(fpow(txy.x, g), fpow(txy.y, g), fpow(tz, g), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);
+    return make_float4(tone_out(txy.x), tone_out(txy.y), tone_out(tz), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);
 #else
     PbrPix px;
     px.N = fnorm(fnrm(f));
@@ -1630,7 +1648,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
     px.NdotV4 = 4.0f * NdotV;
-    px.gVa = sc.a2pi * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
+    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
     f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
               sc.amb[2] * albedo.z * sc.amb_strength);
     if (kAblate & 64) return make_float4(c.x, c.y, c.z, 1.0f);  // diagnostics: 64 = no lights
@@ -1651,9 +1669,8 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         eval_pbr_fast(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv,
                       mk(sc.pl_rad[i][0], sc.pl_rad[i][1], sc.pl_rad[i][2]), att0 * att0, c);
     }
-    const float g = 1.0f / 2.2f;
     const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
-    return make_float4(fpow(t.x, g), fpow(t.y, g), fpow(t.z, g), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);
+    return make_float4(tone_out(t.x), tone_out(t.y), tone_out(t.z), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);
 #endif
 }
 
@@ -1677,9 +1694,12 @@ __device__ __forceinline__ void fast_weights(const TriRec& r, int32_t px, int32_
     const float fx1 = (float)x1, fy1 = (float)y1, fx2 = (float)x2, fy2 = (float)y2;
     const int32_t idx = 256 * px + 128 - r.X[0], idy = 256 * py + 128 - r.Y[0];
     const float dx = (float)idx, dy = (float)idy;
-    const float e0 = __builtin_fmaf((float)(x2 - x1), (float)(idy - y1), -((float)(y2 - y1) * (float)(idx - x1)));
     const float e1 = __builtin_fmaf(-fx2, dy, fy2 * dx);
     const float e2 = __builtin_fmaf(fx1, dy, -fy1 * dx);
+    // TRI_SHADE_TRIM: e0 = S - e1 - e2 with the area in float (a weight then carries an absolute error of a
+    // few 2^-24, far inside the colour bar; depth never uses these weights)
+    const float e0 = (TRI_SHADE_TRIM & 4) ? (__builtin_fmaf(fx1, fy2, -fy1 * fx2) - e1) - e2
+                                    : __builtin_fmaf((float)(x2 - x1), (float)(idy - y1), -((float)(y2 - y1) * (float)(idx - x1)));
     const float q0 = e0 * r.iw[0], q1 = e1 * r.iw[1], q2 = e2 * r.iw[2];
     const float iq = frcp((q0 + q1) + q2);
     w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
@@ -2353,8 +2373,13 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             } else {
                 fetch_fragment<EXACT, SHADOW, ONE>(fp, b, key, px, py, lut, f);
             }
-            const float4 c = EXACT ? fs_exact(fp, f) : fs_fast<ONE>(fp.sc, f);
-            out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
+            if (EXACT) {
+                const float4 c = fs_exact(fp, f);
+                out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
+            } else {
+                const float4 c = fs_fast<ONE>(fp.sc, f);
+                out = fast_u8(c.z) | (fast_u8(c.y) << 8) | (fast_u8(c.x) << 16) | (unorm8(c.w) << 24);
+            }
         }
         const size_t o = (size_t)(py - fp.y0) * fp.W + px;
         b.color[o] = out;

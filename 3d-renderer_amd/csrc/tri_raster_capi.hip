@@ -224,6 +224,8 @@ void shade_constants(const tri_global_ubo& g, const tri_material_record& m, TriS
     sc.a2pi = a2 / 3.14159265359f;
     sc.kg = rr * rr * 0.125f;
     sc.omkg = 1.0f - sc.kg;
+    sc.kgo = sc.kg / sc.omkg;     // omkg >= 0.5 (k <= 0.5 for roughness <= 1)
+    sc.a2pio = sc.a2pi / sc.omkg;
     for (int i = 0; i < 3; ++i) sc.amb[i] = g.ambient_color_intensity[i] * g.ambient_color_intensity[3];
     sc.has_sun = g.light_counts[0] > 0u ? 1u : 0u;
     const float lx = -g.directional_light_direction[0], ly = -g.directional_light_direction[1],

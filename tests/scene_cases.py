@@ -100,6 +100,49 @@ def depth_ties(w=256, h=256):
                         materials=[((1, 1, 1, 1), (0.2, 0.5, 1.0, 0.0))])
 
 
+def pixel_aligned_triangles(w=512, h=256, n=8000, seed=11):
+    """Triangles whose vertices sit on quarter-pixel positions under an exact orthographic mapping (world
+    x, y in pixels: the snap lands on them exactly), so edges run through pixel centres and their row
+    crossings are exact integers — the boundary cases of k_raster's span walk (ceil/floor of -F/A, the
+    top-left bias) — plus horizontal and vertical edges, slivers, and triangles on both sides of the
+    64-px limit of the 32-bit edge set-up. Random depths overlap them (key resolve); both windings are
+    emitted at random, so about half are culled. 8000 triangles over 512x256 keep the frame on 32x32 bins
+    (choose_bin_grid: density >= 0.05), the bin size whose per-lane walk is the span walk."""
+    rng = np.random.default_rng(seed)
+    tris = []
+    for k in range(n):
+        kind = k % 6
+        size = [3, 10, 40, 62, 70, 24][kind] * (0.5 + rng.random())
+        cx, cy = rng.uniform(-20, w + 20), rng.uniform(-20, h + 20)
+        if kind == 5:  # axis-aligned right triangle (one horizontal, one vertical edge)
+            a, b = size * rng.choice([-1, 1]), size * rng.choice([-1, 1])
+            p = [(cx, cy), (cx + a, cy), (cx, cy + b)]
+        elif kind == 3 and k % 12 == 3:  # sliver
+            p = [(cx, cy), (cx + size, cy + 0.25 * rng.integers(1, 4)), (cx + size * 0.5, cy + 0.25)]
+        else:
+            p = [(cx + size * rng.uniform(-1, 1), cy + size * rng.uniform(-1, 1)) for _ in range(3)]
+        q = np.round(np.asarray(p, np.float64) * 4.0) / 4.0  # quarter pixels: exact in float and on the snap
+        z = rng.uniform(0.05, 0.95, size=3)
+        if rng.random() < 0.3:
+            z[:] = z[0]  # flat: depth ties between overlapping flat triangles at equal depth are rarer but exact
+        tris.append([(q[i, 0], q[i, 1], z[i]) for i in range(3)])
+    v = np.zeros(3 * n, abi.VERTEX_DTYPE)
+    v["position"] = np.asarray(tris, F).reshape(-1, 3)
+    v["normal"] = (0, 0, 1)
+    v["color"] = rng.uniform(0.2, 1.0, size=(3 * n, 3)).astype(F)
+    v["texcoord"] = rng.uniform(0, 1, size=(3 * n, 2)).astype(F)
+    idx = np.arange(3 * n, dtype=np.uint32)
+    meshes = np.array([(0, idx.size, 0, 0)], abi.MESH_RANGE_DTYPE)
+    view = np.eye(4, dtype=F)
+    proj = np.eye(4, dtype=F)  # [col][row]: clip = (2x/W - 1, 2y/H - 1, z, 1), powers of two, products exact
+    proj[0, 0], proj[3, 0] = F(2.0 / w), F(-1.0)
+    proj[1, 1], proj[3, 1] = F(2.0 / h), F(-1.0)
+    cam = (w / 2.0, h / 2.0, 50.0)
+    draws = [abi.make_draw(0, np.eye(4, dtype=F), material_index=0)]
+    return scenes.Scene("pixel_aligned", w, h, v, idx, meshes, draws, scenes.pack_ubo(view, proj, cam, []),
+                        materials=[((1, 1, 1, 1), (0.1, 0.5, 1.0, 0.0))])
+
+
 def large_quads(w=1920, h=1080, one_draw=False):
     """Screen-filling quads over 1920x1080 (2040 bins of 32x32): a set-up round whose bins span more than
     k_setup's 1024-cell LDS grid, so binning takes the per-wave reservation path."""

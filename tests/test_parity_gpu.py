@@ -86,6 +86,14 @@ def test_c3_full_4k_1m_triangles(oracle, flags):
     assert_parity(scenes.scene_c3_grid(), oracle, min_covered=3840 * 2160 // 2, flags=flags)
 
 
+@pytest.mark.parametrize("seed", [11, 12])
+def test_pixel_aligned_span_walk(oracle, flags, seed):
+    """Edges through pixel centres (exact-integer row crossings), horizontal/vertical edges, slivers and
+    triangles either side of the 64-px 32-bit set-up limit: the span walk's boundary cases, depth bit-exact
+    against the oracle's per-pixel LEQUAL raster."""
+    assert_parity(sc.pixel_aligned_triangles(seed=seed), oracle, min_covered=100000, flags=flags)
+
+
 def test_textured_srgb_bilinear_repeat(oracle, flags):
     assert_parity(sc.textured_grid(), oracle, min_covered=10000, flags=flags)
 
