@@ -1247,7 +1247,7 @@ __device__ __forceinline__ void raster_serial(const TriRec& r, int32_t cx0, int3
 // Span walk (the per-lane path of 32x32 bins, triangles under 64 px on a side): each row's covered pixels
 // are the integer x with f_k(x) = F_k + A_k (x - cx0) >= 0 for k = 0..2, an interval [L, R] found from the
 // three crossings v_k = -F_k / A_k instead of testing every bbox pixel (the bbox of a C3 triangle is ~3x
-// its area). Exact: with |A_k| < 2^14, |F_k| < 2^21 (converted to float exactly) and v_rcp's 1-ulp
+// its area). Exact: with |A_k| < 2^14, |F_k| < 2^22 (exact in float, and stepped by B_k exactly) and v_rcp's 1-ulp
 // reciprocal, t = fma(-F, 1/A, -/+delta) lies within 2^-16 of v -/+ delta for |v| <= 64, and a
 // non-integer v is at least 1/|A| > 2^-14 from every integer, so with delta = 2^-15 ceil(t) = ceil(v) on
 // the left (A > 0) and floor(t) = floor(v) on the right (A < 0), integer v included; crossings further
@@ -1282,10 +1282,15 @@ __device__ __forceinline__ void raster_span(const TriRec& r, int32_t cx0, int32_
     const int32_t fx0 = 256 * cx0 + 128 - r.X[0];
     float fdy = (float)(256 * (cy0 + sub) + 128 - r.Y[0]);
     uint32_t row = (uint32_t)(((cy0 + sub - oy) << BL) + (cx0 - ox));
+    // the edge values stay exact integers below 2^22 over the bbox: stepped in float without rounding
+    float Ff[3], Bs[3];
 #pragma unroll
-    for (int k = 0; k < 3; ++k) F[k] += B[k] * sub;
+    for (int k = 0; k < 3; ++k) {
+        Ff[k] = (float)(F[k] + B[k] * sub);
+        Bs[k] = (float)(B[k] * step);
+    }
     for (int32_t py = cy0 + sub; py <= cy1; py += step) {
-        const float f0 = (float)F[0], f1 = (float)F[1], f2 = (float)F[2];
+        const float f0 = Ff[0], f1 = Ff[1], f2 = Ff[2];
         const float tl = fmaxf(fmaxf(__builtin_fmaf(f0, nrl[0], dl[0]), __builtin_fmaf(f1, nrl[1], dl[1])),
                                __builtin_fmaf(f2, nrl[2], dl[2]));
         const float tr = fminf(fminf(__builtin_fmaf(f0, nrr[0], dr[0]), __builtin_fmaf(f1, nrr[1], dr[1])),
@@ -1311,7 +1316,7 @@ __device__ __forceinline__ void raster_span(const TriRec& r, int32_t cx0, int32_
                 }
             }
         }
-        F[0] += B[0] * step; F[1] += B[1] * step; F[2] += B[2] * step;
+        Ff[0] += Bs[0]; Ff[1] += Bs[1]; Ff[2] += Bs[2];
         fdy += 256.0f * (float)step;
         row += (uint32_t)step << BL;
     }
