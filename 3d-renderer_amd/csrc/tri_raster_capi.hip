@@ -543,21 +543,20 @@ int check_overflow(tri_ctx* c) {
     TriCounters h;
     HIP_TRY(hipMemcpy(&h, c->d_ctr, sizeof h, hipMemcpyDeviceToHost));
     if (!h.flags) return TRI_OK;
-    const uint32_t zero = 0;
-    HIP_TRY(hipMemcpy(&c->d_ctr->flags, &zero, 4, hipMemcpyHostToDevice));
+    // the resets are stream-ordered before the next frame's kernels (the context's stream is non-blocking:
+    // work on the null stream is not ordered with it)
+    HIP_TRY(hipMemsetAsync(&c->d_ctr->flags, 0, 4, c->stream));
     if (h.flags & TRI_OVF_CLIP_RECORDS) c->ovf_rec_cap *= 4;
     if (h.flags & TRI_OVF_CLIP_VERTS) c->ovf_vert_cap *= 4;
     if (h.flags & TRI_OVF_BIN_LIST) {
         c->bin_cap = std::max<uint32_t>(c->bin_cap * 2, h.bin_max + h.bin_max / 4);
         c->bin_cap = (c->bin_cap + 63) & ~63u;
-        const uint32_t zmax = 0;
-        HIP_TRY(hipMemcpy(&c->d_ctr->bin_max, &zmax, 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemsetAsync(&c->d_ctr->bin_max, 0, 4, c->stream));
     }
     if (h.flags & TRI_OVF_SHADOW_BIN_LIST) {
         c->s_bin_cap = std::max<uint32_t>(c->s_bin_cap * 2, h.sbin_max + h.sbin_max / 4);
         c->s_bin_cap = (c->s_bin_cap + 63) & ~63u;
-        const uint32_t zmax = 0;
-        HIP_TRY(hipMemcpy(&c->d_ctr->sbin_max, &zmax, 4, hipMemcpyHostToDevice));
+        HIP_TRY(hipMemsetAsync(&c->d_ctr->sbin_max, 0, 4, c->stream));
     }
     int rc = ensure_work_buffers(c);
     if (rc) return rc;
@@ -596,7 +595,7 @@ int choose_bin_grid(tri_ctx* c) {
     c->nbins = c->nbx * c->nby;
     c->bin_cap = 0;  // re-derived for the new grid by ensure_work_buffers
     if ((rc = grow(c->d_bin_count, c->cap_bin_count, (size_t)c->nbins))) return rc;
-    HIP_TRY(hipMemset(c->d_bin_count, 0, (size_t)c->nbins * 4));
+    HIP_TRY(hipMemsetAsync(c->d_bin_count, 0, (size_t)c->nbins * 4, c->stream));  // before this frame's k_setup
     return TRI_OK;
 }
 
@@ -799,6 +798,9 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
     const float clear[4] = {0.005f, 0.005f, 0.005f, 1.0f};  // m_ClearColor default (Renderer.h:469)
     c->clear_bgra = unorm8_host(clear[2]) | (unorm8_host(clear[1]) << 8) | (unorm8_host(clear[0]) << 16) |
                     (unorm8_host(clear[3]) << 24);
+    // the counters, LUT and default texture above went through null-stream copies: complete them before
+    // any kernel on the context's non-blocking stream can read them
+    if (hipDeviceSynchronize() != hipSuccess) return bail(fail(TRI_E_HIP, "tri_create: device synchronisation failed"));
     *out = c;
     return TRI_OK;
 }
@@ -978,7 +980,7 @@ int tri_set_shadow(tri_ctx* c, const tri_shadow_config* cfg) {
     if (cfg->size != c->shadow.size) {  // new map grid: fresh (zeroed) queue counters
         HIP_TRY(hipStreamSynchronize(c->stream));
         if ((rc = grow(c->d_sbin_count, c->cap_sbin_count, (size_t)nbx * nbx))) return rc;
-        HIP_TRY(hipMemset(c->d_sbin_count, 0, (size_t)nbx * nbx * 4));
+        HIP_TRY(hipMemsetAsync(c->d_sbin_count, 0, (size_t)nbx * nbx * 4, c->stream));
         c->s_bin_cap = 0;
         c->shadow_rendered = false;
     }

@@ -64,7 +64,9 @@ def test_c4_full_frame_eight_bands(oracle, c3_full, mode):
         scenes.load_scene(grp, s)
         grp.render_frame()
         grp_c, grp_d = grp.readback()
-    assert np.array_equal(grp_d, full_d) and np.array_equal(grp_c, full_c)
+    bad = np.argwhere((grp_d != full_d) | (grp_c != full_c).any(-1))
+    assert len(bad) == 0, f"group frame: {len(bad)} pixels differ, rows {np.unique(bad[:, 0] // rows)} (bands), " \
+                          f"first {bad[:3].tolist()} depth {grp_d[tuple(bad[0])]:#x} vs {full_d[tuple(bad[0])]:#x}"
     oc, od, _ = oracle.render(s)
     assert np.array_equal(full_d, od), int((full_d != od).sum())
     assert int(np.abs(full_c.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL

@@ -21,4 +21,7 @@ run pmc_sized --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_32B_sum TCC_EA0_RDREQ_64B_su
 run pmc_sq --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_INST_ANY || exit $?
 run pmc_sq2 --pmc SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_LDS_BANK_CONFLICT GRBM_GUI_ACTIVE || exit $?
 run pmc_tcc --pmc TCC_HIT_sum TCC_MISS_sum || exit $?
+# L1 address (TA) and data-return (TD) occupancy: every wave-level gather costs the CU ~16 cycles there
+# (tools/td_probe), so k_raster's fragment gathers load these units about as much as its VALU work
+run pmc_tatd --pmc TA_TA_BUSY_sum TA_BUFFER_READ_WAVEFRONTS_sum TD_TD_BUSY_sum TD_TC_STALL_sum GRBM_GUI_ACTIVE || exit $?
 find $OUT -name "*.csv" | head -50

@@ -8,7 +8,8 @@ mkdir -p $dst
 for w in c3 c5; do
   src=gpurun_out/prof_$w
   cp $src/trace/trace_kernel_stats.csv $dst/${w}_kernel_stats.csv
-  for p in fetch write sq sq2 tcc; do
+  for p in fetch write sized sq sq2 tcc tatd; do
+    [ -f $src/pmc_$p/pmc_${p}_counter_collection.csv ] || continue
     gzip -c $src/pmc_$p/pmc_${p}_counter_collection.csv > $dst/${w}_pmc_$p.csv.gz
   done
 done
