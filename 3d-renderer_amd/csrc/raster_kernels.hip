@@ -26,7 +26,7 @@ namespace {
 
 // Diagnostics builds only (tools/build_variant.sh NAME -DTRI_ABLATE=N): 1 = coverage without shading,
 // 2 = shading without coverage, 4 = set-up without binning, 8 = one reservation round per batch,
-// 16 = no reservation atomics, 32 = no queue stores. The shipped library is built with 0, so none of
+// 16 = no reservation atomics, 32 = no queue stores, 1024 = no fragment colour gathers. The shipped library is built with 0, so none of
 // these tests survives into its ISA.
 #ifndef TRI_ABLATE
 #define TRI_ABLATE 0
@@ -91,23 +91,57 @@ __device__ __forceinline__ uint4 ld128(Rsrc r, uint32_t off) {
     const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, 0);
     return make_uint4(v[0], v[1], v[2], v[3]);
 }
-struct FetchBufs {  // k_raster's gather sources
-    Rsrc snap, vary, shade;
+// Record gathers by index (TRI_IDXEN): a structured buffer resource carries the record stride, so a load names
+// its record by index (buffer_load ... idxen) and the texture unit forms index * stride + offset; no VALU
+// multiply per address (the per-pixel gathers of k_raster otherwise spend seven quarter-rate v_mul_lo_u32 on
+// their x12 / x48 offsets). The LLVM intrinsic is bound by name: the compiler sees an ordinary buffer load.
+#ifndef TRI_IDXEN
+#define TRI_IDXEN 1
+#endif
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x3v __attribute__((ext_vector_type(3)));
+__device__ u32x4v tri_sbuf_load_b128(Rsrc r, int vindex, int voffset, int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v4i32");
+__device__ u32x3v tri_sbuf_load_b96(Rsrc r, int vindex, int voffset, int soffset, int aux) __asm("llvm.amdgcn.struct.ptr.buffer.load.v3i32");
+// A buffer of `n` records of `stride` bytes (stride < 2^14): indexed loads when TRI_IDXEN, else byte offsets.
+struct RecBuf {
+    Rsrc r;
+};
+__device__ __forceinline__ RecBuf rec_buf(const void* p, uint32_t stride, uint64_t n) {
+    if (TRI_IDXEN) return RecBuf{__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)stride, (int)(uint32_t)n, 0x00020000)};
+    return RecBuf{make_rsrc(p, (uint64_t)stride * n)};
+}
+template <uint32_t STRIDE>
+__device__ __forceinline__ uint4 rec128(const RecBuf& b, uint32_t i, uint32_t off) {  // off: a constant < STRIDE
+    if (TRI_IDXEN) {
+        const u32x4v v = tri_sbuf_load_b128(b.r, (int)i, (int)off, 0, 0);
+        return make_uint4(v[0], v[1], v[2], v[3]);
+    }
+    return ld128(b.r, i * STRIDE + off);
+}
+template <uint32_t STRIDE>
+__device__ __forceinline__ u32x3v rec96(const RecBuf& b, uint32_t i, uint32_t off) {
+    if (TRI_IDXEN) return tri_sbuf_load_b96(b.r, (int)i, (int)off, 0, 0);
+    const auto q = __builtin_amdgcn_raw_buffer_load_b96(b.r, i * STRIDE + off, 0, 0);
+    return u32x3v{q[0], q[1], q[2]};
+}
+
+struct FetchBufs {  // k_raster's gather sources: 16-B snaps, 48-B varyings, 48-B shade records
+    RecBuf snap, vary, shade;
 };
 __device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const TriDeviceBuffers& b) {
     FetchBufs f;
-    f.snap = make_rsrc(b.snap, 16ull * fp.nslots);
-    f.vary = make_rsrc(b.vary, 48ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
-    f.shade = make_rsrc(b.draw_shade, (uint64_t)sizeof(TriDrawShade) * fp.ndraws);
+    f.snap = rec_buf(b.snap, 16u, fp.nslots);
+    f.vary = rec_buf(b.vary, 48u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
+    f.shade = rec_buf(b.draw_shade, (uint32_t)sizeof(TriDrawShade), fp.ndraws);
     return f;
 }
 __device__ __forceinline__ TriSnap ld_snap(const FetchBufs& fb, uint32_t slot) {
-    const uint4 q = ld128(fb.snap, slot * 16u);
+    const uint4 q = rec128<16>(fb.snap, slot, 0u);
     return TriSnap{(int32_t)q.x, (int32_t)q.y, __uint_as_float(q.z), __uint_as_float(q.w)};
 }
 // The fragment stage's view of a snapped vertex: X, Y and 1/w (12 bytes, one load; z is not needed).
 __device__ __forceinline__ TriSnap ld_snap_xyw(const FetchBufs& fb, uint32_t slot) {
-    const auto q = __builtin_amdgcn_raw_buffer_load_b96(fb.snap, slot * 16u, 0, 0);
+    const u32x3v q = rec96<16>(fb.snap, slot, 0u);
     return TriSnap{(int32_t)q[0], (int32_t)q[1], __uint_as_float(q[2]), 0.0f};
 }
 
@@ -1103,12 +1137,11 @@ template <bool ONE = false>
 __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t p,
                                            uint32_t sl[3], uint32_t& d) {
     if (ONE || fp.one_draw) {
-        const Rsrc ir = make_rsrc(b.indices + fp.draw0.first_index, 12ull * fp.nprims);
-        const auto q = __builtin_amdgcn_raw_buffer_load_b96(ir, p * 12u, 0, 0);
+        const u32x3v q = rec96<12>(rec_buf(b.indices + fp.draw0.first_index, 12u, fp.nprims), p, 0u);
         sl[0] = q[0] - fp.draw0.min_index; sl[1] = q[1] - fp.draw0.min_index; sl[2] = q[2] - fp.draw0.min_index;
         d = 0;
     } else {
-        const uint4 pv = ld128(make_rsrc(b.prim_vs, 16ull * fp.nprims), p * 16u);
+        const uint4 pv = rec128<16>(rec_buf(b.prim_vs, 16u, fp.nprims), p, 0u);
         sl[0] = pv.x; sl[1] = pv.y; sl[2] = pv.z;
         d = pv.w & ~TRI_PRIM_CLIPPED;
     }
@@ -1786,7 +1819,7 @@ struct Taps {
     V4 a0, a1, a2, b0, b1, b2, c0, c1, c2;
 };
 __device__ __forceinline__ V4 ld_vary(const FetchBufs& fb, uint32_t slot, uint32_t j) {
-    const uint4 q = ld128(fb.vary, slot * 48u + j * 16u);  // plain-float views (HIP vector unions defeat SROA)
+    const uint4 q = rec128<48>(fb.vary, slot, j * 16u);  // plain-float views (HIP vector unions defeat SROA)
     return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
 }
 __device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint32_t v1, uint32_t v2) {
@@ -1803,7 +1836,7 @@ struct ShadeRec {
     uint4 st, sd, ss;
 };
 __device__ __forceinline__ ShadeRec load_shade(const FetchBufs& fb, uint32_t d) {
-    return ShadeRec{ld128(fb.shade, d * 48u), ld128(fb.shade, d * 48u + 16u), ld128(fb.shade, d * 48u + 32u)};
+    return ShadeRec{rec128<48>(fb.shade, d, 0u), rec128<48>(fb.shade, d, 16u), rec128<48>(fb.shade, d, 32u)};
 }
 
 
@@ -1869,8 +1902,8 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     }
     uint4 L0, L1, L2;
     if constexpr (SHADOW) {
-        const Rsrc lr = make_rsrc(b.lpos, 16ull * ((uint64_t)fp.nslots + fp.ovf_vert_cap));
-        L0 = ld128(lr, v0 * 16u); L1 = ld128(lr, v1 * 16u); L2 = ld128(lr, v2 * 16u);
+        const RecBuf lr = rec_buf(b.lpos, 16u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
+        L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
     }
     const TriRec r = sub ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
     float w0, w1, w2;
@@ -1879,7 +1912,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     } else {
         fast_weights(r, px, py, w0, w1, w2);
     }
-    if (TRI_COLOUR_LATE) {
+    if (kAblate & 1024) {  // diagnostics: 1024 = no colour gathers (3 of the fragment's 13 loads; same VALU)
+        taps.a2 = V4{w0, w1, w2, 0.0f}; taps.b2 = taps.a2; taps.c2 = taps.a2;
+    } else if (TRI_COLOUR_LATE) {
         taps.a2 = ld_vary(fb, v0, 2); taps.b2 = ld_vary(fb, v1, 2); taps.c2 = ld_vary(fb, v2, 2);
     }
     float vis = 1.0f;

@@ -12,5 +12,5 @@ for a in 0 1 2; do
   env $lib TRI_NOOP=1 timeout -k 10 200 python bench.py --steps 100 --warmup 10 --no-cpu-baseline ${EXTRA} > gpurun_out/ablate_$a.log 2>&1 || exit $?
   python3 -c "
 import json,sys; d=json.loads(open('gpurun_out/ablate_$a.log').read().strip().splitlines()[-1])
-print('ablate=$a fps=%.0f'%d['value'], {k:round(v*1e3,1) for k,v in d['stage_ms'].items()}, 'c2', {k:round(v,4) for k,v in d['secondary'].get('c2_sphere50k_1920x1080',{}).items()})"
+print('ablate=$a fps=%.0f'%d['value'], {k:round(v*1e3,1) for k,v in d['stage_ms'].items()})"
 done
