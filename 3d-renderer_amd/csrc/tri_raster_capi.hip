@@ -715,6 +715,9 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
     if (!cl.empty()) HIP_TRY(hipMemcpy(g->d_clusters, cl.data(), cl.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
     if ((rc = grow(g->d_vbox, g->cap_vbox, std::max<size_t>(vbox.size(), 1)))) return rc;
     if (!vbox.empty()) HIP_TRY(hipMemcpy(g->d_vbox, vbox.data(), vbox.size() * sizeof(TriCluster), hipMemcpyHostToDevice));
+    // null-stream copies are not ordered with the contexts' non-blocking streams: complete them before any
+    // context can launch a frame that reads this geometry
+    HIP_TRY(hipStreamSynchronize(nullptr));
     g->geometry_set = true;
     // versions come from one process-wide counter: a context that switches between geometry objects
     // (tri_bind_geometry, tri_upload_geometry) can never see an equal version on a different object
@@ -911,6 +914,7 @@ int tri_upload_texture(tri_ctx* c, uint32_t slot, const uint8_t* rgba, uint32_t 
     c->d_tex[slot] = nullptr;
     HIP_TRY(hipMalloc(&c->d_tex[slot], (size_t)w * h * 4));
     HIP_TRY(hipMemcpy(c->d_tex[slot], rgba, (size_t)w * h * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipStreamSynchronize(nullptr));  // complete before the next frame on the non-blocking stream
     c->tex_w[slot] = w;
     c->tex_h[slot] = h;
     std::memcpy(&c->tex_solid[slot], rgba, 4);
@@ -926,6 +930,7 @@ int tri_upload_bone_palette(tri_ctx* c, const float* m, uint32_t n) {
     HIP_TRY(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_bones, c->cap_bones, std::max<size_t>(16ull * n, 16)))) return rc;
     if (n) HIP_TRY(hipMemcpy(c->d_bones, m, 64ull * n, hipMemcpyHostToDevice));
+    HIP_TRY(hipStreamSynchronize(nullptr));  // complete before the next frame on the non-blocking stream
     c->nbones = n;
     return TRI_OK;
 }
@@ -943,6 +948,7 @@ int tri_upload_skybox(tri_ctx* c, const uint8_t* faces, uint32_t n) {
     const size_t texels = 6ull * n * n;
     if ((rc = grow(c->d_sky, c->cap_sky, texels))) return rc;
     HIP_TRY(hipMemcpy(c->d_sky, faces, texels * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipStreamSynchronize(nullptr));  // complete before the next frame on the non-blocking stream
     c->sky_size = n;
     const uint32_t* t = reinterpret_cast<const uint32_t*>(faces);
     uint32_t t0;

@@ -72,6 +72,44 @@ def test_c4_full_frame_eight_bands(oracle, c3_full, mode):
     assert int(np.abs(full_c.astype(np.int16) - oc.astype(np.int16)).max()) <= COLOR_TOL
 
 
+def _poison_device_memory(byte=0xFF, chunks=48, size=64 << 20):
+    """Fill device memory with `byte` and release it: buffers allocated next hold that garbage, not fresh zeros."""
+    hip = C.CDLL("libamdhip64.so")
+    ptrs = []
+    for _ in range(chunks):
+        p = C.c_void_p()
+        if hip.hipMalloc(C.byref(p), C.c_size_t(size)) != 0:
+            break
+        hip.hipMemset(p, C.c_int(byte), C.c_size_t(size))
+        ptrs.append(p)
+    hip.hipDeviceSynchronize()
+    for p in ptrs:
+        hip.hipFree(p)
+    return len(ptrs)
+
+
+def test_first_frame_over_reused_device_memory(c3_full):
+    """Regression (round 3): a context's bin counters were zeroed by a null-stream hipMemset that the context's
+    non-blocking stream did not wait for; over recycled device memory the first frame of an 8-band group lost a
+    whole bin (1024 pixels left at the clear depth). Now every reset is stream-ordered. Device memory is
+    poisoned with 0xFF before each fresh context / group renders its first frame."""
+    from trident_raster import raster, scenes
+
+    s = c3_full
+    ref_c, ref_d = _render_single(s, 0)
+    for attempt in range(2):
+        assert _poison_device_memory() > 0
+        with raster.TriGroup(s.width, s.height, [0] * 8, display=0) as grp:
+            scenes.load_scene(grp, s)
+            grp.render_frame()
+            gc, gd = grp.readback()
+        bad = np.argwhere((gd != ref_d) | (gc != ref_c).any(-1))
+        assert len(bad) == 0, f"group, attempt {attempt}: {len(bad)} pixels differ, bands {np.unique(bad[:, 0] // 270)}"
+        assert _poison_device_memory() > 0
+        c, d = _render_single(s, 0)
+        assert np.array_equal(d, ref_d) and np.array_equal(c, ref_c), f"single context, attempt {attempt}"
+
+
 def _copy_frame(ptr, dev, w, h):
     from trident_raster import raster
 
