@@ -92,7 +92,8 @@ def test_first_frame_over_reused_device_memory(c3_full):
     """Regression (round 3): a context's bin counters were zeroed by a null-stream hipMemset that the context's
     non-blocking stream did not wait for; over recycled device memory the first frame of an 8-band group lost a
     whole bin (1024 pixels left at the clear depth). Now every reset is stream-ordered. Device memory is
-    poisoned with 0xFF before each fresh context / group renders its first frame."""
+    poisoned with 0xFF before each fresh context / group renders its first frame. A race, so a guard rather than
+    a proof: tools/group_repro.py caught the pre-fix build in one run of four."""
     from trident_raster import raster, scenes
 
     s = c3_full
