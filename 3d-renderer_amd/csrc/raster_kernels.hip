@@ -2185,12 +2185,6 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ uint32_t wsum[TRI_BLOCK / 64];
     __shared__ uint32_t nbig, nsky;
     const int tid = threadIdx.x;
-#if TRI_STAGGER
-    // experiment: half the first round's workgroups start late, so a CU's workgroups are not all in the
-    // same phase (coverage: latency-bound; shading: VALU-bound) at once
-    if (blockIdx.x < 2048 && ((blockIdx.x >> 8) & 1))
-        for (int s = 0; s < TRI_STAGGER; s += 8128) __builtin_amdgcn_s_sleep(127);
-#endif
     TRI_STAMP(0);
     if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1);  // (TRI_COV_PRIO above)
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
