@@ -1660,13 +1660,13 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     }
     const f3 wp = fworld(f);
     for (uint32_t i = 0; i < sc.npt; ++i) {
-        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
+        const f3 to = sub3(mk(sc.pl[i].pos[0], sc.pl[i].pos[1], sc.pl[i].pos[2]), wp);
         const float d2 = fdot(to, to);
         const float inv = frsq(d2);
-        const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
+        const float att0 = 1.0f - fminf(d2 * inv * sc.pl[i].pos[3], 1.0f);
         if (!(d2 > 1e-8f && att0 > 0.0f)) continue;  // dist <= 1e-4, or beyond the range (see below)
-        eval_pbr_fast_p(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv, f2v{sc.pl_rad[i][0], sc.pl_rad[i][1]},
-                        sc.pl_rad[i][2], att0 * att0, cxy, cz);
+        eval_pbr_fast_p(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv, f2v{sc.pl[i].rad[0], sc.pl[i].rad[1]},
+                        sc.pl[i].rad[2], att0 * att0, cxy, cz);
     }
     const f2v c1 = cxy + splat(1.0f);
     const f2v txy = cxy * f2v{frcp(c1.x), frcp(c1.y)};
@@ -1696,16 +1696,18 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     }
     const f3 wp = fworld(f);
     for (uint32_t i = 0; i < sc.npt; ++i) {
-        const f3 to = sub3(mk(sc.pl_pos[i][0], sc.pl_pos[i][1], sc.pl_pos[i][2]), wp);
+        float lp[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { lp[k] = sc.pl[i].pos[k]; lp[4 + k] = sc.pl[i].rad[k]; }
+        const f3 to = sub3(mk(lp[0], lp[1], lp[2]), wp);
         const float d2 = fdot(to, to);
         const float inv = frsq(d2);
-        const float att0 = 1.0f - fminf(d2 * inv * sc.pl_pos[i][3], 1.0f);
+        const float att0 = 1.0f - fminf(d2 * inv * lp[3], 1.0f);
         // dist <= 1e-4 (Default.frag skips it; d2 = 0 gives att0 = 0 here too), or beyond the light's
         // range: (1 - d/r)^2 = 0 adds exactly nothing. One exact skip instead of two.
         if (!(d2 > 1e-8f && att0 > 0.0f)) continue;
         // L = to / |to| is never formed: N.L and L.V are the dot products with `to`, scaled once
-        eval_pbr_fast(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv,
-                      mk(sc.pl_rad[i][0], sc.pl_rad[i][1], sc.pl_rad[i][2]), att0 * att0, c);
+        eval_pbr_fast(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv, mk(lp[4], lp[5], lp[6]), att0 * att0, c);
     }
     const f3 t = mk(c.x * frcp(c.x + 1.0f), c.y * frcp(c.y + 1.0f), c.z * frcp(c.z + 1.0f));
     return make_float4(tone_out(t.x), tone_out(t.y), tone_out(t.z), ONE ? sc.sbt[3] : (sc.base[3] * f.tw) * f.sw);

@@ -237,10 +237,10 @@ void shade_constants(const tri_global_ubo& g, const tri_material_record& m, TriS
     for (uint32_t i = 0; i < sc.npt; ++i) {
         const tri_point_light& pl = g.point_lights[i];
         for (int k = 0; k < 3; ++k) {
-            sc.pl_pos[i][k] = pl.position_range[k];
-            sc.pl_rad[i][k] = pl.color_intensity[k] * pl.color_intensity[3];
+            sc.pl[i].pos[k] = pl.position_range[k];
+            sc.pl[i].rad[k] = pl.color_intensity[k] * pl.color_intensity[3];
         }
-        sc.pl_pos[i][3] = 1.0f / std::fmax(pl.position_range[3], 1e-4f);
+        sc.pl[i].pos[3] = 1.0f / std::fmax(pl.position_range[3], 1e-4f);
     }
 }
 
