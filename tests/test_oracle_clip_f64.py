@@ -7,7 +7,8 @@ interpolates z_ndc linearly in screen space and keeps the LEQUAL minimum in prim
 below does exactly that with no sub-pixel snap, no guard band and no fan order: it shares no code or
 formulation with the oracle (which clips in float32 with barycentric weights, fans the polygon, snaps to 8
 sub-pixel bits). Where a pixel centre lies at least half a pixel inside the winning float64 polygon, the two
-must agree on coverage and on depth within the error the 1/256-px snap and float32 can introduce.
+must agree on coverage and on depth within the error the 1/256-px snap and float32 can introduce, and (second
+half of the file) on the stored colour within 1 LSB, with Default.vert/Default.frag evaluated in float64.
 """
 import numpy as np
 
@@ -114,3 +115,164 @@ def test_oracle_clipping_and_depth_match_float64_vulkan_rules(oracle):
     assert (err[interior] <= tol[interior]).all(), float((err - tol)[interior].max())
     # the comparison includes pixels of clipped primitives
     assert (interior & clipped).sum() > 1000
+
+
+# ---- the whole fragment path in float64 -----------------------------------------------------------------------
+# Default.vert (world position, normal through transpose(inverse(mat3(model))), colour, uv * scale * tiling +
+# offset) and Default.frag (PBR, Reinhard, 1/2.2 gamma) evaluated in float64 at each pixel centre, with the
+# perspective-correct weights solved from the ORIGINAL triangle's clip-space vertices (homogeneous
+# rasterisation: the weights b with sum b_i (x_i - x w_i) = sum b_i (y_i - y w_i) = 0, sum b_i = 1), so clipping
+# only limits where a triangle is visible, never what it interpolates. Texture taps: sRGB decoded in float64,
+# bilinear, REPEAT, level 0. Nothing here follows the oracle's (or the kernels') operation order.
+def _srgb_to_linear(c):
+    c = c / 255.0
+    return np.where(c <= 0.04045, c / 12.92, ((c + 0.055) / 1.055) ** 2.4)
+
+
+def _sample(tex, u, v):
+    h, w = tex.shape[:2]
+    x, y = u * w - 0.5, v * h - 0.5
+    x0, y0 = np.floor(x), np.floor(y)
+    a, b = (x - x0)[..., None], (y - y0)[..., None]
+    x0, y0 = x0.astype(np.int64) % w, y0.astype(np.int64) % h
+    x1, y1 = (x0 + 1) % w, (y0 + 1) % h
+    lin = np.concatenate([_srgb_to_linear(tex[..., :3].astype(np.float64)), tex[..., 3:4] / 255.0], -1)
+    t00, t10, t01, t11 = lin[y0, x0], lin[y0, x1], lin[y1, x0], lin[y1, x1]
+    return (t00 * (1 - a) + t10 * a) * (1 - b) + (t01 * (1 - a) + t11 * a) * b
+
+
+def _shade(scene, draw, P, N, col, uv):
+    """Default.frag:123-180 in float64 for arrays of fragments of one draw."""
+    g = scene.ubo
+    base, fac = scene.materials[0] if scene.materials else ((1, 1, 1, 1), (0, 1, 1, 0))  # record-0 quirk
+    slot = draw.pc.texture_slot
+    tex = next((t for s, t in scene.textures if s == slot), None)
+    smp = _sample(tex, uv[:, 0], uv[:, 1]) if tex is not None else np.ones((len(P), 4))
+    tint = np.array(draw.pc.tint, np.float64)
+    alb = smp[:, :3] * np.array(base[:3]) * tint[:3] * col
+    met = min(max(fac[0], 0.0), 1.0)
+    rough = min(max(fac[1], 0.045), 1.0)
+    amb_s = min(max(fac[2], 0.0), 1.0)
+    F0 = 0.04 * (1 - met) + alb * met
+    Nn = N / np.linalg.norm(N, axis=1, keepdims=True)
+    V = np.array(g.camera_position[:3], np.float64) - P
+    V /= np.linalg.norm(V, axis=1, keepdims=True)
+    dot = lambda a, b: np.sum(a * b, axis=1)
+
+    def pbr(L, rad):
+        H = V + L
+        H /= np.linalg.norm(H, axis=1, keepdims=True)
+        a2 = (rough * rough) ** 2
+        nh = np.maximum(dot(Nn, H), 0)
+        ndf = a2 / (np.pi * (nh * nh * (a2 - 1) + 1) ** 2)
+        k = (rough + 1) ** 2 / 8
+        nv, nl = np.maximum(dot(Nn, V), 0), np.maximum(dot(Nn, L), 0)
+        geo = nv / np.maximum(nv * (1 - k) + k, 1e-4) * (nl / np.maximum(nl * (1 - k) + k, 1e-4))
+        Fr = F0 + (1 - F0) * (np.clip(1 - np.maximum(dot(H, V), 0), 0, 1) ** 5)[:, None]
+        spec = (ndf * geo)[:, None] * Fr / np.maximum(4 * nv * nl, 1e-4)[:, None]
+        kD = (1 - Fr) * (1 - met)
+        return (kD * alb / np.pi + spec) * rad * nl[:, None]
+
+    direct = np.zeros_like(P)
+    if g.light_counts[0] > 0:
+        d = -np.array(g.directional_light_direction[:3], np.float64)
+        L = np.broadcast_to(d / np.linalg.norm(d), P.shape)
+        direct += pbr(L, np.array(g.directional_light_color[:3]) * g.directional_light_color[3])
+    for i in range(min(g.light_counts[1], 8)):
+        pl = g.point_lights[i]
+        to = np.array(pl.position_range[:3], np.float64) - P
+        dist = np.linalg.norm(to, axis=1)
+        ok = dist > 1e-4
+        att = (1 - np.clip(dist / max(pl.position_range[3], 1e-4), 0, 1)) ** 2
+        rad = np.array(pl.color_intensity[:3]) * pl.color_intensity[3] * att[:, None]
+        contrib = pbr(to / np.where(ok, dist, 1)[:, None], rad)
+        direct += np.where(ok[:, None], contrib, 0)
+    amb = np.array(g.ambient_color_intensity[:3]) * g.ambient_color_intensity[3] * alb * amb_s
+    c = amb + direct
+    c = (c / (c + 1)) ** (1 / 2.2)
+    alpha = base[3] * tint[3] * smp[:, 3]
+    return np.concatenate([c, alpha[:, None]], 1)
+
+
+def f64_colour(scene, fd, margin):
+    """Colour (float64, before the UNORM store) of every pixel with margin >= 0.5 whose winning triangle is
+    found again by depth; returns (colour [H, W, 4], mask)."""
+    W, H = scene.width, scene.height
+    view = np.array(scene.ubo.view, np.float64).reshape(4, 4).T
+    proj = np.array(scene.ubo.projection, np.float64).reshape(4, 4).T
+    out = np.zeros((H, W, 4))
+    done = np.zeros((H, W), bool)
+    ys, xs = np.mgrid[0:H, 0:W] + 0.5
+    xn, yn = (xs - W / 2) / (W / 2), (ys - H / 2) / (H / 2)
+    want = margin >= 0.5
+    vx = scene.vertices
+    for d in scene.draws:
+        m = scene.meshes[d.mesh_index]
+        model = np.array(d.pc.model, np.float64).reshape(4, 4).T
+        nmat = np.linalg.inv(model[:3, :3]).T
+        first, count, base = int(m["first_index"]), int(m["index_count"]), int(m["base_vertex"])
+        tris = scene.indices[first:first + count - count % 3].reshape(-1, 3).astype(np.int64) + base
+        pos = np.c_[vx["position"].astype(np.float64), np.ones(len(vx))]
+        world = (model @ pos.T).T
+        clip = (proj @ view @ world.T).T
+        nrm = (nmat @ vx["normal"].astype(np.float64).T).T
+        nrm /= np.linalg.norm(nrm, axis=1, keepdims=True)
+        uvt = vx["texcoord"].astype(np.float64) * np.array(d.pc.texture_scale) * d.pc.tiling_factor + np.array(d.pc.texture_offset)
+        colv = vx["color"].astype(np.float64)
+        for t in tris:
+            C = clip[t]
+            sxv = C[:, 0] / np.where(C[:, 3] > 0, C[:, 3], np.nan) * W / 2 + W / 2
+            syv = C[:, 1] / np.where(C[:, 3] > 0, C[:, 3], np.nan) * H / 2 + H / 2
+            if np.all(C[:, 3] > 0):  # a bbox for the common case; a clipped triangle tests the whole frame
+                x0, x1 = max(int(np.floor(sxv.min())), 0), min(int(np.ceil(sxv.max())), W - 1)
+                y0, y1 = max(int(np.floor(syv.min())), 0), min(int(np.ceil(syv.max())), H - 1)
+            else:
+                x0, x1, y0, y1 = 0, W - 1, 0, H - 1
+            if x0 > x1 or y0 > y1:
+                continue
+            sl = (slice(y0, y1 + 1), slice(x0, x1 + 1))
+            cand = want[sl] & ~done[sl]
+            if not cand.any():
+                continue
+            px, py = xn[sl][cand], yn[sl][cand]
+            a = C[None, :, 0] - px[:, None] * C[None, :, 3]
+            c = C[None, :, 1] - py[:, None] * C[None, :, 3]
+            b = np.cross(a, c)
+            b /= b.sum(1, keepdims=True)
+            inside = np.all(b >= 0, axis=1)
+            z = (b @ C[:, 2]) / (b @ C[:, 3])
+            hit = inside & (np.abs(z - fd[sl][cand]) <= 1e-9)
+            if not hit.any():
+                continue
+            bh = b[hit]
+            P = bh @ world[t, :3]
+            rgba = _shade(scene, d, P, bh @ nrm[t], bh @ colv[t], bh @ uvt[t])
+            iy, ix = np.nonzero(cand)
+            iy, ix = iy[hit] + y0, ix[hit] + x0
+            out[iy, ix] = rgba
+            done[iy, ix] = True
+    return out, done
+
+
+def _check_colour(oracle, s, min_pixels):
+    bgra, od_bits, _ = oracle.render(s)
+    fd, margin, _, _ = f64_depth(s)
+    ref, mask = f64_colour(s, fd, margin)
+    assert mask.sum() >= min_pixels
+    want = np.rint(np.clip(ref, 0, 1) * 255.0)
+    got = bgra[..., [2, 1, 0, 3]].astype(np.float64)
+    diff = np.abs(got - want)[mask]
+    # float32 against float64 differs by 1 LSB where a value sits on a rounding boundary, never more
+    assert diff.max() <= 1, (diff.max(), np.argwhere(np.abs(got - want).max(-1) * mask > 1)[:5])
+    return diff
+
+
+def test_oracle_colour_matches_float64_shading_textured(oracle):
+    # sun + 4 point lights, an sRGB texture with alpha under REPEAT, tint, uv scale/offset/tiling, vertex colours
+    diff = _check_colour(oracle, sc.textured_grid(320, 180, 30), 30000)
+    assert (diff == 0).mean() > 0.9
+
+
+def test_oracle_colour_matches_float64_shading_clipped(oracle):
+    # a point light over a ground plane cut by the near plane: the visible parts of clipped triangles shaded
+    _check_colour(oracle, sc.near_clip_grid(320, 240, 24), 40000)
