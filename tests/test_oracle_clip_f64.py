@@ -276,3 +276,79 @@ def test_oracle_colour_matches_float64_shading_textured(oracle):
 def test_oracle_colour_matches_float64_shading_clipped(oracle):
     # a point light over a ground plane cut by the near plane: the visible parts of clipped triangles shaded
     _check_colour(oracle, sc.near_clip_grid(320, 240, 24), 40000)
+
+
+# ---- the skybox pass in float64 -------------------------------------------------------------------------------
+# Skybox.cpp:13-36's cube (scaled by 20, Skybox.cpp:74) through Skybox.vert (gl_Position = (P mat4(mat3(View))
+# world).xyww, outDirection = mat3(View) world) rasterised homogeneously: at each pixel the direction is the
+# clip-space convex combination of a triangle's view-space vertices with positive w — the ray's exit point, as a
+# rasteriser interpolating outDirection over the visible face produces it. Skybox.frag samples the cube map at
+# normalize(direction): Vulkan's major-axis face table, sRGB decoded in float64, bilinear within the face.
+# Pixels whose direction lies near a face edge (where seamless filtering takes taps from two faces) are skipped.
+_SKY_POS = np.array([[-1, -1, 1], [1, -1, 1], [1, 1, 1], [-1, 1, 1],
+                     [-1, -1, -1], [1, -1, -1], [1, 1, -1], [-1, 1, -1]], np.float64) * 20.0
+_SKY_IDX = np.array([0, 1, 2, 2, 3, 0, 1, 5, 6, 6, 2, 1, 5, 4, 7, 7, 6, 5,
+                     4, 0, 3, 3, 7, 4, 3, 2, 6, 6, 7, 3, 4, 5, 1, 1, 0, 4]).reshape(-1, 3)
+
+
+def f64_sky(scene):
+    W, H = scene.width, scene.height
+    view = np.array(scene.ubo.view, np.float64).reshape(4, 4).T
+    proj = np.array(scene.ubo.projection, np.float64).reshape(4, 4).T
+    R = view[:3, :3]
+    vpos = _SKY_POS @ R.T  # outDirection at the cube's corners
+    clip = np.c_[vpos, np.ones(8)] @ proj.T
+    ys, xs = np.mgrid[0:H, 0:W] + 0.5
+    xn, yn = ((xs - W / 2) / (W / 2)).ravel(), ((ys - H / 2) / (H / 2)).ravel()
+    dirs = np.full((H * W, 3), np.nan)
+    for t in _SKY_IDX:
+        C = clip[t]
+        a = C[None, :, 0] - xn[:, None] * C[None, :, 3]
+        c = C[None, :, 1] - yn[:, None] * C[None, :, 3]
+        b = np.cross(a, c)
+        s = b.sum(1, keepdims=True)
+        ok = np.abs(s[:, 0]) > 1e-12
+        b = b / np.where(ok[:, None], s, 1)
+        hit = ok & np.all(b >= 0, axis=1) & (b @ C[:, 3] > 0)
+        dirs[hit] = b[hit] @ vpos[t]
+    faces = scene.skybox
+    n = faces.shape[1]
+    lin = _srgb_to_linear(faces[..., :3].astype(np.float64))
+    out = np.full((H * W, 3), np.nan)
+    good = ~np.isnan(dirs[:, 0])
+    d = dirs[good] / np.linalg.norm(dirs[good], axis=1, keepdims=True)
+    ax = np.abs(d)
+    major = np.argmax(ax, axis=1)
+    srt = np.sort(ax, axis=1)
+    x, y, z = d[:, 0], d[:, 1], d[:, 2]
+    # Vulkan's cube map face selection table: (face, sc, tc, ma)
+    face = np.where(major == 0, np.where(x >= 0, 0, 1), np.where(major == 1, np.where(y >= 0, 2, 3), np.where(z >= 0, 4, 5)))
+    sc_ = np.select([face == 0, face == 1, face == 2, face == 3, face == 4], [-z, z, x, x, x], -x)
+    tc_ = np.select([face == 0, face == 1, face == 2, face == 3, face == 4], [-y, -y, z, -z, -y], -y)
+    ma = srt[:, 2]
+    u = (0.5 * sc_ / ma + 0.5) * n - 0.5
+    v = (0.5 * tc_ / ma + 0.5) * n - 0.5
+    i0, j0 = np.floor(u).astype(np.int64), np.floor(v).astype(np.int64)
+    inner = (i0 >= 0) & (i0 + 1 <= n - 1) & (j0 >= 0) & (j0 + 1 <= n - 1) & (srt[:, 2] - srt[:, 1] > 1e-6)
+    a_, b_ = (u - i0)[:, None], (v - j0)[:, None]
+    i0c, j0c = np.clip(i0, 0, n - 2), np.clip(j0, 0, n - 2)
+    t00, t10 = lin[face, j0c, i0c], lin[face, j0c, i0c + 1]
+    t01, t11 = lin[face, j0c + 1, i0c], lin[face, j0c + 1, i0c + 1]
+    col = (t00 * (1 - a_) + t10 * a_) * (1 - b_) + (t01 * (1 - a_) + t11 * a_) * b_
+    idx = np.nonzero(good)[0]
+    out[idx[inner]] = col[inner]
+    return out.reshape(H, W, 3)
+
+
+def test_oracle_skybox_matches_float64_cube_pass(oracle):
+    for rot, fov in (((0.0, 0.0, 0.0), 100.0), ((25.0, 140.0, 10.0), 70.0), ((-80.0, 30.0, 0.0), 90.0)):
+        s = sc.skybox_only(160, 120, fov, rot, sc.cubemap_faces(32, seed=5))
+        bgra, _, _ = oracle.render(s)
+        ref = f64_sky(s)
+        mask = ~np.isnan(ref[..., 0])
+        assert mask.mean() > 0.6, mask.mean()
+        want = np.rint(np.clip(ref, 0, 1) * 255.0)
+        got = bgra[..., [2, 1, 0]].astype(np.float64)
+        diff = np.abs(got - want)[mask]
+        assert diff.max() <= 1, (rot, diff.max())
+        assert (bgra[..., 3] == 255).all()
