@@ -1427,7 +1427,7 @@ __device__ __forceinline__ uint32_t unorm8(float c) {
 // fold the + 0.5 too, but only inline asm reaches it, and the compiler does not guard inline asm against
 // the trans-result hazard: a v_cvt reading a v_exp result in the next slot read a stale register.)
 #ifndef TRI_SHADE_TRIM
-#define TRI_SHADE_TRIM 7  // bits: 1 = G_L denominator, 2 = tone curve, 4 = e0 from the area
+#define TRI_SHADE_TRIM 31  // bits: 1 = G_L denominator, 2 = tone curve, 4 = e0 from the area, 8 = spec_num, 16 = att_base
 #endif
 __device__ __forceinline__ float tone_out(float t) {
     constexpr float g = 1.0f / 2.2f;
@@ -1543,9 +1543,25 @@ __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag&
 // ---- fast build: same algebra, frame constants hoisted, hardware transcendental approximations ---
 // Per light: one v_rsq (half vector) and ONE v_rcp for NDF * G_L / (4 NdotV NdotL) together. For unit
 // V and L, |V + L|^2 = 2 + 2 L.V, N.H = (N.V + N.L) / |V + L| and H.V = (1 + L.V) / |V + L|.
+// G_V NdotL / max(4 NdotV NdotL, 1e-4) (the NDF's a2 / pi and G_L's 1 / (1 - k) folded in), the part of the
+// specular weight before the per-light denominator dd^2 gden. TRI_SHADE_TRIM & 8: for N.L > 0,
+// NdotL / max(4 NdotV NdotL, 1e-4) = min(1 / (4 NdotV), 1e4 NdotL), so with spA = gVa / (4 NdotV) (formed
+// without NdotV: a2 / (4 pi (1 - k) gden_V), finite at NdotV = 0) and spB = 1e4 gVa it is min(spA, spB NdotL):
+// two operations per light instead of four, and one product fewer inside the reciprocal.
+__device__ __forceinline__ float spec_num(float spA, float spB, float NdotV4, float gVa, float NdotL) {
+    if (TRI_SHADE_TRIM & 8) return fminf(spA, spB * NdotL);
+    return (NdotL * gVa) * frcp(fmaxf(NdotV4 * NdotL, 1e-4f));
+}
+// Point-light attenuation (1 - min(d / r, 1))^2's base; TRI_SHADE_TRIM & 16: max(1 - d / r, 0) as one fma
+__device__ __forceinline__ float att_base(float d, float ir) {
+    if (TRI_SHADE_TRIM & 16) return fmaxf(__builtin_fmaf(-d, ir, 1.0f), 0.0f);
+    return 1.0f - fminf(d * ir, 1.0f);
+}
+
 struct PbrPix {
     f3 N, V, F0, omF0, diffK;
     float NdotVr, NdotV4, gVa;  // NdotVr: unclamped N.V; gVa = a2 / pi * G_V
+    float spA, spB;             // TRI_SHADE_TRIM & 8 (spec_num)
 };
 
 // One light with unclamped N.L and L.V given (the caller forms them without normalising L first).
@@ -1562,9 +1578,8 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
     // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
     // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
     const float gden = (TRI_SHADE_TRIM & 1) ? NdotL + sc.kgo : __builtin_fmaf(NdotL, sc.omkg, sc.kg);
-    const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
     // NDF * G_L * G_V / den with NDF = a2 / (pi dd^2), G_L = NdotL / gden
-    const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
+    const float sp = spec_num(px.spA, px.spB, px.NdotV4, px.gVa, NdotL) * frcp((dd * dd) * gden);
     // 1 - max(H.V, 0), clamped to [0, 1]: one clamped subtract
     const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
     const float q2 = q * q;
@@ -1598,6 +1613,7 @@ struct PbrPixP {
     f2v F0xy, omF0xy, diffKxy;
     float F0z, omF0z, diffKz;
     float NdotVr, NdotV4, gVa;
+    float spA, spB;
 };
 __device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const PbrPixP& px, float NdotLr, float LdotV,
                                                 f2v radxy, float radz, float scale, f2v& cxy, float& cz) {
@@ -1610,8 +1626,7 @@ __device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const P
     // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
     // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
     const float gden = (TRI_SHADE_TRIM & 1) ? NdotL + sc.kgo : __builtin_fmaf(NdotL, sc.omkg, sc.kg);
-    const float den = fmaxf(px.NdotV4 * NdotL, 1e-4f);
-    const float sp = (NdotL * px.gVa) * frcp(((dd * dd) * gden) * den);
+    const float sp = spec_num(px.spA, px.spB, px.NdotV4, px.gVa, NdotL) * frcp((dd * dd) * gden);
     const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
     const float q2 = q * q;
     const float p5 = q2 * q2 * q;
@@ -1649,7 +1664,10 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
     px.NdotV4 = 4.0f * NdotV;
-    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
+    const float rgV = frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
+    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * rgV);
+    px.spA = (0.25f * ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi)) * rgV;
+    px.spB = 1e4f * px.gVa;
     f2v cxy = (f2v{sc.amb[0], sc.amb[1]} * albxy) * splat(sc.amb_strength);
     float cz = (sc.amb[2] * albz) * sc.amb_strength;
     if (kAblate & 64) return make_float4(cxy.x, cxy.y, cz, 1.0f);  // diagnostics: 64 = no lights
@@ -1663,7 +1681,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         const f3 to = sub3(mk(sc.pl[i].pos[0], sc.pl[i].pos[1], sc.pl[i].pos[2]), wp);
         const float d2 = fdot(to, to);
         const float inv = frsq(d2);
-        const float att0 = 1.0f - fminf(d2 * inv * sc.pl[i].pos[3], 1.0f);
+        const float att0 = att_base(d2 * inv, sc.pl[i].pos[3]);
         if (!(d2 > 1e-8f && att0 > 0.0f)) continue;  // dist <= 1e-4, or beyond the range (see below)
         eval_pbr_fast_p(sc, px, fdot(px.N, to) * inv, fdot(to, px.V) * inv, f2v{sc.pl[i].rad[0], sc.pl[i].rad[1]},
                         sc.pl[i].rad[2], att0 * att0, cxy, cz);
@@ -1686,7 +1704,10 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
     px.NdotV4 = 4.0f * NdotV;
-    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f)));
+    const float rgV = frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
+    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * rgV);
+    px.spA = (0.25f * ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi)) * rgV;
+    px.spB = 1e4f * px.gVa;
     f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
               sc.amb[2] * albedo.z * sc.amb_strength);
     if (kAblate & 64) return make_float4(c.x, c.y, c.z, 1.0f);  // diagnostics: 64 = no lights
@@ -1702,7 +1723,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         const f3 to = sub3(mk(lp[0], lp[1], lp[2]), wp);
         const float d2 = fdot(to, to);
         const float inv = frsq(d2);
-        const float att0 = 1.0f - fminf(d2 * inv * lp[3], 1.0f);
+        const float att0 = att_base(d2 * inv, lp[3]);
         // dist <= 1e-4 (Default.frag skips it; d2 = 0 gives att0 = 0 here too), or beyond the light's
         // range: (1 - d/r)^2 = 0 adds exactly nothing. One exact skip instead of two.
         if (!(d2 > 1e-8f && att0 > 0.0f)) continue;
