@@ -35,3 +35,23 @@ def hiplib():
     from trident_raster import raster
 
     return raster.load_library()
+
+
+_GPU_SESSION = False
+
+
+def pytest_collection_modifyitems(config, items):
+    global _GPU_SESSION
+    _GPU_SESSION = any(item.get_closest_marker("gpu") for item in items)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _torch_runtime_first():
+    """GPU sessions: torch's HIP runtime initialises before the product library loads ROCm's. A test that
+    hands torch streams or tensors to the library (test_external_stream_orders_output) otherwise finds torch
+    unable to see the GPU when it is the first torch user in a process that already loaded the library."""
+    if _GPU_SESSION and gpu_available():
+        import torch
+
+        torch.cuda.init()
+    yield
