@@ -1,7 +1,8 @@
 // tri_oracle.cpp — TEST INFRASTRUCTURE: CPU restatement of the reference's graphics-pipeline stage,
 // used only as the parity checker (tests/, __graft_entry__.smoke()) and as bench.py's cpu_baseline
 // ("port"). Never linked into the product. Header comment of tri_oracle.h states the parity status
-// ("parity unpinned" against the Vulkan driver; pinned by KATs + committed fixtures).
+// ("parity unpinned" against the Vulkan driver; pinned by KATs + committed fixtures, and cross-checked
+// against an independent float64 restatement in tests/test_oracle_clip_f64.py).
 //
 // It restates, in this order:
 //   * Default.vert main() (Trident-Forge/Assets/Shaders/Default.vert:60-105)
