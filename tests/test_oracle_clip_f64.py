@@ -238,9 +238,12 @@ def f64_colour(scene, fd, margin):
             a = C[None, :, 0] - px[:, None] * C[None, :, 3]
             c = C[None, :, 1] - py[:, None] * C[None, :, 3]
             b = np.cross(a, c)
-            b /= b.sum(1, keepdims=True)
-            inside = np.all(b >= 0, axis=1)
-            z = (b @ C[:, 2]) / (b @ C[:, 3])
+            bs = b.sum(1, keepdims=True)
+            ok = np.abs(bs[:, 0]) > 1e-300  # a degenerate (zero-area) triangle has no weights
+            b = b / np.where(ok[:, None], bs, 1.0)
+            inside = ok & np.all(b >= 0, axis=1)
+            bw = b @ C[:, 3]
+            z = (b @ C[:, 2]) / np.where(inside, bw, 1.0)
             hit = inside & (np.abs(z - fd[sl][cand]) <= 1e-9)
             if not hit.any():
                 continue
@@ -271,6 +274,13 @@ def test_oracle_colour_matches_float64_shading_textured(oracle):
     # sun + 4 point lights, an sRGB texture with alpha under REPEAT, tint, uv scale/offset/tiling, vertex colours
     diff = _check_colour(oracle, sc.textured_grid(320, 180, 30), 30000)
     assert (diff == 0).mean() > 0.9
+
+
+def test_oracle_colour_matches_float64_shading_sphere(oracle):
+    # curved normals out to grazing view angles (N.V -> 0: the 1e-4 clamps of Default.frag), two point lights
+    s = sc.sphere_c2(320, 240, 40, 60)
+    s.skybox = None
+    _check_colour(oracle, s, 6000)
 
 
 def test_oracle_colour_matches_float64_shading_clipped(oracle):

@@ -347,18 +347,18 @@ def test_own_geometry_after_a_shared_one(oracle):
 
 def test_gpu_against_float64_pipeline(flags):
     """The HIP frame against the float64 restatement of the Vulkan rules and the reference shaders
-    (tests/test_oracle_clip_f64.py), without the oracle in between: interior pixels of the textured grid and
-    of the near-clip grid, and the skybox pass. Exact shading holds the oracle's bits, so 1 LSB; the fast
+    (tests/test_oracle_clip_f64.py), without the oracle in between: interior pixels of the textured grid, the
+    near-clip grid and a sphere out to grazing angles, and the skybox pass. Exact shading holds the oracle's bits, so 1 LSB; the fast
     build is within 1 LSB of the oracle, so 2."""
     import test_oracle_clip_f64 as f64
 
     tol = 1 if flags else 2
-    for s in (sc.textured_grid(320, 180, 30), sc.near_clip_grid(320, 240, 24)):
+    for s in (sc.textured_grid(320, 180, 30), sc.near_clip_grid(320, 240, 24), sc.sphere_c2(320, 240, 40, 60)):
         s.skybox = None
         gc, gd, _ = render_gpu(s, flags=flags)
         fd, margin, _, _ = f64.f64_depth(s)
         ref, mask = f64.f64_colour(s, fd, margin)
-        assert mask.sum() > 30000
+        assert mask.sum() > 6000
         want = np.rint(np.clip(ref, 0, 1) * 255.0)
         diff = np.abs(gc[..., [2, 1, 0, 3]].astype(np.float64) - want)[mask]
         assert diff.max() <= tol, (s.name, diff.max())
