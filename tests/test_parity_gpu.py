@@ -348,11 +348,12 @@ def test_own_geometry_after_a_shared_one(oracle):
 def test_gpu_against_float64_pipeline(flags):
     """The HIP frame against the float64 restatement of the Vulkan rules and the reference shaders
     (tests/test_oracle_clip_f64.py), without the oracle in between: interior pixels of the textured grid, the
-    near-clip grid and a sphere out to grazing angles, and the skybox pass. Exact shading holds the oracle's bits, so 1 LSB; the fast
-    build is within 1 LSB of the oracle, so 2."""
+    near-clip grid and a sphere out to grazing angles, and the skybox pass. Both builds are within 1 LSB of the
+    oracle (the exact build's powf / IEEE divides may round a channel differently from glibc's) and the oracle
+    within 1 LSB of float64, so the bar is 2 LSB."""
     import test_oracle_clip_f64 as f64
 
-    tol = 1 if flags else 2
+    tol = 2
     for s in (sc.textured_grid(320, 180, 30), sc.near_clip_grid(320, 240, 24), sc.sphere_c2(320, 240, 40, 60)):
         s.skybox = None
         gc, gd, _ = render_gpu(s, flags=flags)
