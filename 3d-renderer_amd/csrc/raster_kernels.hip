@@ -379,6 +379,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
 // in slot order (its rows' clusters), so the stride spreads them over different workgroups: at N = 8 a
 // workgroup holds at most one, and 3/4 of the launch's dispatches (all empty) are gone. The cluster flags
 // for k_setup are the same lanes' work as in k_vertex, grid-strided.
+static_assert(TRI_VBLOCK == TRI_BLOCK, "k_vertex_band: one workgroup-wide pass per vertex block");
 __global__ __launch_bounds__(TRI_BLOCK) void k_vertex_band(TriFrameParams fp, TriDeviceBuffers b) {
     __shared__ uint32_t blk_vis[TRI_BLOCK / 64];
     const uint32_t tid = threadIdx.x, G = gridDim.x;
@@ -2756,28 +2757,13 @@ static void launch_raster(const TriFrameParams& fp, const TriDeviceBuffers& b, h
     else (void)tri_launch_raster_plain(fp, b, stream);  // raster_plain.hip (errors surface in hipGetLastError)
 }
 
-// TRI_BAND_VERTEX=0: row bands of single-draw frames take k_vertex instead of k_vertex_band (A/B only)
-static bool band_vertex_off() {
-    static const bool off = [] {
-        const char* e = getenv("TRI_BAND_VERTEX");
-        return e && e[0] == '0';
-    }();
-    return off;
-}
-
 hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
                             hipEvent_t* ev) {
-    static const bool debug_sync = getenv("TRI_DEBUG_SYNC") != nullptr;
-    static const char* names[] = {"vertex", "shadow raster", "setup", "raster", "end"};
     auto rec = [&](int i) {
         if (ev) (void)hipEventRecord(ev[i], stream);
-        if (debug_sync) {
-            const hipError_t e = hipStreamSynchronize(stream);
-            fprintf(stderr, "[tri_raster] before %s: %s\n", names[i], hipGetErrorString(e));
-        }
     };
     rec(kStageVertex);
-    if (fp.nslots > 0 && fp.cull_vertex && fp.one_draw && !band_vertex_off())
+    if (fp.nslots > 0 && fp.cull_vertex && fp.one_draw)
         // one workgroup per four vertex blocks (TRI_VBLOCK == TRI_BLOCK slots each)
         hipLaunchKernelGGL(k_vertex_band, dim3((fp.nslots + 4u * TRI_VBLOCK - 1) / (4u * TRI_VBLOCK)), dim3(TRI_BLOCK), 0,
                            stream, fp, b);

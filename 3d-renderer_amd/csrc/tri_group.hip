@@ -45,6 +45,8 @@ struct tri_group {
     uint32_t* frame[2] = {nullptr, nullptr};  // W*H on the display device
     hipEvent_t present_done[2] = {nullptr, nullptr};  // consumer fence per buffer (tri_group_present)
     bool present_armed[2] = {false, false};
+    hipEvent_t blit_done[2] = {nullptr, nullptr};  // per buffer: the group's blit of it (tri_group_blit_linear)
+    bool blit_armed[2] = {false, false};
     bool asm_recorded[2] = {false, false};  // asm_done[p] holds a recorded assembly
     uint64_t frames = 0;                    // frames enqueued
     uint32_t* present = nullptr;            // tri_group_blit_linear's owned target (display device)
@@ -124,6 +126,7 @@ int tri_group_destroy(tri_group* g) {
         for (int p = 0; p < 2; ++p) {
             if (g->frame[p]) (void)hipFree(g->frame[p]);
             if (g->present_done[p]) (void)hipEventDestroy(g->present_done[p]);
+            if (g->blit_done[p]) (void)hipEventDestroy(g->blit_done[p]);
         }
         if (g->present) (void)hipFree(g->present);
     }
@@ -174,7 +177,8 @@ int tri_group_create(const tri_group_config* cfg, tri_group** out) {
     for (int p = 0; p < 2; ++p) {
         if (hipMalloc(&g->frame[p], (size_t)g->W * g->H * 4) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: frame allocation failed"));
-        if (hipEventCreateWithFlags(&g->present_done[p], hipEventDisableTiming) != hipSuccess)
+        if (hipEventCreateWithFlags(&g->present_done[p], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&g->blit_done[p], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: event creation failed"));
         g->band_buf[p].assign(g->n, nullptr);
     }
@@ -275,8 +279,9 @@ int tri_group_render(tri_group* g) {
         uint32_t* out_ptr;
         if (g->dev[r] == ddev) {
             out_ptr = g->frame[p] + (size_t)g->y0[r] * g->W;  // in place
-            // the consumer of frame k - 2 (same buffer) has released it
+            // the consumer of frame k - 2 (same buffer) has released it, and the group's blit has read it
             if (g->present_armed[p]) GH(hipStreamWaitEvent(s, g->present_done[p], 0));
+            if (g->blit_armed[p]) GH(hipStreamWaitEvent(s, g->blit_done[p], 0));
         } else {
             out_ptr = g->band_buf[p][r];
             // frame k - 2's assembly read this buffer
@@ -292,7 +297,8 @@ int tri_group_render(tri_group* g) {
         GH(hipSetDevice(g->udev[u]));
         for (uint32_t r = 0; r < g->n; ++r)
             if (g->urank[r] == (int)u) GH(hipStreamWaitEvent(g->astream[u], g->band_done[r], 0));
-        // the receives into frame[p] wait for the consumer's fence on frame k - 2 as well
+        // the receives into frame[p] wait for the consumer's fence on frame k - 2 as well (the blit of frame
+        // k - 2 ran on this same stream, so it is ordered already)
         if ((int)u == disp && g->present_armed[p]) GH(hipStreamWaitEvent(g->astream[u], g->present_done[p], 0));
     }
     if (!g->comm.empty()) {
@@ -312,6 +318,7 @@ int tri_group_render(tri_group* g) {
     }
     g->asm_recorded[p] = true;
     g->present_armed[p] = false;  // waited for; the consumer re-arms it for this frame
+    g->blit_armed[p] = false;
     ++g->frames;
     return TRI_OK;
 }
@@ -397,9 +404,15 @@ int tri_group_blit_linear(tri_group* g, void* dst, uint32_t width, uint32_t heig
         out = g->present;
         g->present_w = width;
         g->present_h = height;
+    } else {
+        g->present_w = g->present_h = 0;  // the owned target no longer holds the latest blit: read_present fails
     }
-    GH(tri_launch_blit(g->frame[last_parity(g)], (int32_t)g->W, (int32_t)g->H, out, (int32_t)width,
-                       (int32_t)height, tri_internal_unorm_lut(g->ctx[g->display]), s));
+    const uint32_t p = last_parity(g);
+    GH(tri_launch_blit(g->frame[p], (int32_t)g->W, (int32_t)g->H, out, (int32_t)width, (int32_t)height,
+                       tri_internal_unorm_lut(g->ctx[g->display]), s));
+    // the blit reads frame[p] on the assembly stream: frame k + 2's in-place bands (context streams) wait for it
+    GH(hipEventRecord(g->blit_done[p], s));
+    g->blit_armed[p] = true;
     return TRI_OK;
 }
 

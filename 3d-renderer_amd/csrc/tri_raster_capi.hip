@@ -455,14 +455,9 @@ int resolve_draws(tri_ctx* c) {
     return TRI_OK;
 }
 
-// A stride near nchunks / golden ratio, coprime to nchunks (TRI_SETUP_STRIDE=1 restores linear order).
+// A stride near nchunks / golden ratio, coprime to nchunks.
 uint32_t chunk_stride(uint32_t n) {
-    static const long env = [] {
-        const char* e = getenv("TRI_SETUP_STRIDE");
-        return e ? atol(e) : 0L;
-    }();
     if (n <= 2) return 1;
-    if (env > 0) return (uint32_t)env % n ? (uint32_t)env % n : 1u;
     uint32_t s = (uint32_t)((double)n * 0.6180339887) | 1u;
     auto gcd = [](uint32_t a, uint32_t b) { while (b) { const uint32_t t = a % b; a = b; b = t; } return a; };
     while (gcd(s, n) != 1) ++s;
@@ -568,13 +563,13 @@ int check_overflow(tri_ctx* c) {
 // (fewer than 0.05 triangles per pixel, e.g. C2's 50k-triangle sphere at 1080p) on small grids use
 // 16x16 bins: more workgroups to balance, and few triangles span several bins. Dense bands keep 32x32
 // (16x16 measured 10-25 % slower there: more bin entries, each paying its edge set-up).
-// TRI_BIN_LOG2 (4..6) forces a size (diagnostics).
+// -DTRI_FORCE_BIN_LOG2=4..6 forces a size (diagnostics builds only, tools/build_variant.sh).
+#ifndef TRI_FORCE_BIN_LOG2
+#define TRI_FORCE_BIN_LOG2 0
+#endif
 int choose_bin_grid(tri_ctx* c) {
-    static const int forced = [] {
-        const char* e = getenv("TRI_BIN_LOG2");
-        const int v = e ? atoi(e) : 0;
-        return (v >= 4 && v <= 6) ? v : 0;
-    }();
+    constexpr int forced = TRI_FORCE_BIN_LOG2;
+    static_assert(forced == 0 || (forced >= 4 && forced <= 6), "TRI_FORCE_BIN_LOG2: 4, 5 or 6");
     auto bins = [c](int bl) {
         const int32_t bs = 1 << bl;
         return ((c->W + bs - 1) / bs) * ((c->y1 - c->y0 + bs - 1) / bs);
@@ -1126,14 +1121,8 @@ int tri_render(tri_ctx* c) {
     fp.cull_on = culling ? 1u : 0u;
     fp.cull_vertex = fp.cull_on && !c->shadow.size ? 1u : 0u;  // the pre-pass needs every caster
     fp.ncl_total = c->ncl_total;
-    {
-        static const bool multi_off = [] {  // TRI_BAND_SETUP=0: one chunk per k_setup workgroup (A/B only)
-            const char* e = getenv("TRI_BAND_SETUP");
-            return e && e[0] == '0';
-        }();
-        fp.setup_multi = fp.cull_on && fp.one_draw && !c->shadow.size && !multi_off ? 1u : 0u;
-        if (fp.setup_multi) c->last_nchunks = (fp.nchunks + 3u) / 4u;  // the launch's statistics slots
-    }
+    fp.setup_multi = fp.cull_on && fp.one_draw && !c->shadow.size ? 1u : 0u;
+    if (fp.setup_multi) c->last_nchunks = (fp.nchunks + 3u) / 4u;  // the launch's statistics slots
     if (c->shadow.size) {
         fp.shadow_on = 1u;
         fp.s_size = c->shadow.size;
@@ -1260,6 +1249,8 @@ int tri_blit_linear(tri_ctx* c, void* dst, uint32_t width, uint32_t height) {
         out = c->d_present;
         c->present_w = width;
         c->present_h = height;
+    } else {
+        c->present_w = c->present_h = 0;  // the owned target no longer holds the latest blit: read_present fails
     }
     // the alpha half of the decode LUT is the UNORM8 decode b / 255 (IEEE float division)
     HIP_TRY(tri_launch_blit(c->d_color, c->W, c->H, out, (int32_t)width, (int32_t)height, c->d_lut + 256, c->stream));

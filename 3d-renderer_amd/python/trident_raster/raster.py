@@ -182,10 +182,10 @@ class TriRaster:
     def blit(self, width, height, dst_ptr=None):
         """tri_blit_linear: scale the frame to width x height (VK_FILTER_LINEAR presentation blit)."""
         _check(_lib.tri_blit_linear(self._ctx, C.c_void_p(dst_ptr) if dst_ptr else None, width, height))
-        self._present = (width, height)
+        self._present = None if dst_ptr else (width, height)  # a caller-owned dst leaves the owned target stale
 
     def read_present(self):
-        w, h = self._present
+        w, h = getattr(self, "_present", None) or (1, 1)  # nothing owned to read: the library reports TRI_E_STATE
         out = np.empty((h, w, 4), dtype=np.uint8)
         _check(_lib.tri_read_present(self._ctx, _ptr(out)))
         return out
@@ -368,10 +368,10 @@ class TriGroup:
 
     def blit(self, width, height, dst_ptr=None):
         _check(_lib.tri_group_blit_linear(self._g, C.c_void_p(dst_ptr) if dst_ptr else None, width, height))
-        self._present = (width, height)
+        self._present = None if dst_ptr else (width, height)
 
     def read_present(self):
-        w, h = self._present
+        w, h = getattr(self, "_present", None) or (1, 1)  # nothing owned to read: the library reports TRI_E_STATE
         out = np.empty((h, w, 4), dtype=np.uint8)
         _check(_lib.tri_group_read_present(self._g, _ptr(out)))
         return out

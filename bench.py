@@ -298,8 +298,8 @@ def split_candidates(height, world, min_rows=32, inflights=(2,)):
     in `inflights` (a band's kernels are short at large N, and a third frame in flight keeps more of the
     GPU busy: N = 8 rank 4 on one GPU 33.4k frames/s with 2, 39.0k with 3, 33.1k with 4)."""
     base = height / world
-    ds = []
-    for m in (1.0, 1.25, 1.5, 2.0, 2.5):
+    ds = [int(round(base))]  # the equal split always (a small frame or a large world may leave no other)
+    for m in (1.25, 1.5, 2.0, 2.5):
         d = int(round(base * m))
         if height - d >= (world - 1) * min_rows and d not in ds:
             ds.append(d)

@@ -350,17 +350,21 @@ int tri_group_frame(tri_group* group, void** device_bgra8, int32_t* device);
 /* The same buffer as a tri_image (GetViewportTexture's handle for a multi-device viewport). */
 int tri_group_get_output(tri_group* group, tri_image* out);
 /* Consumer fence ("frame k presented"): the caller is done reading the most recent frame once the work
- * already enqueued on hip_stream (a stream on the display device) has run; NULL = done now. Frame k + 2,
- * which reuses that buffer, waits for this point on the device before any band or receive writes it.
- * Without a fence the next-but-one frame overwrites the buffer unconditionally (a caller that reads with
- * tri_group_readback, which synchronises, needs none). */
+ * already enqueued on hip_stream (a stream on the display device) has run; NULL = once the frame's own
+ * assembly (and any tri_group_blit_linear of it) has run on the group's assembly stream, i.e. the caller
+ * reads nothing further on other streams. Frame k + 2, which reuses that buffer, waits for this point on
+ * the device before any band or receive writes it. Without a fence the next-but-one frame overwrites the
+ * buffer unconditionally (a caller that reads with tri_group_readback, which synchronises, needs none);
+ * a tri_group_blit_linear of frame k is always waited for (it reads the buffer on the assembly stream). */
 int tri_group_present(tri_group* group, void* hip_stream);
 /* Binds caller-owned geometry objects: for every band, the one of `geometries` on the band's device
  * (TRI_E_INVALID if a band's device has none). count 0 returns the bands to the group's own per-device
  * copies, which tri_group_upload_geometry fills. The objects must outlive the binding. */
 int tri_group_bind_geometry(tri_group* group, uint32_t count, tri_geometry* const* geometries);
 /* tri_blit_linear / tri_read_present over the assembled frame (the presentation blit of a multi-device
- * viewport, on the display device, stream-ordered after the frame's assembly). */
+ * viewport, on the display device, stream-ordered after the frame's assembly; frame k + 2's bands and
+ * receives wait for the blit of frame k). A blit into a caller-supplied dst does not touch the group's
+ * own present target: tri_group_read_present then fails with TRI_E_STATE until a blit with dst = NULL. */
 int tri_group_blit_linear(tri_group* group, void* dst, uint32_t width, uint32_t height);
 int tri_group_read_present(tri_group* group, uint8_t* bgra8);
 

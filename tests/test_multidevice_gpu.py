@@ -204,6 +204,80 @@ def test_group_blit_matches_single_context():
     assert np.array_equal(got, want)
 
 
+def _hip_device_count():
+    n = C.c_int(0)
+    return n.value if C.CDLL("libamdhip64.so").hipGetDeviceCount(C.byref(n)) == 0 else 0
+
+
+def _camera_frames(oracle, cams, w=320, h=240):
+    from trident_raster import scenes
+
+    frames = []
+    for cam in cams:
+        s = sc.primitives_row(oracle, w, h)
+        view, proj = scenes.editor_camera(cam, (0, 0, 0), 60.0, (w, h))
+        s.ubo = scenes.pack_ubo(view, proj, cam, [{"type": "directional"}])
+        frames.append(s)
+    return frames
+
+
+def test_group_blit_is_fenced_against_the_next_but_one_frame(oracle):
+    """render k, blit k into a caller buffer, render k + 1 and k + 2 without a present fence or a
+    sync: frame k + 2 reuses frame k's buffer, and its in-place bands (context streams) must wait for the
+    blit (assembly stream). The blitted image equals the single-context blit of frame k; read_present
+    refuses after a blit into a caller buffer (the owned target is stale)."""
+    from trident_raster import abi, raster, scenes
+
+    frames = _camera_frames(oracle, [(0.0, 1.0, 6.0), (0.6, 1.3, 6.5), (-0.7, 0.8, 5.5)], 640, 480)
+    with raster.TriRaster(640, 480) as r:
+        scenes.load_scene(r, frames[0])
+        r.render_frame()
+        r.blit(800, 600)
+        want = r.read_present()
+    import torch
+
+    dst = torch.empty((600, 800, 4), dtype=torch.uint8, device="cuda:0")
+    with raster.TriGroup(640, 480, [0] * 4, display=2) as g:
+        scenes.load_scene(g, frames[0])
+        g.render_frame()
+        g.blit(800, 600, dst_ptr=dst.data_ptr())
+        for s in frames[1:]:
+            g.set_frame(s.ubo, s.clear)
+            g.render_frame()
+        g.synchronize()
+        with pytest.raises(RuntimeError):
+            g.read_present()
+        got = dst.cpu().numpy()
+    assert np.array_equal(got, want), int((got != want).any(-1).sum())
+
+
+@pytest.mark.skipif(_hip_device_count() < 2, reason="the RCCL branch of tri_group needs two HIP devices")
+@pytest.mark.parametrize("devices,display", [([0, 1, 0, 1], 0), ([1, 0, 1, 0, 1], 3)])
+def test_group_distinct_devices_rccl_assembly(oracle, devices, display):
+    """the cross-device branch of tri_group (ncclCommInitAll, grouped ncclSend/ncclRecv into the
+    rotating frame buffer, band buffers reused after asm_done). Four frames with different cameras; each
+    assembled frame equals the single-context render, and the k - 1 buffer stays untouched while frame k
+    renders. Skipped on a one-GPU box (runs on the driver's multi-GPU node)."""
+    from trident_raster import raster, scenes
+
+    frames = _camera_frames(oracle, [(0.0, 1.0, 6.0), (0.6, 1.3, 6.5), (-0.7, 0.8, 5.5), (0.2, 1.6, 7.0)])
+    want = [_render_single(s, 0)[0] for s in frames]
+    with raster.TriGroup(320, 240, devices, display=display) as g:
+        scenes.load_scene(g, frames[0])
+        prev = None
+        for k, s in enumerate(frames):
+            g.set_frame(s.ubo, s.clear)
+            g.render_frame()
+            g.synchronize()
+            p, dev = g.frame_pointer()
+            img = _copy_frame(p, dev, 320, 240)
+            assert np.array_equal(img, want[k]), f"frame {k}: {int((img != want[k]).any(-1).sum())} pixels differ"
+            if prev is not None:
+                assert np.array_equal(_copy_frame(prev[0], dev, 320, 240), want[k - 1]), f"frame {k - 1} overwritten"
+            prev = (p, k)
+            g.present()
+
+
 @pytest.fixture(scope="module")
 def app_mod():
     from trident_raster import app

@@ -224,6 +224,8 @@ def test_band_split_partition():
     assert all(2160 - d >= 7 * 32 for d, _ in bench.split_candidates(2160, 8, inflights=(2, 3)))
     assert bench.split_candidates(2160, 2)[-1][0] <= 2160 - 32
     assert {k for _, k in bench.split_candidates(2160, 4, inflights=(2, 3))} == {2, 3}
+    # a small frame over a large world keeps the equal split (no empty candidate list)
+    assert bench.split_candidates(240, 8) == [(30, 2)]
 
 
 def _uneven_worker(rank, world, port, scene_name, out_dir, display_rows, ring):
