@@ -83,7 +83,10 @@ public:
 
     void SetViewport(uint32_t viewportId, const ViewportInfo& info);  // also makes it the active viewport
     // Swapchain extent stand-in (Swapchain.cpp): when set, DrawFrame ends by blitting the active
-    // viewport onto a present image of this size with linear filtering (Renderer.cpp:5346-5361).
+    // viewport onto a present image of this size with linear filtering (Renderer.cpp:5346-5361). With no
+    // active viewport rendered this frame (none registered, or the active one has no target), it renders
+    // the skybox, meshes and sprites straight into the present image at this extent instead — the legacy
+    // direct-to-swapchain path (Renderer.cpp:5233, :5498-5590), camera from GetActiveCamera().
     void SetPresentExtent(uint32_t width, uint32_t height) { m_PresentWidth = width; m_PresentHeight = height; }
     // The last presented image (RGBA8 rows, BGRA reordered) and its size; false before a present.
     bool ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height);
@@ -115,7 +118,8 @@ public:
     // (BGRA reordered to RGBA), optionally the D32 depth.
     bool ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgba, std::vector<float>* depth = nullptr);
     // The exact uniform block + draw list DrawFrame submits for a viewport (GatherMeshDraws +
-    // UpdateUniformBuffer + the push-constant loop): host-only, used to test frame preparation.
+    // UpdateUniformBuffer + the push-constant loop): host-only, used to test frame preparation. Id 0 with
+    // no viewport registered: the legacy present pass's inputs (GetActiveCamera()).
     bool BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::vector<tri_draw>& draws);
     // Rasterizer flags (TRI_FLAG_*) used for viewports created from now on.
     void SetRasterFlags(uint32_t flags) { m_RasterFlags = flags; }
@@ -181,6 +185,9 @@ private:
     void BuildDrawList(std::vector<tri_draw>& out) const;
     const Camera* GetActiveCamera(const ViewportContext& context) const;
     bool PrepareViewport(ViewportContext& context);
+    // One viewport pass: pre-pass / palette / UBO / draws, then tri_render (asynchronous); false on error.
+    bool SubmitTarget(ViewportContext& context, const tri_global_ubo& ubo, const std::vector<tri_draw>& draws,
+                      const tri_shadow_config& shadow, bool shadowOn);
     void RecordFrameTiming(double milliseconds);
 
     Camera* m_EditorCamera = nullptr;
@@ -233,6 +240,8 @@ private:
     uint32_t m_PresentWidth = 0, m_PresentHeight = 0;
     tri_ctx* m_PresentSource = nullptr;    // viewport context the last present was blitted from
     tri_group* m_PresentGroup = nullptr;   // ... or multi-device viewport
+    ViewportContext m_LegacyTarget;        // the legacy path's present-extent target (no active viewport)
+    bool m_PresentLegacy = false;          // the last present was rendered directly (legacy path), not blitted
     uint32_t m_RasterFlags = 0;
 
     glm::vec3 m_AmbientColor{0.03f};

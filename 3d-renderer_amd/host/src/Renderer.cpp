@@ -222,8 +222,12 @@ void Renderer::DestroyViewportTargets() {
         vc.m_HasImage = false;
         vc.m_Width = vc.m_Height = 0;
     }
+    tri_destroy(m_LegacyTarget.m_Ctx);
+    tri_group_destroy(m_LegacyTarget.m_Group);
+    m_LegacyTarget = ViewportContext{};
     m_PresentSource = nullptr;
     m_PresentGroup = nullptr;
+    m_PresentLegacy = false;
     // after every context that bound them
     tri_geometry_destroy(m_SharedGeometry);
     m_SharedGeometry = nullptr;
@@ -909,11 +913,39 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
 
 bool Renderer::BuildFrameInputs(uint32_t viewportId, tri_global_ubo& ubo, std::vector<tri_draw>& draws) {
     auto it = m_Viewports.find(viewportId);
-    if (it == m_Viewports.end()) return false;
+    // viewport id 0 without a registered viewport 0: the legacy present pass when no viewport renders
+    if (it == m_Viewports.end() && (viewportId != 0 || !m_Viewports.empty())) return false;
     GatherDraws();
     PrepareBonePaletteBuffer();
-    UpdateUniformBuffer(GetActiveCamera(it->second), ubo);
+    UpdateUniformBuffer(it != m_Viewports.end() ? GetActiveCamera(it->second) : GetActiveCamera(), ubo);
     BuildDrawList(draws);
+    return true;
+}
+
+bool Renderer::SubmitTarget(ViewportContext& vc, const tri_global_ubo& ubo, const std::vector<tri_draw>& draws,
+                            const tri_shadow_config& shadow, bool shadowOn) {
+    const Target t{vc.m_Ctx, vc.m_Group};
+    if (std::memcmp(&vc.m_Shadow, &shadow, sizeof shadow) != 0) {  // pre-pass on / off / refitted
+        if (t.Shadow(shadowOn ? &shadow : nullptr) != TRI_OK) {
+            LogError("shadow map", tri_last_error());
+            return false;
+        }
+        vc.m_Shadow = shadow;
+    }
+    if (vc.m_BonePalette != m_BonePalette) {  // the bone SSBO (binding 4) of this frame
+        if (t.Bones(m_BonePalette.data(), (uint32_t)(m_BonePalette.size() / 16)) != TRI_OK) {
+            LogError("bone palette", tri_last_error());
+            return false;
+        }
+        vc.m_BonePalette = m_BonePalette;
+    }
+    const float clear[4] = {m_ClearColor.x, m_ClearColor.y, m_ClearColor.z, m_ClearColor.w};
+    if (t.Frame(&ubo, clear) != TRI_OK || t.Draws(draws.data(), (uint32_t)draws.size()) != TRI_OK ||
+        t.Render() != TRI_OK) {
+        LogError("DrawFrame", tri_last_error());
+        return false;
+    }
+    vc.m_HasImage = t.Output(&vc.m_Image) == TRI_OK;
     return true;
 }
 
@@ -926,35 +958,43 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     BuildDrawList(draws);
     tri_shadow_config shadow;
     const bool shadowOn = BuildShadowConfig(shadow);
-    const float clear[4] = {m_ClearColor.x, m_ClearColor.y, m_ClearColor.z, m_ClearColor.w};
     std::vector<ViewportContext*> submitted;
-    for (auto& it : m_Viewports) {  // RecordCommandBuffer's per-viewport render passes
-        ViewportContext& vc = it.second;
-        if (!PrepareViewport(vc)) continue;
-        const Target t{vc.m_Ctx, vc.m_Group};
-        if (std::memcmp(&vc.m_Shadow, &shadow, sizeof shadow) != 0) {  // pre-pass on / off / refitted
-            if (t.Shadow(shadowOn ? &shadow : nullptr) != TRI_OK) {
-                LogError("shadow map", tri_last_error());
-                continue;
-            }
-            vc.m_Shadow = shadow;
-        }
-        if (vc.m_BonePalette != m_BonePalette) {  // the bone SSBO (binding 4) of this frame
-            if (t.Bones(m_BonePalette.data(), (uint32_t)(m_BonePalette.size() / 16)) != TRI_OK) {
-                LogError("bone palette", tri_last_error());
-                continue;
-            }
-            vc.m_BonePalette = m_BonePalette;
-        }
+    tri_global_ubo lastUbo{};
+    // RecordCommandBuffer's per-viewport render passes: the other viewports first, the primary one last
+    // (Renderer.cpp:5208-5221), so the uniform block left bound is the primary viewport's
+    auto pass = [&](ViewportContext& vc) {
+        if (!PrepareViewport(vc)) return;
         tri_global_ubo ubo;
         UpdateUniformBuffer(GetActiveCamera(vc), ubo);
-        if (t.Frame(&ubo, clear) != TRI_OK || t.Draws(draws.data(), (uint32_t)draws.size()) != TRI_OK ||
-            t.Render() != TRI_OK) {
-            LogError("DrawFrame", tri_last_error());
-            continue;
-        }
-        vc.m_HasImage = t.Output(&vc.m_Image) == TRI_OK;
+        if (!SubmitTarget(vc, ubo, draws, shadow, shadowOn)) return;
+        lastUbo = ubo;
         submitted.push_back(&vc);
+    };
+    for (auto& it : m_Viewports)
+        if (it.first != m_ActiveViewportId) pass(it.second);
+    auto active = m_Viewports.find(m_ActiveViewportId);
+    if (active != m_Viewports.end()) pass(active->second);
+    const bool primaryActive = active != m_Viewports.end() &&
+                               std::find(submitted.begin(), submitted.end(), &active->second) != submitted.end();
+    // Legacy direct-to-swapchain path (Renderer.cpp:5233, :5498-5590): without a rendered primary viewport
+    // the skybox, the meshes and the sprites go straight into the present image at the swapchain extent,
+    // cleared to the clear colour, with the uniform block last recorded: the null-camera update
+    // (GetActiveCamera()) when no viewport rendered (:5223-5226), else the last viewport pass's.
+    m_PresentSource = nullptr;
+    m_PresentGroup = nullptr;
+    m_PresentLegacy = false;
+    ViewportContext* legacy = nullptr;
+    if (!primaryActive && m_PresentWidth && m_PresentHeight) {
+        m_LegacyTarget.m_Info.Size = glm::vec2((float)m_PresentWidth, (float)m_PresentHeight);
+        m_LegacyTarget.m_Info.ViewportID = 0;
+        if (PrepareViewport(m_LegacyTarget)) {
+            tri_global_ubo ubo = lastUbo;
+            if (submitted.empty()) UpdateUniformBuffer(GetActiveCamera(), ubo);
+            if (SubmitTarget(m_LegacyTarget, ubo, draws, shadow, shadowOn)) {
+                legacy = &m_LegacyTarget;
+                submitted.push_back(legacy);
+            }
+        }
     }
     // Frame fence (Renderer.cpp:744-760). A frame that outgrew the bin/clip queues has grown them
     // inside tri_synchronize and is re-rendered, so a presented frame is always complete.
@@ -967,14 +1007,14 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
         }
         if (rc != TRI_OK) LogError("frame fence", tri_last_error());
         if (rc == TRI_OK) vc->m_HasImage = t.Output(&vc->m_Image) == TRI_OK;  // a re-render moves a group's buffer
+        if (vc == legacy && rc == TRI_OK) {
+            m_PresentSource = vc->m_Ctx;
+            m_PresentGroup = vc->m_Group;
+            m_PresentLegacy = true;
+        }
     }
     // Primary viewport -> swapchain image, VK_FILTER_LINEAR (Renderer.cpp:5346-5361).
-    m_PresentSource = nullptr;
-    m_PresentGroup = nullptr;
-    auto active = m_Viewports.find(m_ActiveViewportId);
-    if (m_PresentWidth && m_PresentHeight && active != m_Viewports.end() &&
-        (active->second.m_Ctx || active->second.m_Group) &&
-        std::find(submitted.begin(), submitted.end(), &active->second) != submitted.end()) {
+    if (primaryActive && m_PresentWidth && m_PresentHeight) {
         const Target t{active->second.m_Ctx, active->second.m_Group};
         if (t.Blit(m_PresentWidth, m_PresentHeight) == TRI_OK && t.Sync() == TRI_OK) {
             m_PresentSource = active->second.m_Ctx;
@@ -1048,7 +1088,8 @@ bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgb
 bool Renderer::ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height) {
     if (!m_PresentSource && !m_PresentGroup) return false;
     std::vector<uint8_t> bgra((size_t)m_PresentWidth * m_PresentHeight * 4);
-    if (Target{m_PresentSource, m_PresentGroup}.ReadPresent(bgra.data()) != TRI_OK) {
+    const Target t{m_PresentSource, m_PresentGroup};
+    if ((m_PresentLegacy ? t.Readback(bgra.data(), nullptr) : t.ReadPresent(bgra.data())) != TRI_OK) {
         LogError("present readback", tri_last_error());
         return false;
     }

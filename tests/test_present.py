@@ -113,3 +113,63 @@ def test_gpu_shim_presents_the_active_viewport(oracle):
     vp2, _ = a.read_pixels(2, 320, 200, depth=False)
     present = a.read_present(960, 540)
     assert np.array_equal(present, oracle.blit_linear(vp2[..., [2, 1, 0, 3]], 960, 540)[..., [2, 1, 0, 3]])
+
+
+# ---- legacy direct-to-swapchain path (Renderer.cpp:5233, :5498-5590) --------------------------------
+def _legacy_app(with_viewport=False, flags=0):
+    from trident_raster import app, scenes
+
+    a = app.TridentApp(raster_flags=flags)
+    a.set_assets_dir(scenes.ASSETS_DIR)
+    a.set_camera("editor", (0.0, 3.0, 8.0), (-8.0, 15.0, 0.0))
+    a.add_mesh_entity("cube", position=(0.0, 3.0, -2.0), rotation=(0.0, 30.0, 0.0))
+    a.add_mesh_entity("sphere", position=(1.5, 3.0, -1.0))
+    a.add_sprite_entity(position=(-1.5, 2.5, 0.0), tint=(1.0, 0.5, 0.25, 1.0))
+    if with_viewport:
+        a.set_viewport(1, 320, 200)
+    a.set_present_extent(400, 300)
+    return a
+
+
+def test_legacy_pass_inputs_without_viewports():
+    """With no viewport registered, the present pass's uniform block comes from GetActiveCamera() (the
+    reference's null-camera UpdateUniformBuffer, Renderer.cpp:5223-5226): frame_inputs(0) exposes it; once
+    a viewport exists, id 0 names no pass."""
+    a = _legacy_app()
+    ubo, draws = a.frame_inputs(0)
+    assert len(draws) == 3  # cube, sphere, then the sprite (GatherSpriteDraws after the meshes)
+    assert abs(ubo.camera_position[1] - 3.0) < 1e-6
+    a.close()
+    b = _legacy_app(with_viewport=True)
+    with pytest.raises(Exception):
+        b.frame_inputs(0)
+    b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exact", [False, True])
+def test_gpu_shim_legacy_present_without_viewport(oracle, exact):
+    """No SetViewport call: DrawFrame renders the skybox, the meshes and the sprite straight into the present
+    image at the present (swapchain) extent; the image matches the oracle's frame of the same inputs (depth
+    is not stored by that pass, Pipeline.cpp:395)."""
+    from trident_raster import abi, scenes
+
+    a = _legacy_app(flags=abi.TRI_FLAG_EXACT_SHADING if exact else 0)
+    a.draw_frame()
+    a.draw_frame()
+    present = a.read_present(400, 300)
+    ubo, draws = a.frame_inputs(0)
+    vb, ib, ranges = a.geometry()
+    s = scenes.Scene("legacy", 400, 300, vb, ib, ranges, draws, ubo,
+                     materials=[(m[0], m[1]) for m in a.materials()], skybox=scenes.reference_skybox())
+    oc, od, _ = oracle.render(s)
+    assert (od != 0x3F800000).sum() > 2000  # the meshes and the sprite are on screen
+    diff = np.abs(present.astype(np.int16) - oc[..., [2, 1, 0, 3]].astype(np.int16))
+    assert int(diff.max()) <= 1, int(diff.max())
+    # registering a viewport switches the present back to the blit of the primary viewport
+    a.set_viewport(1, 320, 200)
+    a.draw_frame()
+    vp1, _ = a.read_pixels(1, 320, 200, depth=False)
+    assert np.array_equal(a.read_present(400, 300),
+                          oracle.blit_linear(vp1[..., [2, 1, 0, 3]], 400, 300)[..., [2, 1, 0, 3]])
+    a.close()
