@@ -68,6 +68,11 @@ hipError_t tri_launch_raster_plain(const TriFrameParams& fp, const TriDeviceBuff
 hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* dst, int32_t dw, int32_t dh,
                            const float* unorm_lut, hipStream_t stream);
 
+// The band codec (band_codec.hip): B8G8R8A8 <-> 3-byte BGR with a known alpha.
+hipError_t tri_launch_pack_bgr24(const uint32_t* src, uint8_t* dst, uint64_t n, uint32_t alpha, uint32_t* flag,
+                                 hipStream_t stream);
+hipError_t tri_launch_unpack_bgr24(const uint8_t* src, uint32_t* dst, uint64_t n, uint32_t alpha, hipStream_t stream);
+
 // Internal accessors for the group layer (tri_group.hip): a context's stream and device.
 hipStream_t tri_internal_stream(tri_ctx* ctx);
 int tri_internal_device(tri_ctx* ctx);

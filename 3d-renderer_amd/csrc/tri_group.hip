@@ -31,6 +31,7 @@
 
 struct tri_group {
     uint32_t W = 0, H = 0, n = 0, display = 0;
+    uint32_t gflags = 0;               // TRI_GROUP_*
     std::vector<int32_t> dev;        // per band
     std::vector<uint32_t> y0, y1;    // per band rows
     std::vector<tri_ctx*> ctx;       // per band
@@ -42,6 +43,10 @@ struct tri_group {
     std::vector<hipEvent_t> band_done;   // per band: its render of the current frame finished
     std::vector<hipEvent_t> asm_done[2]; // per buffer parity, per distinct device: that frame's assembly finished
     std::vector<uint32_t*> band_buf[2];  // per buffer parity, per band on a non-display device: its colour band
+    std::vector<uint8_t*> band_pack[2];  // ... the band as 3-byte pixels (band_codec.hip), on the band's device
+    std::vector<uint8_t*> rx[2];         // ... its 3-byte pixels received on the display device
+    std::vector<uint32_t*> flag;         // per remote band, on its device: the packer's alpha check (0 = lossless)
+    bool packed_last = false;            // the most recent frame travelled as 3-byte pixels
     uint32_t* frame[2] = {nullptr, nullptr};  // W*H on the display device
     hipEvent_t present_done[2] = {nullptr, nullptr};  // consumer fence per buffer (tri_group_present)
     bool present_armed[2] = {false, false};
@@ -55,6 +60,11 @@ struct tri_group {
 };
 
 namespace {
+
+// A band that travels to the display device (another device, or every band with TRI_GROUP_STAGE_BANDS).
+bool travels(const tri_group* g, uint32_t r) {
+    return r != g->display && (g->dev[r] != g->dev[g->display] || (g->gflags & TRI_GROUP_STAGE_BANDS));
+}
 
 int hip_fail(hipError_t e, const char* what) {
     const std::string m = std::string(what) + ": " + hipGetErrorString(e);
@@ -105,11 +115,16 @@ int tri_group_destroy(tri_group* g) {
     for (ncclComm_t c : g->comm)
         if (c) (void)ncclCommDestroy(c);
     for (int p = 0; p < 2; ++p)
-        for (uint32_t r = 0; r < g->band_buf[p].size(); ++r)
-            if (g->band_buf[p][r]) {
-                (void)hipSetDevice(g->dev[r]);
-                (void)hipFree(g->band_buf[p][r]);
+        for (uint32_t r = 0; r < g->band_buf[p].size(); ++r) {
+            (void)hipSetDevice(g->dev[r]);
+            if (g->band_buf[p][r]) (void)hipFree(g->band_buf[p][r]);
+            if (r < g->band_pack[p].size() && g->band_pack[p][r]) (void)hipFree(g->band_pack[p][r]);
+            if (p == 0 && r < g->flag.size() && g->flag[r]) (void)hipFree(g->flag[r]);
+            if (!g->dev.empty() && r < g->rx[p].size() && g->rx[p][r]) {
+                (void)hipSetDevice(g->dev[g->display]);
+                (void)hipFree(g->rx[p][r]);
             }
+        }
     for (uint32_t r = 0; r < g->band_done.size(); ++r)
         if (g->band_done[r]) {
             (void)hipSetDevice(g->dev[r]);
@@ -147,6 +162,7 @@ int tri_group_create(const tri_group_config* cfg, tri_group** out) {
     g->H = cfg->height;
     g->n = cfg->device_count;
     g->display = cfg->display;
+    g->gflags = cfg->group_flags;
     auto bail = [&](int rc) { tri_group_destroy(g); return rc; };
     for (uint32_t r = 0; r < g->n; ++r) {
         const int32_t d = cfg->devices ? cfg->devices[r] : (int32_t)r;
@@ -181,15 +197,32 @@ int tri_group_create(const tri_group_config* cfg, tri_group** out) {
             hipEventCreateWithFlags(&g->blit_done[p], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: event creation failed"));
         g->band_buf[p].assign(g->n, nullptr);
+        g->band_pack[p].assign(g->n, nullptr);
+        g->rx[p].assign(g->n, nullptr);
     }
+    g->flag.assign(g->n, nullptr);
     g->band_done.assign(g->n, nullptr);
     for (uint32_t r = 0; r < g->n; ++r) {
         if (hipSetDevice(g->dev[r]) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: hipSetDevice failed"));
-        if (g->dev[r] != ddev)
+        if (travels(g, r)) {
+            const size_t px = (size_t)(g->y1[r] - g->y0[r]) * g->W;
             for (int p = 0; p < 2; ++p)
-                if (hipMalloc(&g->band_buf[p][r], (size_t)(g->y1[r] - g->y0[r]) * g->W * 4) != hipSuccess)
+                if (hipMalloc(&g->band_buf[p][r], px * 4) != hipSuccess ||
+                    (!(g->gflags & TRI_GROUP_NO_PACK) && hipMalloc(&g->band_pack[p][r], px * 3) != hipSuccess))
                     return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: band buffer allocation failed"));
+            if (!(g->gflags & TRI_GROUP_NO_PACK)) {
+                if (hipMalloc(&g->flag[r], 4) != hipSuccess || hipMemset(g->flag[r], 0, 4) != hipSuccess)
+                    return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: flag allocation failed"));
+                if (hipSetDevice(ddev) != hipSuccess)
+                    return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: hipSetDevice failed"));
+                for (int p = 0; p < 2; ++p)
+                    if (hipMalloc(&g->rx[p][r], px * 3) != hipSuccess)
+                        return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: receive buffer allocation failed"));
+                if (hipSetDevice(g->dev[r]) != hipSuccess)
+                    return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: hipSetDevice failed"));
+            }
+        }
         if (hipEventCreateWithFlags(&g->band_done[r], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: event creation failed"));
     }
@@ -202,6 +235,7 @@ int tri_group_create(const tri_group_config* cfg, tri_group** out) {
             hipEventCreateWithFlags(&g->asm_done[1][u], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: assembly stream creation failed"));
     }
+    (void)hipDeviceSynchronize();  // the zeroed flags (null stream) before any band's stream packs
     if (g->udev.size() > 1) {  // one RCCL communicator per distinct device, in this process
         g->comm.assign(g->udev.size(), nullptr);
         const ncclResult_t r = ncclCommInitAll(g->comm.data(), (int)g->udev.size(), g->udev.data());
@@ -273,23 +307,34 @@ int tri_group_render(tri_group* g) {
     if (!g) return tri_internal_fail(TRI_E_INVALID, "tri_group_render: null group");
     const int32_t ddev = g->dev[g->display];
     const uint32_t p = (uint32_t)(g->frames & 1u);
+    // 3-byte transfer when every pixel's alpha is provably one value (every band context holds the same
+    // frame state: tri_group_set_* broadcasts it)
+    int32_t alpha = -1;
+    if (!(g->gflags & TRI_GROUP_NO_PACK)) {
+        const int rc = tri_frame_alpha(g->ctx[g->display], &alpha);
+        if (rc) return rc;
+    }
+    const bool pack = alpha >= 0;
     for (uint32_t r = 0; r < g->n; ++r) {
         GH(hipSetDevice(g->dev[r]));
         hipStream_t s = tri_internal_stream(g->ctx[r]);
         uint32_t* out_ptr;
-        if (g->dev[r] == ddev) {
+        if (!travels(g, r)) {
             out_ptr = g->frame[p] + (size_t)g->y0[r] * g->W;  // in place
             // the consumer of frame k - 2 (same buffer) has released it, and the group's blit has read it
             if (g->present_armed[p]) GH(hipStreamWaitEvent(s, g->present_done[p], 0));
             if (g->blit_armed[p]) GH(hipStreamWaitEvent(s, g->blit_done[p], 0));
         } else {
             out_ptr = g->band_buf[p][r];
-            // frame k - 2's assembly read this buffer
+            // frame k - 2's assembly read this buffer (and its packed copy)
             if (g->asm_recorded[p]) GH(hipStreamWaitEvent(s, g->asm_done[p][g->urank[r]], 0));
         }
         int rc = tri_bind_output(g->ctx[r], out_ptr, nullptr);  // depth stays in the band context
         if (rc) return rc;
         if ((rc = tri_render(g->ctx[r]))) return rc;
+        if (pack && travels(g, r))  // B, G, R bytes only, behind the band's raster on its stream
+            GH(tri_launch_pack_bgr24(g->band_buf[p][r], g->band_pack[p][r], (uint64_t)(g->y1[r] - g->y0[r]) * g->W,
+                                     (uint32_t)alpha, g->flag[r], s));
         GH(hipEventRecord(g->band_done[r], s));
     }
     const int disp = g->urank[g->display];
@@ -301,17 +346,32 @@ int tri_group_render(tri_group* g) {
         // k - 2 ran on this same stream, so it is ordered already)
         if ((int)u == disp && g->present_armed[p]) GH(hipStreamWaitEvent(g->astream[u], g->present_done[p], 0));
     }
+    // where band r's bytes land on the display device: straight into the frame, or its receive buffer
+    auto landing = [&](uint32_t r) -> void* {
+        return pack ? static_cast<void*>(g->rx[p][r]) : static_cast<void*>(g->frame[p] + (size_t)g->y0[r] * g->W);
+    };
+    auto source = [&](uint32_t r) -> const void* {
+        return pack ? static_cast<const void*>(g->band_pack[p][r]) : static_cast<const void*>(g->band_buf[p][r]);
+    };
+    auto bytes = [&](uint32_t r) { return (size_t)(g->y1[r] - g->y0[r]) * g->W * (pack ? 3u : 4u); };
     if (!g->comm.empty()) {
         GN(ncclGroupStart());
         for (uint32_t r = 0; r < g->n; ++r) {
             if (g->dev[r] == ddev) continue;
-            const size_t bytes = (size_t)(g->y1[r] - g->y0[r]) * g->W * 4;
-            GN(ncclSend(g->band_buf[p][r], bytes, ncclUint8, disp, g->comm[g->urank[r]], g->astream[g->urank[r]]));
-            GN(ncclRecv(g->frame[p] + (size_t)g->y0[r] * g->W, bytes, ncclUint8, g->urank[r], g->comm[disp],
-                        g->astream[disp]));
+            GN(ncclSend(source(r), bytes(r), ncclUint8, disp, g->comm[g->urank[r]], g->astream[g->urank[r]]));
+            GN(ncclRecv(landing(r), bytes(r), ncclUint8, g->urank[r], g->comm[disp], g->astream[disp]));
         }
         GN(ncclGroupEnd());
     }
+    GH(hipSetDevice(ddev));
+    for (uint32_t r = 0; r < g->n; ++r)  // staged bands on the display device itself: a device-local copy
+        if (travels(g, r) && g->dev[r] == ddev)
+            GH(hipMemcpyAsync(landing(r), source(r), bytes(r), hipMemcpyDeviceToDevice, g->astream[disp]));
+    if (pack)  // restore the 4-byte pixels with the proven alpha, behind the receives
+        for (uint32_t r = 0; r < g->n; ++r)
+            if (travels(g, r))
+                GH(tri_launch_unpack_bgr24(g->rx[p][r], g->frame[p] + (size_t)g->y0[r] * g->W,
+                                           (uint64_t)(g->y1[r] - g->y0[r]) * g->W, (uint32_t)alpha, g->astream[disp]));
     for (size_t u = 0; u < g->udev.size(); ++u) {
         GH(hipSetDevice(g->udev[u]));
         GH(hipEventRecord(g->asm_done[p][u], g->astream[u]));
@@ -319,6 +379,7 @@ int tri_group_render(tri_group* g) {
     g->asm_recorded[p] = true;
     g->present_armed[p] = false;  // waited for; the consumer re-arms it for this frame
     g->blit_armed[p] = false;
+    g->packed_last = pack;
     ++g->frames;
     return TRI_OK;
 }
@@ -346,7 +407,24 @@ int tri_group_synchronize(tri_group* g) {
         GH(hipSetDevice(g->udev[u]));
         GH(hipStreamSynchronize(g->astream[u]));
     }
+    for (uint32_t r = 0; r < g->n && status == TRI_OK; ++r) {  // every packed band kept the proven alpha
+        if (!g->flag[r]) continue;
+        uint32_t f = 0;
+        GH(hipSetDevice(g->dev[r]));
+        GH(hipMemcpy(&f, g->flag[r], 4, hipMemcpyDeviceToHost));
+        if (f) status = tri_internal_fail(TRI_E_STATE, "tri_group: a band's alpha was not the proven value (lossy 3-byte transfer)");
+    }
     return status;
+}
+
+int tri_group_transfer_info(tri_group* g, uint32_t* bytes_per_pixel, uint64_t* inbound_bytes) {
+    if (!g || !bytes_per_pixel || !inbound_bytes) return tri_internal_fail(TRI_E_INVALID, "tri_group_transfer_info: null argument");
+    *bytes_per_pixel = g->packed_last ? 3u : 4u;
+    uint64_t in = 0;
+    for (uint32_t r = 0; r < g->n; ++r)
+        if (g->dev[r] != g->dev[g->display]) in += (uint64_t)(g->y1[r] - g->y0[r]) * g->W * *bytes_per_pixel;
+    *inbound_bytes = in;
+    return TRI_OK;
 }
 
 int tri_group_readback(tri_group* g, uint8_t* bgra, uint32_t* depth) {

@@ -106,6 +106,7 @@ struct tri_ctx {
     uint32_t* d_tex[TRI_MAX_TEXTURE_SLOTS] = {};
     uint32_t tex_w[TRI_MAX_TEXTURE_SLOTS] = {}, tex_h[TRI_MAX_TEXTURE_SLOTS] = {};
     uint32_t tex_solid[TRI_MAX_TEXTURE_SLOTS] = {};  // texel of a 1x1 slot (RGBA8)
+    int16_t tex_alpha[TRI_MAX_TEXTURE_SLOTS] = {};    // the alpha byte every texel of the slot has, or -1
     TriTexDesc texdesc[TRI_MAX_TEXTURE_SLOTS] = {};  // per-slot descriptors, aliases resolved
     bool tex_dirty = true;
     float* d_lut = nullptr;
@@ -913,6 +914,12 @@ int tri_upload_texture(tri_ctx* c, uint32_t slot, const uint8_t* rgba, uint32_t 
     c->tex_w[slot] = w;
     c->tex_h[slot] = h;
     std::memcpy(&c->tex_solid[slot], rgba, 4);
+    c->tex_alpha[slot] = rgba[3];
+    for (size_t i = 1, n = (size_t)w * h; i < n; ++i)
+        if (rgba[4 * i + 3] != rgba[3]) {
+            c->tex_alpha[slot] = -1;
+            break;
+        }
     c->tex_dirty = true;
     return TRI_OK;
 }
@@ -1019,6 +1026,29 @@ int tri_set_frame(tri_ctx* c, const tri_global_ubo* ubo, const float clear[4]) {
         c->clear_bgra = unorm8_host(clear[2]) | (unorm8_host(clear[1]) << 8) | (unorm8_host(clear[0]) << 16) |
                         (unorm8_host(clear[3]) << 24);
     c->frame_set = true;
+    return TRI_OK;
+}
+
+// Default.frag's alpha is (base.a * tint.a) * texture.a (the UNORM decode b / 255, bilinear taps of one value
+// return it exactly), stored as unorm8 by both shading builds; background pixels hold the clear colour's alpha,
+// or 1 where Skybox.frag writes. The same float operations here give the byte each draw can produce.
+int tri_frame_alpha(tri_ctx* c, int32_t* alpha) {
+    if (!c || !alpha) return fail(TRI_E_INVALID, "tri_frame_alpha: null argument");
+    int32_t a = (int32_t)(c->clear_bgra >> 24);
+    bool uniform = !c->sky_size || a == 255;
+    for (const tri_draw& d : c->draws) {
+        if (!uniform) break;
+        int32_t slot = d.pc.texture_slot;
+        if (slot < 0 || slot >= TRI_MAX_TEXTURE_SLOTS || !c->d_tex[slot]) slot = 0;  // unused slots alias slot 0
+        const int16_t ta = c->tex_alpha[slot];
+        if (ta < 0) {
+            uniform = false;
+            break;
+        }
+        const float t = (float)ta / 255.0f;
+        uniform = (int32_t)unorm8_host((c->mat0.base_color_factor[3] * d.pc.tint[3]) * t) == a;
+    }
+    *alpha = uniform ? a : -1;
     return TRI_OK;
 }
 

@@ -186,9 +186,12 @@ class TriGroupConfig(C.Structure):
         ("display", C.c_uint32),
         ("devices", C.POINTER(C.c_int32)),
         ("flags", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("group_flags", C.c_uint32),
     ]
 
+
+TRI_GROUP_NO_PACK = 0x1
+TRI_GROUP_STAGE_BANDS = 0x2
 
 for _s, _n in ((TriImage, 32), (TriGroupConfig, 32), (TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
                (TriShadowConfig, 80)):
@@ -215,6 +218,9 @@ CABI_FUNCTIONS = [
     ("tri_readback", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     ("tri_blit_linear", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_read_present", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("tri_frame_alpha", C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
+    ("tri_pack_bgr24", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("tri_unpack_bgr24", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
     ("tri_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("tri_get_timing", C.c_int, [C.c_void_p, C.POINTER(TriTiming)]),
     ("tri_get_frame_stats", C.c_int, [C.c_void_p, C.POINTER(TriFrameStats)]),
@@ -249,6 +255,7 @@ CABI_FUNCTIONS = [
     ("tri_group_bind_geometry", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_void_p)]),
     ("tri_group_blit_linear", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_group_read_present", C.c_int, [C.c_void_p, C.c_void_p]),
+    ("tri_group_transfer_info", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
 ]
 
 

@@ -153,6 +153,12 @@ class TriRaster:
     def set_stream(self, stream_ptr):
         _check(_lib.tri_set_stream(self._ctx, C.c_void_p(stream_ptr) if stream_ptr else None))
 
+    def frame_alpha(self):
+        """tri_frame_alpha: the alpha byte every pixel of the next frame has, or -1 if not provably uniform."""
+        a = C.c_int32()
+        _check(_lib.tri_frame_alpha(self._ctx, C.byref(a)))
+        return a.value
+
     def bind_geometry(self, geometry):
         """tri_bind_geometry: reference a shared TriGeometry (None: back to the context's own)."""
         _check(_lib.tri_bind_geometry(self._ctx, geometry._g if geometry is not None else None))
@@ -237,6 +243,21 @@ class TriGeometry:
             self._g = None
 
 
+def pack_bgr24(src_ptr, dst_ptr, pixels, alpha, flag_ptr=None, stream_ptr=None):
+    """tri_pack_bgr24: B8G8R8A8 -> 3-byte BGR on the device, stream-ordered (flag: device uint32 set when an
+    alpha byte differs from `alpha`)."""
+    load_library()
+    _check(_lib.tri_pack_bgr24(C.c_void_p(src_ptr), C.c_void_p(dst_ptr), pixels, alpha,
+                               C.c_void_p(flag_ptr) if flag_ptr else None, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
+def unpack_bgr24(src_ptr, dst_ptr, pixels, alpha, stream_ptr=None):
+    """tri_unpack_bgr24: 3-byte BGR -> B8G8R8A8 with the given alpha, stream-ordered."""
+    load_library()
+    _check(_lib.tri_unpack_bgr24(C.c_void_p(src_ptr), C.c_void_p(dst_ptr), pixels, alpha,
+                                 C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
 def copy_device_to_host(ptr, nbytes, device=0):
     """hipMemcpy of `nbytes` at a device pointer (a tri_image handle) into a numpy byte array."""
     hip = C.CDLL("libamdhip64.so")
@@ -252,11 +273,11 @@ class TriGroup:
     """tri_group: one frame over N row-band contexts on the given devices (RCCL gather onto the display
     band's device; bands sharing that device render in place)."""
 
-    def __init__(self, width, height, devices, display=0, flags=0):
+    def __init__(self, width, height, devices, display=0, flags=0, group_flags=0):
         lib = load_library()
         n = len(devices)
         self._devs = (C.c_int32 * n)(*devices)
-        cfg = abi.TriGroupConfig(width, height, n, display, self._devs, flags, 0)
+        cfg = abi.TriGroupConfig(width, height, n, display, self._devs, flags, group_flags)
         g = C.c_void_p()
         _check(lib.tri_group_create(C.byref(cfg), C.byref(g)))
         self._g = g
@@ -375,3 +396,9 @@ class TriGroup:
         out = np.empty((h, w, 4), dtype=np.uint8)
         _check(_lib.tri_group_read_present(self._g, _ptr(out)))
         return out
+
+    def transfer_info(self):
+        """tri_group_transfer_info: (bytes per pixel on the links, inbound RCCL bytes) of the last frame."""
+        bpp, inbound = C.c_uint32(), C.c_uint64()
+        _check(_lib.tri_group_transfer_info(self._g, C.byref(bpp), C.byref(inbound)))
+        return bpp.value, inbound.value

@@ -82,7 +82,70 @@ class _Works:
             w.wait()
 
 
-def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=0, spans=None):
+class BandCodec:
+    """Lossless 3-byte/pixel band transfer: a band whose alpha bytes all equal `alpha`
+    (tri_frame_alpha proves it from the context's state) travels as its B, G, R bytes and is restored on
+    arrival. On the GPU the HIP kernels tri_pack_bgr24 / tri_unpack_bgr24 run on torch's current stream; on
+    the CPU (gloo tests) the same byte shuffle runs in torch. An alpha byte that differs sets `flag` (the
+    sender's check that the transfer stayed lossless); check() raises on it."""
+
+    def __init__(self, alpha, device):
+        import torch
+
+        self.alpha = int(alpha)
+        self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+        self.gpu = device.type == "cuda"
+
+    def pack(self, band, out):
+        """band: int32[n] (B8G8R8A8) -> out: uint8[3n]."""
+        import torch
+
+        n = band.numel()
+        if self.gpu:
+            from trident_raster import raster
+
+            raster.pack_bgr24(band.data_ptr(), out.data_ptr(), n, self.alpha, self.flag.data_ptr(),
+                              torch.cuda.current_stream().cuda_stream)
+            return
+        b = band.view(torch.uint8).view(n, 4)
+        out.view(n, 3).copy_(b[:, :3])
+        if bool((b[:, 3] != self.alpha).any()):
+            self.flag.fill_(1)
+
+    def unpack(self, src, band):
+        """src: uint8[3n] -> band: int32[n] with alpha restored."""
+        import torch
+
+        n = band.numel()
+        if self.gpu:
+            from trident_raster import raster
+
+            raster.unpack_bgr24(src.data_ptr(), band.data_ptr(), n, self.alpha, torch.cuda.current_stream().cuda_stream)
+            return
+        b = band.view(torch.uint8).view(n, 4)
+        b[:, :3].copy_(src.view(n, 3))
+        b[:, 3].fill_(self.alpha)
+
+    def check(self):
+        if int(self.flag.item()):
+            raise RuntimeError("a band's alpha was not the promised uniform value: the 3-byte transfer was lossy")
+
+
+class _Unpacked:
+    """Receive-side handle of a packed gather on the GPU: the unpack ran on the assembly stream behind the
+    receives; wait() makes the current stream wait for it (no host block)."""
+
+    def __init__(self, event):
+        self.event = event
+
+    def wait(self):
+        import torch
+
+        torch.cuda.current_stream().wait_event(self.event)
+
+
+def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=0, spans=None, codec=None,
+                 stage=None, asm_stream=None):
     """Assemble the full frame from the per-rank BGRA8 bands; band r lands at elements
     [spans[r][0], spans[r][0] + spans[r][1]) of the frame (default: equal bands, r * n).
     mode "gather" (default): onto the display rank `dst` only, as one grouped point-to-point exchange
@@ -91,7 +154,10 @@ def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=
     already is the frame's view (BandRenderer renders it in place). "allgather": onto every rank
     (all_gather_into_tensor, equal bands only: (N-1)/N of the frame into every GPU).
     Returns the work handle (None for world 1) with async_op, else the assembled frame (None on a
-    non-display rank in gather mode). gloo backs the same calls in the CPU tests."""
+    non-display rank in gather mode). gloo backs the same calls in the CPU tests.
+    codec (gather mode only): bands travel as 3 bytes per pixel through `stage` (the sender's uint8[3n]
+    buffer; on the display rank a dict rank -> uint8 buffer per remote band), unpacked into the frame on
+    `asm_stream` (GPU) once received."""
     if world == 1:
         return None if async_op else band
     import torch.distributed as dist
@@ -106,10 +172,34 @@ def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=
         own = frame.narrow(0, *spans[dst])
         if own.data_ptr() != band.data_ptr():
             own.copy_(band)
-        ops = [dist.P2POp(dist.irecv, frame.narrow(0, *spans[r]), r) for r in range(world) if r != dst]
+        if codec is None:
+            ops = [dist.P2POp(dist.irecv, frame.narrow(0, *spans[r]), r) for r in range(world) if r != dst]
+        else:
+            ops = [dist.P2POp(dist.irecv, stage[r], r) for r in range(world) if r != dst]
     else:
-        ops = [dist.P2POp(dist.isend, band, dst)]
+        if codec is not None:
+            codec.pack(band, stage)  # on the current (render) stream, before the send that waits on it
+        ops = [dist.P2POp(dist.isend, band if codec is None else stage, dst)]
     work = _Works(dist.batch_isend_irecv(ops))
+    if codec is not None and rank == dst:
+        if frame.is_cuda:
+            import torch
+
+            asm = asm_stream or torch.cuda.current_stream()
+            with torch.cuda.stream(asm):
+                work.wait()  # the assembly stream waits for the receives
+                for r in range(world):
+                    if r != dst:
+                        codec.unpack(stage[r], frame.narrow(0, *spans[r]))
+                ev = torch.cuda.Event()
+                ev.record(asm)
+            work = _Unpacked(ev)
+        else:
+            work.wait()
+            for r in range(world):
+                if r != dst:
+                    codec.unpack(stage[r], frame.narrow(0, *spans[r]))
+            work = _Works([])  # complete (a gloo request is waited for once)
     if async_op:
         return work
     work.wait()
@@ -134,8 +224,10 @@ class GatherRing:
     render stream waits for frame k's gather (work.wait() is a stream wait; the host does not
     block). Throughput is then max(render, gather) per frame instead of their sum."""
 
-    def __init__(self, world, band_elems, frame_elems, make, mode="gather", rank=0, dst=0, nbuf=None, spans=None):
+    def __init__(self, world, band_elems, frame_elems, make, mode="gather", rank=0, dst=0, nbuf=None, spans=None,
+                 codec=None, make_bytes=None):
         self.world, self.mode, self.rank, self.dst, self.spans = world, mode, rank, dst, spans
+        self.codec = codec if (world > 1 and mode == "gather") else None
         self.nbuf = nbuf if nbuf else (2 if world > 1 else 1)
         keeps_frame = world > 1 and (mode == "allgather" or rank == dst)
         if keeps_frame and mode == "gather":
@@ -148,6 +240,26 @@ class GatherRing:
             self.frames = [make(frame_elems) for _ in range(self.nbuf)] if keeps_frame else self.bands
         self.pending = [None] * self.nbuf
         self.k = 0
+        self.stage, self.asm_stream = [None] * self.nbuf, None
+        if self.codec is not None:  # 3-byte staging per slot: the sender's packed band, the receiver's per rank
+            sp = spans or [(r * band_elems, band_elems) for r in range(world)]
+            if rank == dst:
+                self.stage = [{r: make_bytes(3 * sp[r][1]) for r in range(world) if r != dst} for _ in range(self.nbuf)]
+                if self.frames[0].is_cuda:
+                    import torch
+
+                    self.asm_stream = torch.cuda.Stream(self.frames[0].device)
+            else:
+                self.stage = [make_bytes(3 * sp[rank][1]) for _ in range(self.nbuf)]
+
+    @property
+    def inbound_bytes(self):
+        """Bytes the display rank receives per frame (0 elsewhere)."""
+        if self.world == 1 or self.rank != self.dst or self.mode != "gather":
+            return 0
+        sp = self.spans or [(r * self.bands[0].numel(), self.bands[0].numel()) for r in range(self.world)]
+        per = 3 if self.codec is not None else 4
+        return sum(per * sp[r][1] for r in range(self.world) if r != self.dst)
 
     def acquire(self):
         """The band buffer frame k renders into (after frame k-2's gather released it)."""
@@ -161,7 +273,8 @@ class GatherRing:
         """Start frame k's gather of the band returned by acquire()."""
         i = self.k % self.nbuf
         self.pending[i] = gather_bands(self.frames[i], self.bands[i], self.world, async_op=True, mode=self.mode,
-                                       rank=self.rank, dst=self.dst, spans=self.spans)
+                                       rank=self.rank, dst=self.dst, spans=self.spans, codec=self.codec,
+                                       stage=self.stage[i], asm_stream=self.asm_stream)
         self.k += 1
 
     def drain(self):
@@ -169,6 +282,11 @@ class GatherRing:
             if w is not None:
                 w.wait()
                 self.pending[i] = None
+
+    def check(self):
+        """Host check (synchronising): every packed band kept the promised alpha."""
+        if self.codec is not None:
+            self.codec.check()
 
     @property
     def frame(self):
@@ -184,7 +302,7 @@ class BandRenderer:
     (Renderer::DrawFrame waits on the fence of the frame in flight two frames back, Renderer.cpp:752-772)."""
 
     def __init__(self, scene, rank, world, device_index, band_world=None, assembly="gather", inflight=1,
-                 display_rows=None):
+                 display_rows=None, pack="auto"):
         import ctypes as C
 
         import torch
@@ -200,9 +318,7 @@ class BandRenderer:
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
         self.dev = torch.device("cuda", device_index)
         self.inflight = max(1, inflight)
-        spans = [(y0 * W, (y1 - y0) * W) for y0, y1 in self.bands] if world > 1 else None
-        self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
-                               mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1), spans=spans)
+        self.spans = spans = [(y0 * W, (y1 - y0) * W) for y0, y1 in self.bands] if world > 1 else None
         self.depth = [torch.empty(rows * W, dtype=torch.float32, device=self.dev) for _ in range(self.inflight)]
         self.geometry = raster.TriGeometry(device_index)
         self.geometry.upload(scene.vertices, scene.indices, scene.meshes)
@@ -220,6 +336,14 @@ class BandRenderer:
             self.rs.append(r)
             self.streams.append(st)
         self.r = self.rs[0]
+        # 3-byte band transfer when every pixel's alpha is provably one value (every rank proves the same
+        # from the same scene, so sender and receiver agree without a message)
+        self.alpha = self.r.frame_alpha()
+        self.codec = BandCodec(self.alpha, self.dev) if (pack == "auto" and self.alpha >= 0 and world > 1 and
+                                                         assembly == "gather") else None
+        self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
+                               mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1), spans=spans,
+                               codec=self.codec, make_bytes=lambda n: torch.empty(n, dtype=torch.uint8, device=self.dev))
         # the per-frame calls with their ctypes arguments built once (a frame at N = 8 is ~60 us of GPU
         # work, so Python-side marshalling per call would show up in the frame rate)
         self._lib = raster.load_library()
@@ -274,6 +398,78 @@ class BandRenderer:
 
         with torch.cuda.stream(self.streams[0]):
             self.ring.drain()
+
+    def _sync(self):
+        import torch
+
+        if self.dev.type == "cuda":
+            torch.cuda.synchronize(self.dev)
+
+    def render_only_ms(self, frames=100):
+        """Diagnostics (N > 1 line): this rank's frames rendered back to back with no assembly, ms per frame."""
+        import torch
+
+        self.drain()
+        self._sync()
+        t0 = time.perf_counter()
+        for k in range(frames):
+            i = k % self.inflight
+            lib, ctx = self._lib, self._ctxs[i]
+            band = self.ring.bands[k % len(self.ring.bands)]
+            with torch.cuda.stream(self.streams[i]):
+                rc = (lib.tri_bind_output(ctx, self._band_ptrs[band.data_ptr()], self._depth_ptrs[i]) or
+                      lib.tri_set_frame(ctx, self._ubo, self._clear) or lib.tri_set_draws(ctx, self._draws, self._ndraws)
+                      or lib.tri_render(ctx))
+            if rc:
+                self._raster._check(rc)
+        self._sync()
+        return (time.perf_counter() - t0) * 1e3 / frames
+
+    def assembly_only_ms(self, frames=100):
+        """Diagnostics (N > 1 line): the band assembly alone (pack, send/receive, unpack), frames back to back
+        with no rendering, ms per frame. Every rank must call it (it runs the collectives)."""
+        import torch
+
+        self.drain()
+        self._sync()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(self.streams[0]):
+            for _ in range(frames):
+                self.ring.acquire()
+                self.ring.publish()
+            self.ring.drain()
+        self._sync()
+        return (time.perf_counter() - t0) * 1e3 / frames
+
+    def codec_ms(self, bands_rows, frames=200):
+        """Diagnostics (--sim-world): the 3-byte codec's cost on one GPU: packing this rank's band, and the
+        display rank's unpack of every other band of the split (ms per frame each)."""
+        import torch
+
+        W = self.scene.width
+        codec = self.codec or BandCodec(max(self.alpha, 0), self.dev)
+        band = self.ring.bands[0]
+        st = torch.empty(3 * band.numel(), dtype=torch.uint8, device=self.dev)
+        self._sync()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            codec.pack(band, st)
+        self._sync()
+        pack = (time.perf_counter() - t0) * 1e3 / frames
+        remote = [r * W for r in bands_rows[1:]]
+        frame = torch.empty(sum(remote) + 16, dtype=torch.int32, device=self.dev)
+        srcs = [torch.empty(3 * n, dtype=torch.uint8, device=self.dev) for n in remote]
+        self._sync()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            off = 0
+            for n, src in zip(remote, srcs):
+                codec.unpack(src, frame.narrow(0, off, n))
+                off += n
+        self._sync()
+        unpack = (time.perf_counter() - t0) * 1e3 / frames
+        return {"pack_ms_per_band": pack, "unpack_ms_display_all_remote_bands": unpack,
+                "remote_bands": len(remote), "band_pixels": band.numel()}
 
     def latency_ms(self, frames=20):
         """Per-frame latency without overlap: render + gather + wait, host-synchronised each frame."""
@@ -575,6 +771,9 @@ def main():
                     help="frames in flight per rank (contexts taking frames in turn, one stream each)")
     ap.add_argument("--assembly", choices=("gather", "allgather"), default="gather",
                     help="N > 1: bands gathered onto the display rank 0 (default) or all-gathered onto every rank")
+    ap.add_argument("--pack", choices=("auto", "off"), default="auto",
+                    help="N > 1 gather: bands travel as 3 bytes per pixel when tri_frame_alpha proves every alpha "
+                         "byte equal (auto), or always as 4 (off)")
     ap.add_argument("--split", default="auto",
                     help="N > 1 gather: 'auto' (time candidate display-band sizes on the hardware, keep the fastest), "
                          "'equal', or the display rank's row count")
@@ -602,7 +801,7 @@ def main():
 
     def make_renderer(sc, display_rows=None, inflight=None):
         return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=inflight or args.inflight,
-                            display_rows=display_rows)
+                            display_rows=display_rows, pack=args.pack)
 
     def choose_split(sc):
         """((display_rows or None, frames in flight), the autotune log) for a config at this world size."""
@@ -618,7 +817,7 @@ def main():
     inflight = args.inflight
     if args.sim_world and world == 1:
         br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=args.inflight,
-                          display_rows=args.sim_display_rows)
+                          display_rows=args.sim_display_rows, pack=args.pack)
     else:
         (display_rows, inflight), split_log = choose_split(scene)
         br = make_renderer(scene, display_rows, inflight)
@@ -629,6 +828,21 @@ def main():
     stats = br.r.frame_stats()
     latency = br.latency_ms()  # one frame end to end (render + gather), no overlap
     stage = stage_ms(timing)
+    assembly = None
+    if world > 1:  # what sets the rate: the slowest rank's render alone vs the assembly alone (outside the timed region)
+        br.ring.check()  # every packed band kept its alpha (lossless)
+        render_ms = max_over_ranks(br.render_only_ms(), br.dev, dist_on)
+        asm_ms = max_over_ranks(br.assembly_only_ms(), br.dev, dist_on)
+        inbound = br.ring.inbound_bytes if rank == 0 else 0
+        assembly = {"render_ms": render_ms, "assembly_ms": asm_ms, "inbound_bytes_per_frame": inbound,
+                    "band_bytes_per_pixel": 3 if br.codec is not None else 4, "frame_alpha": br.alpha,
+                    "render_bound_fps": 1e3 / render_ms if render_ms > 0 else None,
+                    "assembly_bound_fps": 1e3 / asm_ms if asm_ms > 0 else None,
+                    "bound": "assembly" if asm_ms > render_ms else "render",
+                    "note": "max over ranks; render and assembly each timed alone, back to back, outside the timed region"}
+    elif args.sim_world > 1:  # one band of an N-way split on one GPU: the codec's cost per band
+        assembly = {"sim_world": args.sim_world, "sim_rank": args.sim_rank, "frame_alpha": br.alpha,
+                    "codec": br.codec_ms([y1 - y0 for y0, y1 in br.bands])}
 
     # roofline of the dominant kernel (k_raster = tile_raster_shade): its algorithmic bytes per
     # launch are the colour + depth it must store for its band (4 + 4 B per pixel),
@@ -712,6 +926,7 @@ def main():
                                "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9 if frame_ms > 0 else None,
                                "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if frame_ms > 0 else None},
             "stage_ms": stage,
+            "assembly": assembly,
             "frame_stats": stats,
             "secondary": secondary,
             "cpu_baseline": cpu,

@@ -291,6 +291,20 @@ int tri_blit_linear(tri_ctx* ctx, void* dst, uint32_t width, uint32_t height);
  * w*h*4 bytes of BGRA8. */
 int tri_read_present(tri_ctx* ctx, uint8_t* bgra8);
 
+/* ---- lossless 3-byte band transfer (multi-GPU assembly) ----------------------------
+ * Replaces nothing in the reference (it has no multi-GPU path); it serves tri_group's and the bench's
+ * gather onto the display GPU, whose inbound xGMI bytes bound the N = 8 frame rate.
+ * tri_frame_alpha: the alpha byte EVERY pixel of the next tri_render of ctx will have, proven from the
+ * context's state (material record 0, each draw's tint and texture slot, the clear colour, the skybox),
+ * or -1 when it cannot be proven uniform. A band of such a frame can travel as 3 bytes per pixel. */
+int tri_frame_alpha(tri_ctx* ctx, int32_t* alpha);
+/* B8G8R8A8 (4 B/pixel, device pointer, 4-B aligned) <-> B, G, R bytes (3 B/pixel, device pointer),
+ * stream-ordered on hip_stream (NULL = the null stream). pack: every alpha byte that differs from `alpha`
+ * sets *flag (a device uint32, may be NULL) to nonzero — the transfer would not be lossless; unpack writes
+ * `alpha` into every pixel. */
+int tri_pack_bgr24(const void* bgra8, void* bgr8, uint64_t pixels, uint32_t alpha, uint32_t* flag, void* hip_stream);
+int tri_unpack_bgr24(const void* bgr8, void* bgra8, uint64_t pixels, uint32_t alpha, void* hip_stream);
+
 /* ---- measurement -------------------------------------------------------------------------- */
 /* enable = N > 0: HIP events around every stage of every N-th frame (1 = all frames; sampling keeps
  * the event overhead out of throughput runs); 0 = off. Also resets the accumulators. */
@@ -318,8 +332,14 @@ typedef struct tri_group_config {
     const int32_t* devices; /* N HIP ordinals, NULL = 0..N-1; an ordinal may repeat (bands sharing  *
                              * a device are assembled without copies)                               */
     uint32_t flags;         /* TRI_FLAG_* for every band context                                    */
-    uint32_t reserved;
+    uint32_t group_flags;   /* TRI_GROUP_* (0 = defaults)                                           */
 } tri_group_config;
+/* Bands travel to the display device as 4-byte pixels even when tri_frame_alpha proves a uniform alpha
+ * (default: 3 bytes per pixel then, restored on arrival — lossless, 25 % fewer bytes per link). */
+#define TRI_GROUP_NO_PACK 0x1u
+/* Bands on the display device render into band buffers and travel like remote bands (a device-local copy
+ * instead of RCCL): the remote path's buffers, fences and codec on a single GPU (tests, diagnostics). */
+#define TRI_GROUP_STAGE_BANDS 0x2u
 
 int tri_group_create(const tri_group_config* config, tri_group** out_group);
 int tri_group_destroy(tri_group* group);
@@ -367,6 +387,9 @@ int tri_group_bind_geometry(tri_group* group, uint32_t count, tri_geometry* cons
  * own present target: tri_group_read_present then fails with TRI_E_STATE until a blit with dst = NULL. */
 int tri_group_blit_linear(tri_group* group, void* dst, uint32_t width, uint32_t height);
 int tri_group_read_present(tri_group* group, uint8_t* bgra8);
+/* The most recent frame's band transfer: bytes per pixel on the links (3 when tri_frame_alpha proved a
+ * uniform alpha and packing is on, else 4) and the bytes the display device received over RCCL. */
+int tri_group_transfer_info(tri_group* group, uint32_t* bytes_per_pixel, uint64_t* inbound_bytes);
 
 #ifdef __cplusplus
 } /* extern "C" */

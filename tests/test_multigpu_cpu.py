@@ -349,3 +349,98 @@ def test_autotune_split_picks_the_balanced_display_band(tmp_path):
     d, k, cands = int(picks[0][0]), int(picks[0][1]), [int(x) for x in picks[0][2:]]
     assert cands == [500, 625, 750] * 2
     assert (d, k) == (750, 3), (d, k, cands)  # 1.5 x the equal band: the balance point
+
+
+def _codec_worker(rank, world, port, scene_name, out_dir, display_rows, ring, alpha):
+    """The 3-byte band transfer (bench.BandCodec) over gloo: bands packed by the senders, received as bytes
+    and unpacked into the display rank's frame, one-shot (gather_bands) or through the double buffer."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    sys.path.insert(0, os.path.join(ROOT, "3d-renderer_amd", "python"))
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import torch
+    import torch.distributed as dist
+
+    import bench
+    import oracle_py
+    import scene_cases as sc
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    scene = getattr(sc, scene_name)()
+    W, H = scene.width, scene.height
+    bands = bench.band_split(H, world, display_rows)
+    spans = [(a * W, (b - a) * W) for a, b in bands]
+    col, _, _ = oracle_py.render(scene, band=bands[rank], threads=2)
+    mine = torch.from_numpy(np.ascontiguousarray(col).view(np.int32).reshape(-1).copy())
+    codec = bench.BandCodec(alpha, torch.device("cpu"))
+    u8 = lambda n: torch.zeros(n, dtype=torch.uint8)  # noqa: E731
+    if ring:
+        r = bench.GatherRing(world, spans[rank][1], H * W, lambda n: torch.zeros(n, dtype=torch.int32), rank=rank,
+                             spans=spans, codec=codec, make_bytes=u8)
+        if rank == 0:
+            assert r.inbound_bytes == 3 * sum(n for _, n in spans[1:])
+        for k in range(3):
+            band = r.acquire()
+            band.copy_(mine if k == 2 else torch.full_like(mine, ((alpha << 24) | k) - (1 << 32)))
+            r.publish()
+        r.drain()
+        out = r.frame if rank == 0 else None
+    else:
+        stage = {q: u8(3 * spans[q][1]) for q in range(1, world)} if rank == 0 else u8(3 * spans[rank][1])
+        out = bench.gather_bands(torch.empty(H * W, dtype=torch.int32), mine, world, rank=rank, spans=spans,
+                                 codec=codec, stage=stage)
+    try:
+        codec.check()
+        ok = True
+    except RuntimeError:
+        ok = False
+    np.save(os.path.join(out_dir, f"alpha_ok_{rank}.npy"), np.array(ok))
+    if out is not None:
+        np.save(os.path.join(out_dir, "frame.npy"), out.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,display_rows,ring", [(2, None, False), (3, 200, True), (4, None, True), (4, 90, False)])
+def test_packed_bands_assemble_bit_exact(world, display_rows, ring, oracle, tmp_path):
+    """bands sent as 3 bytes per pixel assemble to the same frame as 4-byte bands (the oracle's
+    full frame), when every alpha byte is the promised 255 (grid_c3: opaque material, tint, white texture and
+    clear colour)."""
+    import torch.multiprocessing as mp
+
+    import scene_cases as sc
+
+    mp.start_processes(_codec_worker, args=(world, _free_port(), "grid_c3", str(tmp_path), display_rows, ring, 255),
+                       nprocs=world, join=True, start_method="spawn")
+    col, _, _ = oracle.render(sc.grid_c3(), threads=4)
+    assert np.array_equal(np.load(tmp_path / "frame.npy"), np.ascontiguousarray(col).view(np.int32).reshape(-1))
+    assert all(bool(np.load(tmp_path / f"alpha_ok_{r}.npy")) for r in range(world))
+
+
+def test_packing_a_non_uniform_alpha_is_flagged(oracle, tmp_path):
+    """The sender's check: a band whose alpha bytes are not all the promised value (the textured grid's texture
+    has alpha) sets the codec's flag, so a lossy 3-byte transfer cannot pass silently."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_codec_worker, args=(2, _free_port(), "textured_grid", str(tmp_path), None, False, 255),
+                       nprocs=2, join=True, start_method="spawn")
+    assert not bool(np.load(tmp_path / "alpha_ok_1.npy"))  # rank 1 packed (and flagged) its band
+
+
+def test_frame_alpha_proof(hiplib):
+    """tri_frame_alpha (host-side proof, no GPU needed... but a context needs a device): checked on the GPU in
+    test_multidevice_gpu; here the codec's CPU byte shuffle round-trips with the alpha restored."""
+    import torch
+
+    import bench
+
+    rng = np.random.default_rng(3)
+    px = rng.integers(0, 2 ** 24, 1003, dtype=np.int64)
+    band = torch.from_numpy((px | (255 << 24)).astype(np.uint32).view(np.int32))
+    codec = bench.BandCodec(255, torch.device("cpu"))
+    st = torch.zeros(3 * 1003, dtype=torch.uint8)
+    codec.pack(band, st)
+    back = torch.zeros_like(band)
+    codec.unpack(st, back)
+    assert torch.equal(back, band)
+    codec.check()
