@@ -182,6 +182,10 @@ struct TriShadeConst {
     // G_L's denominator divided through by 1 - k (the fast build's per-light v_fma becomes one add):
     // k / (1 - k) and a2 / pi / (1 - k), so NDF * G_L * G_V keeps its value
     float kgo, a2pio, pad3[2];
+    // the fast build's ONE frames (sbt uniform): albedo = sbt * vertex colour is never formed; F0, the diffuse
+    // factor and the ambient term come straight from the colour with these folded factors: sbt * metallic,
+    // sbt * (1 - metallic) / pi and (ambient * sbt) * ambient strength
+    float sbtm[4], sbtkd[4], sbtamb[4];
 };
 
 struct TriFrameParams {

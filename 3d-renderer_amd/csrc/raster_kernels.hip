@@ -47,6 +47,18 @@ __device__ unsigned long long g_tri_setup_phase[kPhaseSlots][4];
 #define TRI_SSTAMP(k) do { } while (0)
 #endif
 
+// Every frame kernel takes a pointer to the frame's device-resident TriLaunchArgs (raster_launch.h) and reads
+// its parameters through these references (loads from a read-only, non-aliased argument: scalar loads).
+#define TRI_KARGS const TriLaunchArgs* __restrict__ args_
+#define TRI_BIND_ARGS                         \
+    const TriFrameParams& fp = args_->fp;     \
+    const TriDeviceBuffers& b = args_->b
+// The frame's first kernel records that it started (so the host slot its arguments were copied from is free):
+// one lane, a vector store to fine-grained host memory.
+__device__ __forceinline__ void note_frame_start(const TriLaunchArgs* args) {
+    if (args->host_done) __hip_atomic_store(args->host_done, args->frame_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 constexpr uint64_t kBgKey = 0x3F800001ull << 32;  // above every fragment key (depth bits <= 1.0 after the clamp)
 constexpr float kPi = 3.14159265359f;                                  // Default.frag:65
 
@@ -216,7 +228,10 @@ __device__ __forceinline__ void reset_counters(TriCounters* c) {
 }
 
 #ifndef TRI_RASTER_PLAIN_TU
-__global__ void k_reset(TriDeviceBuffers b) { reset_counters(b.counters); }
+__global__ void k_reset(TRI_KARGS) {
+    reset_counters(args_->b.counters);
+    note_frame_start(args_);
+}
 #endif  // TRI_RASTER_PLAIN_TU
 
 // Default.vert for vertex slot `slot` of draw `dr` (whose first slot is `vbase`).
@@ -337,9 +352,13 @@ __device__ __forceinline__ bool cluster_visible(const TriFrameParams& fp, const 
 // unless the shadow pre-pass needs every caster, skips a block whose box misses the rows. A vertex of any
 // visible primitive is always transformed: its cluster's box lies inside the block's union box.
 #ifndef TRI_RASTER_PLAIN_TU
-__global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TRI_KARGS) {
+    TRI_BIND_ARGS;
     const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
-    if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
+    if (slot == 0) {
+        reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
+        note_frame_start(args_);
+    }
     const bool valid = slot < fp.nslots;
     int d = 0;
     uint32_t vbase = 0;
@@ -380,10 +399,14 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TriFrameParams fp, TriDevi
 // workgroup holds at most one, and 3/4 of the launch's dispatches (all empty) are gone. The cluster flags
 // for k_setup are the same lanes' work as in k_vertex, grid-strided.
 static_assert(TRI_VBLOCK == TRI_BLOCK, "k_vertex_band: one workgroup-wide pass per vertex block");
-__global__ __launch_bounds__(TRI_BLOCK) void k_vertex_band(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) void k_vertex_band(TRI_KARGS) {
+    TRI_BIND_ARGS;
     __shared__ uint32_t blk_vis[TRI_BLOCK / 64];
     const uint32_t tid = threadIdx.x, G = gridDim.x;
-    if (blockIdx.x == 0 && tid == 0) reset_counters(b.counters);
+    if (blockIdx.x == 0 && tid == 0) {
+        reset_counters(b.counters);
+        note_frame_start(args_);
+    }
     const TriDrawDev& dr = fp.draw0;
     for (uint32_t c = blockIdx.x * TRI_BLOCK + tid; c < fp.ncl_total; c += G * TRI_BLOCK)
         b.cvis[c] = cluster_visible(fp, dr, b.clusters[dr.cl_first + c]) ? 1u : 0u;
@@ -876,7 +899,8 @@ __device__ __forceinline__ void bin_pair_box(const TriDeviceBuffers& b, BinBox& 
 // ONE: a single-draw frame (fp.one_draw known set: the draw search, LDS staging and prim_vs records compile
 // away)
 template <bool WITH_SHADOW, bool ONE>
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TRI_KARGS) {
+    TRI_BIND_ARGS;
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     // Frames with a few draws: each draw's primitive base, first index, slot offset and cluster base
@@ -1421,23 +1445,25 @@ __device__ __forceinline__ uint32_t unorm8(float c) {
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
 }
 
-// Fast build's tone curve output (Default.frag:185-189 then the UNORM8 store). TRI_SHADE_TRIM: the channel
-// comes back already scaled by 255 — 255 t^(1/2.2) as one exp2 with log2(255) folded into its argument
-// (t = c / (c + 1) lies in [0, 1), so no clamp is needed). Either form is within a small fraction of an LSB
-// of the IEEE value before rounding, so the stored byte stays within the 1-LSB bar. (v_cvt_rpi_i32_f32 would
-// fold the + 0.5 too, but only inline asm reaches it, and the compiler does not guard inline asm against
-// the trans-result hazard: a v_cvt reading a v_exp result in the next slot read a stale register.)
-#ifndef TRI_SHADE_TRIM
-#define TRI_SHADE_TRIM 31  // bits: 1 = G_L denominator, 2 = tone curve, 4 = e0 from the area, 8 = spec_num, 16 = att_base
-#endif
+// Fast build's tone curve output (Default.frag:185-189 then the UNORM8 store): the channel comes back
+// already scaled by 255 — 255 t^(1/2.2) as one exp2 with log2(255) folded into its argument (t = c / (c + 1)
+// lies in [0, 1), so no clamp is needed), within a small fraction of an LSB of the IEEE value before rounding.
 __device__ __forceinline__ float tone_out(float t) {
     constexpr float g = 1.0f / 2.2f;
-    if (TRI_SHADE_TRIM & 2) return __builtin_amdgcn_exp2f(__builtin_fmaf(g, __builtin_amdgcn_logf(t), 7.99435343685886f));
-    return fpow(t, g);
+    return __builtin_amdgcn_exp2f(__builtin_fmaf(g, __builtin_amdgcn_logf(t), 7.99435343685886f));
 }
-__device__ __forceinline__ uint32_t fast_u8(float v) {  // v: tone_out's value, in [0, 255]
-    if (!(TRI_SHADE_TRIM & 2)) return unorm8(v);
-    return (uint32_t)(int)(v + 0.5f);
+// The fast build's BGRA8 word from tone_out's channels (in [0, 255]) and the alpha byte. TRI_PK_U8:
+// v_cvt_pk_u8_f32 rounds each channel to nearest (ties to even: it differs from floor(v + 0.5) only on an
+// exact .5, inside the 1-LSB bar) and inserts it into its byte — one instruction per channel instead of a
+// round, a conversion and a shift/or.
+#ifndef TRI_PK_U8
+#define TRI_PK_U8 1
+#endif
+__device__ __forceinline__ uint32_t fast_bgra(float r, float g, float b, uint32_t a8) {
+    if (TRI_PK_U8)
+        return __builtin_amdgcn_cvt_pk_u8_f32(r, 2u, __builtin_amdgcn_cvt_pk_u8_f32(g, 1u, __builtin_amdgcn_cvt_pk_u8_f32(b, 0u, a8 << 24)));
+    auto u8 = [](float v) { return (uint32_t)(int)(v + 0.5f); };
+    return u8(b) | (u8(g) << 8) | (u8(r) << 16) | (a8 << 24);
 }
 
 struct __attribute__((aligned(16))) V4 {
@@ -1545,24 +1571,27 @@ __device__ __forceinline__ float4 fs_exact(const TriFrameParams& fp, const Frag&
 // Per light: one v_rsq (half vector) and ONE v_rcp for NDF * G_L / (4 NdotV NdotL) together. For unit
 // V and L, |V + L|^2 = 2 + 2 L.V, N.H = (N.V + N.L) / |V + L| and H.V = (1 + L.V) / |V + L|.
 // G_V NdotL / max(4 NdotV NdotL, 1e-4) (the NDF's a2 / pi and G_L's 1 / (1 - k) folded in), the part of the
-// specular weight before the per-light denominator dd^2 gden. TRI_SHADE_TRIM & 8: for N.L > 0,
+// specular weight before the per-light denominator dd^2 gden. For N.L > 0,
 // NdotL / max(4 NdotV NdotL, 1e-4) = min(1 / (4 NdotV), 1e4 NdotL), so with spA = gVa / (4 NdotV) (formed
 // without NdotV: a2 / (4 pi (1 - k) gden_V), finite at NdotV = 0) and spB = 1e4 gVa it is min(spA, spB NdotL):
-// two operations per light instead of four, and one product fewer inside the reciprocal.
-__device__ __forceinline__ float spec_num(float spA, float spB, float NdotV4, float gVa, float NdotL) {
-    if (TRI_SHADE_TRIM & 8) return fminf(spA, spB * NdotL);
-    return (NdotL * gVa) * frcp(fmaxf(NdotV4 * NdotL, 1e-4f));
+// two operations per light instead of four, and one product fewer inside the reciprocal. TRI_SPEC_IMIN: both
+// operands are non-negative and not NaN (spA > 0; spB >= 0 and N.L > 0 here), so their minimum is the integer
+// minimum of their bits — v_min_i32, which needs no canonicalising v_max of spA in every light as the
+// IEEE-mode v_min_f32 does.
+#ifndef TRI_SPEC_IMIN
+#define TRI_SPEC_IMIN 1
+#endif
+__device__ __forceinline__ float spec_num(float spA, float spB, float NdotL) {
+    if (TRI_SPEC_IMIN) return __int_as_float(min(__float_as_int(spA), __float_as_int(spB * NdotL)));
+    return fminf(spA, spB * NdotL);
 }
-// Point-light attenuation (1 - min(d / r, 1))^2's base; TRI_SHADE_TRIM & 16: max(1 - d / r, 0) as one fma
-__device__ __forceinline__ float att_base(float d, float ir) {
-    if (TRI_SHADE_TRIM & 16) return fmaxf(__builtin_fmaf(-d, ir, 1.0f), 0.0f);
-    return 1.0f - fminf(d * ir, 1.0f);
-}
+// Point-light attenuation (1 - min(d / r, 1))^2's base, max(1 - d / r, 0) as one fma
+__device__ __forceinline__ float att_base(float d, float ir) { return fmaxf(__builtin_fmaf(-d, ir, 1.0f), 0.0f); }
 
 struct PbrPix {
     f3 N, V, F0, omF0, diffK;
-    float NdotVr, NdotV4, gVa;  // NdotVr: unclamped N.V; gVa = a2 / pi * G_V
-    float spA, spB;             // TRI_SHADE_TRIM & 8 (spec_num)
+    float NdotVr;   // unclamped N.V
+    float spA, spB; // spec_num's per-pixel factors
 };
 
 // One light with unclamped N.L and L.V given (the caller forms them without normalising L first).
@@ -1578,9 +1607,9 @@ __device__ __forceinline__ void eval_pbr_fast(const TriShadeConst& sc, const Pbr
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
     // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
     // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
-    const float gden = (TRI_SHADE_TRIM & 1) ? NdotL + sc.kgo : __builtin_fmaf(NdotL, sc.omkg, sc.kg);
+    const float gden = NdotL + sc.kgo;  // G_L's denominator divided through by 1 - k (sc.a2pio carries 1 / (1 - k))
     // NDF * G_L * G_V / den with NDF = a2 / (pi dd^2), G_L = NdotL / gden
-    const float sp = spec_num(px.spA, px.spB, px.NdotV4, px.gVa, NdotL) * frcp((dd * dd) * gden);
+    const float sp = spec_num(px.spA, px.spB, NdotL) * frcp((dd * dd) * gden);
     // 1 - max(H.V, 0), clamped to [0, 1]: one clamped subtract
     const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
     const float q2 = q * q;
@@ -1613,7 +1642,7 @@ struct PbrPixP {
     f3 N, V;
     f2v F0xy, omF0xy, diffKxy;
     float F0z, omF0z, diffKz;
-    float NdotVr, NdotV4, gVa;
+    float NdotVr;
     float spA, spB;
 };
 __device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const PbrPixP& px, float NdotLr, float LdotV,
@@ -1626,8 +1655,8 @@ __device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const P
     const float dd = __builtin_fmaf(NdotH * NdotH, sc.a2m1, 1.0f);
     // Default.frag's max(., 1e-4) on G_L's denominator is the identity here: N.L > 0 and k = (r + 1)^2 / 8
     // >= 0.136 for roughness >= 0.045, so N.L (1 - k) + k >= k
-    const float gden = (TRI_SHADE_TRIM & 1) ? NdotL + sc.kgo : __builtin_fmaf(NdotL, sc.omkg, sc.kg);
-    const float sp = spec_num(px.spA, px.spB, px.NdotV4, px.gVa, NdotL) * frcp((dd * dd) * gden);
+    const float gden = NdotL + sc.kgo;
+    const float sp = spec_num(px.spA, px.spB, NdotL) * frcp((dd * dd) * gden);
     const float q = sat(1.0f - __builtin_fmaf(LdotV, ih, ih));
     const float q2 = q * q;
     const float p5 = q2 * q2 * q;
@@ -1637,6 +1666,11 @@ __device__ __forceinline__ void eval_pbr_fast_p(const TriShadeConst& sc, const P
 }
 #endif
 
+// TRI_ONE_FOLD: single-draw solid frames shade from the vertex colour with host-folded factors (TriShadeConst::
+// sbtm / sbtkd / sbtamb), never forming the albedo (-6 VALU per pixel)
+#ifndef TRI_ONE_FOLD
+#define TRI_ONE_FOLD 1
+#endif
 template <bool ONE = false>
 __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f) {
 #pragma clang fp contract(fast)
@@ -1664,11 +1698,10 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.diffKz = albz * kd;
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
-    px.NdotV4 = 4.0f * NdotV;
     const float rgV = frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
-    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * rgV);
-    px.spA = (0.25f * ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi)) * rgV;
-    px.spB = 1e4f * px.gVa;
+    const float gVa = sc.a2pio * (NdotV * rgV);  // a2 / pi * G_V / (1 - k)
+    px.spA = (0.25f * sc.a2pio) * rgV;
+    px.spB = 1e4f * gVa;
     f2v cxy = (f2v{sc.amb[0], sc.amb[1]} * albxy) * splat(sc.amb_strength);
     float cz = (sc.amb[2] * albz) * sc.amb_strength;
     if (kAblate & 64) return make_float4(cxy.x, cxy.y, cz, 1.0f);  // diagnostics: 64 = no lights
@@ -1695,22 +1728,30 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     PbrPix px;
     px.N = fnorm(fnrm(f));
     px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), fworld(f)));
-    const f3 albedo = ONE ? mul(mk(sc.sbt[0], sc.sbt[1], sc.sbt[2]), fvcol(f))
-                          : mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])), ftint(f)), fvcol(f));
     const float m = sc.metallic;
     const float om = 0.04f * (1.0f - m);
-    px.F0 = mk(__builtin_fmaf(albedo.x, m, om), __builtin_fmaf(albedo.y, m, om), __builtin_fmaf(albedo.z, m, om));
+    f3 c;
+    if (ONE && TRI_ONE_FOLD) {  // albedo = sbt * colour: every term from the colour and a folded factor (TriShadeConst::sbtm)
+        const f3 col = fvcol(f);
+        px.F0 = mk(__builtin_fmaf(col.x, sc.sbtm[0], om), __builtin_fmaf(col.y, sc.sbtm[1], om),
+                   __builtin_fmaf(col.z, sc.sbtm[2], om));
+        px.diffK = mul(col, mk(sc.sbtkd[0], sc.sbtkd[1], sc.sbtkd[2]));
+        c = mul(col, mk(sc.sbtamb[0], sc.sbtamb[1], sc.sbtamb[2]));
+    } else {
+        const f3 albedo = ONE ? mul(mk(sc.sbt[0], sc.sbt[1], sc.sbt[2]), fvcol(f))
+                              : mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])), ftint(f)), fvcol(f));
+        px.F0 = mk(__builtin_fmaf(albedo.x, m, om), __builtin_fmaf(albedo.y, m, om), __builtin_fmaf(albedo.z, m, om));
+        px.diffK = muls(albedo, (1.0f - m) * (1.0f / kPi));
+        c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
+               sc.amb[2] * albedo.z * sc.amb_strength);
+    }
     px.omF0 = mk(1.0f - px.F0.x, 1.0f - px.F0.y, 1.0f - px.F0.z);
-    px.diffK = muls(albedo, (1.0f - m) * (1.0f / kPi));
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
-    px.NdotV4 = 4.0f * NdotV;
     const float rgV = frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
-    px.gVa = ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi) * (NdotV * rgV);
-    px.spA = (0.25f * ((TRI_SHADE_TRIM & 1) ? sc.a2pio : sc.a2pi)) * rgV;
-    px.spB = 1e4f * px.gVa;
-    f3 c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
-              sc.amb[2] * albedo.z * sc.amb_strength);
+    const float gVa = sc.a2pio * (NdotV * rgV);  // a2 / pi * G_V / (1 - k)
+    px.spA = (0.25f * sc.a2pio) * rgV;
+    px.spB = 1e4f * gVa;
     if (kAblate & 64) return make_float4(c.x, c.y, c.z, 1.0f);  // diagnostics: 64 = no lights
     if (sc.has_sun && f.vis > 0.0f) {  // vis = 0 (fully shadowed): the sun adds exactly nothing
         const f3 L = mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]);
@@ -1758,10 +1799,9 @@ __device__ __forceinline__ void fast_weights(const TriRec& r, int32_t px, int32_
     const float dx = (float)idx, dy = (float)idy;
     const float e1 = __builtin_fmaf(-fx2, dy, fy2 * dx);
     const float e2 = __builtin_fmaf(fx1, dy, -fy1 * dx);
-    // TRI_SHADE_TRIM: e0 = S - e1 - e2 with the area in float (a weight then carries an absolute error of a
-    // few 2^-24, far inside the colour bar; depth never uses these weights)
-    const float e0 = (TRI_SHADE_TRIM & 4) ? (__builtin_fmaf(fx1, fy2, -fy1 * fx2) - e1) - e2
-                                    : __builtin_fmaf((float)(x2 - x1), (float)(idy - y1), -((float)(y2 - y1) * (float)(idx - x1)));
+    // e0 = S - e1 - e2 with the area in float (a weight then carries an absolute error of a few 2^-24, far
+    // inside the colour bar; depth never uses these weights)
+    const float e0 = (__builtin_fmaf(fx1, fy2, -fy1 * fx2) - e1) - e2;
     const float q0 = e0 * r.iw[0], q1 = e1 * r.iw[1], q2 = e2 * r.iw[2];
     const float iq = frcp((q0 + q1) + q2);
     w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
@@ -1901,25 +1941,34 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
 // Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
 // Writes the fragment through `put(field_index, value)` (fields in Frag order), so one body serves
 // the single-pixel Frag and the lane-pair FragP without an intermediate in scratch memory.
-template <bool EXACT, bool SHADOW, bool ONE, typename Put>
+// CLIPM: 0 = the key may name a clipped sub-triangle (tested per pixel), 1 = it never does (the shading loop
+// defers clipped pixels, TRI_CLIP_DEFER), 2 = it always does (the deferred pass).
+template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0, typename Put>
 __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
                                                   int32_t px, int32_t py, const float* lut, Put&& put) {
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
-    const uint32_t sub = low & 7u;  // >= 1: sub-triangle `sub` of a clipped primitive
+    const uint32_t sub = CLIPM == 1 ? 0u : (low & 7u);  // >= 1: sub-triangle `sub` of a clipped primitive
     const FetchBufs fb = fetch_bufs(fp, b);
-    uint32_t sl[3], d;
-    prim_slots<ONE>(fp, b, prim, sl, d);
-    // Every gather that needs only the slots is issued before the first wait: the snapped vertices and
-    // the varyings are one round trip after the index fetch (the snaps are loaded for a clipped primitive
-    // too, unused: its sub-triangle's record names its slots).
-    const TriSnap a0 = ld_snap_xyw(fb, sl[0]), a1 = ld_snap_xyw(fb, sl[1]), a2 = ld_snap_xyw(fb, sl[2]);
-    uint32_t v0 = sl[0], v1 = sl[2], v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
-    // the varyings are gathered before the (rare) clipped branch: its record loads are waited for inside
-    // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
-    Taps taps = load_taps(fb, v0, v1, v2);
+    uint32_t sl[3] = {0, 0, 0}, d = 0;
+    TriSnap a0{}, a1{}, a2{};
+    uint32_t v0 = 0, v1 = 0, v2 = 0;
+    Taps taps;
+    if (CLIPM != 2) {
+        prim_slots<ONE>(fp, b, prim, sl, d);
+        // Every gather that needs only the slots is issued before the first wait: the snapped vertices and
+        // the varyings are one round trip after the index fetch (the snaps are loaded for a clipped primitive
+        // too, unused: its sub-triangle's record names its slots).
+        a0 = ld_snap_xyw(fb, sl[0]); a1 = ld_snap_xyw(fb, sl[1]); a2 = ld_snap_xyw(fb, sl[2]);
+        v0 = sl[0]; v1 = sl[2]; v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
+        // the varyings are gathered before the (rare) clipped branch: its record loads are waited for inside
+        // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
+        taps = load_taps(fb, v0, v1, v2);
+    } else if (!ONE) {
+        prim_slots<ONE>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
+    }
     TriRec rc;
-    if (sub) {  // a clipped primitive's sub-triangle: its own slots, its varyings gathered again
+    if (CLIPM == 2 || (CLIPM == 0 && sub)) {  // a clipped primitive's sub-triangle: its own slots and varyings
         rc = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
         v0 = rc.v[0]; v1 = rc.v[1]; v2 = rc.v[2];
         taps = load_taps(fb, v0, v1, v2);
@@ -1929,7 +1978,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         const RecBuf lr = rec_buf(b.lpos, 16u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
         L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
     }
-    const TriRec r = sub ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
+    const TriRec r = (CLIPM == 2 || (CLIPM == 0 && sub)) ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
     float w0, w1, w2;
     if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
         exact_weights(r, px, py, w0, w1, w2);
@@ -1954,10 +2003,10 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     fetch_attrs<EXACT, ONE>(fp, fb, taps, d, w0, w1, w2, lut, put);
 }
 
-template <bool EXACT, bool SHADOW, bool ONE>
+template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0>
 __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
                                                int32_t px, int32_t py, const float* lut, Frag& f) {
-    fetch_fragment_to<EXACT, SHADOW, ONE>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
+    fetch_fragment_to<EXACT, SHADOW, ONE, CLIPM>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2138,22 +2187,13 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 // wave no longer issues its longest triangle's whole bbox walk while most lanes idle. A row job steps
 // exactly like raster_serial (integer edge functions, float depth offsets in steps of 256: exact), so
 // the keys are bit-identical.
-#ifndef TRI_COV_SHARE
-// 32x32 bins: lanes per triangle when the bin has at most TRI_COV_SHARE_MAX entries. Two lanes per triangle
-// paid with the per-pixel bbox walk (round 2); with the span walk one lane per triangle is faster (C3 k_raster
-// 95.3 -> 94.0 us; four lanes 94.5)
-#define TRI_COV_SHARE 1
-#endif
-#ifndef TRI_COV_SHARE_MAX
-#define TRI_COV_SHARE_MAX (TRI_BLOCK / TRI_COV_SHARE)  // one entry per lane group
-#endif
+// 32x32 bins: one lane per triangle (two lanes per triangle paid with the per-pixel bbox walk in round 2; with
+// the span walk one lane per triangle is faster: C3 k_raster 95.3 -> 94.0 us, four lanes 94.5)
 // lanes per triangle in the shadow pre-pass's per-lane walk (two paid with the per-texel walk; with the span
 // walk one: C5 k_shadow_raster 44.5 -> 43.9 us)
 #ifndef TRI_SHADOW_SHARE
 #define TRI_SHADOW_SHARE 1
 #endif
-static_assert((TRI_COV_SHARE & (TRI_COV_SHARE - 1)) == 0 && TRI_BLOCK % TRI_COV_SHARE == 0,
-              "TRI_COV_SHARE must be a power of two dividing the workgroup (each lane group owns one entry)");
 // Raised wave priority (s_setprio 1) from a 32x32 bin's start to the end of its coverage: the latency-bound
 // init and coverage phases issue ahead of other workgroups' shading waves (C3 k_raster 101.7 -> 99.6 us,
 // round 3 A/B; at 16x16 bins it was slower, so BL == 5 only). Scheduling only: output unchanged.
@@ -2195,6 +2235,21 @@ __device__ __forceinline__ void cov_row(const CovEntry& c, uint32_t r, uint64_t*
     }
 }
 
+// Default.frag for one fragment, stored as B8G8R8A8_UNORM
+template <bool EXACT, bool ONE>
+__device__ __forceinline__ uint32_t shade_bgra(const TriFrameParams& fp, const Frag& f) {
+    if (EXACT) {
+        const float4 c = fs_exact(fp, f);
+        return unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
+    }
+    const float4 c = fs_fast<ONE>(fp.sc, f);
+    return fast_bgra(c.x, c.y, c.z, unorm8(c.w));
+}
+
+#ifndef TRI_CLIP_DEFER
+#define TRI_CLIP_DEFER 1
+#endif
+
 // One bin: coverage into the LDS key tile, then shading and stores. Reached by the whole workgroup.
 template <bool EXACT, int BL, bool SHADOW, bool ONE = false>
 __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDeviceBuffers& b, const int bin) {
@@ -2222,13 +2277,12 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
 #ifndef TRI_QUEUE_PREFETCH
 #define TRI_QUEUE_PREFETCH 1  // round-3 A/B: C3 k_raster 98.9 -> 98.0 us, C5 195.6 -> 193.3 us
 #endif
-    // the lane's first queue entry for either lane split of the per-lane walk, in flight likewise (entries
-    // past the count are loaded and ignored: the queue holds bin_cap >= 256 slots)
-    uint32_t pre1 = 0, pre2 = 0;
+    // the lane's first queue entry of the per-lane walk, in flight likewise (entries past the count are loaded
+    // and ignored: the queue holds bin_cap >= 256 slots)
+    uint32_t pre1 = 0;
     if constexpr (TRI_QUEUE_PREFETCH && !(TRI_COV_BALANCED && BL == 4)) {
         const Rsrc qr = make_rsrc(b.bin_list + (size_t)bin * fp.bin_cap, 4ull * fp.bin_cap);
         pre1 = __builtin_amdgcn_raw_buffer_load_b32(qr, (uint32_t)tid * 4u, 0, 0);
-        pre2 = TRI_COV_SHARE > 1 ? __builtin_amdgcn_raw_buffer_load_b32(qr, (uint32_t)(tid / TRI_COV_SHARE) * 4u, 0, 0) : pre1;
     }
     for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = kBgKey;
     if (fp.need_lut)
@@ -2322,10 +2376,8 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
         __syncthreads();  // cov / jobs / wsum are reused by the next pass
     }
   } else {
-    // `share` lanes per triangle when the bin has few entries (lanes would idle otherwise); each takes
-    // every share-th row of its bbox. Uniform per workgroup.
     auto cover = [&](uint32_t i, int32_t sub, int32_t step, bool first) {
-        const uint32_t ri = (TRI_QUEUE_PREFETCH && first) ? (step > 1 ? pre2 : pre1) : queue[i];
+        const uint32_t ri = (TRI_QUEUE_PREFETCH && first) ? pre1 : queue[i];
         const TriRec r = load_entry<ONE>(fp, b, ri);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
@@ -2346,8 +2398,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     // (Pairing only as many entries as there are spare lanes when the bin holds 129..256 entries, so that
     // every lane works, measured slower: 105.5 -> 109.8 us at C3. The duplicated fetch and set-up of a
     // pair costs issue slots the CU's other workgroups would use; a wave with no entry costs none.)
-    const int share = TRI_COV_SHARE > 1 && (s1 - s0) <= (uint32_t)TRI_COV_SHARE_MAX ? TRI_COV_SHARE : 1;
-    for (uint32_t i = s0 + tid / share; i < s1; i += TRI_BLOCK / share) cover(i, tid % share, share, i < (uint32_t)(TRI_BLOCK / share));
+    for (uint32_t i = s0 + tid; i < s1; i += TRI_BLOCK) cover(i, 0, 1, i < (uint32_t)TRI_BLOCK);
     __syncthreads();
   }
     TRI_STAMP(2);
@@ -2396,10 +2447,26 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     const bool sky_const = sky_on && !EXACT && fp.sky_mode == TRI_SKY_UNIFORM;
     const bool sky_queue = sky_on && !sky_const;
     const uint32_t bg_bgra = sky_const ? fp.sky_bgra : fp.clear_bgra;
+    // Clipped sub-triangles' pixels (rare: near-plane and guard-band crossings) are shaded after the loop, from
+    // a per-wave LDS queue (a wave shades exactly BIN * BIN / 4 pixels, so its slice never overflows): the
+    // loop then carries no clipped branch and no register merge at its join.
+    constexpr bool kDefer = TRI_CLIP_DEFER && BL <= 5;
+    constexpr int kWaveQ = BIN * BIN / (TRI_BLOCK / 64);
+    __shared__ uint16_t clipq[kDefer ? BIN * BIN : 1];
+    uint32_t nclip = 0;  // this wave's deferred pixels (wave-uniform)
     for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
         const bool in = lx < bw;
         const uint64_t key = in ? keys[(ly << BL) + lx] : 0ull;
         const bool bg = in && key == kBgKey;
+        if constexpr (kDefer) {
+            const bool clipped = in && !bg && ((uint32_t)key & 7u) != 0u;
+            const uint64_t m = __ballot(clipped);
+            if (m) {  // uniform
+                if (clipped) clipq[(tid >> 6) * kWaveQ + nclip + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
+                nclip += (uint32_t)__builtin_popcountll(m);
+            }
+            if (clipped) continue;
+        }
         if (sky_queue) {  // wave-aggregated append (uniform control flow here)
             const uint64_t m = __ballot(bg);
             if (m) {
@@ -2430,19 +2497,27 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
                 const float k0 = __uint_as_float(((uint32_t)key & 0x7FFFFFu) | 0x3F000000u);
                 for (int q = 0; q < 20; ++q) (&f.wx)[q] = k0 + 0.01f * q;
             } else {
-                fetch_fragment<EXACT, SHADOW, ONE>(fp, b, key, px, py, lut, f);
+                fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f);
             }
-            if (EXACT) {
-                const float4 c = fs_exact(fp, f);
-                out = unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
-            } else {
-                const float4 c = fs_fast<ONE>(fp.sc, f);
-                out = fast_u8(c.z) | (fast_u8(c.y) << 8) | (fast_u8(c.x) << 16) | (unorm8(c.w) << 24);
-            }
+            out = shade_bgra<EXACT, ONE>(fp, f);
         }
         const size_t o = (size_t)(py - fp.y0) * fp.W + px;
         b.color[o] = out;
         if (fp.write_depth) b.depth[o] = z;
+    }
+    if constexpr (kDefer) {  // this wave's clipped pixels (its own LDS slice: no workgroup barrier)
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t i = (uint32_t)(tid & 63); i < nclip; i += 64) {
+            const uint32_t li = clipq[(tid >> 6) * kWaveQ + i];
+            const int32_t qx = (int32_t)(li & (BIN - 1)), qy = (int32_t)(li >> BL);
+            const uint64_t key = keys[li];
+            const int32_t px = ox + qx, py = oy + qy;
+            Frag f;
+            fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f);
+            const size_t o = (size_t)(py - fp.y0) * fp.W + px;
+            b.color[o] = shade_bgra<EXACT, ONE>(fp, f);
+            if (fp.write_depth) b.depth[o] = __uint_as_float((uint32_t)(key >> 32));
+        }
     }
 #ifdef TRI_PHASE_TIMING
     __syncthreads();
@@ -2475,7 +2550,8 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
 // (13 VGPRs spilled by values hoisted out of the bin loop, and a static bin order that balances worse
 // than the dispatcher's).
 template <bool EXACT, int BL, bool SHADOW>
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? TRI_RASTER_WAVES_SHADOW : TRI_RASTER_WAVES) : 3))) void k_raster(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? TRI_RASTER_WAVES_SHADOW : TRI_RASTER_WAVES) : 3))) void k_raster(TRI_KARGS) {
+    TRI_BIND_ARGS;
     raster_bin<EXACT, BL, SHADOW>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
 // Frames without the shadow pre-pass: this instantiation lives in its own translation unit
@@ -2483,7 +2559,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
 // copied into VGPR pairs, and without them the fast build fits 7 waves/SIMD with no spill (C3 k_raster
 // 117 -> 112 us). Frames with the pre-pass keep k_raster<.., true> (5 waves, SLP: faster there).
 template <bool EXACT, int BL, bool ONE>
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES_PLAIN : 3))) void k_raster_plain(TriFrameParams fp, TriDeviceBuffers b) {
+// The fast single-draw solid instantiation (C3's) at 8 waves/SIMD: with its parameters read through the frame's
+// argument pointer the compiler fills a 7-wave budget (71 VGPRs) where 8 waves fit in 58 with a few SGPRs
+// spilled to VGPR lanes.
+#ifndef TRI_RASTER_WAVES_PLAIN_ONE
+#define TRI_RASTER_WAVES_PLAIN_ONE 8
+#endif
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? ((ONE && !EXACT) ? TRI_RASTER_WAVES_PLAIN_ONE : TRI_RASTER_WAVES_PLAIN) : 3))) void k_raster_plain(TRI_KARGS) {
+    TRI_BIND_ARGS;
     raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
 
@@ -2611,7 +2694,8 @@ __device__ __forceinline__ void shadow_span(const TriFrameParams& fp, const TriR
 }
 
 #ifndef TRI_RASTER_PLAIN_TU
-__global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TriFrameParams fp, TriDeviceBuffers b) {
+__global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TRI_KARGS) {
+    TRI_BIND_ARGS;
     constexpr int BIN = 32;
     __shared__ uint32_t dep[BIN * BIN];
     __shared__ uint32_t bigq[kBigQueue];
@@ -2722,24 +2806,22 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__
 }  // namespace
 
 #ifdef TRI_RASTER_PLAIN_TU
-hipError_t tri_launch_raster_plain(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream) {
-    const dim3 g(fp.nbins), t(TRI_BLOCK);
+const void* tri_raster_plain_kernel(const TriFrameParams& fp) {
     // ONE: a single draw over a 1x1 texture slot (the common untextured mesh), the specialised instantiation
     const bool one = fp.one_draw && fp.shade_solid;
-    auto go = [&](auto kernel) { hipLaunchKernelGGL(kernel, g, t, 0, stream, fp, b); };
     const int bl = fp.bin_log2 == 5 ? 5 : fp.bin_log2 == 4 ? 4 : 6;
     const int sel = (fp.exact_shading ? 1 : 0) | (one ? 2 : 0);
+    auto f = [](auto kernel) { return reinterpret_cast<const void*>(kernel); };
     if (bl == 5) {
-        if (sel == 0) go(k_raster_plain<false, 5, false>); else if (sel == 1) go(k_raster_plain<true, 5, false>);
-        else if (sel == 2) go(k_raster_plain<false, 5, true>); else go(k_raster_plain<true, 5, true>);
-    } else if (bl == 4) {
-        if (sel == 0) go(k_raster_plain<false, 4, false>); else if (sel == 1) go(k_raster_plain<true, 4, false>);
-        else if (sel == 2) go(k_raster_plain<false, 4, true>); else go(k_raster_plain<true, 4, true>);
-    } else {
-        if (sel == 0) go(k_raster_plain<false, 6, false>); else if (sel == 1) go(k_raster_plain<true, 6, false>);
-        else if (sel == 2) go(k_raster_plain<false, 6, true>); else go(k_raster_plain<true, 6, true>);
+        if (sel == 0) return f(k_raster_plain<false, 5, false>); if (sel == 1) return f(k_raster_plain<true, 5, false>);
+        if (sel == 2) return f(k_raster_plain<false, 5, true>); return f(k_raster_plain<true, 5, true>);
     }
-    return hipGetLastError();
+    if (bl == 4) {
+        if (sel == 0) return f(k_raster_plain<false, 4, false>); if (sel == 1) return f(k_raster_plain<true, 4, false>);
+        if (sel == 2) return f(k_raster_plain<false, 4, true>); return f(k_raster_plain<true, 4, true>);
+    }
+    if (sel == 0) return f(k_raster_plain<false, 6, false>); if (sel == 1) return f(k_raster_plain<true, 6, false>);
+    if (sel == 2) return f(k_raster_plain<false, 6, true>); return f(k_raster_plain<true, 6, true>);
 }
 #ifdef TRI_PHASE_TIMING
 extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {  // k_raster_plain's stamps
@@ -2751,55 +2833,61 @@ extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {  // 
 hipError_t tri_kernels_init() { return hipSuccess; }
 
 template <bool EXACT, int BL>
-static void launch_raster(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream) {
-    const dim3 g(fp.nbins), t(TRI_BLOCK);
-    if (fp.shadow_on) hipLaunchKernelGGL((k_raster<EXACT, BL, true>), g, t, 0, stream, fp, b);
-    else (void)tri_launch_raster_plain(fp, b, stream);  // raster_plain.hip (errors surface in hipGetLastError)
+static const void* raster_kernel(const TriFrameParams& fp) {
+    if (fp.shadow_on) return reinterpret_cast<const void*>(k_raster<EXACT, BL, true>);
+    return tri_raster_plain_kernel(fp);  // raster_plain.hip
 }
 
-hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
-                            hipEvent_t* ev) {
-    auto rec = [&](int i) {
-        if (ev) (void)hipEventRecord(ev[i], stream);
-    };
-    rec(kStageVertex);
+void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan) {
+    plan.n = 0;
+    auto add = [&](const void* f, dim3 g, dim3 t, int stage) { plan.k[plan.n++] = TriKernelLaunch{f, g, t, stage}; };
+    auto F = [](auto kernel) { return reinterpret_cast<const void*>(kernel); };
+    const dim3 t(TRI_BLOCK);
     if (fp.nslots > 0 && fp.cull_vertex && fp.one_draw)
         // one workgroup per four vertex blocks (TRI_VBLOCK == TRI_BLOCK slots each)
-        hipLaunchKernelGGL(k_vertex_band, dim3((fp.nslots + 4u * TRI_VBLOCK - 1) / (4u * TRI_VBLOCK)), dim3(TRI_BLOCK), 0,
-                           stream, fp, b);
+        add(F(k_vertex_band), dim3((fp.nslots + 4u * TRI_VBLOCK - 1) / (4u * TRI_VBLOCK)), t, kStageVertex);
     else if (fp.nslots > 0)
         // with cluster culling every (draw, cluster) flag needs a lane, even when a mesh has fewer vertices
-        hipLaunchKernelGGL(k_vertex, dim3(((fp.cull_on && fp.ncl_total > fp.nslots ? fp.ncl_total : fp.nslots) + TRI_BLOCK - 1) / TRI_BLOCK),
-                           dim3(TRI_BLOCK), 0, stream, fp, b);
+        add(F(k_vertex), dim3(((fp.cull_on && fp.ncl_total > fp.nslots ? fp.ncl_total : fp.nslots) + TRI_BLOCK - 1) / TRI_BLOCK),
+            t, kStageVertex);
     else
-        hipLaunchKernelGGL(k_reset, dim3(1), dim3(1), 0, stream, b);
-    rec(kStageSetup);
+        add(F(k_reset), dim3(1), dim3(1), kStageVertex);
     if (fp.nchunks > 0) {  // with the pre-pass, one set-up pass bins each primitive for the frame and the map
-        const dim3 g(fp.setup_multi ? (fp.nchunks + 3u) / 4u : fp.nchunks), t(TRI_BLOCK);
-        if (fp.shadow_on) {
-            if (fp.one_draw) hipLaunchKernelGGL((k_setup<true, true>), g, t, 0, stream, fp, b);
-            else hipLaunchKernelGGL((k_setup<true, false>), g, t, 0, stream, fp, b);
-        } else {
-            if (fp.one_draw) hipLaunchKernelGGL((k_setup<false, true>), g, t, 0, stream, fp, b);
-            else hipLaunchKernelGGL((k_setup<false, false>), g, t, 0, stream, fp, b);
+        const dim3 g(fp.setup_multi ? (fp.nchunks + 3u) / 4u : fp.nchunks);
+        const void* k = fp.shadow_on ? (fp.one_draw ? F(k_setup<true, true>) : F(k_setup<true, false>))
+                                     : (fp.one_draw ? F(k_setup<false, true>) : F(k_setup<false, false>));
+        add(k, g, t, kStageSetup);
+    }
+    if (fp.shadow_on)  // the map's depth raster, before the frame's raster samples it
+        add(F(k_shadow_raster), dim3(fp.s_nbins), t, kStageShadow);
+    const void* r;
+    if (fp.bin_log2 == 5) r = fp.exact_shading ? raster_kernel<true, 5>(fp) : raster_kernel<false, 5>(fp);
+    else if (fp.bin_log2 == 4) r = fp.exact_shading ? raster_kernel<true, 4>(fp) : raster_kernel<false, 4>(fp);
+    else r = fp.exact_shading ? raster_kernel<true, 6>(fp) : raster_kernel<false, 6>(fp);
+    add(r, dim3(fp.nbins), t, kStageRaster);
+}
+
+hipError_t tri_run_plan(const TriFramePlan& plan, TriLaunchArgs* d_args, const TriLaunchArgs* h_args,
+                        hipStream_t stream, hipEvent_t* ev) {
+    hipError_t e = hipMemcpyAsync(d_args, h_args, sizeof(TriLaunchArgs), hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+    bool setup_stamped = false;
+    for (uint32_t i = 0; i < plan.n; ++i) {
+        const TriKernelLaunch& k = plan.k[i];
+        if (ev) {
+            // stamps in the order the stages run; a frame without set-up still stamps it (zero length)
+            if ((k.stage == kStageRaster || k.stage == kStageShadow) && !setup_stamped) {
+                (void)hipEventRecord(ev[kStageSetup], stream);
+                setup_stamped = true;
+            }
+            if (k.stage == kStageSetup) setup_stamped = true;
+            (void)hipEventRecord(ev[k.stage], stream);
         }
+        void* kargs[] = {&d_args};
+        e = hipLaunchKernel(k.func, k.grid, k.block, kargs, 0, stream);
+        if (e != hipSuccess) return e;
     }
-    if (fp.shadow_on) {  // the map's depth raster, before the frame's raster samples it
-        rec(kStageShadow);
-        hipLaunchKernelGGL(k_shadow_raster, dim3(fp.s_nbins), dim3(TRI_BLOCK), 0, stream, fp, b);
-    }
-    rec(kStageRaster);
-    if (fp.bin_log2 == 5) {
-        if (fp.exact_shading) launch_raster<true, 5>(fp, b, stream);
-        else launch_raster<false, 5>(fp, b, stream);
-    } else if (fp.bin_log2 == 4) {
-        if (fp.exact_shading) launch_raster<true, 4>(fp, b, stream);
-        else launch_raster<false, 4>(fp, b, stream);
-    } else {
-        if (fp.exact_shading) launch_raster<true, 6>(fp, b, stream);
-        else launch_raster<false, 6>(fp, b, stream);
-    }
-    rec(kStageCount);
+    if (ev) (void)hipEventRecord(ev[kStageCount], stream);
     return hipGetLastError();
 }
 

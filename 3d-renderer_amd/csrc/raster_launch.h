@@ -48,21 +48,43 @@ struct TriDeviceBuffers {
     uint32_t* shadow_map;        // s_size * s_size float32 depth bits
 };
 
+// One frame's arguments, device-resident (DESIGN.md §2 "host cost"): tri_render fills a pinned host slot,
+// one host-to-device copy moves it, and every kernel of the frame takes a pointer to it (a 16-B argument
+// instead of a 1.8-KB by-value block per launch). The frame's first kernel stores frame_id into the pinned
+// word host_done, which tells tri_render when the host slot the copy read can be written again.
+struct TriLaunchArgs {
+    TriFrameParams fp;
+    TriDeviceBuffers b;
+    uint32_t* host_done;
+    uint32_t frame_id;
+};
+
+// The kernels of one frame in launch order (which instantiation, grid, block) — computed on the host from the
+// frame's parameters; the same plan is launched directly or as a cached HIP graph.
+struct TriKernelLaunch {
+    const void* func;
+    dim3 grid, block;
+    int stage;  // TriStage stamped before this launch when timing (-1: none)
+};
+struct TriFramePlan {
+    uint32_t n = 0;
+    TriKernelLaunch k[4];
+};
+void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan);
+// k_raster_plain's instantiation for a frame without the shadow pre-pass (raster_plain.hip)
+const void* tri_raster_plain_kernel(const TriFrameParams& fp);
+
 // Event stamps of one frame, in launch order: vertex, setup (+ clip, + the shadow map binning), shadow-map
 // raster (only with the pre-pass), raster, end.
 enum TriStage { kStageVertex = 0, kStageShadow, kStageSetup, kStageRaster, kStageCount };
 
 hipError_t tri_kernels_init();
 
-// One frame = 3 dependent launches on `stream` (k_vertex, k_setup with in-wave clipping, k_raster),
-// 5 with the shadow pre-pass (k_setup<shadow> and k_shadow_raster after k_vertex); `events` (may be
-// null) gets kStageCount + 1 stamps (the kStageShadow stamp only when the pre-pass runs).
-hipError_t tri_launch_frame(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream,
-                            hipEvent_t* events);
-
-// k_raster for frames without the shadow pre-pass (raster_plain.hip: raster_kernels.hip compiled again
-// without SLP vectorisation, instantiating only that kernel).
-hipError_t tri_launch_raster_plain(const TriFrameParams& fp, const TriDeviceBuffers& b, hipStream_t stream);
+// One frame = the copy of *h_args into *d_args, then 3 dependent launches on `stream` (k_vertex, k_setup
+// with in-wave clipping, k_raster), 4 with the shadow pre-pass (k_shadow_raster after k_setup<shadow>);
+// `events` (may be null) gets kStageCount + 1 stamps (the kStageShadow stamp only when the pre-pass runs).
+hipError_t tri_run_plan(const TriFramePlan& plan, TriLaunchArgs* d_args, const TriLaunchArgs* h_args,
+                        hipStream_t stream, hipEvent_t* events);
 
 // Presentation blit (tri_blit_linear): src W x H B8G8R8A8 -> dst dw x dh, linear, clamp-to-edge.
 hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* dst, int32_t dw, int32_t dh,

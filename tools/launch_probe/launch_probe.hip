@@ -69,6 +69,31 @@ int main() {
         (void)hipGraphLaunch(ge, s);
     };
     printf("e graph of 3, params updated: %.2f us/frame\n", burst_us(s, e));
+    // f: a graph of a pinned-host -> device parameter copy + the 3 kernels reading the device copy (small args):
+    // the host writes the slot, then one graph launch (no node updates)
+    hipGraph_t gf; hipGraphExec_t gfe;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    CK(hipMemcpyAsync(dp, hp, sizeof(Big), hipMemcpyHostToDevice, s));
+    for (int k = 0; k < 3; ++k) hipLaunchKernelGGL(k_small, g, t, 0, s, dp, out);
+    CK(hipStreamEndCapture(s, &gf));
+    CK(hipGraphInstantiate(&gfe, gf, nullptr, nullptr, 0));
+    auto f = [&] { hp[0].w[7]++; (void)hipGraphLaunch(gfe, s); };
+    printf("f graph: pinned param copy + 3 kernels: %.2f us/frame\n", burst_us(s, f));
+    CK(hipStreamSynchronize(s));
+    {
+        auto t0 = clk::now();
+        for (int i = 0; i < 2000; ++i) f();
+        CK(hipStreamSynchronize(s));
+        printf("f drained: %.2f us/frame\n", std::chrono::duration<double, std::micro>(clk::now() - t0).count() / 2000);
+    }
+    // g: the same graph without the copy node (device-resident parameters)
+    hipGraph_t gg; hipGraphExec_t gge;
+    CK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    for (int k = 0; k < 3; ++k) hipLaunchKernelGGL(k_small, g, t, 0, s, dp, out);
+    CK(hipStreamEndCapture(s, &gg));
+    CK(hipGraphInstantiate(&gge, gg, nullptr, nullptr, 0));
+    auto gl = [&] { (void)hipGraphLaunch(gge, s); };
+    printf("g graph of 3 (16 B args): %.2f us/frame\n", burst_us(s, gl));
     // the GPU-side cost of the copy: frames back to back, drained
     for (auto* f : {"b", "c"}) {
         CK(hipStreamSynchronize(s));
