@@ -41,6 +41,10 @@ static_assert(TRI_MAX_CLIP_POLY <= TRI_MAX_CLIP_VERTS, "clip polygon buffers");
 #define TRI_GUARD_BAND_PX 16000.0f
 #define TRI_MAX_PPT 8  // primitives per k_setup thread
 
+#ifndef TRI_SNAP_F
+#define TRI_SNAP_F 1
+#endif
+
 #define TRI_SKY_RAY 0u
 #define TRI_SKY_PERSP 1u
 #define TRI_SKY_UNIFORM 2u
@@ -63,7 +67,10 @@ struct __attribute__((aligned(16))) TriVsSkin {
 };
 
 // Per-vertex window-space record written by k_vertex (the perspective divide + viewport transform
-// + 8-bit snap are done once per vertex): X (signed 24 bits) | outcode << 24, Y, 1/w, z_ndc.
+// + 8-bit snap are done once per vertex): X (signed 24 bits) | outcode << 24, Y, 1/w, z_ndc. With TRI_SNAP_F
+// (the main pass; the shadow map's lsnap keeps the packed form) X and Y are stored as floats — they are
+// integers below 2^22 in magnitude, so exactly — and the outcode goes to its own byte per slot: the fragment
+// stage's weights then start from float differences (no per-pixel sign extension and conversions).
 struct __attribute__((aligned(16))) TriSnap {
     int32_t xo;
     int32_t y;

@@ -47,16 +47,24 @@ __device__ unsigned long long g_tri_setup_phase[kPhaseSlots][4];
 #define TRI_SSTAMP(k) do { } while (0)
 #endif
 
-// Every frame kernel takes a pointer to the frame's device-resident TriLaunchArgs (raster_launch.h) and reads
-// its parameters through these references (loads from a read-only, non-aliased argument: scalar loads).
+// Launch arguments (raster_launch.h): the frame's first kernel takes TriLaunchArgs by value and publishes it
+// (TRI_FIRST_KARGS / TRI_PUBLISH_ARGS); the later kernels read the published copy through a read-only,
+// non-aliased pointer (TRI_KARGS / TRI_BIND_ARGS: scalar loads).
+#define TRI_FIRST_KARGS TriLaunchArgs a_, TriLaunchArgs* __restrict__ pub_
+#define TRI_BIND_FIRST_ARGS                   \
+    const TriFrameParams& fp = a_.fp;         \
+    const TriDeviceBuffers& b = a_.b
 #define TRI_KARGS const TriLaunchArgs* __restrict__ args_
 #define TRI_BIND_ARGS                         \
     const TriFrameParams& fp = args_->fp;     \
     const TriDeviceBuffers& b = args_->b
-// The frame's first kernel records that it started (so the host slot its arguments were copied from is free):
-// one lane, a vector store to fine-grained host memory.
-__device__ __forceinline__ void note_frame_start(const TriLaunchArgs* args) {
-    if (args->host_done) __hip_atomic_store(args->host_done, args->frame_id, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+// Workgroup 0 of the first kernel copies its by-value arguments to the device copy, 16 B per lane.
+__device__ __forceinline__ void publish_args(const TriLaunchArgs& a, TriLaunchArgs* dst) {
+    if (blockIdx.x != 0) return;
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    const u4* src = reinterpret_cast<const u4*>(&a);
+    u4* d = reinterpret_cast<u4*>(dst);
+    for (uint32_t i = threadIdx.x; i < sizeof(TriLaunchArgs) / 16; i += blockDim.x) d[i] = src[i];
 }
 
 constexpr uint64_t kBgKey = 0x3F800001ull << 32;  // above every fragment key (depth bits <= 1.0 after the clamp)
@@ -157,6 +165,17 @@ __device__ __forceinline__ TriSnap ld_snap_xyw(const FetchBufs& fb, uint32_t slo
     return TriSnap{(int32_t)q[0], (int32_t)q[1], __uint_as_float(q[2]), 0.0f};
 }
 
+// The main pass's snapped vertex fields (TRI_SNAP_F: exact floats + a separate outcode byte).
+__device__ __forceinline__ int32_t snap_X(const TriSnap& s) {
+    return TRI_SNAP_F ? (int32_t)__int_as_float(s.xo) : (s.xo << 8) >> 8;
+}
+__device__ __forceinline__ int32_t snap_Y(const TriSnap& s) { return TRI_SNAP_F ? (int32_t)__int_as_float(s.y) : s.y; }
+__device__ __forceinline__ float snap_Xf(const TriSnap& s) { return TRI_SNAP_F ? __int_as_float(s.xo) : (float)snap_X(s); }
+__device__ __forceinline__ float snap_Yf(const TriSnap& s) { return TRI_SNAP_F ? __int_as_float(s.y) : (float)s.y; }
+__device__ __forceinline__ uint32_t snap_oc(const TriDeviceBuffers& b, const TriSnap& s, uint32_t slot) {
+    return TRI_SNAP_F ? (uint32_t)b.oc[slot] : (uint32_t)s.xo >> 24;
+}
+
 // ((c0*x + c1*y) + c2*z) + c3*w, column-major, no FMA (matches the oracle bit-for-bit)
 __device__ __forceinline__ float4 mat_vec_seq(const float* m, float4 v) {
     float4 r;
@@ -228,9 +247,9 @@ __device__ __forceinline__ void reset_counters(TriCounters* c) {
 }
 
 #ifndef TRI_RASTER_PLAIN_TU
-__global__ void k_reset(TRI_KARGS) {
-    reset_counters(args_->b.counters);
-    note_frame_start(args_);
+__global__ __launch_bounds__(TRI_BLOCK) void k_reset(TRI_FIRST_KARGS) {  // a frame with no vertex work
+    if (threadIdx.x == 0) reset_counters(a_.b.counters);
+    publish_args(a_, pub_);
 }
 #endif  // TRI_RASTER_PLAIN_TU
 
@@ -239,7 +258,8 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
                                             const TriDrawDev& dr, uint32_t vbase) {
     const int64_t gi = (int64_t)dr.base_vertex + (int64_t)(dr.min_index + (slot - vbase));
     if (gi < 0 || (uint64_t)gi >= b.vertex_count) {
-        b.snap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
+        b.snap[slot] = TriSnap{TRI_SNAP_F ? 0 : (int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
+        if (TRI_SNAP_F) b.oc[slot] = (uint8_t)TRI_OC_BAD;
         if (fp.shadow_on) b.lsnap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
         return;
     }
@@ -292,14 +312,20 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
     // recomputed by the clipper from `vary`; a non-finite position (w != 1) is marked for clipping
     if (dr.clip_from_world && oc == 0u && !(world.w == 1.0f)) oc = TRI_OC_CLIP;
     if (oc != 0u || !dr.clip_from_world) b.clip[slot] = clip;
-    TriSnap sn{(int32_t)(oc << 24), 0, 0.0f, 0.0f};
+    TriSnap sn{TRI_SNAP_F ? 0 : (int32_t)(oc << 24), 0, 0.0f, 0.0f};
     if (!(oc & TRI_OC_CLIP)) {
         int32_t X, Y;
         snap_compute(fp, clip, X, Y, sn.z, sn.iw);
-        sn.xo = (X & 0x00FFFFFF) | (int32_t)(oc << 24);  // |X| < 2^22 inside the guard band
-        sn.y = Y;
+        if (TRI_SNAP_F) {  // |X|, |Y| < 2^22 inside the guard band: exact as floats
+            sn.xo = __float_as_int((float)X);
+            sn.y = __float_as_int((float)Y);
+        } else {
+            sn.xo = (X & 0x00FFFFFF) | (int32_t)(oc << 24);
+            sn.y = Y;
+        }
     }
     b.snap[slot] = sn;
+    if (TRI_SNAP_F) b.oc[slot] = (uint8_t)oc;
     float4* vo = b.vary + 3u * slot;
     vo[0] = make_float4(world.x, world.y, world.z, u);
     vo[1] = make_float4(nnx, nny, nnz, v);
@@ -352,13 +378,11 @@ __device__ __forceinline__ bool cluster_visible(const TriFrameParams& fp, const 
 // unless the shadow pre-pass needs every caster, skips a block whose box misses the rows. A vertex of any
 // visible primitive is always transformed: its cluster's box lies inside the block's union box.
 #ifndef TRI_RASTER_PLAIN_TU
-__global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TRI_KARGS) {
-    TRI_BIND_ARGS;
+__global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TRI_FIRST_KARGS) {
+    TRI_BIND_FIRST_ARGS;
+    publish_args(a_, pub_);
     const uint32_t slot = blockIdx.x * TRI_BLOCK + threadIdx.x;
-    if (slot == 0) {
-        reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
-        note_frame_start(args_);
-    }
+    if (slot == 0) reset_counters(b.counters);  // per-frame counters, consumed from k_setup on
     const bool valid = slot < fp.nslots;
     int d = 0;
     uint32_t vbase = 0;
@@ -399,14 +423,12 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TRI_KARGS) {
 // workgroup holds at most one, and 3/4 of the launch's dispatches (all empty) are gone. The cluster flags
 // for k_setup are the same lanes' work as in k_vertex, grid-strided.
 static_assert(TRI_VBLOCK == TRI_BLOCK, "k_vertex_band: one workgroup-wide pass per vertex block");
-__global__ __launch_bounds__(TRI_BLOCK) void k_vertex_band(TRI_KARGS) {
-    TRI_BIND_ARGS;
+__global__ __launch_bounds__(TRI_BLOCK) void k_vertex_band(TRI_FIRST_KARGS) {
+    TRI_BIND_FIRST_ARGS;
+    publish_args(a_, pub_);
     __shared__ uint32_t blk_vis[TRI_BLOCK / 64];
     const uint32_t tid = threadIdx.x, G = gridDim.x;
-    if (blockIdx.x == 0 && tid == 0) {
-        reset_counters(b.counters);
-        note_frame_start(args_);
-    }
+    if (blockIdx.x == 0 && tid == 0) reset_counters(b.counters);
     const TriDrawDev& dr = fp.draw0;
     for (uint32_t c = blockIdx.x * TRI_BLOCK + tid; c < fp.ncl_total; c += G * TRI_BLOCK)
         b.cvis[c] = cluster_visible(fp, dr, b.clusters[dr.cl_first + c]) ? 1u : 0u;
@@ -609,7 +631,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
     if (lane < 3) {
         ClipVert v;
         const uint32_t sl = lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2);
-        if (cfw && ((uint32_t)b.snap[sl].xo >> 24) == 0u) {  // not stored by k_vertex: world.w == 1
+        if (cfw && snap_oc(b, b.snap[sl], sl) == 0u) {  // not stored by k_vertex: world.w == 1
             const float4 wv = b.vary[3u * sl];
             v.c = mat_vec_seq(fp.pv, make_float4(wv.x, wv.y, wv.z, 1.0f));
         } else {
@@ -1018,14 +1040,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 sl0[t] = vb + i0; sl1[t] = vb + i1; sl2[t] = vb + i2;
                 if (!culled) {
                     const TriSnap a0 = b.snap[sl0[t]], a1 = b.snap[sl1[t]], a2 = b.snap[sl2[t]];
-                    const uint32_t oc0 = (uint32_t)a0.xo >> 24, oc1 = (uint32_t)a1.xo >> 24, oc2 = (uint32_t)a2.xo >> 24;
+                    const uint32_t oc0 = snap_oc(b, a0, sl0[t]), oc1 = snap_oc(b, a1, sl1[t]), oc2 = snap_oc(b, a2, sl2[t]);
                     // invalid vertex, or trivial reject: all three vertices outside one clip half-space
                     if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
                         if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
                             needs_clip[t] = true;
                         } else {
-                            const int32_t X[3] = {(a0.xo << 8) >> 8, (a1.xo << 8) >> 8, (a2.xo << 8) >> 8};
-                            const int32_t Y[3] = {a0.y, a1.y, a2.y};
+                            const int32_t X[3] = {snap_X(a0), snap_X(a1), snap_X(a2)};
+                            const int32_t Y[3] = {snap_Y(a0), snap_Y(a1), snap_Y(a2)};
                             const float z[3] = {a0.z, a1.z, a2.z};
                             const float iw[3] = {a0.iw, a1.iw, a2.iw};
                             TriRec r;
@@ -1145,8 +1167,8 @@ __device__ __forceinline__ TriRec load_rec(const TriRec* recs, uint32_t i) {
 __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3], const TriSnap& a0,
                                                  const TriSnap& a1, const TriSnap& a2) {
     TriRec r;
-    r.X[0] = (a0.xo << 8) >> 8; r.X[1] = (a2.xo << 8) >> 8; r.X[2] = (a1.xo << 8) >> 8;
-    r.Y[0] = a0.y; r.Y[1] = a2.y; r.Y[2] = a1.y;
+    r.X[0] = snap_X(a0); r.X[1] = snap_X(a2); r.X[2] = snap_X(a1);
+    r.Y[0] = snap_Y(a0); r.Y[1] = snap_Y(a2); r.Y[2] = snap_Y(a1);
     r.z[0] = a0.z; r.z[1] = a2.z; r.z[2] = a1.z;
     r.iw[0] = a0.iw; r.iw[1] = a2.iw; r.iw[2] = a1.iw;
     r.v[0] = sl[0]; r.v[1] = sl[2]; r.v[2] = sl[1];
@@ -1807,6 +1829,22 @@ __device__ __forceinline__ void fast_weights(const TriRec& r, int32_t px, int32_
     w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
 }
 
+// fast_weights of the unclipped triangle rec_from_snaps(a0, a1, a2) would build (v1 <-> v2 swapped), straight
+// from the TRI_SNAP_F floats: the vertex differences and the pixel-centre offsets are exact in float either way,
+// so the weights are the same bits without the integer sign extensions and conversions.
+__device__ __forceinline__ void fast_weights_snaps(const TriSnap& a0, const TriSnap& a1, const TriSnap& a2, int32_t px,
+                                                   int32_t py, float& w0, float& w1, float& w2) {
+    const float X0 = snap_Xf(a0), Y0 = snap_Yf(a0);
+    const float fx1 = snap_Xf(a2) - X0, fy1 = snap_Yf(a2) - Y0, fx2 = snap_Xf(a1) - X0, fy2 = snap_Yf(a1) - Y0;
+    const float dx = (float)(256 * px + 128) - X0, dy = (float)(256 * py + 128) - Y0;
+    const float e1 = __builtin_fmaf(-fx2, dy, fy2 * dx);
+    const float e2 = __builtin_fmaf(fx1, dy, -fy1 * dx);
+    const float e0 = (__builtin_fmaf(fx1, fy2, -fy1 * fx2) - e1) - e2;
+    const float q0 = e0 * a0.iw, q1 = e1 * a2.iw, q2 = e2 * a1.iw;
+    const float iq = frcp((q0 + q1) + q2);
+    w0 = q0 * iq; w1 = q1 * iq; w2 = q2 * iq;
+}
+
 // Perspective-correct barycentric weights of pixel (px, py) in the oracle's order: exact int64 edge
 // functions at the pixel centre, IEEE divides (the EXACT build's interpolation; the shadow lookup uses
 // them in both builds so its compare sees the oracle's light-space depth bit for bit).
@@ -1941,11 +1979,54 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
 // Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
 // Writes the fragment through `put(field_index, value)` (fields in Frag order), so one body serves
 // the single-pixel Frag and the lane-pair FragP without an intermediate in scratch memory.
+// The shadow pre-pass's sun visibility of one fragment (oracle shadow_visibility): the light-space position
+// interpolated with the EXACT perspective weights (in both shading builds, so the compare sees the oracle's bits
+// and never flips a texel), then the 2x2 compare. k_raster<.., SHADOW> evaluates it for every visible pixel in a
+// pass of its own before shading (TRI_SHADOW_VIS_PASS), so the shading loop does not hold the light-space
+// gathers, the exact weights and the map taps in its registers.
+__device__ __forceinline__ float fragment_shadow_vis(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
+                                                     int32_t px, int32_t py) {
+    const uint32_t low = (uint32_t)key;
+    const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
+    const uint32_t sub = low & 7u;
+    const FetchBufs fb = fetch_bufs(fp, b);
+    const RecBuf lr = rec_buf(b.lpos, 16u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
+    TriRec r;
+    uint32_t v0, v1, v2;
+    if (sub) {
+        r = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
+        v0 = r.v[0]; v1 = r.v[1]; v2 = r.v[2];
+    } else {
+        uint32_t sl[3], d;
+        prim_slots<false>(fp, b, prim, sl, d);
+        const TriSnap a0 = ld_snap_xyw(fb, sl[0]), a1 = ld_snap_xyw(fb, sl[1]), a2 = ld_snap_xyw(fb, sl[2]);
+        v0 = sl[0]; v1 = sl[2]; v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
+        r = rec_from_snaps(prim, sl, a0, a1, a2);
+    }
+    const uint4 L0 = rec128<16>(lr, v0, 0u), L1 = rec128<16>(lr, v1, 0u), L2 = rec128<16>(lr, v2, 0u);
+    float e0, e1, e2;
+    exact_weights(r, px, py, e0, e1, e2);
+    auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
+        return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
+    };
+    return shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
+}
+
+// A separate visibility pass (round 4 A/B, C5 k_raster at 5 waves/SIMD): 188.6 -> 206.4 us, at 6 waves 197 us —
+// the pass fetches each fragment's index and snapped vertices a second time and the shading loop's register
+// peak is not the lookup's; off.
+#ifndef TRI_SHADOW_VIS_PASS
+#define TRI_SHADOW_VIS_PASS 0
+#endif
+
 // CLIPM: 0 = the key may name a clipped sub-triangle (tested per pixel), 1 = it never does (the shading loop
-// defers clipped pixels, TRI_CLIP_DEFER), 2 = it always does (the deferred pass).
+// defers clipped pixels, TRI_CLIP_DEFER), 2 = it always does (the deferred pass). pre_vis: the fragment's sun
+// visibility from the visibility pass (SHADOW with TRI_SHADOW_VIS_PASS).
 template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0, typename Put>
 __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                                  int32_t px, int32_t py, const float* lut, Put&& put) {
+                                                  int32_t px, int32_t py, const float* lut, Put&& put,
+                                                  float pre_vis = 1.0f) {
+    constexpr bool kInlineVis = SHADOW && !TRI_SHADOW_VIS_PASS;
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
     const uint32_t sub = CLIPM == 1 ? 0u : (low & 7u);  // >= 1: sub-triangle `sub` of a clipped primitive
@@ -1974,14 +2055,17 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         taps = load_taps(fb, v0, v1, v2);
     }
     uint4 L0, L1, L2;
-    if constexpr (SHADOW) {
+    if constexpr (kInlineVis) {
         const RecBuf lr = rec_buf(b.lpos, 16u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
         L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
     }
-    const TriRec r = (CLIPM == 2 || (CLIPM == 0 && sub)) ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
+    const bool from_rec = CLIPM == 2 || (CLIPM == 0 && sub);
+    const TriRec r = from_rec ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
     float w0, w1, w2;
     if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
         exact_weights(r, px, py, w0, w1, w2);
+    } else if (TRI_SNAP_F && CLIPM == 1) {  // never clipped here: the floats of the snaps directly
+        fast_weights_snaps(a0, a1, a2, px, py, w0, w1, w2);
     } else {
         fast_weights(r, px, py, w0, w1, w2);
     }
@@ -1990,8 +2074,8 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     } else if (TRI_COLOUR_LATE) {
         taps.a2 = ld_vary(fb, v0, 2); taps.b2 = ld_vary(fb, v1, 2); taps.c2 = ld_vary(fb, v2, 2);
     }
-    float vis = 1.0f;
-    if constexpr (SHADOW) {  // light-space position at the pixel with the oracle's weights, then the compare
+    float vis = SHADOW ? pre_vis : 1.0f;
+    if constexpr (kInlineVis) {  // light-space position at the pixel with the oracle's weights, then the compare
         float e0 = w0, e1 = w1, e2 = w2;
         if (!EXACT && !(kAblate & 512)) exact_weights(r, px, py, e0, e1, e2);  // 512: fast weights (diagnostics)
         auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
@@ -2005,8 +2089,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
 
 template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0>
 __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                               int32_t px, int32_t py, const float* lut, Frag& f) {
-    fetch_fragment_to<EXACT, SHADOW, ONE, CLIPM>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
+                                               int32_t px, int32_t py, const float* lut, Frag& f, float pre_vis = 1.0f) {
+    fetch_fragment_to<EXACT, SHADOW, ONE, CLIPM>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; },
+                                                 pre_vis);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2454,6 +2539,17 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     constexpr int kWaveQ = BIN * BIN / (TRI_BLOCK / 64);
     __shared__ uint16_t clipq[kDefer ? BIN * BIN : 1];
     uint32_t nclip = 0;  // this wave's deferred pixels (wave-uniform)
+    // the sun visibility of every visible pixel, by the lane that shades it (no barrier: each lane reads back
+    // only its own pixels)
+    constexpr bool kVisPass = SHADOW && TRI_SHADOW_VIS_PASS;
+    __shared__ float visl[kVisPass ? BIN * BIN : 1];
+    if constexpr (kVisPass) {
+        for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
+            if (lx >= bw) continue;
+            const uint64_t key = keys[(ly << BL) + lx];
+            if (key != kBgKey) visl[(ly << BL) + lx] = fragment_shadow_vis(fp, b, key, ox + lx, oy + ly);
+        }
+    }
     for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
         const bool in = lx < bw;
         const uint64_t key = in ? keys[(ly << BL) + lx] : 0ull;
@@ -2497,7 +2593,8 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
                 const float k0 = __uint_as_float(((uint32_t)key & 0x7FFFFFu) | 0x3F000000u);
                 for (int q = 0; q < 20; ++q) (&f.wx)[q] = k0 + 0.01f * q;
             } else {
-                fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f);
+                fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f,
+                                                                    kVisPass ? visl[(ly << BL) + lx] : 1.0f);
             }
             out = shade_bgra<EXACT, ONE>(fp, f);
         }
@@ -2513,7 +2610,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             const uint64_t key = keys[li];
             const int32_t px = ox + qx, py = oy + qy;
             Frag f;
-            fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f);
+            fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f, kVisPass ? visl[li] : 1.0f);
             const size_t o = (size_t)(py - fp.y0) * fp.W + px;
             b.color[o] = shade_bgra<EXACT, ONE>(fp, f);
             if (fp.write_depth) b.depth[o] = __uint_as_float((uint32_t)(key >> 32));
@@ -2851,7 +2948,7 @@ void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan) {
         add(F(k_vertex), dim3(((fp.cull_on && fp.ncl_total > fp.nslots ? fp.ncl_total : fp.nslots) + TRI_BLOCK - 1) / TRI_BLOCK),
             t, kStageVertex);
     else
-        add(F(k_reset), dim3(1), dim3(1), kStageVertex);
+        add(F(k_reset), dim3(1), dim3(TRI_BLOCK), kStageVertex);
     if (fp.nchunks > 0) {  // with the pre-pass, one set-up pass bins each primitive for the frame and the map
         const dim3 g(fp.setup_multi ? (fp.nchunks + 3u) / 4u : fp.nchunks);
         const void* k = fp.shadow_on ? (fp.one_draw ? F(k_setup<true, true>) : F(k_setup<true, false>))
@@ -2867,10 +2964,9 @@ void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan) {
     add(r, dim3(fp.nbins), t, kStageRaster);
 }
 
-hipError_t tri_run_plan(const TriFramePlan& plan, TriLaunchArgs* d_args, const TriLaunchArgs* h_args,
+hipError_t tri_run_plan(const TriFramePlan& plan, const TriLaunchArgs& args, TriLaunchArgs* d_args,
                         hipStream_t stream, hipEvent_t* ev) {
-    hipError_t e = hipMemcpyAsync(d_args, h_args, sizeof(TriLaunchArgs), hipMemcpyHostToDevice, stream);
-    if (e != hipSuccess) return e;
+    hipError_t e = hipSuccess;
     bool setup_stamped = false;
     for (uint32_t i = 0; i < plan.n; ++i) {
         const TriKernelLaunch& k = plan.k[i];
@@ -2883,8 +2979,9 @@ hipError_t tri_run_plan(const TriFramePlan& plan, TriLaunchArgs* d_args, const T
             if (k.stage == kStageSetup) setup_stamped = true;
             (void)hipEventRecord(ev[k.stage], stream);
         }
-        void* kargs[] = {&d_args};
-        e = hipLaunchKernel(k.func, k.grid, k.block, kargs, 0, stream);
+        void* first[] = {const_cast<TriLaunchArgs*>(&args), &d_args};
+        void* later[] = {&d_args};
+        e = hipLaunchKernel(k.func, k.grid, k.block, i == 0 ? first : later, 0, stream);
         if (e != hipSuccess) return e;
     }
     if (ev) (void)hipEventRecord(ev[kStageCount], stream);

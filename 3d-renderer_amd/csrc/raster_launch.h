@@ -23,7 +23,8 @@ struct TriDeviceBuffers {
     const uint32_t* sky;         // 6 * sky_size^2 RGBA8 sRGB texels (+X,-X,+Y,-Y,+Z,-Z)
     const float* srgb_lut;       // 256 sRGB -> linear (host, double) + 256 alpha b/255
     float4* clip;                // nslots (read only when a primitive is clipped)
-    TriSnap* snap;               // nslots
+    TriSnap* snap;               // nslots (TRI_SNAP_F: {X, Y as exact floats, 1/w, z})
+    uint8_t* oc;                 // nslots outcodes (TRI_SNAP_F; otherwise they ride in snap's X word)
     float4* vary;                // 3 * (nslots + ovf_vert_cap)
     TriRec* recs;                // ovf_rec_cap clipped sub-triangles
     uint32_t* clip_slot;         // nprims: first sub-triangle record of a clipped primitive
@@ -48,21 +49,22 @@ struct TriDeviceBuffers {
     uint32_t* shadow_map;        // s_size * s_size float32 depth bits
 };
 
-// One frame's arguments, device-resident (DESIGN.md §2 "host cost"): tri_render fills a pinned host slot,
-// one host-to-device copy moves it, and every kernel of the frame takes a pointer to it (a 16-B argument
-// instead of a 1.8-KB by-value block per launch). The frame's first kernel stores frame_id into the pinned
-// word host_done, which tells tri_render when the host slot the copy read can be written again.
+// One frame's arguments (DESIGN.md §2 "launch cost"). The frame's first kernel (k_vertex, k_vertex_band or
+// k_reset) takes them by value — kernel-argument memory, which its many short waves read fastest — and its
+// workgroup 0 publishes them to a device copy that every later kernel of the frame reads through a 16-B
+// pointer argument (k_setup, k_shadow_raster, k_raster: one kernarg block of 1.8 KB per frame instead of one
+// per launch). Stream order makes the copy complete before k_setup starts and keeps the next frame's copy
+// behind this frame's raster.
 struct TriLaunchArgs {
     TriFrameParams fp;
     TriDeviceBuffers b;
-    uint32_t* host_done;
-    uint32_t frame_id;
 };
+static_assert(sizeof(TriLaunchArgs) % 16 == 0, "TriLaunchArgs moves in 16-B pieces");
 
 // The kernels of one frame in launch order (which instantiation, grid, block) — computed on the host from the
 // frame's parameters; the same plan is launched directly or as a cached HIP graph.
 struct TriKernelLaunch {
-    const void* func;
+    const void* func;  // the first launch takes (TriLaunchArgs by value, TriLaunchArgs* copy); the others the copy
     dim3 grid, block;
     int stage;  // TriStage stamped before this launch when timing (-1: none)
 };
@@ -80,10 +82,10 @@ enum TriStage { kStageVertex = 0, kStageShadow, kStageSetup, kStageRaster, kStag
 
 hipError_t tri_kernels_init();
 
-// One frame = the copy of *h_args into *d_args, then 3 dependent launches on `stream` (k_vertex, k_setup
-// with in-wave clipping, k_raster), 4 with the shadow pre-pass (k_shadow_raster after k_setup<shadow>);
-// `events` (may be null) gets kStageCount + 1 stamps (the kStageShadow stamp only when the pre-pass runs).
-hipError_t tri_run_plan(const TriFramePlan& plan, TriLaunchArgs* d_args, const TriLaunchArgs* h_args,
+// One frame = 3 dependent launches on `stream` (k_vertex, k_setup with in-wave clipping, k_raster), 4 with the
+// shadow pre-pass (k_shadow_raster after k_setup<shadow>); `events` (may be null) gets kStageCount + 1 stamps
+// (the kStageShadow stamp only when the pre-pass runs).
+hipError_t tri_run_plan(const TriFramePlan& plan, const TriLaunchArgs& args, TriLaunchArgs* d_args,
                         hipStream_t stream, hipEvent_t* events);
 
 // Presentation blit (tri_blit_linear): src W x H B8G8R8A8 -> dst dw x dh, linear, clamp-to-edge.

@@ -144,6 +144,7 @@ struct tri_ctx {
     // work buffers
     float4* d_clip = nullptr; size_t cap_clip = 0;
     TriSnap* d_snap = nullptr; size_t cap_snap = 0;
+    uint8_t* d_oc = nullptr; size_t cap_oc = 0;
     int32_t bin_log2 = 6;
     float4* d_vary = nullptr; size_t cap_vary = 0;
     TriRec* d_recs = nullptr; size_t cap_recs = 0;
@@ -174,24 +175,11 @@ struct tri_ctx {
     uint32_t* d_color = nullptr;
     float* d_depth = nullptr;
 
-    // device-resident frame arguments (TriLaunchArgs): one device copy read by the frame's
-    // kernels, a ring of pinned host slots tri_render fills, and the pinned word the frame's first kernel
-    // stamps with its frame id (a host slot is rewritten only after the frame that last used it started)
-    static constexpr uint32_t kArgSlots = 8;
+    // the frame's arguments: built here by tri_render, passed by value to the frame's first kernel, which
+    // publishes them to d_args for the later kernels (raster_launch.h)
+    TriLaunchArgs args{};
     TriLaunchArgs* d_args = nullptr;
-    TriLaunchArgs* h_args = nullptr;
-    uint32_t* h_done = nullptr;
-    uint32_t frame_id = 0;
-    // each distinct launch plan as HIP graphs (the H2D copy of a host slot + the kernels), one per host slot,
-    // built on first use: a frame is then one hipGraphLaunch
-    struct GraphEntry {
-        TriFramePlan plan;
-        hipGraphExec_t exec[kArgSlots] = {};
-        uint64_t used = 0;
-    };
-    std::vector<GraphEntry> graphs;
-    uint64_t graph_clock = 0;
-    bool use_graph = true;
+    bool launched = false;  // a frame was enqueued (tri_set_stream orders the next one behind it)
 
     bool timing = false;
     uint32_t timing_period = 1, timing_counter = 0;  // time every timing_period-th frame
@@ -207,74 +195,6 @@ int make_current(tri_ctx* c) {
     return TRI_OK;
 }
 
-bool same_plan(const TriFramePlan& a, const TriFramePlan& b) {
-    if (a.n != b.n) return false;
-    for (uint32_t i = 0; i < a.n; ++i) {
-        const TriKernelLaunch &x = a.k[i], &y = b.k[i];
-        if (x.func != y.func || x.grid.x != y.grid.x || x.grid.y != y.grid.y || x.grid.z != y.grid.z ||
-            x.block.x != y.block.x || x.block.y != y.block.y || x.block.z != y.block.z)
-            return false;
-    }
-    return true;
-}
-
-// The graph of `plan` reading host slot `slot`: the slot's H2D copy into d_args, then the kernels in order.
-// nullptr when HIP cannot build it (the caller then launches the plan directly, with the same effect).
-hipGraphExec_t graph_for(tri_ctx* c, const TriFramePlan& plan, uint32_t slot) {
-    tri_ctx::GraphEntry* e = nullptr;
-    for (auto& g : c->graphs)
-        if (same_plan(g.plan, plan)) e = &g;
-    if (!e) {
-        if (c->graphs.size() >= 6) {  // evict the least recently used plan
-            auto lru = std::min_element(c->graphs.begin(), c->graphs.end(),
-                                        [](const auto& a, const auto& b) { return a.used < b.used; });
-            for (auto& x : lru->exec)
-                if (x) (void)hipGraphExecDestroy(x);
-            c->graphs.erase(lru);
-        }
-        c->graphs.emplace_back();
-        e = &c->graphs.back();
-        e->plan = plan;
-    }
-    e->used = ++c->graph_clock;
-    if (e->exec[slot]) return e->exec[slot];
-    hipGraph_t g = nullptr;
-    if (hipGraphCreate(&g, 0) != hipSuccess) return nullptr;
-    hipGraphNode_t prev = nullptr;
-    bool ok = hipGraphAddMemcpyNode1D(&prev, g, nullptr, 0, c->d_args, &c->h_args[slot], sizeof(TriLaunchArgs),
-                                      hipMemcpyHostToDevice) == hipSuccess;
-    TriLaunchArgs* dargs = c->d_args;
-    for (uint32_t i = 0; ok && i < plan.n; ++i) {
-        hipKernelNodeParams p{};
-        p.func = const_cast<void*>(plan.k[i].func);
-        p.gridDim = plan.k[i].grid;
-        p.blockDim = plan.k[i].block;
-        p.sharedMemBytes = 0;
-        void* kargs[] = {&dargs};
-        p.kernelParams = kargs;
-        p.extra = nullptr;
-        hipGraphNode_t node = nullptr;
-        ok = hipGraphAddKernelNode(&node, g, &prev, 1, &p) == hipSuccess;
-        prev = node;
-    }
-    hipGraphExec_t x = nullptr;
-    if (ok && hipGraphInstantiate(&x, g, nullptr, nullptr, 0) != hipSuccess) x = nullptr;
-    (void)hipGraphDestroy(g);
-    e->exec[slot] = x;
-    return x;
-}
-
-// Host slot of frame `fid`: before it is rewritten, the frame that used it kArgSlots frames ago has started
-// (its first kernel stamped h_done, so its H2D copy is complete). Almost always immediate; a host far ahead of
-// the GPU waits here (spin, then the stream).
-int claim_arg_slot(tri_ctx* c, uint32_t fid) {
-    if (fid <= tri_ctx::kArgSlots) return TRI_OK;
-    const uint32_t need = fid - tri_ctx::kArgSlots;
-    auto started = [&] { return (int32_t)(__atomic_load_n(c->h_done, __ATOMIC_ACQUIRE) - need) >= 0; };
-    for (int i = 0; i < 4096 && !started(); ++i) __builtin_ia32_pause();
-    if (!started()) HIP_TRY(hipStreamSynchronize(c->stream));  // every enqueued frame has run
-    return TRI_OK;
-}
 
 // transpose(inverse(mat3(M))) exactly as Default.vert:95 evaluates it per vertex (glm cofactor
 // form, same float operation order as the oracle); out[c*3+r] = NM[c][r] = inverse[r][c].
@@ -575,6 +495,7 @@ int ensure_work_buffers(tri_ctx* c) {
     if (realloc) HIP_TRY(hipStreamSynchronize(c->stream));
     if ((rc = grow(c->d_clip, c->cap_clip, std::max<size_t>(c->nslots, 1)))) return rc;
     if ((rc = grow(c->d_snap, c->cap_snap, std::max<size_t>(c->nslots, 1)))) return rc;
+    if ((rc = grow(c->d_oc, c->cap_oc, std::max<size_t>(c->nslots, 1)))) return rc;
     if ((rc = grow(c->d_vary, c->cap_vary, nvary))) return rc;
     if ((rc = grow(c->d_recs, c->cap_recs, nrec))) return rc;
     if ((rc = grow(c->d_clip_slot, c->cap_clip_slot, std::max<size_t>(c->nprims, 1)))) return rc;
@@ -873,12 +794,8 @@ int tri_create(const tri_config* cfg, tri_ctx** out) {
     c->d_depth = c->d_depth_own;
     if (hipMemset(c->d_ctr, 0, sizeof(TriCounters)) != hipSuccess)
         return bail(fail(TRI_E_HIP, "tri_create: memset failed"));
-    if (hipMalloc(&c->d_args, sizeof(TriLaunchArgs)) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&c->h_args), sizeof(TriLaunchArgs) * tri_ctx::kArgSlots) != hipSuccess ||
-        hipHostMalloc(reinterpret_cast<void**>(&c->h_done), 64, hipHostMallocCoherent) != hipSuccess)
-        return bail(fail(TRI_E_OOM, "tri_create: argument ring allocation failed"));
-    std::memset(c->h_args, 0, sizeof(TriLaunchArgs) * tri_ctx::kArgSlots);
-    *c->h_done = 0;
+    if (hipMalloc(&c->d_args, sizeof(TriLaunchArgs)) != hipSuccess)
+        return bail(fail(TRI_E_OOM, "tri_create: argument copy allocation failed"));
     float lut[512];
     for (int i = 0; i < 256; ++i) {  // R8G8B8A8_SRGB decode (sRGB EOTF), evaluated in double
         lut[i] = srgb_decode(i);
@@ -907,17 +824,12 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_lut); f(c->d_bones); f(c->d_sky);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase); f(c->d_cbase); f(c->d_cvis);
-    f(c->d_clip); f(c->d_snap); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
+    f(c->d_clip); f(c->d_snap); f(c->d_oc); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
     f(c->d_bin_count); f(c->d_bin_list); f(c->d_ctr);
     f(c->d_color_own); f(c->d_depth_own); f(c->d_present);
     f(c->d_lpos); f(c->d_lsnap); f(c->d_sbin_count); f(c->d_sbin_list); f(c->d_shadow);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
-    for (auto& g : c->graphs)
-        for (auto& x : g.exec)
-            if (x) (void)hipGraphExecDestroy(x);
     f(c->d_args);
-    if (c->h_args) (void)hipHostFree(c->h_args);
-    if (c->h_done) (void)hipHostFree(c->h_done);
     if (c->stage_free) (void)hipEventDestroy(c->stage_free);
     for (auto& v : {std::cref(c->pending), std::cref(c->free_sets)})
         for (const TimingSet& t : v.get())
@@ -930,7 +842,7 @@ int tri_destroy(tri_ctx* c) {
 int tri_set_stream(tri_ctx* c, void* s) {
     if (!c) return fail(TRI_E_INVALID, "tri_set_stream: null context");
     hipStream_t next = s ? static_cast<hipStream_t>(s) : c->own_stream;
-    if (next != c->stream && c->frame_id) {
+    if (next != c->stream && c->launched) {
         // the next frame's argument copy must not overtake the previous frame's kernels on the old stream
         int rc = make_current(c);
         if (rc) return rc;
@@ -1205,15 +1117,9 @@ int tri_render(tri_ctx* c) {
     if ((rc = choose_bin_grid(c))) return rc;
     if ((rc = ensure_work_buffers(c))) return rc;
 
-    // this frame's host slot (free once the frame kArgSlots back started), filled in place
-    const uint32_t fid = ++c->frame_id;
-    const uint32_t slot = fid % tri_ctx::kArgSlots;
-    if ((rc = claim_arg_slot(c, fid))) return rc;
-    TriLaunchArgs& ha = c->h_args[slot];
+    TriLaunchArgs& ha = c->args;  // passed by value at launch: free to rewrite for the next frame
     TriFrameParams& fp = ha.fp;
     std::memset(&fp, 0, sizeof fp);
-    ha.host_done = c->h_done;
-    ha.frame_id = fid;
     fp.W = c->W; fp.H = c->H; fp.y0 = c->y0; fp.y1 = c->y1;
     fp.nbx = c->nbx; fp.nby = c->nby; fp.nbins = c->nbins;
     fp.bin_log2 = c->bin_log2;
@@ -1314,6 +1220,7 @@ int tri_render(tri_ctx* c) {
     b.sky = c->d_sky;
     b.clip = c->d_clip;
     b.snap = c->d_snap;
+    b.oc = c->d_oc;
     b.vary = c->d_vary;
     b.recs = c->d_recs;
     b.clip_slot = c->d_clip_slot;
@@ -1349,9 +1256,8 @@ int tri_render(tri_ctx* c) {
     ts.shadow = fp.shadow_on != 0;
     TriFramePlan plan;
     tri_plan_frame(fp, plan);
-    hipGraphExec_t gx = (!timed && c->use_graph) ? graph_for(c, plan, slot) : nullptr;
-    if (gx) HIP_TRY(hipGraphLaunch(gx, c->stream));
-    else HIP_TRY(tri_run_plan(plan, c->d_args, &ha, c->stream, ev));
+    HIP_TRY(tri_run_plan(plan, ha, c->d_args, c->stream, ev));
+    c->launched = true;
     if (timed) c->pending.push_back(ts);
     if (fp.shadow_on) c->shadow_rendered = true;
     return TRI_OK;
