@@ -7,7 +7,9 @@
 //                          vertices with an outcode on draws with clip_from_world (the clipper recomputes the rest)
 //   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, 1/w, z_ndc} (the fragment stage
 //                          loads the first 12 bytes: it needs no depth)
-//   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}
+//   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}; 36 B/slot {world.xyz},
+//                          {normal.xyz}, {color.xyz} on single-draw solid frames (TriFrameParams::vary36);
+//                          none but the clipper's polygon vertices (object space, 36 B) with vary_obj
 //   prim_vs   16 B/prim    {vertex slots 0..2, draw | clipped flag}, written by k_setup for the
 //                          primitives it bins or clips on frames with several draws: k_raster's one-load
 //                          route from a primitive id to its vertices and draw (instead of a draw search);
@@ -233,6 +235,14 @@ struct TriFrameParams {
     // k_vertex skip vertex blocks (off while the shadow pre-pass needs every caster); setup_multi: k_setup
     // runs a quarter of the chunks' workgroups, four strided chunks each (single-draw bands, no pre-pass)
     uint32_t cull_on, cull_vertex, ncl_total, setup_multi;
+    // vary36: single-draw solid frames without the pre-pass (k_raster_plain's ONE instantiation) store 36-B
+    // varyings {world.xyz, N.xyz, colour.xyz} — no texture coordinates, which nothing samples — instead of 48 B.
+    // vary_obj (such frames whose draw is affine, unskinned, with a conformal normal matrix, over unit object
+    // normals): k_vertex writes no varyings at all; the fragment stage gathers the object-space position,
+    // normal and colour from the vertex records (vin + vin_base) and, when obj_xform, carries the interpolated
+    // position and normal through the model and normal matrices (linear maps: the same values up to
+    // rounding); the clipper writes object-space 36-B records for its polygon vertices.
+    uint32_t vary36, vary_obj, obj_xform, vin_base;
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
     uint32_t shadow_on, s_size, s_nbx, s_nbins;
     uint32_t s_bin_cap;

@@ -145,13 +145,37 @@ __device__ __forceinline__ u32x3v rec96(const RecBuf& b, uint32_t i, uint32_t of
     return u32x3v{q[0], q[1], q[2]};
 }
 
-struct FetchBufs {  // k_raster's gather sources: 16-B snaps, 48-B varyings, 48-B shade records
-    RecBuf snap, vary, shade;
+// k_raster's gather sources: 16-B snaps, varyings, 48-B shade records. `src` holds an unclipped primitive's
+// vertex attributes: the varyings, or with vary_obj the draw's own vertex records (48 B, the first 36 B read).
+struct FetchBufs {
+    RecBuf snap, vary, src, shade;
 };
+// The varying record: 48 B {world, u}{N, v}{colour, 0}, or 36 B {world}{N}{colour} on single-draw solid frames
+// (TriFrameParams::vary36 — exactly the frames k_raster_plain<.., ONE> shades). TRI_VARY36 = 0 keeps 48 B.
+// TRI_VARY_OBJ = 0 keeps world-space varyings on every frame (TriFrameParams::vary_obj).
+#ifndef TRI_VARY36
+#define TRI_VARY36 1
+#endif
+#ifndef TRI_VARY_OBJ
+#define TRI_VARY_OBJ 1
+#endif
+__device__ __forceinline__ bool vary36_mode(const TriFrameParams& fp) { return TRI_VARY36 && fp.vary36; }
+__device__ __forceinline__ bool obj_mode(const TriFrameParams& fp) { return TRI_VARY36 && TRI_VARY_OBJ && fp.vary_obj; }
+struct F3 {
+    float x, y, z;
+};
+// Attribute j (0 position, 1 normal, 2 colour) of vertex record vin_base + slot, object space (vary_obj)
+__device__ __forceinline__ F3 vin_attr(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot, int j) {
+    const float* q = reinterpret_cast<const float*>(b.vin) + 12u * (fp.vin_base + slot) + 3 * j;
+    return F3{q[0], q[1], q[2]};
+}
+template <bool ONE = false>
 __device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const TriDeviceBuffers& b) {
     FetchBufs f;
     f.snap = rec_buf(b.snap, 16u, fp.nslots);
-    f.vary = rec_buf(b.vary, 48u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
+    f.vary = rec_buf(b.vary, (ONE && TRI_VARY36) ? 36u : 48u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
+    f.src = f.vary;
+    if (ONE && obj_mode(fp)) f.src = rec_buf(b.vin + fp.vin_base, 48u, fp.nslots);
     f.shade = rec_buf(b.draw_shade, (uint32_t)sizeof(TriDrawShade), fp.ndraws);
     return f;
 }
@@ -253,6 +277,31 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_reset(TRI_FIRST_KARGS) {  // a fr
 }
 #endif  // TRI_RASTER_PLAIN_TU
 
+// The clip position, outcode and snap of a vertex at `world` (its clip position kept when the clipper needs it).
+__device__ __forceinline__ void store_snap(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
+                                           const TriDrawDev& dr, float4 world) {
+    const float4 clip = mat_vec_seq(fp.pv, world);
+    uint32_t oc = outcode(fp, clip);
+    // clip_from_world draws: a vertex without an outcode has world.w == 1 and its clip position is
+    // recomputed by the clipper from `vary` (or its record); a non-finite position (w != 1) is marked for clipping
+    if (dr.clip_from_world && oc == 0u && !(world.w == 1.0f)) oc = TRI_OC_CLIP;
+    if (oc != 0u || !dr.clip_from_world) b.clip[slot] = clip;
+    TriSnap sn{TRI_SNAP_F ? 0 : (int32_t)(oc << 24), 0, 0.0f, 0.0f};
+    if (!(oc & TRI_OC_CLIP)) {
+        int32_t X, Y;
+        snap_compute(fp, clip, X, Y, sn.z, sn.iw);
+        if (TRI_SNAP_F) {  // |X|, |Y| < 2^22 inside the guard band: exact as floats
+            sn.xo = __float_as_int((float)X);
+            sn.y = __float_as_int((float)Y);
+        } else {
+            sn.xo = (X & 0x00FFFFFF) | (int32_t)(oc << 24);
+            sn.y = Y;
+        }
+    }
+    b.snap[slot] = sn;
+    if (TRI_SNAP_F) b.oc[slot] = (uint8_t)oc;
+}
+
 // Default.vert for vertex slot `slot` of draw `dr` (whose first slot is `vbase`).
 __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
                                             const TriDrawDev& dr, uint32_t vbase) {
@@ -261,6 +310,14 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
         b.snap[slot] = TriSnap{TRI_SNAP_F ? 0 : (int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
         if (TRI_SNAP_F) b.oc[slot] = (uint8_t)TRI_OC_BAD;
         if (fp.shadow_on) b.lsnap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
+        return;
+    }
+    if (obj_mode(fp)) {  // no varyings to write: the position stream alone (12 B), then the snap
+        const Rsrc pr = make_rsrc(b.vpos, 12ull * b.vertex_count);
+        const auto q = __builtin_amdgcn_raw_buffer_load_b96(pr, (uint32_t)gi * 12u, 0, 0);
+        const float4 world = mat_vec_seq(dr.model, make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]),
+                                                               __uint_as_float(q[2]), 1.0f));
+        store_snap(fp, b, slot, dr, world);
         return;
     }
     // three 16-byte loads (a plain struct load is split into overlapping per-field loads)
@@ -306,30 +363,18 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
     nnx = nnx * inv; nny = nny * inv; nnz = nnz * inv;
     const float u = (in.u * dr.tex_scale[0]) * dr.tiling + dr.tex_offset[0];
     const float v = (in.v * dr.tex_scale[1]) * dr.tiling + dr.tex_offset[1];
-    const float4 clip = mat_vec_seq(fp.pv, world);
-    uint32_t oc = outcode(fp, clip);
-    // clip_from_world draws: a vertex without an outcode has world.w == 1 and its clip position is
-    // recomputed by the clipper from `vary`; a non-finite position (w != 1) is marked for clipping
-    if (dr.clip_from_world && oc == 0u && !(world.w == 1.0f)) oc = TRI_OC_CLIP;
-    if (oc != 0u || !dr.clip_from_world) b.clip[slot] = clip;
-    TriSnap sn{TRI_SNAP_F ? 0 : (int32_t)(oc << 24), 0, 0.0f, 0.0f};
-    if (!(oc & TRI_OC_CLIP)) {
-        int32_t X, Y;
-        snap_compute(fp, clip, X, Y, sn.z, sn.iw);
-        if (TRI_SNAP_F) {  // |X|, |Y| < 2^22 inside the guard band: exact as floats
-            sn.xo = __float_as_int((float)X);
-            sn.y = __float_as_int((float)Y);
-        } else {
-            sn.xo = (X & 0x00FFFFFF) | (int32_t)(oc << 24);
-            sn.y = Y;
-        }
+    store_snap(fp, b, slot, dr, world);
+    if (vary36_mode(fp)) {  // 36-B record: three 12-B stores (the slot's bytes are 4-B aligned)
+        F3* vo = reinterpret_cast<F3*>(b.vary) + 3u * slot;
+        vo[0] = F3{world.x, world.y, world.z};
+        vo[1] = F3{nnx, nny, nnz};
+        vo[2] = F3{in.cr, in.cg, in.cb};
+    } else {
+        float4* vo = b.vary + 3u * slot;
+        vo[0] = make_float4(world.x, world.y, world.z, u);
+        vo[1] = make_float4(nnx, nny, nnz, v);
+        vo[2] = make_float4(in.cr, in.cg, in.cb, 0.0f);
     }
-    b.snap[slot] = sn;
-    if (TRI_SNAP_F) b.oc[slot] = (uint8_t)oc;
-    float4* vo = b.vary + 3u * slot;
-    vo[0] = make_float4(world.x, world.y, world.z, u);
-    vo[1] = make_float4(nnx, nny, nnz, v);
-    vo[2] = make_float4(in.cr, in.cg, in.cb, 0.0f);
     if (fp.shadow_on) shadow_vertex(fp, b, slot, world);
 }
 
@@ -632,7 +677,15 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
         ClipVert v;
         const uint32_t sl = lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2);
         if (cfw && snap_oc(b, b.snap[sl], sl) == 0u) {  // not stored by k_vertex: world.w == 1
-            const float4 wv = b.vary[3u * sl];
+            F3 wv;
+            if (obj_mode(fp)) {  // k_vertex's world position, recomputed from the record (same operations)
+                const F3 p = vin_attr(fp, b, sl, 0);
+                const float4 w = mat_vec_seq(fp.draw0.model, make_float4(p.x, p.y, p.z, 1.0f));
+                wv = F3{w.x, w.y, w.z};
+            } else {
+                wv = vary36_mode(fp) ? reinterpret_cast<const F3*>(b.vary)[3u * sl]
+                                     : F3{b.vary[3u * sl].x, b.vary[3u * sl].y, b.vary[3u * sl].z};
+            }
             v.c = mat_vec_seq(fp.pv, make_float4(wv.x, wv.y, wv.z, 1.0f));
         } else {
             v.c = b.clip[sl];
@@ -688,15 +741,30 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
     const float* src = buf[cur];
     if ((int)lane < n) {  // varyings of polygon vertex `lane` from the source triangle's barycentrics
         const ClipVert s = cv_load(src + lane * kClipStride);
-        const float4* v0 = b.vary + 3u * sl0;
-        const float4* v1 = b.vary + 3u * sl1;
-        const float4* v2 = b.vary + 3u * sl2;
-        float4* vo = b.vary + 3u * (sbase + lane);
+        if (vary36_mode(fp)) {  // (object-space attributes from the vertex records with vary_obj)
+            const F3* v0 = reinterpret_cast<const F3*>(b.vary) + 3u * sl0;
+            const F3* v1 = reinterpret_cast<const F3*>(b.vary) + 3u * sl1;
+            const F3* v2 = reinterpret_cast<const F3*>(b.vary) + 3u * sl2;
+            F3* vo = reinterpret_cast<F3*>(b.vary) + 3u * (sbase + lane);
+            const bool obj = obj_mode(fp);
 #pragma unroll
-        for (int j = 0; j < 3; ++j) {
-            const float4 x = v0[j], y = v1[j], z = v2[j];
-            vo[j] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
-                                (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, (s.b0 * x.w + s.b1 * y.w) + s.b2 * z.w);
+            for (int j = 0; j < 3; ++j) {
+                const F3 x = obj ? vin_attr(fp, b, sl0, j) : v0[j], y = obj ? vin_attr(fp, b, sl1, j) : v1[j],
+                         z = obj ? vin_attr(fp, b, sl2, j) : v2[j];
+                vo[j] = F3{(s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
+                           (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z};
+            }
+        } else {
+            const float4* v0 = b.vary + 3u * sl0;
+            const float4* v1 = b.vary + 3u * sl1;
+            const float4* v2 = b.vary + 3u * sl2;
+            float4* vo = b.vary + 3u * (sbase + lane);
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const float4 x = v0[j], y = v1[j], z = v2[j];
+                vo[j] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
+                                    (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, (s.b0 * x.w + s.b1 * y.w) + s.b2 * z.w);
+            }
         }
         if constexpr (LPOS) {  // shadow pre-pass on: the polygon vertex's light-space position, same weights
             const float4 x = b.lpos[sl0], y = b.lpos[sl1], z = b.lpos[sl2];
@@ -1920,16 +1988,25 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
 struct Taps {
     V4 a0, a1, a2, b0, b1, b2, c0, c1, c2;
 };
+// SRC: an unclipped primitive's vertex (fb.src), else a clipped polygon's (fb.vary); the same buffer unless ONE.
+template <bool ONE = false, bool SRC = false>
 __device__ __forceinline__ V4 ld_vary(const FetchBufs& fb, uint32_t slot, uint32_t j) {
+    if (ONE && TRI_VARY36) {  // 36-B prefixes: 12-B pieces, no texture coordinate (the stride is the buffer's)
+        const u32x3v q = rec96<36>(SRC ? fb.src : fb.vary, slot, j * 12u);
+        return V4{__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), 0.0f};
+    }
     const uint4 q = rec128<48>(fb.vary, slot, j * 16u);  // plain-float views (HIP vector unions defeat SROA)
     return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
 }
+template <bool ONE = false, bool SRC = false>
 __device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint32_t v1, uint32_t v2) {
     Taps t;
-    t.a0 = ld_vary(fb, v0, 0); t.a1 = ld_vary(fb, v0, 1);
-    t.b0 = ld_vary(fb, v1, 0); t.b1 = ld_vary(fb, v1, 1);
-    t.c0 = ld_vary(fb, v2, 0); t.c1 = ld_vary(fb, v2, 1);
-    if (!TRI_COLOUR_LATE) { t.a2 = ld_vary(fb, v0, 2); t.b2 = ld_vary(fb, v1, 2); t.c2 = ld_vary(fb, v2, 2); }
+    t.a0 = ld_vary<ONE, SRC>(fb, v0, 0); t.a1 = ld_vary<ONE, SRC>(fb, v0, 1);
+    t.b0 = ld_vary<ONE, SRC>(fb, v1, 0); t.b1 = ld_vary<ONE, SRC>(fb, v1, 1);
+    t.c0 = ld_vary<ONE, SRC>(fb, v2, 0); t.c1 = ld_vary<ONE, SRC>(fb, v2, 1);
+    if (!TRI_COLOUR_LATE) {
+        t.a2 = ld_vary<ONE, SRC>(fb, v0, 2); t.b2 = ld_vary<ONE, SRC>(fb, v1, 2); t.c2 = ld_vary<ONE, SRC>(fb, v2, 2);
+    }
     return t;
 }
 
@@ -1953,8 +2030,24 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
     const V4 &a0 = t.a0, &a1 = t.a1, &a2 = t.a2, &b0 = t.b0, &b1 = t.b1, &b2 = t.b2, &c0 = t.c0, &c1 = t.c1, &c2 = t.c2;
     // field-wise stores (a struct-valued f3 store is ABI-coerced to <2 x float> + float, which
     // keeps the pixel-pair path's fragments from being promoted to registers)
-    put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
-    put(3, ip(a1.x, b1.x, c1.x)); put(4, ip(a1.y, b1.y, c1.y)); put(5, ip(a1.z, b1.z, c1.z));
+    if (ONE && obj_mode(fp) && fp.obj_xform) {  // object-space position and normal: the model / normal matrices
+        const float px = ip(a0.x, b0.x, c0.x), py = ip(a0.y, b0.y, c0.y), pz = ip(a0.z, b0.z, c0.z);
+        const float nx = ip(a1.x, b1.x, c1.x), ny = ip(a1.y, b1.y, c1.y), nz = ip(a1.z, b1.z, c1.z);
+        const float* m = fp.draw0.model;  // column-major, affine (vary_obj)
+        const float* n = fp.draw0.nm;     // NM[c*3+r]
+        auto row = [](float c0v, float c1v, float c2v, float x, float y, float z, float w) {
+            return __builtin_fmaf(c0v, x, __builtin_fmaf(c1v, y, __builtin_fmaf(c2v, z, w)));
+        };
+        put(0, row(m[0], m[4], m[8], px, py, pz, m[12]));
+        put(1, row(m[1], m[5], m[9], px, py, pz, m[13]));
+        put(2, row(m[2], m[6], m[10], px, py, pz, m[14]));
+        put(3, row(n[0], n[3], n[6], nx, ny, nz, 0.0f));
+        put(4, row(n[1], n[4], n[7], nx, ny, nz, 0.0f));
+        put(5, row(n[2], n[5], n[8], nx, ny, nz, 0.0f));
+    } else {
+        put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
+        put(3, ip(a1.x, b1.x, c1.x)); put(4, ip(a1.y, b1.y, c1.y)); put(5, ip(a1.z, b1.z, c1.z));
+    }
     put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
     const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
     put(9, u); put(10, v);
@@ -2030,7 +2123,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
     const uint32_t sub = CLIPM == 1 ? 0u : (low & 7u);  // >= 1: sub-triangle `sub` of a clipped primitive
-    const FetchBufs fb = fetch_bufs(fp, b);
+    const FetchBufs fb = fetch_bufs<ONE>(fp, b);
     uint32_t sl[3] = {0, 0, 0}, d = 0;
     TriSnap a0{}, a1{}, a2{};
     uint32_t v0 = 0, v1 = 0, v2 = 0;
@@ -2044,7 +2137,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         v0 = sl[0]; v1 = sl[2]; v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
         // the varyings are gathered before the (rare) clipped branch: its record loads are waited for inside
         // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
-        taps = load_taps(fb, v0, v1, v2);
+        taps = load_taps<ONE, true>(fb, v0, v1, v2);
     } else if (!ONE) {
         prim_slots<ONE>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
     }
@@ -2052,7 +2145,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     if (CLIPM == 2 || (CLIPM == 0 && sub)) {  // a clipped primitive's sub-triangle: its own slots and varyings
         rc = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
         v0 = rc.v[0]; v1 = rc.v[1]; v2 = rc.v[2];
-        taps = load_taps(fb, v0, v1, v2);
+        taps = load_taps<ONE>(fb, v0, v1, v2);
     }
     uint4 L0, L1, L2;
     if constexpr (kInlineVis) {
@@ -2072,7 +2165,12 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     if (kAblate & 1024) {  // diagnostics: 1024 = no colour gathers (3 of the fragment's 13 loads; same VALU)
         taps.a2 = V4{w0, w1, w2, 0.0f}; taps.b2 = taps.a2; taps.c2 = taps.a2;
     } else if (TRI_COLOUR_LATE) {
-        taps.a2 = ld_vary(fb, v0, 2); taps.b2 = ld_vary(fb, v1, 2); taps.c2 = ld_vary(fb, v2, 2);
+        if (ONE && !from_rec) {  // an unclipped primitive's vertices (with CLIPM 0 a per-lane choice: both masked)
+            taps.a2 = ld_vary<ONE, true>(fb, v0, 2); taps.b2 = ld_vary<ONE, true>(fb, v1, 2);
+            taps.c2 = ld_vary<ONE, true>(fb, v2, 2);
+        } else {
+            taps.a2 = ld_vary<ONE>(fb, v0, 2); taps.b2 = ld_vary<ONE>(fb, v1, 2); taps.c2 = ld_vary<ONE>(fb, v2, 2);
+        }
     }
     float vis = SHADOW ? pre_vis : 1.0f;
     if constexpr (kInlineVis) {  // light-space position at the pixel with the oracle's weights, then the compare

@@ -75,8 +75,12 @@ struct tri_geometry {
     bool shared = false;
     uint64_t version = 0;  // bumped by every upload (contexts re-resolve their draws)
     TriVsIn* d_vin = nullptr; size_t cap_vin = 0;
+    float* d_pos = nullptr; size_t cap_pos = 0;  // 3 floats per vertex (k_vertex's stream with vary_obj)
     TriVsSkin* d_skin = nullptr; size_t cap_skin = 0;
     bool has_skin_data = false;
+    // every vertex has a finite position and a unit normal (|n|^2 within 1e-5 of 1): a draw over it may keep
+    // its varyings in object space (TriFrameParams::vary_obj)
+    bool obj_ok = false;
     uint64_t nverts = 0;
     uint32_t* d_idx = nullptr; size_t cap_idx = 0;
     uint64_t nidx = 0;
@@ -140,6 +144,8 @@ struct tri_ctx {
     uint32_t ndraws = 0, nslots = 0, nprims = 0;
     bool any_skin = false;
     TriDrawDev draw0{};  // the resolved draw when there is exactly one (passed by value to the kernels)
+    bool draw0_obj = false;    // draw0 may keep object-space varyings (draw_obj_ok)
+    bool draw0_xform = false;  // ... and its model matrix is not the identity
 
     // work buffers
     float4* d_clip = nullptr; size_t cap_clip = 0;
@@ -219,6 +225,32 @@ void normal_matrix(const float* M, float* out) {
 }
 
 float clamp01(float x) { return std::fmin(std::fmax(x, 0.0f), 1.0f); }
+
+bool identity_model(const float* m) {
+    for (int i = 0; i < 16; ++i)
+        if (m[i] != ((i % 5 == 0) ? 1.0f : 0.0f)) return false;
+    return true;
+}
+
+// Object-space varyings (TriFrameParams::vary_obj) are the world-space ones up to rounding when the draw is
+// affine and unskinned (clip_from_world: world = A p + t, a linear map of the interpolated position), its normal
+// matrix is conformal (orthogonal columns of one length s, so normalize(NM n) = NM n / s for every unit n and the
+// fragment's normalize sees the same direction) and every object normal is unit, with all its vertex records
+// in the vertex buffer.
+bool draw_obj_ok(const tri_geometry& g, const TriDrawDev& d) {
+    if (!g.obj_ok || !d.clip_from_world || d.vert_count == 0) return false;
+    const int64_t first = (int64_t)d.base_vertex + (int64_t)d.min_index;
+    if (first < 0 || (uint64_t)first + d.vert_count > g.nverts) return false;
+    double c[3][3];
+    for (int k = 0; k < 3; ++k)
+        for (int r = 0; r < 3; ++r) c[k][r] = d.nm[k * 3 + r];
+    auto dot = [&](int a, int b) { return c[a][0] * c[b][0] + c[a][1] * c[b][1] + c[a][2] * c[b][2]; };
+    const double s2 = (dot(0, 0) + dot(1, 1) + dot(2, 2)) / 3.0;
+    if (!(s2 > 0.0) || !std::isfinite(s2)) return false;
+    const double tol = 1e-5 * s2;
+    return std::fabs(dot(0, 0) - s2) <= tol && std::fabs(dot(1, 1) - s2) <= tol && std::fabs(dot(2, 2) - s2) <= tol &&
+           std::fabs(dot(0, 1)) <= tol && std::fabs(dot(0, 2)) <= tol && std::fabs(dot(1, 2)) <= tol;
+}
 
 // Default.frag frame constants hoisted for the fast shading build (Default.frag:131-174).
 void shade_constants(const tri_global_ubo& g, const tri_material_record& m, TriShadeConst& sc) {
@@ -456,6 +488,8 @@ int resolve_draws(tri_ctx* c) {
         c->draw0 = dd[0];
         c->shade0 = ds[0];
     }
+    c->draw0_obj = n == 1 && draw_obj_ok(*c->geom, dd[0]);
+    c->draw0_xform = c->draw0_obj && !identity_model(dd[0].model);
     c->nslots = (uint32_t)vslots;
     c->nprims = (uint32_t)prims;
     c->ncl_total = (uint32_t)ncl;
@@ -616,12 +650,15 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
     // AoS 100-byte Vertex -> 48-byte shading records (+ 32-byte skin records when weights exist)
     std::vector<TriVsIn> vin(nv);
     std::vector<TriVsSkin> skin;
-    bool has_skin = false;
+    bool has_skin = false, obj_ok = true;
     for (uint64_t i = 0; i < nv; ++i) {
         const tri_vertex& s = v[i];
         TriVsIn& o = vin[i];
         o.px = s.position[0]; o.py = s.position[1]; o.pz = s.position[2];
         o.nx = s.normal[0]; o.ny = s.normal[1]; o.nz = s.normal[2];
+        const double n2 = (double)o.nx * o.nx + (double)o.ny * o.ny + (double)o.nz * o.nz;
+        obj_ok = obj_ok && std::fabs(n2 - 1.0) <= 1e-5 && std::isfinite(o.px) && std::isfinite(o.py) &&
+                 std::isfinite(o.pz);
         o.cr = s.color[0]; o.cg = s.color[1]; o.cb = s.color[2];
         o.u = s.texcoord[0]; o.v = s.texcoord[1]; o.pad = 0.0f;
         has_skin = has_skin || s.bone_weights[0] > 0.f || s.bone_weights[1] > 0.f || s.bone_weights[2] > 0.f ||
@@ -637,8 +674,17 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
         HIP_TRY(hipMemcpy(g->d_skin, skin.data(), nv * sizeof(TriVsSkin), hipMemcpyHostToDevice));
     }
     g->has_skin_data = has_skin;
+    g->obj_ok = obj_ok;
     if ((rc = grow(g->d_vin, g->cap_vin, std::max<uint64_t>(nv, 1)))) return rc;
     if (nv) HIP_TRY(hipMemcpy(g->d_vin, vin.data(), nv * sizeof(TriVsIn), hipMemcpyHostToDevice));
+    {
+        std::vector<float> pos(3 * nv);
+        for (uint64_t i = 0; i < nv; ++i) {
+            pos[3 * i] = vin[i].px; pos[3 * i + 1] = vin[i].py; pos[3 * i + 2] = vin[i].pz;
+        }
+        if ((rc = grow(g->d_pos, g->cap_pos, std::max<uint64_t>(3 * nv, 3)))) return rc;
+        if (nv) HIP_TRY(hipMemcpy(g->d_pos, pos.data(), nv * 12, hipMemcpyHostToDevice));
+    }
     if ((rc = grow(g->d_idx, g->cap_idx, std::max<uint64_t>(ni, 1)))) return rc;
     if (ni) HIP_TRY(hipMemcpy(g->d_idx, idx, ni * 4, hipMemcpyHostToDevice));
     g->nverts = nv;
@@ -733,8 +779,10 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
 
 void free_geometry(tri_geometry& g) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(g.d_vin); f(g.d_skin); f(g.d_idx); f(g.d_clusters); f(g.d_vbox);
-    g.d_vin = nullptr; g.d_skin = nullptr; g.d_idx = nullptr; g.d_clusters = nullptr; g.d_vbox = nullptr;
+    f(g.d_vin); f(g.d_pos); f(g.d_skin); f(g.d_idx); f(g.d_clusters); f(g.d_vbox);
+    g.d_vin = nullptr; g.d_pos = nullptr; g.d_skin = nullptr; g.d_idx = nullptr; g.d_clusters = nullptr;
+    g.d_vbox = nullptr;
+    g.cap_vin = g.cap_pos = g.cap_skin = g.cap_idx = g.cap_clusters = g.cap_vbox = 0;
 }
 
 }  // namespace
@@ -1149,6 +1197,11 @@ int tri_render(tri_ctx* c) {
     fp.one_draw = c->ndraws == 1 ? 1u : 0u;
     if (fp.one_draw) fp.draw0 = c->draw0;
     fp.shade_solid = (fp.one_draw && c->shade0.tex.w == 1 && c->shade0.tex.h == 1) ? 1u : 0u;
+    // the frames k_raster_plain<.., ONE> shades keep 36-B varyings (no texture coordinates)
+    fp.vary36 = (fp.shade_solid && !c->shadow.size) ? 1u : 0u;
+    fp.vary_obj = fp.vary36 && c->draw0_obj ? 1u : 0u;
+    fp.obj_xform = fp.vary_obj && c->draw0_xform ? 1u : 0u;
+    fp.vin_base = fp.vary_obj ? (uint32_t)((int64_t)c->draw0.base_vertex + (int64_t)c->draw0.min_index) : 0u;
     fp.ovf_rec_cap = c->ovf_rec_cap;
     fp.ovf_vert_cap = c->ovf_vert_cap;
     fp.bin_cap = c->bin_cap;
@@ -1208,6 +1261,7 @@ int tri_render(tri_ctx* c) {
 
     TriDeviceBuffers& b = ha.b;
     b.vin = c->geom->d_vin;
+    b.vpos = c->geom->d_pos;
     b.vskin = c->any_skin ? c->geom->d_skin : nullptr;
     b.bones = c->d_bones;
     b.vertex_count = c->geom->nverts;

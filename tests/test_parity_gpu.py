@@ -109,6 +109,36 @@ def test_near_plane_clipping(oracle, flags):
         assert r.frame_stats()["triangles_clipped"] > 0
 
 
+@pytest.mark.parametrize("case", ["scaled", "offset", "nonuniform", "unnormalised"])
+def test_object_space_varyings(oracle, flags, case):
+    """Single-draw solid frames keep their varyings in object space (TriFrameParams::vary_obj) when the draw
+    is affine with a conformal normal matrix over unit normals: the near-clip ground plane (clipped polygons)
+    under a uniformly scaled, turned model, and with its vertex records offset in the buffer (base vertex and
+    minimum index). A non-uniform scale and non-unit normals take the world-space varyings instead. Every
+    case stays within the 1-LSB bar with depth bit-exact."""
+    from trident_raster import abi, scenes
+
+    s = sc.near_clip_grid()
+    if case == "scaled":
+        s.draws = [abi.make_draw(0, scenes.compose_transform((0.3, 0.0, -5.0), (-90.0, 20.0, 0.0), (1.7, 1.7, 1.7)),
+                                 material_index=0)]
+    elif case == "nonuniform":
+        s.draws = [abi.make_draw(0, scenes.compose_transform((0.0, 0.0, -5.0), (-90.0, 0.0, 0.0), (1.0, 2.0, 0.5)),
+                                 material_index=0)]
+    elif case == "unnormalised":
+        v = s.vertices.copy()
+        v["normal"] *= np.random.default_rng(5).uniform(0.5, 1.5, size=(v.shape[0], 1)).astype(np.float32)
+        s.vertices = v
+    else:  # 1000 records ahead of the mesh, 7 of them below its smallest index
+        pad = np.zeros(1000 + 7, s.vertices.dtype)
+        pad["position"] = 1e30  # never referenced (finite, with unit normals: the records stay eligible)
+        pad["normal"] = (0.0, 0.0, 1.0)
+        s.vertices = np.concatenate([pad[:1000], pad[1000:], s.vertices])
+        s.indices = s.indices + np.uint32(7)
+        s.meshes = np.array([(0, s.indices.size, 1000, 0)], abi.MESH_RANGE_DTYPE)
+    assert_parity(s, oracle, min_covered=10000, flags=flags)
+
+
 def test_depth_ties_and_far_clip(oracle, flags):
     assert_parity(sc.depth_ties(), oracle, min_covered=1000, flags=flags)
 

@@ -1,9 +1,10 @@
 #!/bin/bash
 # Round 4 (f): per-kernel durations (rocprofv3 kernel trace, one frame in flight) of r3trims, snapint (the packed
-# int snaps) and the current build; then the C3 rate A/B of the three, twice.
+# int snaps), novary36 (48-B varyings), noobj (36-B world varyings) and the current build (object-space varyings); then the C3 rate A/B of the three, twice.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out && export TMPDIR=/tmp
 V=3d-renderer_amd/lib/variants
-for lib in $V/r3trims.so $V/snapint.so 3d-renderer_amd/lib/libtri_raster.so; do
+timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1; rc=$?; tail -3 gpurun_out/gpu_tests.log; [ $rc = 0 ] || { grep -E "FAILED|Error" gpurun_out/gpu_tests.log | head; exit 1; }
+for lib in $V/r3trims.so $V/snapint.so $V/novary36.so $V/noobj.so 3d-renderer_amd/lib/libtri_raster.so; do
   n=$(basename $lib .so)
   TRI_RASTER_LIB=$lib timeout -k 10 200 rocprofv3 --kernel-trace --stats -d gpurun_out/kt_$n -o kt --output-format csv -- python3 bench.py --steps 50 --warmup 5 --no-cpu-baseline --no-secondary --inflight 1 > gpurun_out/kt_$n.log 2>&1 || { echo "$n trace failed"; tail -5 gpurun_out/kt_$n.log; exit 1; }
   f=$(find gpurun_out/kt_$n -name "*kernel_stats.csv" | head -1)
@@ -12,4 +13,4 @@ import csv,sys
 for r in csv.DictReader(open('$f')):
     if any(k in r['Name'] for k in ('k_vertex','k_setup','k_raster','k_reset')): print('  %-60s %8s calls avg %8.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3))"
 done
-EXTRA="--no-secondary" bash tools/ab.sh "TRI_RASTER_LIB=$V/r3trims.so" "TRI_RASTER_LIB=$V/snapint.so" "" "TRI_RASTER_LIB=$V/r3trims.so" "TRI_RASTER_LIB=$V/snapint.so" ""
+EXTRA="--no-secondary" bash tools/ab.sh "TRI_RASTER_LIB=$V/r3trims.so" "TRI_RASTER_LIB=$V/snapint.so" "TRI_RASTER_LIB=$V/novary36.so" "TRI_RASTER_LIB=$V/noobj.so" "" "TRI_RASTER_LIB=$V/r3trims.so" "TRI_RASTER_LIB=$V/snapint.so" "TRI_RASTER_LIB=$V/novary36.so" "TRI_RASTER_LIB=$V/noobj.so" ""
