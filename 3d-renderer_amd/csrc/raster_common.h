@@ -239,7 +239,7 @@ struct TriFrameParams {
     // varyings {world.xyz, N.xyz, colour.xyz} — no texture coordinates, which nothing samples — instead of 48 B.
     // vary_obj (such frames whose draw is affine, unskinned, with a conformal normal matrix, over unit object
     // normals): k_vertex writes no varyings at all; the fragment stage gathers the object-space position,
-    // normal and colour from the vertex records (vin + vin_base) and, when obj_xform, carries the interpolated
+    // normal and colour from the 36-B object records (vattr + vin_base) and, when obj_xform, carries the interpolated
     // position and normal through the model and normal matrices (linear maps: the same values up to
     // rounding); the clipper writes object-space 36-B records for its polygon vertices.
     uint32_t vary36, vary_obj, obj_xform, vin_base;

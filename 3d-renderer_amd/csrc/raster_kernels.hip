@@ -146,7 +146,7 @@ __device__ __forceinline__ u32x3v rec96(const RecBuf& b, uint32_t i, uint32_t of
 }
 
 // k_raster's gather sources: 16-B snaps, varyings, 48-B shade records. `src` holds an unclipped primitive's
-// vertex attributes: the varyings, or with vary_obj the draw's own vertex records (48 B, the first 36 B read).
+// vertex attributes: the varyings, or with vary_obj the draw's own 36-B object-space records (vattr).
 struct FetchBufs {
     RecBuf snap, vary, src, shade;
 };
@@ -166,7 +166,7 @@ struct F3 {
 };
 // Attribute j (0 position, 1 normal, 2 colour) of vertex record vin_base + slot, object space (vary_obj)
 __device__ __forceinline__ F3 vin_attr(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot, int j) {
-    const float* q = reinterpret_cast<const float*>(b.vin) + 12u * (fp.vin_base + slot) + 3 * j;
+    const float* q = b.vattr + 9u * (fp.vin_base + slot) + 3 * j;
     return F3{q[0], q[1], q[2]};
 }
 template <bool ONE = false>
@@ -175,7 +175,7 @@ __device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const 
     f.snap = rec_buf(b.snap, 16u, fp.nslots);
     f.vary = rec_buf(b.vary, (ONE && TRI_VARY36) ? 36u : 48u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
     f.src = f.vary;
-    if (ONE && obj_mode(fp)) f.src = rec_buf(b.vin + fp.vin_base, 48u, fp.nslots);
+    if (ONE && obj_mode(fp)) f.src = rec_buf(b.vattr + 9u * fp.vin_base, 36u, fp.nslots);
     f.shade = rec_buf(b.draw_shade, (uint32_t)sizeof(TriDrawShade), fp.ndraws);
     return f;
 }
@@ -678,7 +678,8 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
         const uint32_t sl = lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2);
         if (cfw && snap_oc(b, b.snap[sl], sl) == 0u) {  // not stored by k_vertex: world.w == 1
             F3 wv;
-            if (obj_mode(fp)) {  // k_vertex's world position, recomputed from the record (same operations)
+            if (!LPOS && obj_mode(fp)) {  // k_vertex's world position, from the record (same operations; never
+                                          // with the shadow pre-pass)
                 const F3 p = vin_attr(fp, b, sl, 0);
                 const float4 w = mat_vec_seq(fp.draw0.model, make_float4(p.x, p.y, p.z, 1.0f));
                 wv = F3{w.x, w.y, w.z};
@@ -746,7 +747,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
             const F3* v1 = reinterpret_cast<const F3*>(b.vary) + 3u * sl1;
             const F3* v2 = reinterpret_cast<const F3*>(b.vary) + 3u * sl2;
             F3* vo = reinterpret_cast<F3*>(b.vary) + 3u * (sbase + lane);
-            const bool obj = obj_mode(fp);
+            const bool obj = !LPOS && obj_mode(fp);
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
                 const F3 x = obj ? vin_attr(fp, b, sl0, j) : v0[j], y = obj ? vin_attr(fp, b, sl1, j) : v1[j],
@@ -1955,8 +1956,17 @@ __device__ __forceinline__ void exact_weights(const TriRec& r, int32_t px, int32
 // Shadow lookup (oracle shadow_visibility): the fraction of the 2x2 bilinear depth compare
 // (zref - bias <= map) that passes at light-NDC point (lx, ly, lz); 1 outside the map. IEEE mul/add in
 // the oracle's order (this file is compiled without contraction).
-__device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint32_t* smap, float lx, float ly, float lz) {
+// AMB: also report whether a perturbation of (lx, ly, lz) by a few ulps could change the result by more than a
+// proportional amount — a tap's depth compare within kVisEps of flipping, or the point within kVisEps of the
+// map's border (where the lookup jumps to 1). Elsewhere the fraction is continuous in the point (the bilinear
+// weights are, across texel boundaries too), so a nearby point gives a nearby value.
+constexpr float kVisEps = 1.0e-5f;
+template <bool AMB = false>
+__device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint32_t* smap, float lx, float ly, float lz,
+                                           bool* amb = nullptr) {
     const float u = lx * 0.5f + 0.5f, v = ly * 0.5f + 0.5f;
+    if (AMB)
+        *amb = fabsf(u) <= kVisEps || fabsf(u - 1.0f) <= kVisEps || fabsf(v) <= kVisEps || fabsf(v - 1.0f) <= kVisEps;
     if (!(u >= 0.0f && u <= 1.0f && v >= 0.0f && v <= 1.0f)) return 1.0f;
     const int32_t n = (int32_t)fp.s_size;
     const float fx = u * (float)n - 0.5f, fy = v * (float)n - 0.5f;
@@ -1966,10 +1976,15 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
     const float zref = lz - fp.s_bias;
     const int32_t ia = min(max(i0, 0), n - 1), ib = min(max(i0 + 1, 0), n - 1);
     const int32_t ja = min(max(j0, 0), n - 1), jb = min(max(j0 + 1, 0), n - 1);
-    const float c00 = zref <= __uint_as_float(smap[(size_t)ja * n + ia]) ? 1.0f : 0.0f;
-    const float c10 = zref <= __uint_as_float(smap[(size_t)ja * n + ib]) ? 1.0f : 0.0f;
-    const float c01 = zref <= __uint_as_float(smap[(size_t)jb * n + ia]) ? 1.0f : 0.0f;
-    const float c11 = zref <= __uint_as_float(smap[(size_t)jb * n + ib]) ? 1.0f : 0.0f;
+    const float m00 = __uint_as_float(smap[(size_t)ja * n + ia]), m10 = __uint_as_float(smap[(size_t)ja * n + ib]);
+    const float m01 = __uint_as_float(smap[(size_t)jb * n + ia]), m11 = __uint_as_float(smap[(size_t)jb * n + ib]);
+    if (AMB)
+        *amb = *amb || fabsf(zref - m00) <= kVisEps || fabsf(zref - m10) <= kVisEps || fabsf(zref - m01) <= kVisEps ||
+               fabsf(zref - m11) <= kVisEps;
+    const float c00 = zref <= m00 ? 1.0f : 0.0f;
+    const float c10 = zref <= m10 ? 1.0f : 0.0f;
+    const float c01 = zref <= m01 ? 1.0f : 0.0f;
+    const float c11 = zref <= m11 ? 1.0f : 0.0f;
     const float l0 = c00 + a * (c10 - c00), l1 = c01 + a * (c11 - c01);
     return l0 + bb * (l1 - l0);
 }
@@ -2111,6 +2126,18 @@ __device__ __forceinline__ float fragment_shadow_vis(const TriFrameParams& fp, c
 #ifndef TRI_SHADOW_VIS_PASS
 #define TRI_SHADOW_VIS_PASS 0
 #endif
+// The fast build's shadow instantiation:
+//  TRI_SHADOW_FAST_VIS: the lookup takes the fast weights, and only a lane whose lookup is ambiguous
+//    (shadow_vis<true>: a depth compare or the map border within kVisEps) recomputes it with the exact weights.
+//    Elsewhere the fraction is continuous in the light-space point, which the fast weights move by a few ulps.
+//  TRI_SHADOW_SHARED_WEIGHTS (default): the fragment shades with the exact weights the lookup needs (one computation).
+//  neither: both weights per fragment (round 3).
+#ifndef TRI_SHADOW_FAST_VIS
+#define TRI_SHADOW_FAST_VIS 0
+#endif
+#ifndef TRI_SHADOW_SHARED_WEIGHTS
+#define TRI_SHADOW_SHARED_WEIGHTS 1
+#endif
 
 // CLIPM: 0 = the key may name a clipped sub-triangle (tested per pixel), 1 = it never does (the shading loop
 // defers clipped pixels, TRI_CLIP_DEFER), 2 = it always does (the deferred pass). pre_vis: the fragment's sun
@@ -2155,7 +2182,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     const bool from_rec = CLIPM == 2 || (CLIPM == 0 && sub);
     const TriRec r = from_rec ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
     float w0, w1, w2;
-    if (EXACT) {  // exact int64 edge functions, IEEE divides (oracle order)
+    // exact int64 edge functions, IEEE divides (oracle order). The shadow lookup needs these weights in both
+    // builds (TRI_SHADOW_SHARED_WEIGHTS: the fast build shades with them too instead of forming its own)
+    if (EXACT || (kInlineVis && TRI_SHADOW_SHARED_WEIGHTS && !TRI_SHADOW_FAST_VIS)) {
         exact_weights(r, px, py, w0, w1, w2);
     } else if (TRI_SNAP_F && CLIPM == 1) {  // never clipped here: the floats of the snaps directly
         fast_weights_snaps(a0, a1, a2, px, py, w0, w1, w2);
@@ -2175,11 +2204,28 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     float vis = SHADOW ? pre_vis : 1.0f;
     if constexpr (kInlineVis) {  // light-space position at the pixel with the oracle's weights, then the compare
         float e0 = w0, e1 = w1, e2 = w2;
-        if (!EXACT && !(kAblate & 512)) exact_weights(r, px, py, e0, e1, e2);  // 512: fast weights (diagnostics)
-        auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
-            return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
-        };
-        vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
+        if (!EXACT && TRI_SHADOW_FAST_VIS) {
+            auto ixf = [&](uint32_t a, uint32_t bq, uint32_t c) {
+                return interp_exact(w0, w1, w2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
+            };
+            bool amb = false;
+            vis = shadow_vis<true>(fp, b.shadow_map, ixf(L0.x, L1.x, L2.x), ixf(L0.y, L1.y, L2.y),
+                                   ixf(L0.z, L1.z, L2.z), &amb);
+            if (amb) {  // rare: the oracle's weights decide this lane's lookup
+                exact_weights(r, px, py, e0, e1, e2);
+                auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
+                    return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
+                };
+                vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
+            }
+        } else {
+            if (!EXACT && !TRI_SHADOW_SHARED_WEIGHTS && !(kAblate & 512))  // 512: fast weights (diagnostics)
+                exact_weights(r, px, py, e0, e1, e2);
+            auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
+                return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
+            };
+            vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
+        }
     }
     put(19, vis);
     fetch_attrs<EXACT, ONE>(fp, fb, taps, d, w0, w1, w2, lut, put);

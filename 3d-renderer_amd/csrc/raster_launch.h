@@ -13,6 +13,7 @@
 struct TriDeviceBuffers {
     const TriVsIn* vin;
     const float* vpos;           // 12 B per vertex: the positions alone (k_vertex's only input with vary_obj)
+    const float* vattr;          // 36 B per vertex {pos, normal, colour}: the fragment stage's records with vary_obj
     const TriVsSkin* vskin;      // may be null when no draw skins
     const float* bones;
     uint64_t vertex_count;

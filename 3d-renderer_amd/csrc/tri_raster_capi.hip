@@ -76,6 +76,7 @@ struct tri_geometry {
     uint64_t version = 0;  // bumped by every upload (contexts re-resolve their draws)
     TriVsIn* d_vin = nullptr; size_t cap_vin = 0;
     float* d_pos = nullptr; size_t cap_pos = 0;  // 3 floats per vertex (k_vertex's stream with vary_obj)
+    float* d_attr = nullptr; size_t cap_attr = 0;  // 9 floats per vertex {pos, normal, colour} (k_raster's, vary_obj)
     TriVsSkin* d_skin = nullptr; size_t cap_skin = 0;
     bool has_skin_data = false;
     // every vertex has a finite position and a unit normal (|n|^2 within 1e-5 of 1): a draw over it may keep
@@ -677,13 +678,18 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
     g->obj_ok = obj_ok;
     if ((rc = grow(g->d_vin, g->cap_vin, std::max<uint64_t>(nv, 1)))) return rc;
     if (nv) HIP_TRY(hipMemcpy(g->d_vin, vin.data(), nv * sizeof(TriVsIn), hipMemcpyHostToDevice));
-    {
-        std::vector<float> pos(3 * nv);
+    {  // the object-space streams of vary_obj frames: positions (k_vertex) and 36-B attribute records (k_raster)
+        std::vector<float> pos(3 * nv), attr(9 * nv);
         for (uint64_t i = 0; i < nv; ++i) {
-            pos[3 * i] = vin[i].px; pos[3 * i + 1] = vin[i].py; pos[3 * i + 2] = vin[i].pz;
+            const TriVsIn& o = vin[i];
+            pos[3 * i] = o.px; pos[3 * i + 1] = o.py; pos[3 * i + 2] = o.pz;
+            const float a[9] = {o.px, o.py, o.pz, o.nx, o.ny, o.nz, o.cr, o.cg, o.cb};
+            std::memcpy(&attr[9 * i], a, sizeof a);
         }
         if ((rc = grow(g->d_pos, g->cap_pos, std::max<uint64_t>(3 * nv, 3)))) return rc;
+        if ((rc = grow(g->d_attr, g->cap_attr, std::max<uint64_t>(9 * nv, 9)))) return rc;
         if (nv) HIP_TRY(hipMemcpy(g->d_pos, pos.data(), nv * 12, hipMemcpyHostToDevice));
+        if (nv) HIP_TRY(hipMemcpy(g->d_attr, attr.data(), nv * 36, hipMemcpyHostToDevice));
     }
     if ((rc = grow(g->d_idx, g->cap_idx, std::max<uint64_t>(ni, 1)))) return rc;
     if (ni) HIP_TRY(hipMemcpy(g->d_idx, idx, ni * 4, hipMemcpyHostToDevice));
@@ -779,10 +785,10 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
 
 void free_geometry(tri_geometry& g) {
     auto f = [](void* p) { if (p) (void)hipFree(p); };
-    f(g.d_vin); f(g.d_pos); f(g.d_skin); f(g.d_idx); f(g.d_clusters); f(g.d_vbox);
-    g.d_vin = nullptr; g.d_pos = nullptr; g.d_skin = nullptr; g.d_idx = nullptr; g.d_clusters = nullptr;
-    g.d_vbox = nullptr;
-    g.cap_vin = g.cap_pos = g.cap_skin = g.cap_idx = g.cap_clusters = g.cap_vbox = 0;
+    f(g.d_vin); f(g.d_pos); f(g.d_attr); f(g.d_skin); f(g.d_idx); f(g.d_clusters); f(g.d_vbox);
+    g.d_vin = nullptr; g.d_pos = nullptr; g.d_attr = nullptr; g.d_skin = nullptr; g.d_idx = nullptr;
+    g.d_clusters = nullptr; g.d_vbox = nullptr;
+    g.cap_vin = g.cap_pos = g.cap_attr = g.cap_skin = g.cap_idx = g.cap_clusters = g.cap_vbox = 0;
 }
 
 }  // namespace
@@ -1262,6 +1268,7 @@ int tri_render(tri_ctx* c) {
     TriDeviceBuffers& b = ha.b;
     b.vin = c->geom->d_vin;
     b.vpos = c->geom->d_pos;
+    b.vattr = c->geom->d_attr;
     b.vskin = c->any_skin ? c->geom->d_skin : nullptr;
     b.bones = c->d_bones;
     b.vertex_count = c->geom->nverts;
