@@ -17,6 +17,7 @@
 // fragment stage has two builds: EXACT (IEEE div/sqrt/powf, the oracle's operation order) and the
 // default fast build (v_rcp/v_rsq/v_exp/v_log, hoisted frame constants), both within 1 LSB of the
 // oracle's UNORM8 output.
+#define TRI_KERNEL_TU 1  // device pointers in TriDeviceBuffers carry the global address space (raster_launch.h)
 #include "raster_launch.h"
 
 #include <hip/hip_runtime.h>
@@ -164,9 +165,10 @@ __device__ __forceinline__ bool obj_mode(const TriFrameParams& fp) { return TRI_
 struct F3 {
     float x, y, z;
 };
+__device__ __forceinline__ F3 ldF3(TRI_G const F3* p) { return F3{p->x, p->y, p->z}; }
 // Attribute j (0 position, 1 normal, 2 colour) of vertex record vin_base + slot, object space (vary_obj)
 __device__ __forceinline__ F3 vin_attr(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot, int j) {
-    const float* q = b.vattr + 9u * (fp.vin_base + slot) + 3 * j;
+    TRI_G const float* q = b.vattr + 9u * (fp.vin_base + slot) + 3 * j;
     return F3{q[0], q[1], q[2]};
 }
 template <bool ONE = false>
@@ -196,6 +198,26 @@ __device__ __forceinline__ int32_t snap_X(const TriSnap& s) {
 __device__ __forceinline__ int32_t snap_Y(const TriSnap& s) { return TRI_SNAP_F ? (int32_t)__int_as_float(s.y) : s.y; }
 __device__ __forceinline__ float snap_Xf(const TriSnap& s) { return TRI_SNAP_F ? __int_as_float(s.xo) : (float)snap_X(s); }
 __device__ __forceinline__ float snap_Yf(const TriSnap& s) { return TRI_SNAP_F ? __int_as_float(s.y) : (float)s.y; }
+// k_setup's gathers of a primitive's indices, snapped vertices and outcodes as buffer loads from wave-uniform
+// descriptors (TRI_SETUP_RSRC): a record index per lane, no 64-bit address arithmetic, one 12-B index load.
+#ifndef TRI_SETUP_RSRC
+#define TRI_SETUP_RSRC 1
+#endif
+struct SetupBufs {
+    RecBuf snap;
+    Rsrc oc;
+};
+__device__ __forceinline__ TriSnap setup_snap(const SetupBufs& sb, const TriDeviceBuffers& b, uint32_t slot) {
+    if (!TRI_SETUP_RSRC) return b.snap[slot];
+    const uint4 q = rec128<16>(sb.snap, slot, 0u);
+    return TriSnap{(int32_t)q.x, (int32_t)q.y, __uint_as_float(q.z), __uint_as_float(q.w)};
+}
+__device__ __forceinline__ uint32_t setup_oc(const SetupBufs& sb, const TriDeviceBuffers& b, const TriSnap& s,
+                                             uint32_t slot) {
+    if (!TRI_SNAP_F) return (uint32_t)s.xo >> 24;
+    if (!TRI_SETUP_RSRC) return (uint32_t)b.oc[slot];
+    return (uint32_t)__builtin_amdgcn_raw_buffer_load_b8(sb.oc, slot, 0, 0);
+}
 __device__ __forceinline__ uint32_t snap_oc(const TriDeviceBuffers& b, const TriSnap& s, uint32_t slot) {
     return TRI_SNAP_F ? (uint32_t)b.oc[slot] : (uint32_t)s.xo >> 24;
 }
@@ -344,7 +366,7 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
             if (bi < 0 || bi >= dr.bone_count) continue;
             const uint32_t buf = (uint32_t)(dr.bone_offset + bi);
             if (buf >= fp.bone_count) continue;
-            const float* bm = b.bones + 16ull * buf;
+            TRI_G const float* bm = b.bones + 16ull * buf;
 #pragma unroll
             for (int i = 0; i < 16; ++i) s[i] = s[i] + w * bm[i];
         }
@@ -365,7 +387,7 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
     const float v = (in.v * dr.tex_scale[1]) * dr.tiling + dr.tex_offset[1];
     store_snap(fp, b, slot, dr, world);
     if (vary36_mode(fp)) {  // 36-B record: three 12-B stores (the slot's bytes are 4-B aligned)
-        F3* vo = reinterpret_cast<F3*>(b.vary) + 3u * slot;
+        TRI_G F3* vo = reinterpret_cast<TRI_G F3*>(b.vary) + 3u * slot;
         vo[0] = F3{world.x, world.y, world.z};
         vo[1] = F3{nnx, nny, nnz};
         vo[2] = F3{in.cr, in.cg, in.cb};
@@ -439,9 +461,10 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TRI_FIRST_KARGS) {
     if (fp.cull_on) {  // uniform
         if (slot < fp.ncl_total) {  // this lane's (draw, cluster) flag
             const int cd = fp.one_draw ? 0 : find_range(b.draw_cbase, (int)fp.ndraws, slot);
-            const TriDrawDev& dr = fp.one_draw ? fp.draw0 : b.draws[cd];
             const uint32_t lc = slot - (fp.one_draw ? 0u : b.draw_cbase[cd]);
-            b.cvis[slot] = cluster_visible(fp, dr, b.clusters[dr.cl_first + lc]) ? 1u : 0u;
+            const bool vis = fp.one_draw ? cluster_visible(fp, fp.draw0, b.clusters[fp.draw0.cl_first + lc])
+                                         : cluster_visible(fp, b.draws[cd], b.clusters[b.draws[cd].cl_first + lc]);
+            b.cvis[slot] = vis ? 1u : 0u;
         }
         const uint32_t blk = (slot - vbase) / TRI_VBLOCK;
         uint64_t pending = __ballot(valid);
@@ -451,13 +474,16 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TRI_FIRST_KARGS) {
             const uint32_t gb = (uint32_t)__builtin_amdgcn_readlane((int)blk, l);
             const bool mine = valid && d == gd && blk == gb;
             pending &= ~__ballot(mine);
-            const TriDrawDev& dr = fp.one_draw ? fp.draw0 : b.draws[gd];
-            const bool any = cluster_visible(fp, dr, b.vbox[dr.vblk_first + gb]);
+            const bool any = fp.one_draw ? cluster_visible(fp, fp.draw0, b.vbox[fp.draw0.vblk_first + gb])
+                                         : cluster_visible(fp, b.draws[gd], b.vbox[b.draws[gd].vblk_first + gb]);
             if (mine) needed = any;
         }
     }
     if (!valid || (fp.cull_vertex && !needed)) return;
-    vertex_slot(fp, b, slot, fp.one_draw ? fp.draw0 : b.draws[d], vbase);
+    // two calls, not one through a selected reference: each sees its draw's address space (kernel arguments or
+    // global memory), so a single draw's constants are scalar loads
+    if (fp.one_draw) vertex_slot(fp, b, slot, fp.draw0, vbase);
+    else vertex_slot(fp, b, slot, b.draws[d], vbase);
 }
 
 // Row bands of single-draw frames (cull_vertex && one_draw): a quarter of k_vertex's workgroups, each owning
@@ -640,10 +666,16 @@ __device__ __forceinline__ float plane_dist(const TriFrameParams& fp, int plane,
     }
 }
 
-__device__ __forceinline__ void cv_store(float* p, const ClipVert& v) {
+// The polygons live in LDS: the pointers say so (a generic pointer would make every access a flat instruction)
+#if defined(__HIP_DEVICE_COMPILE__)
+#define TRI_LDS __attribute__((address_space(3)))
+#else
+#define TRI_LDS
+#endif
+__device__ __forceinline__ void cv_store(TRI_LDS float* p, const ClipVert& v) {
     p[0] = v.c.x; p[1] = v.c.y; p[2] = v.c.z; p[3] = v.c.w; p[4] = v.b0; p[5] = v.b1; p[6] = v.b2;
 }
-__device__ __forceinline__ ClipVert cv_load(const float* p) {
+__device__ __forceinline__ ClipVert cv_load(TRI_LDS const float* p) {
     ClipVert v;
     v.c = make_float4(p[0], p[1], p[2], p[3]);
     v.b0 = p[4]; v.b1 = p[5]; v.b2 = p[6];
@@ -667,12 +699,12 @@ __device__ __forceinline__ void wave_lds_sync() {
 // Clip primitive `prim` (vertex slots sl[3]) with the whole wave; lanes that set up a fan
 // sub-triangle bin it. Must be reached by the whole wave.
 template <bool LPOS>
-__device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const TriDeviceBuffers& b, float* poly,
+__device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const TriDeviceBuffers& b, TRI_LDS float* poly,
                                                uint32_t prim, uint32_t sl0, uint32_t sl1, uint32_t sl2, bool cfw,
                                                uint32_t& nsetup, uint32_t& nentries) {
     const uint32_t lane = lanes_below(~0ull);
     const uint64_t below = (lane == 63) ? 0x7FFFFFFFFFFFFFFFull : ((1ull << lane) - 1ull);
-    float* buf[2] = {poly, poly + TRI_MAX_CLIP_VERTS * kClipStride};
+    TRI_LDS float* buf[2] = {poly, poly + TRI_MAX_CLIP_VERTS * kClipStride};
     if (lane < 3) {
         ClipVert v;
         const uint32_t sl = lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2);
@@ -684,7 +716,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
                 const float4 w = mat_vec_seq(fp.draw0.model, make_float4(p.x, p.y, p.z, 1.0f));
                 wv = F3{w.x, w.y, w.z};
             } else {
-                wv = vary36_mode(fp) ? reinterpret_cast<const F3*>(b.vary)[3u * sl]
+                wv = vary36_mode(fp) ? ldF3(reinterpret_cast<TRI_G const F3*>(b.vary) + 3u * sl)
                                      : F3{b.vary[3u * sl].x, b.vary[3u * sl].y, b.vary[3u * sl].z};
             }
             v.c = mat_vec_seq(fp.pv, make_float4(wv.x, wv.y, wv.z, 1.0f));
@@ -739,19 +771,19 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
         return;
     }
     const uint32_t sbase = fp.nslots + vbase;
-    const float* src = buf[cur];
+    TRI_LDS const float* src = buf[cur];
     if ((int)lane < n) {  // varyings of polygon vertex `lane` from the source triangle's barycentrics
         const ClipVert s = cv_load(src + lane * kClipStride);
         if (vary36_mode(fp)) {  // (object-space attributes from the vertex records with vary_obj)
-            const F3* v0 = reinterpret_cast<const F3*>(b.vary) + 3u * sl0;
-            const F3* v1 = reinterpret_cast<const F3*>(b.vary) + 3u * sl1;
-            const F3* v2 = reinterpret_cast<const F3*>(b.vary) + 3u * sl2;
-            F3* vo = reinterpret_cast<F3*>(b.vary) + 3u * (sbase + lane);
+            TRI_G const F3* v0 = reinterpret_cast<TRI_G const F3*>(b.vary) + 3u * sl0;
+            TRI_G const F3* v1 = reinterpret_cast<TRI_G const F3*>(b.vary) + 3u * sl1;
+            TRI_G const F3* v2 = reinterpret_cast<TRI_G const F3*>(b.vary) + 3u * sl2;
+            TRI_G F3* vo = reinterpret_cast<TRI_G F3*>(b.vary) + 3u * (sbase + lane);
             const bool obj = !LPOS && obj_mode(fp);
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
-                const F3 x = obj ? vin_attr(fp, b, sl0, j) : v0[j], y = obj ? vin_attr(fp, b, sl1, j) : v1[j],
-                         z = obj ? vin_attr(fp, b, sl2, j) : v2[j];
+                const F3 x = obj ? vin_attr(fp, b, sl0, j) : ldF3(v0 + j), y = obj ? vin_attr(fp, b, sl1, j) : ldF3(v1 + j),
+                         z = obj ? vin_attr(fp, b, sl2, j) : ldF3(v2 + j);
                 vo[j] = F3{(s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
                            (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z};
             }
@@ -990,8 +1022,15 @@ __device__ __forceinline__ void bin_pair_box(const TriDeviceBuffers& b, BinBox& 
 // ONE: a single-draw frame (fp.one_draw known set: the draw search, LDS staging and prim_vs records compile
 // away)
 template <bool WITH_SHADOW, bool ONE>
+// TRI_SETUP_PRIO: k_setup's waves at a raised issue priority (s_setprio). With two frames in flight the set-up of
+// one frame shares the CUs with the other's raster; its waves are latency chains that hold registers and LDS
+// while they wait, so finishing each chain sooner returns those resources to the raster sooner.
+#ifndef TRI_SETUP_PRIO
+#define TRI_SETUP_PRIO 0
+#endif
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TRI_KARGS) {
     TRI_BIND_ARGS;
+    if constexpr (TRI_SETUP_PRIO > 0) __builtin_amdgcn_s_setprio(TRI_SETUP_PRIO);
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     // Frames with a few draws: each draw's primitive base, first index, slot offset and cluster base
@@ -1050,6 +1089,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     __syncthreads();
     uint32_t nsetup = 0, nentries = 0, sentries = 0;
     const uint32_t lane = lanes_below(~0ull);
+    const SetupBufs sbuf{rec_buf(b.snap, 16u, fp.nslots), make_rsrc(b.oc, fp.nslots)};
+    const RecBuf ibuf = rec_buf(b.indices + fp.draw0.first_index, 12u, fp.nprims);  // single-draw frames
     uint32_t round_base = 0;  // binning rounds so far (the bin box alternates its two halves per round)
     for (uint32_t ci = 0; ci < (multi ? (uint32_t)(TRI_BLOCK / 64) : 1u); ++ci) {
     if (multi && !chunk_vis[ci]) continue;  // uniform
@@ -1083,9 +1124,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
                 // visible primitives skip one dependent load (a culled one wastes 12 bytes)
                 const uint32_t* ip;
                 if (ONE || fp.one_draw) {  // kernel-argument constants: the index fetch starts at once
-                    ip = b.indices + fp.draw0.first_index + 3u * p[t];
                     vb = 0u - fp.draw0.min_index;
-                    i0 = ip[0]; i1 = ip[1]; i2 = ip[2];
+                    if (TRI_SETUP_RSRC) {
+                        const u32x3v q = rec96<12>(ibuf, p[t], 0u);
+                        i0 = q[0]; i1 = q[1]; i2 = q[2];
+                    } else {
+                        ip = b.indices + fp.draw0.first_index + 3u * p[t];
+                        i0 = ip[0]; i1 = ip[1]; i2 = ip[2];
+                    }
                     if (fp.cull_on) culled = !b.cvis[p[t] / TRI_CLUSTER_PRIMS];
                 } else if (lds_draws) {
                     d = find_range_lds(dpb, (int)fp.ndraws, p[t]);
@@ -1108,8 +1154,10 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             if (p[t] < fp.nprims && (!culled || WITH_SHADOW)) {
                 sl0[t] = vb + i0; sl1[t] = vb + i1; sl2[t] = vb + i2;
                 if (!culled) {
-                    const TriSnap a0 = b.snap[sl0[t]], a1 = b.snap[sl1[t]], a2 = b.snap[sl2[t]];
-                    const uint32_t oc0 = snap_oc(b, a0, sl0[t]), oc1 = snap_oc(b, a1, sl1[t]), oc2 = snap_oc(b, a2, sl2[t]);
+                    const TriSnap a0 = setup_snap(sbuf, b, sl0[t]), a1 = setup_snap(sbuf, b, sl1[t]),
+                                  a2 = setup_snap(sbuf, b, sl2[t]);
+                    const uint32_t oc0 = setup_oc(sbuf, b, a0, sl0[t]), oc1 = setup_oc(sbuf, b, a1, sl1[t]),
+                                   oc2 = setup_oc(sbuf, b, a2, sl2[t]);
                     // invalid vertex, or trivial reject: all three vertices outside one clip half-space
                     if (!((oc0 | oc1 | oc2) & TRI_OC_BAD) && !(oc0 & oc1 & oc2 & TRI_OC_REJECT)) {
                         if ((oc0 | oc1 | oc2) & TRI_OC_CLIP) {
@@ -1146,7 +1194,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
             uint64_t cm = __ballot(needs_clip[t]);  // rare: the wave clips its primitives one at a time
             if (cm) {
                 if (lane == 0) atomicAdd(&b.counters->tris_clipped, (uint32_t)__builtin_popcountll(cm));
-                float* poly = clip_poly[threadIdx.x >> 6];
+                TRI_LDS float* poly = (TRI_LDS float*)clip_poly[threadIdx.x >> 6];
                 while (cm) {
                     const int src = __builtin_ctzll(cm);
                     cm &= cm - 1;
@@ -1513,8 +1561,9 @@ __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, floa
     const float a = u - fu, bb = v - fv;
     const uint32_t x0 = wrap_repeat(fu, t.w), y0 = wrap_repeat(fv, t.h);
     const uint32_t x1 = (x0 + 1 == t.w) ? 0u : x0 + 1, y1 = (y0 + 1 == t.h) ? 0u : y0 + 1;
-    const uint32_t p00 = t.texels[y0 * t.w + x0], p10 = t.texels[y0 * t.w + x1];
-    const uint32_t p01 = t.texels[y1 * t.w + x0], p11 = t.texels[y1 * t.w + x1];
+    TRI_G const uint32_t* tx = (TRI_G const uint32_t*)t.texels;  // device texture memory (global loads)
+    const uint32_t p00 = tx[y0 * t.w + x0], p10 = tx[y0 * t.w + x1];
+    const uint32_t p01 = tx[y1 * t.w + x0], p11 = tx[y1 * t.w + x1];
     float4 r;
     float* rp = &r.x;
 #pragma unroll

@@ -10,45 +10,58 @@
 #endif
 #define TRI_SETUP_WGS_PER_CU TRI_SETUP_WAVES
 
+// Device pointers in the global address space (device compilation only; the host sees plain pointers of the same
+// size). The later kernels of a frame read these pointers from the device copy of their arguments, not from
+// kernel-argument memory, so without the qualifier the compiler cannot tell them from LDS pointers: every access
+// became a flat instruction, which counts against the LDS wait counter too (a wait for an LDS result then also
+// waits for every outstanding memory load).
+// (Only in the kernels' translation units, TRI_KERNEL_TU: host code elsewhere fills the struct with plain pointers,
+// and the device pass of a host-only file still type-checks those assignments.)
+#if defined(__HIP_DEVICE_COMPILE__) && defined(TRI_KERNEL_TU)
+#define TRI_G __attribute__((address_space(1)))
+#else
+#define TRI_G
+#endif
+
 struct TriDeviceBuffers {
-    const TriVsIn* vin;
-    const float* vpos;           // 12 B per vertex: the positions alone (k_vertex's only input with vary_obj)
-    const float* vattr;          // 36 B per vertex {pos, normal, colour}: the fragment stage's records with vary_obj
-    const TriVsSkin* vskin;      // may be null when no draw skins
-    const float* bones;
+    TRI_G const TriVsIn* vin;
+    TRI_G const float* vpos;           // 12 B per vertex: the positions alone (k_vertex's only input with vary_obj)
+    TRI_G const float* vattr;          // 36 B per vertex {pos, normal, colour}: the fragment stage's records with vary_obj
+    TRI_G const TriVsSkin* vskin;      // may be null when no draw skins
+    TRI_G const float* bones;
     uint64_t vertex_count;
-    const uint32_t* indices;
-    const TriDrawDev* draws;
-    const TriDrawShade* draw_shade;
-    const uint32_t* draw_vbase;  // ndraws+1
-    const uint32_t* draw_pbase;  // ndraws+1
-    const uint32_t* sky;         // 6 * sky_size^2 RGBA8 sRGB texels (+X,-X,+Y,-Y,+Z,-Z)
-    const float* srgb_lut;       // 256 sRGB -> linear (host, double) + 256 alpha b/255
-    float4* clip;                // nslots (read only when a primitive is clipped)
-    TriSnap* snap;               // nslots (TRI_SNAP_F: {X, Y as exact floats, 1/w, z})
-    uint8_t* oc;                 // nslots outcodes (TRI_SNAP_F; otherwise they ride in snap's X word)
-    float4* vary;                // 3 * (nslots + ovf_vert_cap)
-    TriRec* recs;                // ovf_rec_cap clipped sub-triangles
-    uint32_t* clip_slot;         // nprims: first sub-triangle record of a clipped primitive
-    uint4* prim_vs;              // nprims: {vertex slot 0, 1, 2, draw | TRI_PRIM_CLIPPED} of every
+    TRI_G const uint32_t* indices;
+    TRI_G const TriDrawDev* draws;
+    TRI_G const TriDrawShade* draw_shade;
+    TRI_G const uint32_t* draw_vbase;  // ndraws+1
+    TRI_G const uint32_t* draw_pbase;  // ndraws+1
+    TRI_G const uint32_t* sky;         // 6 * sky_size^2 RGBA8 sRGB texels (+X,-X,+Y,-Y,+Z,-Z)
+    TRI_G const float* srgb_lut;       // 256 sRGB -> linear (host, double) + 256 alpha b/255
+    TRI_G float4* clip;                // nslots (read only when a primitive is clipped)
+    TRI_G TriSnap* snap;               // nslots (TRI_SNAP_F: {X, Y as exact floats, 1/w, z})
+    TRI_G uint8_t* oc;                 // nslots outcodes (TRI_SNAP_F; otherwise they ride in snap's X word)
+    TRI_G float4* vary;                // 3 * (nslots + ovf_vert_cap)
+    TRI_G TriRec* recs;                // ovf_rec_cap clipped sub-triangles
+    TRI_G uint32_t* clip_slot;         // nprims: first sub-triangle record of a clipped primitive
+    TRI_G uint4* prim_vs;              // nprims: {vertex slot 0, 1, 2, draw | TRI_PRIM_CLIPPED} of every
                                  // primitive k_setup passed on (visible or clipped)
-    uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
-    uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)
-    TriCounters* counters;
-    uint2* setup_stats;          // nchunks {triangles set up, bin entries} per k_setup workgroup
-    uint32_t* color;             // band rows * W
-    float* depth;                // band rows * W (may be null)
+    TRI_G uint32_t* bin_count;         // nbins entry counters (zero between frames: k_raster re-zeroes)
+    TRI_G uint32_t* bin_list;          // nbins * bin_cap record ids (fixed-capacity queue per bin)
+    TRI_G TriCounters* counters;
+    TRI_G uint2* setup_stats;          // nchunks {triangles set up, bin entries} per k_setup workgroup
+    TRI_G uint32_t* color;             // band rows * W
+    TRI_G float* depth;                // band rows * W (may be null)
     // cluster culling (only when TriFrameParams::cull_on)
-    const TriCluster* clusters;  // all meshes' clusters
-    const TriCluster* vbox;      // per mesh vertex block: the union box of the clusters referencing it
-    const uint32_t* draw_cbase;  // ndraws+1: first (draw, cluster) pair of each draw
-    uint32_t* cvis;              // ncl_total visibility flags, written by k_vertex each frame
+    TRI_G const TriCluster* clusters;  // all meshes' clusters
+    TRI_G const TriCluster* vbox;      // per mesh vertex block: the union box of the clusters referencing it
+    TRI_G const uint32_t* draw_cbase;  // ndraws+1: first (draw, cluster) pair of each draw
+    TRI_G uint32_t* cvis;              // ncl_total visibility flags, written by k_vertex each frame
     // shadow-map pre-pass (only when TriFrameParams::shadow_on)
-    float4* lpos;                // nslots + ovf_vert_cap: light-NDC position per vertex slot (xyz, 0)
-    TriSnap* lsnap;              // nslots: the light-NDC position snapped to the map ({X | outcode << 24, Y, 1, z})
-    uint32_t* sbin_count;        // s_nbins shadow-map bin counters (zeroed by k_shadow_raster)
-    uint32_t* sbin_list;         // s_nbins * s_bin_cap primitive ids
-    uint32_t* shadow_map;        // s_size * s_size float32 depth bits
+    TRI_G float4* lpos;                // nslots + ovf_vert_cap: light-NDC position per vertex slot (xyz, 0)
+    TRI_G TriSnap* lsnap;              // nslots: the light-NDC position snapped to the map ({X | outcode << 24, Y, 1, z})
+    TRI_G uint32_t* sbin_count;        // s_nbins shadow-map bin counters (zeroed by k_shadow_raster)
+    TRI_G uint32_t* sbin_list;         // s_nbins * s_bin_cap primitive ids
+    TRI_G uint32_t* shadow_map;        // s_size * s_size float32 depth bits
 };
 
 // One frame's arguments (DESIGN.md §2 "launch cost"). The frame's first kernel (k_vertex, k_vertex_band or
