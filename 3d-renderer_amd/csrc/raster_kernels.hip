@@ -1021,16 +1021,10 @@ __device__ __forceinline__ void bin_pair_box(const TriDeviceBuffers& b, BinBox& 
 // positions. A separate instantiation keeps that code, and its registers, out of other frames.
 // ONE: a single-draw frame (fp.one_draw known set: the draw search, LDS staging and prim_vs records compile
 // away)
+// One set-up workgroup: chunk workgroup `bid` of `nblk`.
 template <bool WITH_SHADOW, bool ONE>
-// TRI_SETUP_PRIO: k_setup's waves at a raised issue priority (s_setprio). With two frames in flight the set-up of
-// one frame shares the CUs with the other's raster; its waves are latency chains that hold registers and LDS
-// while they wait, so finishing each chain sooner returns those resources to the raster sooner.
-#ifndef TRI_SETUP_PRIO
-#define TRI_SETUP_PRIO 0
-#endif
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TRI_KARGS) {
-    TRI_BIND_ARGS;
-    if constexpr (TRI_SETUP_PRIO > 0) __builtin_amdgcn_s_setprio(TRI_SETUP_PRIO);
+__device__ __forceinline__ void setup_body(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t bid,
+                                           uint32_t nblk) {
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     // Frames with a few draws: each draw's primitive base, first index, slot offset and cluster base
@@ -1040,7 +1034,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     const bool lds_draws = !ONE && !fp.one_draw && fp.ndraws <= (uint32_t)kLdsDraws;
     __shared__ BinBox bin_box;
     // Row bands of single-draw frames (fp.setup_multi): a quarter of the chunks' workgroups, each owning the
-    // four chunks blockIdx.x + i * gridDim.x. Wave i reads chunk i's cluster flags, and the workgroup sets up
+    // four chunks bid + i * nblk. Wave i reads chunk i's cluster flags, and the workgroup sets up
     // and bins the visible ones in turn (a band's visible chunks are contiguous, so the stride gives each
     // workgroup at most one at N = 8, and 3/4 of the launch's mostly empty dispatches are gone).
     __shared__ uint32_t chunk_vis[TRI_BLOCK / 64];
@@ -1054,7 +1048,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     };
     if constexpr (ONE && !WITH_SHADOW) {
         if (multi) {
-            const uint32_t w = threadIdx.x / 64u, ck = blockIdx.x + w * gridDim.x;
+            const uint32_t w = threadIdx.x / 64u, ck = bid + w * nblk;
             const bool vis = ck < fp.nchunks && chunk_visible(ck);
             if ((threadIdx.x & 63u) == 0) chunk_vis[w] = vis ? 1u : 0u;
             __syncthreads();
@@ -1062,14 +1056,14 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
 #pragma unroll
             for (int i = 0; i < TRI_BLOCK / 64; ++i) any = any || chunk_vis[i] != 0u;
             if (!any) {
-                if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(0u, 0u);
+                if (threadIdx.x == 0) b.setup_stats[bid] = make_uint2(0u, 0u);
                 return;
             }
         } else if (fp.cull_on) {
             // A row band's chunk whose clusters k_vertex culled (most chunks at N = 8): the whole workgroup
             // leaves before the LDS set-up and the binning barriers (its cluster flags: a few scalar loads)
-            if (!chunk_visible((uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks))) {
-                if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(0u, 0u);
+            if (!chunk_visible((uint32_t)(((uint64_t)bid * fp.chunk_stride) % fp.nchunks))) {
+                if (threadIdx.x == 0) b.setup_stats[bid] = make_uint2(0u, 0u);
                 return;
             }
         }
@@ -1097,7 +1091,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     // Spread concurrently running workgroups over the primitive stream: meshes are usually
     // index-ordered in screen space, and neighbouring chunks hammering the same bin counters
     // serialise their atomics. The stride is coprime to nchunks, so the remap is a bijection.
-    const uint32_t chunk = multi ? blockIdx.x + ci * gridDim.x : (uint32_t)(((uint64_t)blockIdx.x * fp.chunk_stride) % fp.nchunks);
+    const uint32_t chunk = multi ? bid + ci * nblk : (uint32_t)(((uint64_t)bid * fp.chunk_stride) % fp.nchunks);
     const uint32_t chunk0 = chunk * (uint32_t)(TRI_BLOCK * fp.ppt);
     // Two primitives per lane, set up and binned together: both index/vertex fetch chains are in
     // flight at once, and the queue reservations of both are batched (one atomic round trip per
@@ -1222,9 +1216,16 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_S
     __syncthreads();
     // Statistics go to a per-workgroup slot with a plain store: same-address global atomics from
     // every workgroup serialise across the XCDs (measured: +34 us per frame at 4K/1M).
-    if (threadIdx.x == 0) b.setup_stats[blockIdx.x] = make_uint2(red[0], red[1]);
+    if (threadIdx.x == 0) b.setup_stats[bid] = make_uint2(red[0], red[1]);
     TRI_SSTAMP(3);
 }
+
+template <bool WITH_SHADOW, bool ONE>
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TRI_KARGS) {
+    TRI_BIND_ARGS;
+    setup_body<WITH_SHADOW, ONE>(fp, b, blockIdx.x, gridDim.x);
+}
+
 
 // ------------------------------------------------------------------------------------------
 // tile_raster_shade: coverage
@@ -2005,17 +2006,8 @@ __device__ __forceinline__ void exact_weights(const TriRec& r, int32_t px, int32
 // Shadow lookup (oracle shadow_visibility): the fraction of the 2x2 bilinear depth compare
 // (zref - bias <= map) that passes at light-NDC point (lx, ly, lz); 1 outside the map. IEEE mul/add in
 // the oracle's order (this file is compiled without contraction).
-// AMB: also report whether a perturbation of (lx, ly, lz) by a few ulps could change the result by more than a
-// proportional amount — a tap's depth compare within kVisEps of flipping, or the point within kVisEps of the
-// map's border (where the lookup jumps to 1). Elsewhere the fraction is continuous in the point (the bilinear
-// weights are, across texel boundaries too), so a nearby point gives a nearby value.
-constexpr float kVisEps = 1.0e-5f;
-template <bool AMB = false>
-__device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint32_t* smap, float lx, float ly, float lz,
-                                           bool* amb = nullptr) {
+__device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint32_t* smap, float lx, float ly, float lz) {
     const float u = lx * 0.5f + 0.5f, v = ly * 0.5f + 0.5f;
-    if (AMB)
-        *amb = fabsf(u) <= kVisEps || fabsf(u - 1.0f) <= kVisEps || fabsf(v) <= kVisEps || fabsf(v - 1.0f) <= kVisEps;
     if (!(u >= 0.0f && u <= 1.0f && v >= 0.0f && v <= 1.0f)) return 1.0f;
     const int32_t n = (int32_t)fp.s_size;
     const float fx = u * (float)n - 0.5f, fy = v * (float)n - 0.5f;
@@ -2027,9 +2019,6 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
     const int32_t ja = min(max(j0, 0), n - 1), jb = min(max(j0 + 1, 0), n - 1);
     const float m00 = __uint_as_float(smap[(size_t)ja * n + ia]), m10 = __uint_as_float(smap[(size_t)ja * n + ib]);
     const float m01 = __uint_as_float(smap[(size_t)jb * n + ia]), m11 = __uint_as_float(smap[(size_t)jb * n + ib]);
-    if (AMB)
-        *amb = *amb || fabsf(zref - m00) <= kVisEps || fabsf(zref - m10) <= kVisEps || fabsf(zref - m01) <= kVisEps ||
-               fabsf(zref - m11) <= kVisEps;
     const float c00 = zref <= m00 ? 1.0f : 0.0f;
     const float c10 = zref <= m10 ? 1.0f : 0.0f;
     const float c01 = zref <= m01 ? 1.0f : 0.0f;
@@ -2175,15 +2164,10 @@ __device__ __forceinline__ float fragment_shadow_vis(const TriFrameParams& fp, c
 #ifndef TRI_SHADOW_VIS_PASS
 #define TRI_SHADOW_VIS_PASS 0
 #endif
-// The fast build's shadow instantiation:
-//  TRI_SHADOW_FAST_VIS: the lookup takes the fast weights, and only a lane whose lookup is ambiguous
-//    (shadow_vis<true>: a depth compare or the map border within kVisEps) recomputes it with the exact weights.
-//    Elsewhere the fraction is continuous in the light-space point, which the fast weights move by a few ulps.
-//  TRI_SHADOW_SHARED_WEIGHTS (default): the fragment shades with the exact weights the lookup needs (one computation).
-//  neither: both weights per fragment (round 3).
-#ifndef TRI_SHADOW_FAST_VIS
-#define TRI_SHADOW_FAST_VIS 0
-#endif
+// The fast build's shadow instantiation shades with the exact weights its lookup needs (TRI_SHADOW_SHARED_WEIGHTS:
+// one weight computation per fragment instead of two; C5 +1 % over both). Rejected (round 4): the lookup from
+// the fast weights, recomputed with the exact ones only where a depth compare or the map border is within a few
+// ulps: the fallback's registers cost 5 spilled VGPRs and C5 -3 %.
 #ifndef TRI_SHADOW_SHARED_WEIGHTS
 #define TRI_SHADOW_SHARED_WEIGHTS 1
 #endif
@@ -2233,7 +2217,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     float w0, w1, w2;
     // exact int64 edge functions, IEEE divides (oracle order). The shadow lookup needs these weights in both
     // builds (TRI_SHADOW_SHARED_WEIGHTS: the fast build shades with them too instead of forming its own)
-    if (EXACT || (kInlineVis && TRI_SHADOW_SHARED_WEIGHTS && !TRI_SHADOW_FAST_VIS)) {
+    if (EXACT || (kInlineVis && TRI_SHADOW_SHARED_WEIGHTS)) {
         exact_weights(r, px, py, w0, w1, w2);
     } else if (TRI_SNAP_F && CLIPM == 1) {  // never clipped here: the floats of the snaps directly
         fast_weights_snaps(a0, a1, a2, px, py, w0, w1, w2);
@@ -2253,28 +2237,12 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     float vis = SHADOW ? pre_vis : 1.0f;
     if constexpr (kInlineVis) {  // light-space position at the pixel with the oracle's weights, then the compare
         float e0 = w0, e1 = w1, e2 = w2;
-        if (!EXACT && TRI_SHADOW_FAST_VIS) {
-            auto ixf = [&](uint32_t a, uint32_t bq, uint32_t c) {
-                return interp_exact(w0, w1, w2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
-            };
-            bool amb = false;
-            vis = shadow_vis<true>(fp, b.shadow_map, ixf(L0.x, L1.x, L2.x), ixf(L0.y, L1.y, L2.y),
-                                   ixf(L0.z, L1.z, L2.z), &amb);
-            if (amb) {  // rare: the oracle's weights decide this lane's lookup
-                exact_weights(r, px, py, e0, e1, e2);
-                auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
-                    return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
-                };
-                vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
-            }
-        } else {
-            if (!EXACT && !TRI_SHADOW_SHARED_WEIGHTS && !(kAblate & 512))  // 512: fast weights (diagnostics)
-                exact_weights(r, px, py, e0, e1, e2);
-            auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
-                return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
-            };
-            vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
-        }
+        if (!EXACT && !TRI_SHADOW_SHARED_WEIGHTS && !(kAblate & 512))  // 512: fast weights (diagnostics)
+            exact_weights(r, px, py, e0, e1, e2);
+        auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
+            return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
+        };
+        vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
     }
     put(19, vis);
     fetch_attrs<EXACT, ONE>(fp, fb, taps, d, w0, w1, w2, lut, put);

@@ -17,3 +17,4 @@ for r in csv.DictReader(open('$f')):
     if any(k in r['Name'] for k in ('k_vertex','k_setup','k_raster','k_reset')): print('  %-60s %8s calls avg %8.2f us' % (r['Name'][:60], r['Calls'], float(r['AverageNs'])/1e3))"
 done
 bash tools/ab.sh $ab "" $ab ""
+timeout -k 10 120 python tools/host_overhead.py c2 > gpurun_out/host_c2.txt 2>&1 && timeout -k 10 120 python tools/host_overhead.py c3 > gpurun_out/host_c3.txt 2>&1; cat gpurun_out/host_c2.txt gpurun_out/host_c3.txt
