@@ -150,6 +150,8 @@ __device__ __forceinline__ u32x3v rec96(const RecBuf& b, uint32_t i, uint32_t of
 // vertex attributes: the varyings, or with vary_obj the draw's own 36-B object-space records (vattr).
 struct FetchBufs {
     RecBuf snap, vary, src, shade;
+    const void* shade_base;  // the shade records for scalar loads (load_shade)
+    uint32_t shade_bytes;
 };
 // The varying record: 48 B {world, u}{N, v}{colour, 0}, or 36 B {world}{N}{colour} on single-draw solid frames
 // (TriFrameParams::vary36 — exactly the frames k_raster_plain<.., ONE> shades). TRI_VARY36 = 0 keeps 48 B.
@@ -159,6 +161,13 @@ struct FetchBufs {
 #endif
 #ifndef TRI_VARY_OBJ
 #define TRI_VARY_OBJ 1
+#endif
+// TRI_LPOS_WORLD: with the shadow pre-pass, the light-space vertex positions come from the world positions in the
+// varyings (k_vertex's own operations on the same floats, so the same bits) instead of a stored lpos per vertex
+// slot: no lpos stores in k_vertex, three 16-B gathers fewer per fragment (fp.lpos_world: every draw affine and
+// unskinned, so world.w == 1 as k_vertex used it). The clipper's polygon vertices keep stored, interpolated ones.
+#ifndef TRI_LPOS_WORLD
+#define TRI_LPOS_WORLD 1
 #endif
 __device__ __forceinline__ bool vary36_mode(const TriFrameParams& fp) { return TRI_VARY36 && fp.vary36; }
 __device__ __forceinline__ bool obj_mode(const TriFrameParams& fp) { return TRI_VARY36 && TRI_VARY_OBJ && fp.vary_obj; }
@@ -179,6 +188,8 @@ __device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const 
     f.src = f.vary;
     if (ONE && obj_mode(fp)) f.src = rec_buf(b.vattr + 9u * fp.vin_base, 36u, fp.nslots);
     f.shade = rec_buf(b.draw_shade, (uint32_t)sizeof(TriDrawShade), fp.ndraws);
+    f.shade_base = (const void*)b.draw_shade;
+    f.shade_bytes = (uint32_t)sizeof(TriDrawShade) * fp.ndraws;
     return f;
 }
 __device__ __forceinline__ TriSnap ld_snap(const FetchBufs& fb, uint32_t slot) {
@@ -266,7 +277,8 @@ __device__ __forceinline__ uint32_t outcode(const TriFrameParams& fp, float4 c);
 __device__ __forceinline__ void shadow_vertex(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
                                               float4 world) {
     const float4 l = mat_vec_seq(fp.lvp, world);
-    b.lpos[slot] = make_float4(l.x, l.y, l.z, 0.0f);
+    // with lpos_world the readers recompute it from the world position in the varyings (same operations)
+    if (!(TRI_LPOS_WORLD && fp.lpos_world)) b.lpos[slot] = make_float4(l.x, l.y, l.z, 0.0f);
     uint32_t oc = 0;
     if (l.x + 1.0f < 0.0f) oc |= TRI_OC_XNEG;
     if (1.0f - l.x < 0.0f) oc |= TRI_OC_XPOS;
@@ -800,7 +812,14 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
             }
         }
         if constexpr (LPOS) {  // shadow pre-pass on: the polygon vertex's light-space position, same weights
-            const float4 x = b.lpos[sl0], y = b.lpos[sl1], z = b.lpos[sl2];
+            auto lp = [&](uint32_t sl) {  // (see shadow_vertex: not stored with lpos_world)
+                if (TRI_LPOS_WORLD && fp.lpos_world) {
+                    const float4 w = b.vary[3u * sl];
+                    return mat_vec_seq(fp.lvp, make_float4(w.x, w.y, w.z, 1.0f));
+                }
+                return b.lpos[sl];
+            };
+            const float4 x = lp(sl0), y = lp(sl1), z = lp(sl2);
             b.lpos[sbase + lane] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x,
                                                (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
                                                (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, 0.0f);
@@ -1552,6 +1571,15 @@ __device__ __forceinline__ uint32_t wrap_repeat(float f, uint32_t n) {  // REPEA
     return (uint32_t)r;
 }
 
+// TRI_TEXEL_PAIRS / TRI_MAP_PAIRS: the bilinear footprint of a texture / the shadow map as two 8-B row loads
+// instead of four 4-B gathers (C5's fragment stage is bound by the texture units' data return, which costs per
+// load instruction)
+#ifndef TRI_TEXEL_PAIRS
+#define TRI_TEXEL_PAIRS 1
+#endif
+#ifndef TRI_MAP_PAIRS
+#define TRI_MAP_PAIRS 1
+#endif
 // texture(): R8G8B8A8_SRGB decode before LINEAR filtering, REPEAT, level 0 (Renderer.cpp:3592-3607)
 __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, float v0, const float* lut) {
     if (t.w == 1 && t.h == 1)  // 1x1 (the default white slot): all four taps are texel (0,0)
@@ -1563,8 +1591,17 @@ __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, floa
     const uint32_t x0 = wrap_repeat(fu, t.w), y0 = wrap_repeat(fv, t.h);
     const uint32_t x1 = (x0 + 1 == t.w) ? 0u : x0 + 1, y1 = (y0 + 1 == t.h) ? 0u : y0 + 1;
     TRI_G const uint32_t* tx = (TRI_G const uint32_t*)t.texels;  // device texture memory (global loads)
-    const uint32_t p00 = tx[y0 * t.w + x0], p10 = tx[y0 * t.w + x1];
-    const uint32_t p01 = tx[y1 * t.w + x0], p11 = tx[y1 * t.w + x1];
+    uint32_t p00, p10, p01, p11;
+    if (TRI_TEXEL_PAIRS && x1 == x0 + 1) {  // the two taps of a row are adjacent: one 8-B load per row
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        u2 r0, r1;
+        __builtin_memcpy(&r0, tx + y0 * t.w + x0, 8);
+        __builtin_memcpy(&r1, tx + y1 * t.w + x0, 8);
+        p00 = r0.x; p10 = r0.y; p01 = r1.x; p11 = r1.y;
+    } else {  // REPEAT wrapped x1 to column 0
+        p00 = tx[y0 * t.w + x0]; p10 = tx[y0 * t.w + x1];
+        p01 = tx[y1 * t.w + x0]; p11 = tx[y1 * t.w + x1];
+    }
     float4 r;
     float* rp = &r.x;
 #pragma unroll
@@ -2017,8 +2054,19 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
     const float zref = lz - fp.s_bias;
     const int32_t ia = min(max(i0, 0), n - 1), ib = min(max(i0 + 1, 0), n - 1);
     const int32_t ja = min(max(j0, 0), n - 1), jb = min(max(j0 + 1, 0), n - 1);
-    const float m00 = __uint_as_float(smap[(size_t)ja * n + ia]), m10 = __uint_as_float(smap[(size_t)ja * n + ib]);
-    const float m01 = __uint_as_float(smap[(size_t)jb * n + ia]), m11 = __uint_as_float(smap[(size_t)jb * n + ib]);
+    float m00, m10, m01, m11;
+    TRI_G const uint32_t* sm = (TRI_G const uint32_t*)smap;
+    if (TRI_MAP_PAIRS && ib == ia + 1) {  // adjacent columns: one 8-B load per row (as sample_tex)
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        u2 r0, r1;
+        __builtin_memcpy(&r0, sm + (size_t)ja * n + ia, 8);
+        __builtin_memcpy(&r1, sm + (size_t)jb * n + ia, 8);
+        m00 = __uint_as_float(r0.x); m10 = __uint_as_float(r0.y);
+        m01 = __uint_as_float(r1.x); m11 = __uint_as_float(r1.y);
+    } else {  // a clamped column at the map's edge
+        m00 = __uint_as_float(sm[(size_t)ja * n + ia]); m10 = __uint_as_float(sm[(size_t)ja * n + ib]);
+        m01 = __uint_as_float(sm[(size_t)jb * n + ia]); m11 = __uint_as_float(sm[(size_t)jb * n + ib]);
+    }
     const float c00 = zref <= m00 ? 1.0f : 0.0f;
     const float c10 = zref <= m10 ? 1.0f : 0.0f;
     const float c01 = zref <= m01 ? 1.0f : 0.0f;
@@ -2067,7 +2115,26 @@ __device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint
 struct ShadeRec {
     uint4 st, sd, ss;
 };
+// TRI_SHADE_SCALAR: when every lane of the wave shades the same draw (the common case: a bin is mostly one
+// mesh), the record comes through three scalar buffer loads instead of three wave-wide gathers (the texture
+// units' data return is what C5's fragment stage waits on).
+#ifndef TRI_SHADE_SCALAR
+#define TRI_SHADE_SCALAR 1
+#endif
+__device__ u32x4v tri_s_buffer_load_v4(u32x4v rsrc, int offset, int aux) __asm("llvm.amdgcn.s.buffer.load.v4i32");
 __device__ __forceinline__ ShadeRec load_shade(const FetchBufs& fb, uint32_t d) {
+    if (TRI_SHADE_SCALAR) {
+        const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+        if (__ballot(d != d0) == 0ull) {  // wave-uniform draw
+            const uint64_t base = (uint64_t)fb.shade_base;  // a raw descriptor: base, 0 stride, size, flags
+            const u32x4v r = u32x4v{(uint32_t)base, (uint32_t)(base >> 32) & 0xFFFFu, fb.shade_bytes, 0x00020000u};
+            const int off = (int)(d0 * (uint32_t)sizeof(TriDrawShade));
+            const u32x4v a = tri_s_buffer_load_v4(r, off, 0), b = tri_s_buffer_load_v4(r, off + 16, 0),
+                         c = tri_s_buffer_load_v4(r, off + 32, 0);
+            return ShadeRec{make_uint4(a[0], a[1], a[2], a[3]), make_uint4(b[0], b[1], b[2], b[3]),
+                            make_uint4(c[0], c[1], c[2], c[3])};
+        }
+    }
     return ShadeRec{rec128<48>(fb.shade, d, 0u), rec128<48>(fb.shade, d, 16u), rec128<48>(fb.shade, d, 32u)};
 }
 
@@ -2125,45 +2192,9 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
 // Interpolate the visible triangle's varyings at pixel (px, py) (perspective-correct).
 // Writes the fragment through `put(field_index, value)` (fields in Frag order), so one body serves
 // the single-pixel Frag and the lane-pair FragP without an intermediate in scratch memory.
-// The shadow pre-pass's sun visibility of one fragment (oracle shadow_visibility): the light-space position
-// interpolated with the EXACT perspective weights (in both shading builds, so the compare sees the oracle's bits
-// and never flips a texel), then the 2x2 compare. k_raster<.., SHADOW> evaluates it for every visible pixel in a
-// pass of its own before shading (TRI_SHADOW_VIS_PASS), so the shading loop does not hold the light-space
-// gathers, the exact weights and the map taps in its registers.
-__device__ __forceinline__ float fragment_shadow_vis(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                                     int32_t px, int32_t py) {
-    const uint32_t low = (uint32_t)key;
-    const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
-    const uint32_t sub = low & 7u;
-    const FetchBufs fb = fetch_bufs(fp, b);
-    const RecBuf lr = rec_buf(b.lpos, 16u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
-    TriRec r;
-    uint32_t v0, v1, v2;
-    if (sub) {
-        r = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
-        v0 = r.v[0]; v1 = r.v[1]; v2 = r.v[2];
-    } else {
-        uint32_t sl[3], d;
-        prim_slots<false>(fp, b, prim, sl, d);
-        const TriSnap a0 = ld_snap_xyw(fb, sl[0]), a1 = ld_snap_xyw(fb, sl[1]), a2 = ld_snap_xyw(fb, sl[2]);
-        v0 = sl[0]; v1 = sl[2]; v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
-        r = rec_from_snaps(prim, sl, a0, a1, a2);
-    }
-    const uint4 L0 = rec128<16>(lr, v0, 0u), L1 = rec128<16>(lr, v1, 0u), L2 = rec128<16>(lr, v2, 0u);
-    float e0, e1, e2;
-    exact_weights(r, px, py, e0, e1, e2);
-    auto ix = [&](uint32_t a, uint32_t bq, uint32_t c) {
-        return interp_exact(e0, e1, e2, __uint_as_float(a), __uint_as_float(bq), __uint_as_float(c));
-    };
-    return shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
-}
-
-// A separate visibility pass (round 4 A/B, C5 k_raster at 5 waves/SIMD): 188.6 -> 206.4 us, at 6 waves 197 us —
-// the pass fetches each fragment's index and snapped vertices a second time and the shading loop's register
-// peak is not the lookup's; off.
-#ifndef TRI_SHADOW_VIS_PASS
-#define TRI_SHADOW_VIS_PASS 0
-#endif
+// Rejected (round 4): the sun visibility of every visible pixel in a pass of its own before shading, so that
+// the shading loop would not hold the light-space gathers and the map taps in its registers: C5 k_raster
+// 188.6 -> 206.4 us (the pass fetches each fragment's index and snapped vertices a second time).
 // The fast build's shadow instantiation shades with the exact weights its lookup needs (TRI_SHADOW_SHARED_WEIGHTS:
 // one weight computation per fragment instead of two; C5 +1 % over both). Rejected (round 4): the lookup from
 // the fast weights, recomputed with the exact ones only where a depth compare or the map border is within a few
@@ -2173,13 +2204,11 @@ __device__ __forceinline__ float fragment_shadow_vis(const TriFrameParams& fp, c
 #endif
 
 // CLIPM: 0 = the key may name a clipped sub-triangle (tested per pixel), 1 = it never does (the shading loop
-// defers clipped pixels, TRI_CLIP_DEFER), 2 = it always does (the deferred pass). pre_vis: the fragment's sun
-// visibility from the visibility pass (SHADOW with TRI_SHADOW_VIS_PASS).
+// defers clipped pixels, TRI_CLIP_DEFER), 2 = it always does (the deferred pass).
 template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0, typename Put>
 __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                                  int32_t px, int32_t py, const float* lut, Put&& put,
-                                                  float pre_vis = 1.0f) {
-    constexpr bool kInlineVis = SHADOW && !TRI_SHADOW_VIS_PASS;
+                                                  int32_t px, int32_t py, const float* lut, Put&& put) {
+    constexpr bool kInlineVis = SHADOW;
     const uint32_t low = (uint32_t)key;
     const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
     const uint32_t sub = CLIPM == 1 ? 0u : (low & 7u);  // >= 1: sub-triangle `sub` of a clipped primitive
@@ -2207,12 +2236,26 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         v0 = rc.v[0]; v1 = rc.v[1]; v2 = rc.v[2];
         taps = load_taps<ONE>(fb, v0, v1, v2);
     }
+    const bool from_rec = CLIPM == 2 || (CLIPM == 0 && sub);
+    // the three vertices' light-space positions: gathered (lpos), or with fp.lpos_world recomputed from the world
+    // positions the varyings already carry — k_vertex's own operations on the same floats, so the same bits, and
+    // three 16-B gathers fewer per pixel. A clipped sub-triangle's vertices keep the clipper's interpolated ones.
     uint4 L0, L1, L2;
     if constexpr (kInlineVis) {
         const RecBuf lr = rec_buf(b.lpos, 16u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
-        L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
+        if (TRI_LPOS_WORLD && fp.lpos_world) {
+            auto lw = [&](const V4& t) {
+                const float4 l = mat_vec_seq(fp.lvp, make_float4(t.x, t.y, t.z, 1.0f));
+                return make_uint4(__float_as_uint(l.x), __float_as_uint(l.y), __float_as_uint(l.z), 0u);
+            };
+            L0 = lw(taps.a0); L1 = lw(taps.b0); L2 = lw(taps.c0);
+            if (from_rec) {
+                L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
+            }
+        } else {
+            L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
+        }
     }
-    const bool from_rec = CLIPM == 2 || (CLIPM == 0 && sub);
     const TriRec r = from_rec ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
     float w0, w1, w2;
     // exact int64 edge functions, IEEE divides (oracle order). The shadow lookup needs these weights in both
@@ -2234,7 +2277,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
             taps.a2 = ld_vary<ONE>(fb, v0, 2); taps.b2 = ld_vary<ONE>(fb, v1, 2); taps.c2 = ld_vary<ONE>(fb, v2, 2);
         }
     }
-    float vis = SHADOW ? pre_vis : 1.0f;
+    float vis = 1.0f;
     if constexpr (kInlineVis) {  // light-space position at the pixel with the oracle's weights, then the compare
         float e0 = w0, e1 = w1, e2 = w2;
         if (!EXACT && !TRI_SHADOW_SHARED_WEIGHTS && !(kAblate & 512))  // 512: fast weights (diagnostics)
@@ -2250,9 +2293,8 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
 
 template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0>
 __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                               int32_t px, int32_t py, const float* lut, Frag& f, float pre_vis = 1.0f) {
-    fetch_fragment_to<EXACT, SHADOW, ONE, CLIPM>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; },
-                                                 pre_vis);
+                                               int32_t px, int32_t py, const float* lut, Frag& f) {
+    fetch_fragment_to<EXACT, SHADOW, ONE, CLIPM>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2700,17 +2742,6 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     constexpr int kWaveQ = BIN * BIN / (TRI_BLOCK / 64);
     __shared__ uint16_t clipq[kDefer ? BIN * BIN : 1];
     uint32_t nclip = 0;  // this wave's deferred pixels (wave-uniform)
-    // the sun visibility of every visible pixel, by the lane that shades it (no barrier: each lane reads back
-    // only its own pixels)
-    constexpr bool kVisPass = SHADOW && TRI_SHADOW_VIS_PASS;
-    __shared__ float visl[kVisPass ? BIN * BIN : 1];
-    if constexpr (kVisPass) {
-        for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
-            if (lx >= bw) continue;
-            const uint64_t key = keys[(ly << BL) + lx];
-            if (key != kBgKey) visl[(ly << BL) + lx] = fragment_shadow_vis(fp, b, key, ox + lx, oy + ly);
-        }
-    }
     for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
         const bool in = lx < bw;
         const uint64_t key = in ? keys[(ly << BL) + lx] : 0ull;
@@ -2754,8 +2785,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
                 const float k0 = __uint_as_float(((uint32_t)key & 0x7FFFFFu) | 0x3F000000u);
                 for (int q = 0; q < 20; ++q) (&f.wx)[q] = k0 + 0.01f * q;
             } else {
-                fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f,
-                                                                    kVisPass ? visl[(ly << BL) + lx] : 1.0f);
+                fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f);
             }
             out = shade_bgra<EXACT, ONE>(fp, f);
         }
@@ -2771,7 +2801,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             const uint64_t key = keys[li];
             const int32_t px = ox + qx, py = oy + qy;
             Frag f;
-            fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f, kVisPass ? visl[li] : 1.0f);
+            fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f);
             const size_t o = (size_t)(py - fp.y0) * fp.W + px;
             b.color[o] = shade_bgra<EXACT, ONE>(fp, f);
             if (fp.write_depth) b.depth[o] = __uint_as_float((uint32_t)(key >> 32));
