@@ -2077,14 +2077,12 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
 
 // The varyings of the triangle's three vertex slots: 16-B gathers, issued before the weights are
 // computed (their addresses need only the slots, the weights need the snapped vertices too). With
-// TRI_COLOUR_LATE (k_raster_plain) the three colour gathers are issued once the weights are done and the
+// TRI_COLOUR_LATE the three colour gathers are issued once the weights are done and the
 // snapped vertices' registers are free: the peak register count falls enough for 7 waves/SIMD.
+// Both translation units (round 4: the shadow instantiation too, 92 -> 86 VGPRs, which with 6 waves/SIMD spills
+// 6 instead of 20: C5 k_raster 166.5 -> 158.7 us).
 #ifndef TRI_COLOUR_LATE
-#ifdef TRI_RASTER_PLAIN_TU
 #define TRI_COLOUR_LATE 1
-#else
-#define TRI_COLOUR_LATE 0
-#endif
 #endif
 struct Taps {
     V4 a0, a1, a2, b0, b1, b2, c0, c1, c2;
@@ -2444,7 +2442,8 @@ __device__ __forceinline__ uint32_t sky_bgra_persp(const TriFrameParams& fp, con
 #define TRI_RASTER_WAVES_PLAIN 7  // k_raster_plain (raster_plain.hip, no SLP): 69 VGPRs, no spill
 #endif
 #ifndef TRI_RASTER_WAVES_SHADOW
-#define TRI_RASTER_WAVES_SHADOW 5  // with the shadow lookup (6 spilled: C5 raster 207 us at 5 vs 213 at 6)
+#define TRI_RASTER_WAVES_SHADOW 6  // the fast build's shadow instantiation (80 VGPRs, 6 spilled: C5 raster 158.7 us
+                                   // against 166.5 at 5 waves; the exact build keeps 5)
 #endif
 
 // bbox∩bin pixels above which a triangle is rasterized by the whole workgroup (cooperatively):
@@ -2838,7 +2837,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
 // (13 VGPRs spilled by values hoisted out of the bin loop, and a static bin order that balances worse
 // than the dispatcher's).
 template <bool EXACT, int BL, bool SHADOW>
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? TRI_RASTER_WAVES_SHADOW : TRI_RASTER_WAVES) : 3))) void k_raster(TRI_KARGS) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? (EXACT ? 5 : TRI_RASTER_WAVES_SHADOW) : TRI_RASTER_WAVES) : 3))) void k_raster(TRI_KARGS) {
     TRI_BIND_ARGS;
     raster_bin<EXACT, BL, SHADOW>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
