@@ -1580,6 +1580,9 @@ __device__ __forceinline__ uint32_t wrap_repeat(float f, uint32_t n) {  // REPEA
 #ifndef TRI_MAP_PAIRS
 #define TRI_MAP_PAIRS 1
 #endif
+// Two adjacent 4-B texels as one 8-B load (4-B aligned: a dwordx2 load needs no more)
+typedef uint32_t u32x2a __attribute__((ext_vector_type(2), aligned(4)));
+__device__ __forceinline__ u32x2a ld_pair(TRI_G const uint32_t* p) { return *reinterpret_cast<TRI_G const u32x2a*>(p); }
 // texture(): R8G8B8A8_SRGB decode before LINEAR filtering, REPEAT, level 0 (Renderer.cpp:3592-3607)
 __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, float v0, const float* lut) {
     if (t.w == 1 && t.h == 1)  // 1x1 (the default white slot): all four taps are texel (0,0)
@@ -1593,10 +1596,7 @@ __device__ __forceinline__ float4 sample_tex(const TriTexDesc& t, float u0, floa
     TRI_G const uint32_t* tx = (TRI_G const uint32_t*)t.texels;  // device texture memory (global loads)
     uint32_t p00, p10, p01, p11;
     if (TRI_TEXEL_PAIRS && x1 == x0 + 1) {  // the two taps of a row are adjacent: one 8-B load per row
-        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-        u2 r0, r1;
-        __builtin_memcpy(&r0, tx + y0 * t.w + x0, 8);
-        __builtin_memcpy(&r1, tx + y1 * t.w + x0, 8);
+        const u32x2a r0 = ld_pair(tx + y0 * t.w + x0), r1 = ld_pair(tx + y1 * t.w + x0);
         p00 = r0.x; p10 = r0.y; p01 = r1.x; p11 = r1.y;
     } else {  // REPEAT wrapped x1 to column 0
         p00 = tx[y0 * t.w + x0]; p10 = tx[y0 * t.w + x1];
@@ -2057,10 +2057,7 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
     float m00, m10, m01, m11;
     TRI_G const uint32_t* sm = (TRI_G const uint32_t*)smap;
     if (TRI_MAP_PAIRS && ib == ia + 1) {  // adjacent columns: one 8-B load per row (as sample_tex)
-        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-        u2 r0, r1;
-        __builtin_memcpy(&r0, sm + (size_t)ja * n + ia, 8);
-        __builtin_memcpy(&r1, sm + (size_t)jb * n + ia, 8);
+        const u32x2a r0 = ld_pair(sm + (size_t)ja * n + ia), r1 = ld_pair(sm + (size_t)jb * n + ia);
         m00 = __uint_as_float(r0.x); m10 = __uint_as_float(r0.y);
         m01 = __uint_as_float(r1.x); m11 = __uint_as_float(r1.y);
     } else {  // a clamped column at the map's edge
@@ -2337,12 +2334,14 @@ __device__ __forceinline__ f3 face_dir(int face, float sc, float tc) {
 }
 
 struct SkyTex {
-    const uint32_t* t;
+    TRI_G const uint32_t* t;
     int32_t n;
     const float* lut;
-    __device__ __forceinline__ f3 texel(int face, int32_t i, int32_t j) const {
-        const uint32_t p = t[((uint32_t)face * (uint32_t)n + (uint32_t)j) * (uint32_t)n + (uint32_t)i];
+    __device__ __forceinline__ f3 decode(uint32_t p) const {
         return mk(lut[p & 0xFFu], lut[(p >> 8) & 0xFFu], lut[(p >> 16) & 0xFFu]);
+    }
+    __device__ __forceinline__ f3 texel(int face, int32_t i, int32_t j) const {
+        return decode(t[((uint32_t)face * (uint32_t)n + (uint32_t)j) * (uint32_t)n + (uint32_t)i]);
     }
     __device__ __forceinline__ f3 across(int face, int32_t i, int32_t j) const {
         const float sc = 2.0f * (((float)i + 0.5f) / (float)n) - 1.0f;
@@ -2369,8 +2368,15 @@ struct SkyTex {
         const float fu = floorf(u), fv = floorf(v);
         const float a = u - fu, bb = v - fv;
         const int32_t i0 = (int32_t)fu, j0 = (int32_t)fv;
-        const f3 t00 = fetch(face, i0, j0), t10 = fetch(face, i0 + 1, j0);
-        const f3 t01 = fetch(face, i0, j0 + 1), t11 = fetch(face, i0 + 1, j0 + 1);
+        f3 t00, t10, t01, t11;
+        if (TRI_TEXEL_PAIRS && i0 >= 0 && i0 + 1 < n && j0 >= 0 && j0 + 1 < n) {  // inside the face: 8-B row loads
+            TRI_G const uint32_t* r = t + ((uint32_t)face * (uint32_t)n + (uint32_t)j0) * (uint32_t)n + (uint32_t)i0;
+            const u32x2a r0 = ld_pair(r), r1 = ld_pair(r + n);
+            t00 = decode(r0.x); t10 = decode(r0.y); t01 = decode(r1.x); t11 = decode(r1.y);
+        } else {  // a tap across an edge or corner of the face (seamless filtering)
+            t00 = fetch(face, i0, j0); t10 = fetch(face, i0 + 1, j0);
+            t01 = fetch(face, i0, j0 + 1); t11 = fetch(face, i0 + 1, j0 + 1);
+        }
         auto lp = [](float x, float y, float w) { return x + w * (y - x); };
         return mk(lp(lp(t00.x, t10.x, a), lp(t01.x, t11.x, a), bb), lp(lp(t00.y, t10.y, a), lp(t01.y, t11.y, a), bb),
                   lp(lp(t00.z, t10.z, a), lp(t01.z, t11.z, a), bb));

@@ -488,6 +488,12 @@ class BandRenderer:
         return ts[len(ts) // 2]
 
 
+# Frames in flight per config at N = 1 (round 4, same-box A/B of the whole bench line): the 1M-triangle 4K frame
+# hides more of its front end behind the other frames' raster at 3 (C3 +2.3 %), while C2 and C5 lose 9-11 % at 3
+# (their per-context buffers and the extra stream cost more than the overlap gains).
+DEFAULT_INFLIGHT = {"c3": 3, "c2": 2, "c5": 2, "c1": 2}
+
+
 def split_candidates(height, world, min_rows=32, inflights=(2,)):
     """(display rows, frames in flight) pairs autotune_split tries: the equal split and display bands up to
     2.5x it, as long as every other rank keeps at least `min_rows` rows (one bin row), at each frame count
@@ -767,8 +773,9 @@ def main():
     ap.add_argument("--sim-rank", type=int, default=0)
     ap.add_argument("--sim-display-rows", type=int, default=None,
                     help="diagnostics: the simulated split's display band (rank 0) size, the others sharing the rest")
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="frames in flight per rank (contexts taking frames in turn, one stream each)")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="frames in flight per rank (contexts taking frames in turn, one stream each); default per "
+                         "config (DEFAULT_INFLIGHT)")
     ap.add_argument("--assembly", choices=("gather", "allgather"), default="gather",
                     help="N > 1: bands gathered onto the display rank 0 (default) or all-gathered onto every rank")
     ap.add_argument("--pack", choices=("auto", "off"), default="auto",
@@ -799,24 +806,27 @@ def main():
 
     scene = build_scene(args.config)
 
+    def inflight_for(sc):
+        return args.inflight or DEFAULT_INFLIGHT.get(sc.name.split("_")[0], 2)
+
     def make_renderer(sc, display_rows=None, inflight=None):
-        return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=inflight or args.inflight,
+        return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=inflight or inflight_for(sc),
                             display_rows=display_rows, pack=args.pack)
 
     def choose_split(sc):
         """((display_rows or None, frames in flight), the autotune log) for a config at this world size."""
         if world == 1 or args.assembly != "gather" or args.split == "equal":
-            return (None, args.inflight), None
+            return (None, inflight_for(sc)), None
         if args.split != "auto":
-            return (int(args.split), args.inflight), None
+            return (int(args.split), inflight_for(sc)), None
         return autotune_split(lambda d, k: make_renderer(sc, d, k), sc.height, world, dist_on,
                               warm_seconds=args.warm_seconds,
                               inflights=tuple(int(k) for k in args.inflight_candidates.split(",")))
 
     split_log = None
-    inflight = args.inflight
+    inflight = inflight_for(scene)
     if args.sim_world and world == 1:
-        br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=args.inflight,
+        br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=inflight_for(scene),
                           display_rows=args.sim_display_rows, pack=args.pack)
     else:
         (display_rows, inflight), split_log = choose_split(scene)
@@ -861,16 +871,18 @@ def main():
             s2 = build_scene(key)
             (d2, k2), log2 = choose_split(s2)
             br2 = make_renderer(s2, d2, k2)
-            n2 = max(args.steps, 50) if key == "c2" else max(args.steps // 2, 20)
+            # enough frames that the pipeline's fill and drain (about one frame latency, 50 us at C2, 280 us at C5)
+            # stay under 1 % of the timed region whatever --steps the headline uses
+            n2 = max(args.steps, 200) if key == "c2" else max(args.steps, 100)
             dt2, t2, _ = timed_run(br2, n2, args.warmup, dist_on, warm_seconds=args.warm_seconds)
             fps2 = n2 / dt2
             st2 = stage_ms(t2)
             entry = {"frames_per_s": fps2, "mpix_per_s": fps2 * s2.width * s2.height / 1e6, "ms_per_frame": 1e3 / fps2,
                      "stage_ms": st2, "kernel_samples": int(t2["frames"]) if t2 else 0, "triangles": s2.triangles,
                      "algorithmic_bytes": s2.algorithmic_bytes(rows=br2.rows)}
+            entry["frames_in_flight"] = k2
             if world > 1:
                 entry["bands"] = [y1 - y0 for y0, y1 in br2.bands]
-                entry["frames_in_flight"] = k2
                 entry["split_autotune"] = log2
             if s2.shadow is not None:
                 entry["shadow_map"] = f"{s2.shadow.size}^2 D32 pre-pass for the sun (tri_set_shadow, DESIGN.md 5d)"
