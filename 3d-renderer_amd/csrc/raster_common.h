@@ -243,9 +243,6 @@ struct TriFrameParams {
     // position and normal through the model and normal matrices (linear maps: the same values up to
     // rounding); the clipper writes object-space 36-B records for its polygon vertices.
     uint32_t vary36, vary_obj, obj_xform, vin_base;
-    // lpos_world (shadow pre-pass frames whose draws are all affine and unskinned): the fragment stage recomputes
-    // the vertices' light-space positions from their world positions instead of gathering lpos
-    uint32_t lpos_world, pad_l[3];
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
     uint32_t shadow_on, s_size, s_nbx, s_nbins;
     uint32_t s_bin_cap;

@@ -27,8 +27,9 @@ namespace {
 
 // Diagnostics builds only (tools/build_variant.sh NAME -DTRI_ABLATE=N): 1 = coverage without shading,
 // 2 = shading without coverage, 4 = set-up without binning, 8 = one reservation round per batch,
-// 16 = no reservation atomics, 32 = no queue stores, 1024 = no fragment colour gathers. The shipped library is built with 0, so none of
-// these tests survives into its ISA.
+// 16 = no reservation atomics, 32 = no queue stores, 64 = no lights, 128 = no texture sample, 256 = no varyings
+// fetch, 1024 = no fragment colour gathers, 2048 = no shadow lookup (and the fast weights). The shipped library is
+// built with 0, so none of these tests survives into its ISA.
 #ifndef TRI_ABLATE
 #define TRI_ABLATE 0
 #endif
@@ -162,13 +163,6 @@ struct FetchBufs {
 #ifndef TRI_VARY_OBJ
 #define TRI_VARY_OBJ 1
 #endif
-// TRI_LPOS_WORLD: with the shadow pre-pass, the light-space vertex positions come from the world positions in the
-// varyings (k_vertex's own operations on the same floats, so the same bits) instead of a stored lpos per vertex
-// slot: no lpos stores in k_vertex, three 16-B gathers fewer per fragment (fp.lpos_world: every draw affine and
-// unskinned, so world.w == 1 as k_vertex used it). The clipper's polygon vertices keep stored, interpolated ones.
-#ifndef TRI_LPOS_WORLD
-#define TRI_LPOS_WORLD 1
-#endif
 __device__ __forceinline__ bool vary36_mode(const TriFrameParams& fp) { return TRI_VARY36 && fp.vary36; }
 __device__ __forceinline__ bool obj_mode(const TriFrameParams& fp) { return TRI_VARY36 && TRI_VARY_OBJ && fp.vary_obj; }
 struct F3 {
@@ -277,8 +271,7 @@ __device__ __forceinline__ uint32_t outcode(const TriFrameParams& fp, float4 c);
 __device__ __forceinline__ void shadow_vertex(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
                                               float4 world) {
     const float4 l = mat_vec_seq(fp.lvp, world);
-    // with lpos_world the readers recompute it from the world position in the varyings (same operations)
-    if (!(TRI_LPOS_WORLD && fp.lpos_world)) b.lpos[slot] = make_float4(l.x, l.y, l.z, 0.0f);
+    b.lpos[slot] = make_float4(l.x, l.y, l.z, 0.0f);
     uint32_t oc = 0;
     if (l.x + 1.0f < 0.0f) oc |= TRI_OC_XNEG;
     if (1.0f - l.x < 0.0f) oc |= TRI_OC_XPOS;
@@ -812,14 +805,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
             }
         }
         if constexpr (LPOS) {  // shadow pre-pass on: the polygon vertex's light-space position, same weights
-            auto lp = [&](uint32_t sl) {  // (see shadow_vertex: not stored with lpos_world)
-                if (TRI_LPOS_WORLD && fp.lpos_world) {
-                    const float4 w = b.vary[3u * sl];
-                    return mat_vec_seq(fp.lvp, make_float4(w.x, w.y, w.z, 1.0f));
-                }
-                return b.lpos[sl];
-            };
-            const float4 x = lp(sl0), y = lp(sl1), z = lp(sl2);
+            const float4 x = b.lpos[sl0], y = b.lpos[sl1], z = b.lpos[sl2];
             b.lpos[sbase + lane] = make_float4((s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x,
                                                (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
                                                (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z, 0.0f);
@@ -2232,30 +2218,19 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         taps = load_taps<ONE>(fb, v0, v1, v2);
     }
     const bool from_rec = CLIPM == 2 || (CLIPM == 0 && sub);
-    // the three vertices' light-space positions: gathered (lpos), or with fp.lpos_world recomputed from the world
-    // positions the varyings already carry — k_vertex's own operations on the same floats, so the same bits, and
-    // three 16-B gathers fewer per pixel. A clipped sub-triangle's vertices keep the clipper's interpolated ones.
+    // the three vertices' light-space positions (rejected in round 4: recomputing them from the varyings' world
+    // positions, k_vertex's own operations and so the same bits, instead of three 16-B gathers: 63 VALU per pixel
+    // for 3 gathers, C5 k_raster +3.5 us)
     uint4 L0, L1, L2;
     if constexpr (kInlineVis) {
         const RecBuf lr = rec_buf(b.lpos, 16u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
-        if (TRI_LPOS_WORLD && fp.lpos_world) {
-            auto lw = [&](const V4& t) {
-                const float4 l = mat_vec_seq(fp.lvp, make_float4(t.x, t.y, t.z, 1.0f));
-                return make_uint4(__float_as_uint(l.x), __float_as_uint(l.y), __float_as_uint(l.z), 0u);
-            };
-            L0 = lw(taps.a0); L1 = lw(taps.b0); L2 = lw(taps.c0);
-            if (from_rec) {
-                L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
-            }
-        } else {
-            L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
-        }
+        L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
     }
     const TriRec r = from_rec ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
     float w0, w1, w2;
     // exact int64 edge functions, IEEE divides (oracle order). The shadow lookup needs these weights in both
     // builds (TRI_SHADOW_SHARED_WEIGHTS: the fast build shades with them too instead of forming its own)
-    if (EXACT || (kInlineVis && TRI_SHADOW_SHARED_WEIGHTS)) {
+    if (EXACT || (kInlineVis && TRI_SHADOW_SHARED_WEIGHTS && !(kAblate & 2048))) {
         exact_weights(r, px, py, w0, w1, w2);
     } else if (TRI_SNAP_F && CLIPM == 1) {  // never clipped here: the floats of the snaps directly
         fast_weights_snaps(a0, a1, a2, px, py, w0, w1, w2);
@@ -2273,7 +2248,8 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         }
     }
     float vis = 1.0f;
-    if constexpr (kInlineVis) {  // light-space position at the pixel with the oracle's weights, then the compare
+    if constexpr (kInlineVis && !(kAblate & 2048)) {  // light-space position at the pixel with the oracle's weights,
+                                                       // then the compare (diagnostics: 2048 = no lookup)
         float e0 = w0, e1 = w1, e2 = w2;
         if (!EXACT && !TRI_SHADOW_SHARED_WEIGHTS && !(kAblate & 512))  // 512: fast weights (diagnostics)
             exact_weights(r, px, py, e0, e1, e2);

@@ -144,7 +144,6 @@ struct tri_ctx {
     hipEvent_t stage_free = nullptr;
     uint32_t ndraws = 0, nslots = 0, nprims = 0;
     bool any_skin = false;
-    bool all_affine = true;  // every draw clip_from_world (affine, unskinned): TriFrameParams::lpos_world
     TriDrawDev draw0{};  // the resolved draw when there is exactly one (passed by value to the kernels)
     bool draw0_obj = false;    // draw0 may keep object-space varyings (draw_obj_ok)
     bool draw0_xform = false;  // ... and its model matrix is not the identity
@@ -406,7 +405,7 @@ int resolve_draws(tri_ctx* c) {
     std::vector<TriDrawShade> ds(n);
     std::vector<uint32_t> vb(n + 1), pb(n + 1), cbase(n + 1);
     uint64_t vslots = 0, prims = 0, ncl = 0;
-    bool skin = false, affine = true;
+    bool skin = false;
     for (uint32_t d = 0; d < n; ++d) {
         const tri_draw& src = c->draws[d];
         TriDrawDev& o = dd[d];
@@ -427,7 +426,6 @@ int resolve_draws(tri_ctx* c) {
         o.bone_count = src.pc.bone_count;
         o.clip_from_world = (o.bone_count <= 0 && o.model[3] == 0.0f && o.model[7] == 0.0f && o.model[11] == 0.0f &&
                              o.model[15] == 1.0f) ? 1u : 0u;
-        affine = affine && o.clip_from_world;
         vb[d] = (uint32_t)vslots;
         pb[d] = (uint32_t)prims;
         cbase[d] = (uint32_t)ncl;
@@ -497,7 +495,6 @@ int resolve_draws(tri_ctx* c) {
     c->nprims = (uint32_t)prims;
     c->ncl_total = (uint32_t)ncl;
     c->any_skin = skin;
-    c->all_affine = affine;
     c->draws_dirty = false;
     return TRI_OK;
 }
@@ -1249,7 +1246,6 @@ int tri_render(tri_ctx* c) {
         fp.s_g = (2.0f * TRI_GUARD_BAND_PX) / (float)c->shadow.size - 1.0f;
         fp.s_bias = c->shadow.depth_bias;
         fp.s_slope = c->shadow.slope_bias;
-        fp.lpos_world = c->all_affine ? 1u : 0u;
         std::memcpy(fp.lvp, c->shadow.light_view_proj, 64);
     }
     std::memcpy(fp.pv, c->pv, 64);
