@@ -243,6 +243,10 @@ struct TriFrameParams {
     // position and normal through the model and normal matrices (linear maps: the same values up to
     // rounding); the clipper writes object-space 36-B records for its polygon vertices.
     uint32_t vary36, vary_obj, obj_xform, vin_base;
+    // obj_ucol (vary_obj frames whose vertices all carry one colour, ucol — meshes without vertex colours are
+    // imported white): the fragment stage takes the colour from here instead of three gathers and an interpolation
+    uint32_t obj_ucol;
+    float ucol[3];
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
     uint32_t shadow_on, s_size, s_nbx, s_nbins;
     uint32_t s_bin_cap;

@@ -2149,7 +2149,11 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const Fetc
         put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
         put(3, ip(a1.x, b1.x, c1.x)); put(4, ip(a1.y, b1.y, c1.y)); put(5, ip(a1.z, b1.z, c1.z));
     }
-    put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
+    if (ONE && obj_mode(fp) && fp.obj_ucol) {  // one colour for every vertex (its interpolation is the colour)
+        put(6, fp.ucol[0]); put(7, fp.ucol[1]); put(8, fp.ucol[2]);
+    } else {
+        put(6, ip(a2.x, b2.x, c2.x)); put(7, ip(a2.y, b2.y, c2.y)); put(8, ip(a2.z, b2.z, c2.z));
+    }
     const float u = ip(a0.w, b0.w, c0.w), v = ip(a1.w, b1.w, c1.w);
     put(9, u); put(10, v);
     if (ONE || fp.shade_solid) {  // uniform: one draw with a 1x1 slot, its texel and tint are kernel arguments
@@ -2239,6 +2243,8 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     }
     if (kAblate & 1024) {  // diagnostics: 1024 = no colour gathers (3 of the fragment's 13 loads; same VALU)
         taps.a2 = V4{w0, w1, w2, 0.0f}; taps.b2 = taps.a2; taps.c2 = taps.a2;
+    } else if (ONE && TRI_VARY_OBJ && obj_mode(fp) && fp.obj_ucol) {
+        // one colour for every vertex: fetch_attrs takes it from the frame arguments
     } else if (TRI_COLOUR_LATE) {
         if (ONE && !from_rec) {  // an unclipped primitive's vertices (with CLIPM 0 a per-lane choice: both masked)
             taps.a2 = ld_vary<ONE, true>(fb, v0, 2); taps.b2 = ld_vary<ONE, true>(fb, v1, 2);

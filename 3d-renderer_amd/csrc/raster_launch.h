@@ -23,6 +23,12 @@
 #define TRI_G
 #endif
 
+// TRI_UCOL: vary_obj frames over a geometry whose vertices share one colour take it from the frame arguments
+// (TriFrameParams::obj_ucol)
+#ifndef TRI_UCOL
+#define TRI_UCOL 1
+#endif
+
 struct TriDeviceBuffers {
     TRI_G const TriVsIn* vin;
     TRI_G const float* vpos;           // 12 B per vertex: the positions alone (k_vertex's only input with vary_obj)

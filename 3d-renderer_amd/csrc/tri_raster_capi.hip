@@ -82,6 +82,8 @@ struct tri_geometry {
     // every vertex has a finite position and a unit normal (|n|^2 within 1e-5 of 1): a draw over it may keep
     // its varyings in object space (TriFrameParams::vary_obj)
     bool obj_ok = false;
+    bool uni_col = false;  // every vertex has the colour ucol (TriFrameParams::obj_ucol)
+    float ucol[3] = {0.0f, 0.0f, 0.0f};
     uint64_t nverts = 0;
     uint32_t* d_idx = nullptr; size_t cap_idx = 0;
     uint64_t nidx = 0;
@@ -147,6 +149,7 @@ struct tri_ctx {
     TriDrawDev draw0{};  // the resolved draw when there is exactly one (passed by value to the kernels)
     bool draw0_obj = false;    // draw0 may keep object-space varyings (draw_obj_ok)
     bool draw0_xform = false;  // ... and its model matrix is not the identity
+    bool draw0_ucol = false;   // ... and every vertex of its geometry has one colour
 
     // work buffers
     float4* d_clip = nullptr; size_t cap_clip = 0;
@@ -491,6 +494,7 @@ int resolve_draws(tri_ctx* c) {
     }
     c->draw0_obj = n == 1 && draw_obj_ok(*c->geom, dd[0]);
     c->draw0_xform = c->draw0_obj && !identity_model(dd[0].model);
+    c->draw0_ucol = c->draw0_obj && c->geom->uni_col;
     c->nslots = (uint32_t)vslots;
     c->nprims = (uint32_t)prims;
     c->ncl_total = (uint32_t)ncl;
@@ -676,6 +680,10 @@ int geometry_upload(tri_geometry* g, const tri_vertex* v, uint64_t nv, const uin
     }
     g->has_skin_data = has_skin;
     g->obj_ok = obj_ok;
+    g->uni_col = nv > 0;
+    for (uint64_t i = 0; i < nv && g->uni_col; ++i)
+        g->uni_col = vin[i].cr == vin[0].cr && vin[i].cg == vin[0].cg && vin[i].cb == vin[0].cb;
+    if (g->uni_col) { g->ucol[0] = vin[0].cr; g->ucol[1] = vin[0].cg; g->ucol[2] = vin[0].cb; }
     if ((rc = grow(g->d_vin, g->cap_vin, std::max<uint64_t>(nv, 1)))) return rc;
     if (nv) HIP_TRY(hipMemcpy(g->d_vin, vin.data(), nv * sizeof(TriVsIn), hipMemcpyHostToDevice));
     {  // the object-space streams of vary_obj frames: positions (k_vertex) and 36-B attribute records (k_raster)
@@ -1208,6 +1216,8 @@ int tri_render(tri_ctx* c) {
     fp.vary_obj = fp.vary36 && c->draw0_obj ? 1u : 0u;
     fp.obj_xform = fp.vary_obj && c->draw0_xform ? 1u : 0u;
     fp.vin_base = fp.vary_obj ? (uint32_t)((int64_t)c->draw0.base_vertex + (int64_t)c->draw0.min_index) : 0u;
+    fp.obj_ucol = TRI_UCOL && fp.vary_obj && c->draw0_ucol ? 1u : 0u;
+    if (fp.obj_ucol) std::memcpy(fp.ucol, c->geom->ucol, sizeof fp.ucol);
     fp.ovf_rec_cap = c->ovf_rec_cap;
     fp.ovf_vert_cap = c->ovf_vert_cap;
     fp.bin_cap = c->bin_cap;
