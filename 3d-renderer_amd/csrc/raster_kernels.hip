@@ -1030,6 +1030,10 @@ __device__ __forceinline__ void bin_pair_box(const TriDeviceBuffers& b, BinBox& 
 template <bool WITH_SHADOW, bool ONE>
 __device__ __forceinline__ void setup_body(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t bid,
                                            uint32_t nblk) {
+    if constexpr (WITH_SHADOW) {  // the map to 1.0 before k_shadow_raster's parts merge into it (coalesced stores)
+        const uint32_t nt = fp.s_size * fp.s_size;
+        for (uint32_t i = bid * TRI_BLOCK + threadIdx.x; i < nt; i += nblk * TRI_BLOCK) b.shadow_map[i] = 0x3F800000u;
+    }
     __shared__ uint32_t red[2];
     __shared__ float clip_poly[kWavesPerBlock][2 * TRI_MAX_CLIP_VERTS * kClipStride];
     // Frames with a few draws: each draw's primitive base, first index, slot offset and cluster base
@@ -2827,6 +2831,9 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
 template <bool EXACT, int BL, bool SHADOW>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? (SHADOW ? (EXACT ? 5 : TRI_RASTER_WAVES_SHADOW) : TRI_RASTER_WAVES) : 3))) void k_raster(TRI_KARGS) {
     TRI_BIND_ARGS;
+    if constexpr (SHADOW)  // the map bins' counts for the next frame (k_shadow_raster's parts only read them)
+        for (uint32_t i = blockIdx.x * TRI_BLOCK + threadIdx.x; i < fp.s_nbins; i += gridDim.x * TRI_BLOCK)
+            b.sbin_count[i] = 0u;
     raster_bin<EXACT, BL, SHADOW>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
 // Frames without the shadow pre-pass: this instantiation lives in its own translation unit
@@ -2968,32 +2975,49 @@ __device__ __forceinline__ void shadow_span(const TriFrameParams& fp, const TriR
     }
 }
 
+// The map's bins are very uneven (C5: 1294 of 4096 hold casters, 773 on average, 4042 at most — the light sees
+// the grid at a grazing angle), and one workgroup per bin made the heaviest bins the whole kernel. Each bin now
+// has TRI_SHADOW_PARTS workgroups: part p takes the bin's entries in blocks of 256, every TRI_SHADOW_PARTS-th block,
+// into its own LDS tile. A bin with one block keeps one workgroup and stores its tile; with more, every part
+// atomicMin's the texels it covered into the map, which k_setup<true> cleared to 1.0 (k_raster zeroes the bins'
+// counts for the next frame: the parts of a bin cannot tell which of them reads its count last).
+#ifndef TRI_SHADOW_PARTS
+#define TRI_SHADOW_PARTS 4
+#endif
 #ifndef TRI_RASTER_PLAIN_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TRI_KARGS) {
     TRI_BIND_ARGS;
     constexpr int BIN = 32;
+    constexpr uint32_t kParts = TRI_SHADOW_PARTS;
     __shared__ uint32_t dep[BIN * BIN];
     __shared__ uint32_t bigq[kBigQueue];
     __shared__ uint32_t nbig, nentries;
     const int tid = threadIdx.x;
-    const int bin = xcd_bin(blockIdx.x, (int)fp.s_nbins);
+    // parts of one bin lie s_nbins workgroups apart: the same XCD (s_nbins is a multiple of 8) and its L2
+    const uint32_t part = blockIdx.x / fp.s_nbins;
+    const int bin = xcd_bin((int)(blockIdx.x - part * fp.s_nbins), (int)fp.s_nbins);
     const int32_t S = (int32_t)fp.s_size;
     const int32_t ox = (bin % (int)fp.s_nbx) * BIN, oy = (bin / (int)fp.s_nbx) * BIN;
     const int32_t bw = min(BIN, S - ox), bh = min(BIN, S - oy);
-    for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) dep[i] = 0x3F800000u;  // clear 1.0
     if (tid == 0) {
         nbig = 0;
         const uint32_t cnt = b.sbin_count[bin];
-        b.sbin_count[bin] = 0;  // consumed: ready for the next frame
-        if (cnt > fp.s_bin_cap) note_shadow_bin_overflow(b, cnt);
+        if (cnt > fp.s_bin_cap && part == 0) note_shadow_bin_overflow(b, cnt);
         nentries = min(cnt, fp.s_bin_cap);
     }
     __syncthreads();
-    const uint32_t* queue = b.sbin_list + (size_t)bin * fp.s_bin_cap;
     const uint32_t n = nentries;
+    // nothing for this part (the map is already 1.0 there: k_setup<true> cleared it — unless the frame had no
+    // primitives, no k_setup, and part 0 writes the empty tile itself)
+    const bool store_empty = part == 0 && fp.nchunks == 0;
+    if (n <= part * (uint32_t)TRI_BLOCK && !store_empty) return;
+    for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) dep[i] = 0x3F800000u;  // clear 1.0
+    __syncthreads();
+    const uint32_t* queue = b.sbin_list + (size_t)bin * fp.s_bin_cap;
     const int share = n <= (uint32_t)(TRI_BLOCK / TRI_SHADOW_SHARE) ? TRI_SHADOW_SHARE : 1;
     const int sub = tid % share;
-    for (uint32_t i = tid / share; i < n; i += TRI_BLOCK / share) {
+    const uint32_t step = share > 1 ? (uint32_t)(TRI_BLOCK / share) : (uint32_t)TRI_BLOCK * kParts;
+    for (uint32_t i = tid / share + part * (uint32_t)TRI_BLOCK; i < n; i += step) {
         const uint32_t ri = queue[i];
         const TriRec r = load_shadow_entry(fp, b, ri);
         int32_t cx0, cx1, cy0, cy1;
@@ -3036,9 +3060,14 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TRI_KARGS) {
         }
     }
     __syncthreads();
+    const bool alone = n <= (uint32_t)TRI_BLOCK || kParts == 1 || store_empty;  // one part: its tile is the bin's
     for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) {
         const int32_t ly = i >> 5, lx = i & 31;
-        if (lx < bw && ly < bh) b.shadow_map[(size_t)(oy + ly) * S + ox + lx] = dep[i];
+        if (lx < bw && ly < bh) {
+            const size_t o = (size_t)(oy + ly) * S + ox + lx;
+            if (alone) b.shadow_map[o] = dep[i];
+            else if (dep[i] != 0x3F800000u) atomicMin(&b.shadow_map[o], dep[i]);  // depth bits order as integers
+        }
     }
 }
 #endif  // TRI_RASTER_PLAIN_TU
@@ -3134,7 +3163,7 @@ void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan) {
         add(k, g, t, kStageSetup);
     }
     if (fp.shadow_on)  // the map's depth raster, before the frame's raster samples it
-        add(F(k_shadow_raster), dim3(fp.s_nbins), t, kStageShadow);
+        add(F(k_shadow_raster), dim3(fp.s_nbins * TRI_SHADOW_PARTS), t, kStageShadow);
     const void* r;
     if (fp.bin_log2 == 5) r = fp.exact_shading ? raster_kernel<true, 5>(fp) : raster_kernel<false, 5>(fp);
     else if (fp.bin_log2 == 4) r = fp.exact_shading ? raster_kernel<true, 4>(fp) : raster_kernel<false, 4>(fp);

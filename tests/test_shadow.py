@@ -235,3 +235,27 @@ def test_gpu_c5_full_4k_textures_and_shadow(oracle, mode):
     flags = abi.TRI_FLAG_EXACT_SHADING if mode == "exact" else 0
     om = assert_shadow_parity(s, oracle, flags, min_covered=3840 * 2160 // 2)
     assert (om != 0x3F800000).sum() > 100000
+
+
+@pytest.mark.gpu
+def test_gpu_shadow_map_refreshed_every_frame(oracle):
+    """The map is rebuilt from scratch each frame: after a frame without any draw it is all 1.0 (no caster, no
+    set-up pass), and the next frame with casters matches the oracle again (the bins' counts were reset)."""
+    from trident_raster import raster, scenes
+
+    s = sc.shadow_scene(oracle, 256, 192, 256)
+    om = np.zeros((s.shadow.size, s.shadow.size), np.uint32)
+    oracle.render(s, shadow_map_out=om)
+    with raster.TriRaster(s.width, s.height) as r:
+        scenes.load_scene(r, s)
+        r.render_frame()
+        first = r.read_shadow_map()
+        r.set_draws([])
+        r.render_frame()
+        empty = r.read_shadow_map()
+        r.set_draws(s.draws)
+        r.render_frame()
+        again = r.read_shadow_map()
+    assert np.array_equal(first, om) and (om != 0x3F800000).sum() > 1000
+    assert (empty == 0x3F800000).all()
+    assert np.array_equal(again, om)
