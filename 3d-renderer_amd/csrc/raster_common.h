@@ -2,6 +2,8 @@
 // HBM layout:
 //   VsIn      48 B/vertex  {pos.xyz, normal.xyz, color.xyz, uv.xy, pad} (the 44 B of the 100-byte
 //                          Trident Vertex that reach the output; Vertex.h:9-78)
+//   vpos      12 B/vertex  position stream, vattr 36 B/vertex {pos, normal, colour}: the same vertices split for
+//                          vary_obj frames (k_vertex reads only vpos; the fragment stage gathers vattr records)
 //   VsSkin    32 B/vertex  {bone indices, bone weights}, only when any draw has BoneCount > 0
 //   clip      16 B/slot    float4 clip-space position per (draw, vertex) VS invocation; written only for
 //                          vertices with an outcode on draws with clip_from_world (the clipper recomputes the rest)
