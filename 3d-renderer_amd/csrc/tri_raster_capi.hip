@@ -14,6 +14,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <chrono>
 
 namespace {
 
@@ -1154,12 +1155,28 @@ int tri_bind_output(tri_ctx* c, void* color, void* depth) {
     return TRI_OK;
 }
 
+// Diagnostics builds only (-DTRI_HOST_TIMING): tri_render's host time split at its phase boundaries (entry,
+// current device, state checks and buffers, frame arguments, launches), read by tools/host_breakdown.py.
+#ifdef TRI_HOST_TIMING
+static double g_host_ns[5];
+static uint64_t g_host_calls;
+#define TRI_HSTAMP(k) const auto hs##k = std::chrono::steady_clock::now()
+extern "C" void tri_debug_host_times(double* out, int reset) {
+    for (int i = 0; i < 5; ++i) out[i] = g_host_calls ? g_host_ns[i] / (double)g_host_calls : 0.0;
+    if (reset) { for (double& x : g_host_ns) x = 0.0; g_host_calls = 0; }
+}
+#else
+#define TRI_HSTAMP(k) do { } while (0)
+#endif
+
 int tri_render(tri_ctx* c) {
+    TRI_HSTAMP(0);
     if (!c) return fail(TRI_E_INVALID, "tri_render: null context");
     if (!c->frame_set) return fail(TRI_E_STATE, "tri_render: tri_set_frame was not called");
     if (!c->draws.empty() && !c->geom->geometry_set) return fail(TRI_E_STATE, "tri_render: draws without geometry");
     int rc = make_current(c);
     if (rc) return rc;
+    TRI_HSTAMP(1);
     if ((rc = upload_texture_table(c))) return rc;
     if (c->geom->version != c->geom_seen) {  // (shared) geometry changed since the draws were resolved
         c->draws_dirty = true;
@@ -1179,6 +1196,7 @@ int tri_render(tri_ctx* c) {
     if ((rc = choose_bin_grid(c))) return rc;
     if ((rc = ensure_work_buffers(c))) return rc;
 
+    TRI_HSTAMP(2);
     TriLaunchArgs& ha = c->args;  // passed by value at launch: free to rewrite for the next frame
     TriFrameParams& fp = ha.fp;
     std::memset(&fp, 0, sizeof fp);
@@ -1327,10 +1345,18 @@ int tri_render(tri_ctx* c) {
     ts.shadow = fp.shadow_on != 0;
     TriFramePlan plan;
     tri_plan_frame(fp, plan);
+    TRI_HSTAMP(3);
     HIP_TRY(tri_run_plan(plan, ha, c->d_args, c->stream, ev));
     c->launched = true;
     if (timed) c->pending.push_back(ts);
     if (fp.shadow_on) c->shadow_rendered = true;
+#ifdef TRI_HOST_TIMING
+    const auto hs4 = std::chrono::steady_clock::now();
+    const std::chrono::steady_clock::time_point t[5] = {hs0, hs1, hs2, hs3, hs4};
+    for (int i = 0; i < 4; ++i) g_host_ns[i] += (double)std::chrono::duration_cast<std::chrono::nanoseconds>(t[i + 1] - t[i]).count();
+    g_host_ns[4] += (double)std::chrono::duration_cast<std::chrono::nanoseconds>(hs4 - hs0).count();
+    ++g_host_calls;
+#endif
     return TRI_OK;
 }
 
