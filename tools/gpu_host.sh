@@ -1,5 +1,6 @@
 #!/bin/bash
-# tri_render's host cost by phase (tools/host_breakdown.py on a TRI_HOST_TIMING build) under HIP runtime settings.
+# tri_render's host cost by phase (tools/host_breakdown.py) under HIP runtime settings. Build the diagnostics
+# library first: tools/build_variant.sh hostt -DTRI_HOST_TIMING
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" && mkdir -p gpurun_out
 L=3d-renderer_amd/lib/variants/hostt.so
 for setting in "" ROC_USE_FGS_KERNARG=0 ROC_USE_FGS_KERNARG=1 DEBUG_CLR_KERNARG_HDP_FLUSH_WA=0 DEBUG_CLR_KERNARG_HDP_FLUSH_WA=1 \
