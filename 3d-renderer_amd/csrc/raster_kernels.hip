@@ -18,6 +18,13 @@
 // default fast build (v_rcp/v_rsq/v_exp/v_log, hoisted frame constants), both within 1 LSB of the
 // oracle's UNORM8 output.
 #define TRI_KERNEL_TU 1  // device pointers in TriDeviceBuffers carry the global address space (raster_launch.h)
+// This file is compiled three times: raster_plain.hip (TRI_RASTER_PLAIN_TU: k_raster_plain), vertex_stage.hip
+// (TRI_VERTEX_TU: k_reset, k_vertex, k_vertex_band) and on its own (everything else, and the frame plan).
+#if defined(TRI_RASTER_PLAIN_TU) || defined(TRI_VERTEX_TU)
+#define TRI_MAIN_TU 0
+#else
+#define TRI_MAIN_TU 1
+#endif
 #include "raster_launch.h"
 
 #include <hip/hip_runtime.h>
@@ -297,12 +304,12 @@ __device__ __forceinline__ void reset_counters(TriCounters* c) {
     c->bin_entries = 0;  // `flags` / `bin_max` are sticky (cleared by the host)
 }
 
-#ifndef TRI_RASTER_PLAIN_TU
+#ifdef TRI_VERTEX_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_reset(TRI_FIRST_KARGS) {  // a frame with no vertex work
     if (threadIdx.x == 0) reset_counters(a_.b.counters);
     publish_args(a_, pub_);
 }
-#endif  // TRI_RASTER_PLAIN_TU
+#endif
 
 // The clip position, outcode and snap of a vertex at `world` (its clip position kept when the clipper needs it).
 __device__ __forceinline__ void store_snap(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot,
@@ -449,7 +456,7 @@ __device__ __forceinline__ bool cluster_visible(const TriFrameParams& fp, const 
 // box of its 256-slot vertex block (the clusters referencing it, precomputed at upload: one load) and,
 // unless the shadow pre-pass needs every caster, skips a block whose box misses the rows. A vertex of any
 // visible primitive is always transformed: its cluster's box lies inside the block's union box.
-#ifndef TRI_RASTER_PLAIN_TU
+#ifdef TRI_VERTEX_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_vertex(TRI_FIRST_KARGS) {
     TRI_BIND_FIRST_ARGS;
     publish_args(a_, pub_);
@@ -520,7 +527,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_vertex_band(TRI_FIRST_KARGS) {
         if (slot < fp.nslots) vertex_slot(fp, b, slot, dr, 0u);
     }
 }
-#endif  // TRI_RASTER_PLAIN_TU
+#endif
 
 // ------------------------------------------------------------------------------------------
 // tri_setup_bin
@@ -2984,7 +2991,7 @@ __device__ __forceinline__ void shadow_span(const TriFrameParams& fp, const TriR
 #ifndef TRI_SHADOW_PARTS
 #define TRI_SHADOW_PARTS 4
 #endif
-#ifndef TRI_RASTER_PLAIN_TU
+#if TRI_MAIN_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TRI_KARGS) {
     TRI_BIND_ARGS;
     constexpr int BIN = 32;
@@ -3070,7 +3077,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TRI_KARGS) {
         }
     }
 }
-#endif  // TRI_RASTER_PLAIN_TU
+#endif
 
 // ------------------------------------------------------------------------------------------
 // presentation blit (Renderer.cpp:5346-5361, vkCmdBlitImage with VK_FILTER_LINEAR): one lane per
@@ -3078,7 +3085,7 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_shadow_raster(TRI_KARGS) {
 // bilinearly over clamp-to-edge taps on UNORM values (b / 255), rounded to UNORM8. Same float
 // operation order as the oracle's blit_linear (bit-exact). Rows are coalesced per wave.
 // ------------------------------------------------------------------------------------------
-#ifndef TRI_RASTER_PLAIN_TU
+#if TRI_MAIN_TU
 __global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__ src, int32_t w, int32_t h,
                                                     uint32_t* __restrict__ dst, int32_t dw, int32_t dh, float sx,
                                                     float sy, const float* __restrict__ lut) {
@@ -3105,9 +3112,16 @@ __global__ __launch_bounds__(TRI_BLOCK) void k_blit(const uint32_t* __restrict__
     }
     dst[(size_t)y * dw + x] = out;
 }
-#endif  // TRI_RASTER_PLAIN_TU
+#endif
 
 }  // namespace
+
+#ifdef TRI_VERTEX_TU
+const void* tri_vertex_stage_kernel(TriFrontKernel k) {
+    auto f = [](auto kernel) { return reinterpret_cast<const void*>(kernel); };
+    return k == kFrontVertex ? f(k_vertex) : k == kFrontBand ? f(k_vertex_band) : f(k_reset);
+}
+#endif
 
 #ifdef TRI_RASTER_PLAIN_TU
 const void* tri_raster_plain_kernel(const TriFrameParams& fp) {
@@ -3133,7 +3147,9 @@ extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {  // 
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
-#else  // the main translation unit
+#endif  // TRI_RASTER_PLAIN_TU
+
+#if TRI_MAIN_TU
 hipError_t tri_kernels_init() { return hipSuccess; }
 
 template <bool EXACT, int BL>
@@ -3149,13 +3165,13 @@ void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan) {
     const dim3 t(TRI_BLOCK);
     if (fp.nslots > 0 && fp.cull_vertex && fp.one_draw)
         // one workgroup per four vertex blocks (TRI_VBLOCK == TRI_BLOCK slots each)
-        add(F(k_vertex_band), dim3((fp.nslots + 4u * TRI_VBLOCK - 1) / (4u * TRI_VBLOCK)), t, kStageVertex);
+        add(tri_vertex_stage_kernel(kFrontBand), dim3((fp.nslots + 4u * TRI_VBLOCK - 1) / (4u * TRI_VBLOCK)), t, kStageVertex);
     else if (fp.nslots > 0)
         // with cluster culling every (draw, cluster) flag needs a lane, even when a mesh has fewer vertices
-        add(F(k_vertex), dim3(((fp.cull_on && fp.ncl_total > fp.nslots ? fp.ncl_total : fp.nslots) + TRI_BLOCK - 1) / TRI_BLOCK),
+        add(tri_vertex_stage_kernel(kFrontVertex), dim3(((fp.cull_on && fp.ncl_total > fp.nslots ? fp.ncl_total : fp.nslots) + TRI_BLOCK - 1) / TRI_BLOCK),
             t, kStageVertex);
     else
-        add(F(k_reset), dim3(1), dim3(TRI_BLOCK), kStageVertex);
+        add(tri_vertex_stage_kernel(kFrontReset), dim3(1), dim3(TRI_BLOCK), kStageVertex);
     if (fp.nchunks > 0) {  // with the pre-pass, one set-up pass bins each primitive for the frame and the map
         const dim3 g(fp.setup_multi ? (fp.nchunks + 3u) / 4u : fp.nchunks);
         const void* k = fp.shadow_on ? (fp.one_draw ? F(k_setup<true, true>) : F(k_setup<true, false>))
@@ -3209,4 +3225,4 @@ extern "C" int tri_debug_setup_times(unsigned long long* out, int nslots) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tri_setup_phase), n, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 #endif
-#endif  // TRI_RASTER_PLAIN_TU
+#endif

@@ -96,6 +96,10 @@ struct TriFramePlan {
 void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan);
 // k_raster_plain's instantiation for a frame without the shadow pre-pass (raster_plain.hip)
 const void* tri_raster_plain_kernel(const TriFrameParams& fp);
+// The frame's first kernel (vertex_stage.hip): k_vertex, k_vertex_band (row bands with cluster culling) or k_reset
+// (a frame without vertex work)
+enum TriFrontKernel { kFrontVertex = 0, kFrontBand, kFrontReset };
+const void* tri_vertex_stage_kernel(TriFrontKernel k);
 
 // Event stamps of one frame, in launch order: vertex, setup (+ clip, + the shadow map binning), shadow-map
 // raster (only with the pre-pass), raster, end.
