@@ -709,15 +709,25 @@ def cpu_baseline(scene, seconds):
                       f"({scene.triangles} tris) rendered by oracle/tri_oracle.cpp, {dt:.1f} s"}
 
 
-def pmc_kernel(workload, kernel):
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_summary.json")
+
+
+def pmc_kernel(workload, kernel, path=PMC_SUMMARY):
     """Per-launch PMC means of one kernel from the committed rocprofv3 summary (profiles/pmc_summary.json,
-    written by tools/prof_summary.py from tools/profile.sh's passes), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    written by tools/prof_summary.py from tools/profile.sh's passes), or None. The file must travel with the
+    tree to the GPU box (.gpurunignore may not exclude it: round 4 lost roofline.traffic that way), so a
+    missing or unreadable summary, or one without this workload's kernel, is reported on stderr."""
     try:
         with open(path) as f:
-            return json.load(f).get(workload, {}).get(kernel)
-    except (OSError, ValueError):
+            entry = json.load(f).get(workload, {}).get(kernel)
+    except (OSError, ValueError) as e:
+        print(f"bench.py: WARNING: no PMC summary ({path}: {e}); roofline.traffic and roofline_valu will be null",
+              file=sys.stderr, flush=True)
         return None
+    if entry is None:
+        print(f"bench.py: WARNING: {path} has no {kernel} entry for {workload}; roofline.traffic and roofline_valu "
+              "will be null", file=sys.stderr, flush=True)
+    return entry
 
 
 # CDNA4 VALU issue: a wave64 vector instruction occupies its SIMD for 2 cycles (MI355X_MICROARCH.md),
@@ -736,6 +746,15 @@ def valu_roofline(pmc, kernel_ms):
             "achieved": achieved / 1e9, "peak": VALU_PEAK_WAVE_INSTS / 1e9, "unit": "G wave-instructions/s",
             "frac": achieved / VALU_PEAK_WAVE_INSTS,
             "source": "profiles/pmc_summary.json SQ_INSTS_VALU / roofline.kernel_ms"}
+
+
+def valu_floor_frac(pmc, raster_bytes):
+    """The HBM fraction k_raster could reach if it ran at the VALU issue peak: its algorithmic bytes over the
+    time its SQ_INSTS_VALU take at VALU_PEAK_WAVE_INSTS (the cap the VALU work alone puts on roofline.frac)."""
+    if not pmc or "SQ_INSTS_VALU" not in pmc:
+        return None
+    floor_s = float(pmc["SQ_INSTS_VALU"]) / VALU_PEAK_WAVE_INSTS
+    return raster_bytes / floor_s / 1e9 / HBM_PEAK_GBS
 
 
 def stage_ms(timing):
@@ -921,8 +940,12 @@ def main():
                        "split_autotune": split_log},
             "mpix_per_s": fps * W * H / 1e6,
             "latency_ms": latency,
+            # the contract prices k_raster against HBM; what actually binds it is VALU issue together with the
+            # L1 gather path (the VALU floor alone caps this frac near 0.17), see roofline_valu
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
+                         "binding": "valu issue + TA/TD gather path (roofline_valu), not HBM bytes",
+                         "valu_floor_frac": valu_floor_frac(pmc if br.rows == H else None, raster_bytes),
                          "measured_copy_GBs": copy_gbs,
                          "kernel": "k_raster",
                          "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]) if timing else 0,
