@@ -171,9 +171,12 @@ struct TriCounters {  // per-frame fields are zeroed before every frame; `flags`
 struct TriShadeConst {
     float cam[4];
     float base[4];        // MaterialUniformBuffer[0].BaseColorFactor
-    float metallic, roughness, amb_strength, pad0;
+    float metallic, roughness, amb_strength;
+    float om;             // the fast build's 0.04 (1 - metallic), F0's dielectric term
     float amb[4];         // AmbientColorIntensity.rgb * .w
-    uint32_t has_sun, npt, pad1, pad2;
+    uint32_t has_sun, npt;
+    uint32_t a8;          // ONE frames: the fragment alpha sbt[3] as its UNORM8 byte (uniform)
+    float kd;             // (1 - metallic) / pi, the diffuse factor
     float sun_l[4];       // normalize(-DirectionalLightDirection)
     float sun_rad[4];     // DirectionalLightColor.rgb * .w
     // per point light, position and radiance side by side: the light loop reads one 32-B record per light
@@ -192,7 +195,9 @@ struct TriShadeConst {
     float sbt[4];
     // G_L's denominator divided through by 1 - k (the fast build's per-light v_fma becomes one add):
     // k / (1 - k) and a2 / pi / (1 - k), so NDF * G_L * G_V keeps its value
-    float kgo, a2pio, pad3[2];
+    // and spec_num's uniform factors 0.25 a2pio (spA / rgV) and 1e4 a2pio (spB / (NdotV rgV)); the host folds every
+    // frame constant the fragment stage would otherwise form per pixel from scalars (no SALU float ops on gfx950)
+    float kgo, a2pio, spAk, spBk;
     // the fast build's ONE frames (sbt uniform): albedo = sbt * vertex colour is never formed; F0, the diffuse
     // factor and the ambient term come straight from the colour with these folded factors: sbt * metallic,
     // sbt * (1 - metallic) / pi and (ambient * sbt) * ambient strength

@@ -1863,20 +1863,19 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         albz = ((f.sz * sc.base[2]) * f.tz) * f.cz;
     }
     const float m = sc.metallic;
-    const float om = 0.04f * (1.0f - m);
+    const float om = sc.om;
     px.F0xy = pk_fma(albxy, splat(m), splat(om));
     px.F0z = __builtin_fmaf(albz, m, om);
     px.omF0xy = splat(1.0f) - px.F0xy;
     px.omF0z = 1.0f - px.F0z;
-    const float kd = (1.0f - m) * (1.0f / kPi);
+    const float kd = sc.kd;
     px.diffKxy = albxy * splat(kd);
     px.diffKz = albz * kd;
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
     const float rgV = frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
-    const float gVa = sc.a2pio * (NdotV * rgV);  // a2 / pi * G_V / (1 - k)
-    px.spA = (0.25f * sc.a2pio) * rgV;
-    px.spB = 1e4f * gVa;
+    px.spA = sc.spAk * rgV;                   // 0.25 a2 / pi / (1 - k) / max(G_V's denominator, 1e-4)
+    px.spB = sc.spBk * (NdotV * rgV);         // 1e4 a2 / pi * G_V / (1 - k)
     f2v cxy = (f2v{sc.amb[0], sc.amb[1]} * albxy) * splat(sc.amb_strength);
     float cz = (sc.amb[2] * albz) * sc.amb_strength;
     if (kAblate & 64) return make_float4(cxy.x, cxy.y, cz, 1.0f);  // diagnostics: 64 = no lights
@@ -1904,7 +1903,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.N = fnorm(fnrm(f));
     px.V = fnorm(sub3(mk(sc.cam[0], sc.cam[1], sc.cam[2]), fworld(f)));
     const float m = sc.metallic;
-    const float om = 0.04f * (1.0f - m);
+    const float om = sc.om;  // 0.04 (1 - metallic), folded on the host with the other frame constants
     f3 c;
     if (ONE && TRI_ONE_FOLD) {  // albedo = sbt * colour: every term from the colour and a folded factor (TriShadeConst::sbtm)
         const f3 col = fvcol(f);
@@ -1916,7 +1915,7 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
         const f3 albedo = ONE ? mul(mk(sc.sbt[0], sc.sbt[1], sc.sbt[2]), fvcol(f))
                               : mul(mul(mul(ftex(f), mk(sc.base[0], sc.base[1], sc.base[2])), ftint(f)), fvcol(f));
         px.F0 = mk(__builtin_fmaf(albedo.x, m, om), __builtin_fmaf(albedo.y, m, om), __builtin_fmaf(albedo.z, m, om));
-        px.diffK = muls(albedo, (1.0f - m) * (1.0f / kPi));
+        px.diffK = muls(albedo, sc.kd);
         c = mk(sc.amb[0] * albedo.x * sc.amb_strength, sc.amb[1] * albedo.y * sc.amb_strength,
                sc.amb[2] * albedo.z * sc.amb_strength);
     }
@@ -1924,9 +1923,8 @@ __device__ __forceinline__ float4 fs_fast(const TriShadeConst& sc, const Frag& f
     px.NdotVr = fdot(px.N, px.V);
     const float NdotV = fmaxf(px.NdotVr, 0.0f);
     const float rgV = frcp(fmaxf(__builtin_fmaf(NdotV, sc.omkg, sc.kg), 1e-4f));
-    const float gVa = sc.a2pio * (NdotV * rgV);  // a2 / pi * G_V / (1 - k)
-    px.spA = (0.25f * sc.a2pio) * rgV;
-    px.spB = 1e4f * gVa;
+    px.spA = sc.spAk * rgV;                   // 0.25 a2 / pi / (1 - k) / max(G_V's denominator, 1e-4)
+    px.spB = sc.spBk * (NdotV * rgV);         // 1e4 a2 / pi * G_V / (1 - k)
     if (kAblate & 64) return make_float4(c.x, c.y, c.z, 1.0f);  // diagnostics: 64 = no lights
     if (sc.has_sun && f.vis > 0.0f) {  // vis = 0 (fully shadowed): the sun adds exactly nothing
         const f3 L = mk(sc.sun_l[0], sc.sun_l[1], sc.sun_l[2]);
@@ -2529,7 +2527,7 @@ __device__ __forceinline__ uint32_t shade_bgra(const TriFrameParams& fp, const F
         return unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
     }
     const float4 c = fs_fast<ONE>(fp.sc, f);
-    return fast_bgra(c.x, c.y, c.z, unorm8(c.w));
+    return fast_bgra(c.x, c.y, c.z, ONE ? fp.sc.a8 : unorm8(c.w));  // ONE: the uniform alpha byte, host-folded
 }
 
 #ifndef TRI_CLIP_DEFER

@@ -101,6 +101,7 @@ struct tri_ctx {
     int device = 0;
     int32_t W = 0, H = 0, y0 = 0, y1 = 0, nbx = 0, nby = 0, nbins = 0;
     int cu_count = 256;  // compute units of the device (k_setup's grid sizing)
+    uint32_t last_path = 0;  // tri_frame_stats.path of the last frame built
     hipStream_t own_stream = nullptr;
     hipStream_t stream = nullptr;
 
@@ -272,6 +273,10 @@ void shade_constants(const tri_global_ubo& g, const tri_material_record& m, TriS
     sc.omkg = 1.0f - sc.kg;
     sc.kgo = sc.kg / sc.omkg;     // omkg >= 0.5 (k <= 0.5 for roughness <= 1)
     sc.a2pio = sc.a2pi / sc.omkg;
+    sc.spAk = 0.25f * sc.a2pio;
+    sc.spBk = 1e4f * sc.a2pio;
+    sc.om = 0.04f * (1.0f - sc.metallic);
+    sc.kd = (1.0f - sc.metallic) * (1.0f / 3.14159265359f);
     for (int i = 0; i < 3; ++i) sc.amb[i] = g.ambient_color_intensity[i] * g.ambient_color_intensity[3];
     sc.has_sun = g.light_counts[0] > 0u ? 1u : 0u;
     const float lx = -g.directional_light_direction[0], ly = -g.directional_light_direction[1],
@@ -1236,6 +1241,9 @@ int tri_render(tri_ctx* c) {
     fp.vin_base = fp.vary_obj ? (uint32_t)((int64_t)c->draw0.base_vertex + (int64_t)c->draw0.min_index) : 0u;
     fp.obj_ucol = TRI_UCOL && fp.vary_obj && c->draw0_ucol ? 1u : 0u;
     if (fp.obj_ucol) std::memcpy(fp.ucol, c->geom->ucol, sizeof fp.ucol);
+    c->last_path = (fp.shade_solid ? TRI_PATH_ONE_DRAW : 0u) | (fp.vary_obj ? TRI_PATH_VARY_OBJ : 0u) |
+                   (fp.obj_xform ? TRI_PATH_OBJ_XFORM : 0u) | (fp.obj_ucol ? TRI_PATH_OBJ_UCOL : 0u) |
+                   (c->shadow.size ? TRI_PATH_SHADOW : 0u);
     fp.ovf_rec_cap = c->ovf_rec_cap;
     fp.ovf_vert_cap = c->ovf_vert_cap;
     fp.bin_cap = c->bin_cap;
@@ -1285,7 +1293,8 @@ int tri_render(tri_ctx* c) {
         std::memcpy(fp.sc.tint, c->shade0.tint, 16);
         for (int i = 0; i < 3; ++i) fp.sc.sbt[i] = (fp.sc.solid[i] * fp.sc.base[i]) * fp.sc.tint[i];
         fp.sc.sbt[3] = (fp.sc.base[3] * fp.sc.tint[3]) * fp.sc.solid[3];
-        const float kd = (1.0f - fp.sc.metallic) * (1.0f / 3.14159265359f);
+        fp.sc.a8 = (uint32_t)(int)(std::fmin(std::fmax(fp.sc.sbt[3], 0.0f), 1.0f) * 255.0f + 0.5f);  // unorm8
+        const float kd = fp.sc.kd;
         for (int i = 0; i < 3; ++i) {
             fp.sc.sbtm[i] = fp.sc.sbt[i] * fp.sc.metallic;
             fp.sc.sbtkd[i] = fp.sc.sbt[i] * kd;
@@ -1471,6 +1480,7 @@ int tri_get_frame_stats(tri_ctx* c, tri_frame_stats* out) {
     out->bins_x = (uint32_t)c->nbx;
     out->bins_y = (uint32_t)c->nby;
     out->bin_size = 1u << c->bin_log2;
+    out->path = c->last_path;
     return TRI_OK;
 }
 

@@ -156,8 +156,16 @@ typedef struct tri_frame_stats {
     uint64_t triangles_clipped; /* primitives that went through geometric clipping */
     uint64_t bin_entries;       /* (triangle, bin) pairs                           */
     uint64_t vertices_shaded;   /* vertex-shader invocations                       */
-    uint32_t bins_x, bins_y, bin_size, reserved;
+    uint32_t bins_x, bins_y, bin_size;
+    uint32_t path;              /* TRI_PATH_* bits: the fragment path the last frame took (diagnostics) */
 } tri_frame_stats;
+
+/* tri_frame_stats.path bits */
+#define TRI_PATH_ONE_DRAW   0x1u  /* one draw over a 1x1 texture slot: the single-draw solid instantiation */
+#define TRI_PATH_VARY_OBJ   0x2u  /* object-space varyings (no per-frame varying writes)                   */
+#define TRI_PATH_OBJ_XFORM  0x4u  /* ... carried through a non-identity model / normal matrix per pixel     */
+#define TRI_PATH_OBJ_UCOL   0x8u  /* ... one vertex colour for the whole geometry                           */
+#define TRI_PATH_SHADOW    0x10u  /* the shadow-map pre-pass ran                                            */
 
 /* Shadow-map pre-pass (BASELINE.json config 5). The reference reserves the switch
  * (LightComponent::m_ShadowCaster, Trident/src/ECS/Components/LightComponent.h:33) but renders no shadow
