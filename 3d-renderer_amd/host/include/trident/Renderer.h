@@ -242,6 +242,8 @@ private:
     tri_group* m_PresentGroup = nullptr;   // ... or multi-device viewport
     ViewportContext m_LegacyTarget;        // the legacy path's present-extent target (no active viewport)
     bool m_PresentLegacy = false;          // the last present was rendered directly (legacy path), not blitted
+    // the extent the last present was produced at (SetPresentExtent may change before ReadPresentPixels)
+    uint32_t m_PresentedWidth = 0, m_PresentedHeight = 0;
     uint32_t m_RasterFlags = 0;
 
     glm::vec3 m_AmbientColor{0.03f};

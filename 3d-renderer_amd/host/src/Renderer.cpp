@@ -983,6 +983,7 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     m_PresentSource = nullptr;
     m_PresentGroup = nullptr;
     m_PresentLegacy = false;
+    m_PresentedWidth = m_PresentedHeight = 0;
     ViewportContext* legacy = nullptr;
     if (!primaryActive && m_PresentWidth && m_PresentHeight) {
         m_LegacyTarget.m_Info.Size = glm::vec2((float)m_PresentWidth, (float)m_PresentHeight);
@@ -1011,6 +1012,8 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
             m_PresentSource = vc->m_Ctx;
             m_PresentGroup = vc->m_Group;
             m_PresentLegacy = true;
+            m_PresentedWidth = (uint32_t)vc->m_Info.Size.x;  // the target PrepareViewport sized
+            m_PresentedHeight = (uint32_t)vc->m_Info.Size.y;
         }
     }
     // Primary viewport -> swapchain image, VK_FILTER_LINEAR (Renderer.cpp:5346-5361).
@@ -1019,6 +1022,8 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
         if (t.Blit(m_PresentWidth, m_PresentHeight) == TRI_OK && t.Sync() == TRI_OK) {
             m_PresentSource = active->second.m_Ctx;
             m_PresentGroup = active->second.m_Group;
+            m_PresentedWidth = m_PresentWidth;  // the blit's destination extent
+            m_PresentedHeight = m_PresentHeight;
         } else {
             LogError("present blit", tri_last_error());
         }
@@ -1087,7 +1092,9 @@ bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgb
 
 bool Renderer::ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height) {
     if (!m_PresentSource && !m_PresentGroup) return false;
-    std::vector<uint8_t> bgra((size_t)m_PresentWidth * m_PresentHeight * 4);
+    // sized from the extent the present was produced at, not the current SetPresentExtent (a resize between
+    // DrawFrame and this read would otherwise under-size the buffer the readback fills)
+    std::vector<uint8_t> bgra((size_t)m_PresentedWidth * m_PresentedHeight * 4);
     const Target t{m_PresentSource, m_PresentGroup};
     if ((m_PresentLegacy ? t.Readback(bgra.data(), nullptr) : t.ReadPresent(bgra.data())) != TRI_OK) {
         LogError("present readback", tri_last_error());
@@ -1100,8 +1107,8 @@ bool Renderer::ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, ui
         rgba[i + 2] = bgra[i + 0];
         rgba[i + 3] = bgra[i + 3];
     }
-    width = m_PresentWidth;
-    height = m_PresentHeight;
+    width = m_PresentedWidth;
+    height = m_PresentedHeight;
     return true;
 }
 

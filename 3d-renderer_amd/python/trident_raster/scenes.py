@@ -402,6 +402,27 @@ def scene_c3_grid(width=3840, height=2160, n=708, skybox=None):
                  materials=[((1.0, 1.0, 1.0, 1.0), (0.1, 0.6, 1.0, 0.0))], skybox=_sky(skybox))
 
 
+# The C3 grid as a Forge entity would hand it over: a non-identity ComposeTransform (Renderer.cpp:417-427) —
+# 20 deg of yaw and a uniform 0.95 scale, translated so that the grid's centre (0, 0, -5) stays in place.
+C3_TRS_YAW, C3_TRS_SCALE = 20.0, 0.95
+
+
+def c3_trs_model():
+    th = np.radians(C3_TRS_YAW)
+    s = C3_TRS_SCALE
+    pos = (5.0 * s * np.sin(th), 0.0, -5.0 + 5.0 * s * np.cos(th))
+    return compose_transform(pos, (0.0, C3_TRS_YAW, 0.0), (s, s, s))
+
+
+def scene_c3_trs(width=3840, height=2160, n=708, skybox=None):
+    """C3 under a translate + yaw + uniform-scale draw (the general object-space path: the fragment stage carries
+    the interpolated position and normal through the model and normal matrices) instead of an identity model."""
+    s = scene_c3_grid(width, height, n, skybox)
+    s.draws = [abi.make_draw(0, c3_trs_model(), material_index=0)]
+    s.name = f"c3trs_grid1m_{width}x{height}"
+    return s
+
+
 def procedural_texture(size, seed):
     """A seeded RGBA8 sRGB texture (bands + noise), opaque: every bilinear tap differs."""
     rng = np.random.default_rng(seed)

@@ -30,6 +30,8 @@ def build_scene(name):
 
     if name == "c3":
         return scenes.scene_c3_grid(3840, 2160, 708)
+    if name == "c3trs":  # the C3 grid under a translate + yaw + uniform-scale ComposeTransform (general path)
+        return scenes.scene_c3_trs(3840, 2160, 708)
     if name == "c2":
         return scenes.scene_c2_sphere(1920, 1080)
     if name == "c1":
@@ -491,7 +493,7 @@ class BandRenderer:
 # Frames in flight per config at N = 1 (round 4, same-box A/B of the whole bench line): the 1M-triangle 4K frame
 # hides more of its front end behind the other frames' raster at 3 (C3 +2.3 %), while C2 and C5 lose 9-11 % at 3
 # (their per-context buffers and the extra stream cost more than the overlap gains).
-DEFAULT_INFLIGHT = {"c3": 3, "c2": 2, "c5": 2, "c1": 2}
+DEFAULT_INFLIGHT = {"c3": 3, "c3trs": 3, "c2": 2, "c5": 2, "c1": 2}
 
 
 def split_candidates(height, world, min_rows=32, inflights=(2,)):
@@ -886,13 +888,16 @@ def main():
 
     secondary = {}
     if not args.no_secondary and args.config == "c3":
-        for key in ("c2", "c5"):  # the other BASELINE.json GPU configs, same timing protocol
+        # the other BASELINE.json GPU configs, same timing protocol, and C3's grid under a non-identity model matrix
+        # (how every Forge entity arrives: Renderer.cpp:417-427), so the headline's identity-draw path has its
+        # general-path cost beside it
+        for key in ("c2", "c5", "c3trs"):
             s2 = build_scene(key)
             (d2, k2), log2 = choose_split(s2)
             br2 = make_renderer(s2, d2, k2)
             # enough frames that the pipeline's fill and drain (about one frame latency, 50 us at C2, 280 us at C5)
             # stay under 1 % of the timed region whatever --steps the headline uses
-            n2 = max(args.steps, 200) if key == "c2" else max(args.steps, 100)
+            n2 = max(args.steps, 200) if key in ("c2", "c3trs") else max(args.steps, 100)
             dt2, t2, _ = timed_run(br2, n2, args.warmup, dist_on, warm_seconds=args.warm_seconds)
             fps2 = n2 / dt2
             st2 = stage_ms(t2)
@@ -900,6 +905,7 @@ def main():
                      "stage_ms": st2, "kernel_samples": int(t2["frames"]) if t2 else 0, "triangles": s2.triangles,
                      "algorithmic_bytes": s2.algorithmic_bytes(rows=br2.rows)}
             entry["frames_in_flight"] = k2
+            entry["fragment_path"] = br2.r.frame_stats()["path"]  # tri_frame_stats.path (TRI_PATH_* bits)
             if world > 1:
                 entry["bands"] = [y1 - y0 for y0, y1 in br2.bands]
                 entry["split_autotune"] = log2

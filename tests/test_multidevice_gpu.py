@@ -330,22 +330,33 @@ def test_group_staged_bands_packed_transfer(oracle, scene_name, group_flags, bpp
 
 @pytest.mark.skipif(_hip_device_count() < 2, reason="the RCCL branch of tri_group needs two HIP devices")
 @pytest.mark.parametrize("devices,display", [([0, 1, 0, 1], 0), ([1, 0, 1, 0, 1], 3)])
-def test_group_distinct_devices_rccl_assembly(oracle, devices, display):
-    """ADVICE r3: the cross-device branch of tri_group (ncclCommInitAll, grouped ncclSend/ncclRecv into the
-    rotating frame buffer, band buffers reused after asm_done). Four frames with different cameras; each
-    assembled frame equals the single-context render, and the k - 1 buffer stays untouched while frame k
-    renders. Skipped on a one-GPU box (runs on the driver's multi-GPU node)."""
-    from trident_raster import raster, scenes
+@pytest.mark.parametrize("no_pack", [False, True])
+def test_group_distinct_devices_rccl_assembly(oracle, devices, display, no_pack):
+    """ADVICE r3/r4: the cross-device branch of tri_group (ncclCommInitAll, grouped ncclSend/ncclRecv into the
+    rotating frame buffer, band buffers reused after asm_done), with the 3-byte band packing on (the default when
+    the frame's alpha is proven) and off (TRI_GROUP_NO_PACK). Four frames with different cameras; each assembled
+    frame equals the single-context render, the k - 1 buffer stays untouched while frame k renders, and
+    transfer_info reports the bytes per pixel and the display device's inbound bytes of the remote bands.
+    Skipped on a one-GPU box (runs on the driver's multi-GPU node)."""
+    from trident_raster import abi, raster, scenes
 
     frames = _camera_frames(oracle, [(0.0, 1.0, 6.0), (0.6, 1.3, 6.5), (-0.7, 0.8, 5.5), (0.2, 1.6, 7.0)])
     want = [_render_single(s, 0)[0] for s in frames]
-    with raster.TriGroup(320, 240, devices, display=display) as g:
+    with raster.TriRaster(320, 240, device=0) as r:
+        scenes.load_scene(r, frames[0])
+        alpha = r.frame_alpha()
+    bpp = 4 if (no_pack or alpha < 0) else 3
+    n, H, W = len(devices), 240, 320
+    inbound = sum(((k + 1) * H // n - k * H // n) * W * bpp for k in range(n) if devices[k] != devices[display])
+    with raster.TriGroup(320, 240, devices, display=display,
+                         group_flags=abi.TRI_GROUP_NO_PACK if no_pack else 0) as g:
         scenes.load_scene(g, frames[0])
         prev = None
         for k, s in enumerate(frames):
             g.set_frame(s.ubo, s.clear)
             g.render_frame()
             g.synchronize()
+            assert g.transfer_info() == (bpp, inbound)
             p, dev = g.frame_pointer()
             img = _copy_frame(p, dev, 320, 240)
             assert np.array_equal(img, want[k]), f"frame {k}: {int((img != want[k]).any(-1).sum())} pixels differ"

@@ -80,6 +80,22 @@ def test_c3_grid_720p(oracle, flags):
     assert_parity(sc.grid_c3(1280, 720, 200), oracle, min_covered=1280 * 720 // 2, flags=flags)
 
 
+def test_c3_trs_draw_720p(oracle, flags):
+    """The C3 grid (all 999,698 triangles) under bench.py's c3trs draw: translate + 20 deg yaw + uniform 0.95 scale
+    (ComposeTransform, Renderer.cpp:417-427). The fragment stage takes the general object-space path: the
+    interpolated position and normal carried through the model and normal matrices per pixel."""
+    from trident_raster import abi, raster, scenes
+
+    s = scenes.scene_c3_trs(1280, 720, 708)
+    assert_parity(s, oracle, min_covered=1280 * 720 // 2, flags=flags)
+    with raster.TriRaster(s.width, s.height, flags=flags) as r:
+        scenes.load_scene(r, s)
+        r.render_frame()
+        path = r.frame_stats()["path"]
+    want = abi.TRI_PATH_ONE_DRAW | abi.TRI_PATH_VARY_OBJ | abi.TRI_PATH_OBJ_XFORM
+    assert path & want == want, hex(path)
+
+
 def test_c3_full_4k_1m_triangles(oracle, flags):
     from trident_raster import scenes
 

@@ -173,3 +173,20 @@ def test_gpu_shim_legacy_present_without_viewport(oracle, exact):
     assert np.array_equal(a.read_present(400, 300),
                           oracle.blit_linear(vp1[..., [2, 1, 0, 3]], 400, 300)[..., [2, 1, 0, 3]])
     a.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("with_viewport", [False, True])
+def test_gpu_present_read_after_extent_change(with_viewport):
+    """a SetPresentExtent between DrawFrame and ReadPresentPixels (a window resize) must not change
+    the size of the image the read returns — it is the one the last present produced, legacy or blit."""
+    a = _legacy_app(with_viewport=with_viewport)
+    a.draw_frame()
+    before = a.read_present(400, 300)
+    a.set_present_extent(200, 150)  # smaller: the old code sized the host buffer from this
+    assert np.array_equal(a.read_present(400, 300), before)
+    with pytest.raises(Exception):
+        a.read_present(200, 150)
+    a.draw_frame()  # the next present is produced at the new extent
+    assert a.read_present(200, 150).shape == (150, 200, 4)
+    a.close()
