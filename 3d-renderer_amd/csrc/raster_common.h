@@ -1,7 +1,7 @@
 // raster_common.h — device-side data layout shared by the HIP kernels and the C-ABI host code.
 // HBM layout:
-//   VsIn      48 B/vertex  {pos.xyz, normal.xyz, color.xyz, uv.xy, pad} (the 44 B of the 100-byte
-//                          Trident Vertex that reach the output; Vertex.h:9-78)
+//   VsIn      48 B/vertex  {pos.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, pad} (the 44 B of the 100-byte
+//                          Trident Vertex that reach the output, Vertex.h:9-78, in the 48-B varying record's layout)
 //   vpos      12 B/vertex  position stream, vattr 36 B/vertex {pos, normal, colour}: the same vertices split for
 //                          vary_obj frames (k_vertex reads only vpos; the fragment stage gathers vattr records)
 //   VsSkin    32 B/vertex  {bone indices, bone weights}, only when any draw has BoneCount > 0
@@ -9,7 +9,8 @@
 //                          vertices with an outcode on draws with clip_from_world (the clipper recomputes the rest)
 //   snap      16 B/slot    {X (24-bit 8.8 fixed) | outcode << 24, Y, 1/w, z_ndc} (the fragment stage
 //                          loads the first 12 bytes: it needs no depth)
-//   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0}; 36 B/slot {world.xyz},
+//   vary      48 B/slot    {world.xyz, uv.x}, {normal.xyz, uv.y}, {color.xyz, 0} (VsIn's layout: obj48 frames read
+//                          the object-space input records with the same code); 36 B/slot {world.xyz},
 //                          {normal.xyz}, {color.xyz} on single-draw solid frames (TriFrameParams::vary36);
 //                          none but the clipper's polygon vertices (object space, 36 B) with vary_obj
 //   prim_vs   16 B/prim    {vertex slots 0..2, draw | clipped flag}, written by k_setup for the
@@ -44,6 +45,7 @@ static_assert(TRI_MAX_CLIP_POLY <= TRI_MAX_CLIP_VERTS, "clip polygon buffers");
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f
 #define TRI_MAX_PPT 8  // primitives per k_setup thread
+#define TRI_OBJ48_DRAWS 16  // draws a frame may hold for object-space varyings outside the ONE instantiation
 
 #ifndef TRI_SNAP_F
 #define TRI_SNAP_F 1
@@ -60,9 +62,9 @@ static_assert(TRI_MAX_CLIP_POLY <= TRI_MAX_CLIP_VERTS, "clip polygon buffers");
 #define TRI_OVF_SHADOW_BIN_LIST 0x8u
 
 struct __attribute__((aligned(16))) TriVsIn {
-    float px, py, pz, nx;
-    float ny, nz, cr, cg;
-    float cb, u, v, pad;
+    float px, py, pz, u;
+    float nx, ny, nz, v;
+    float cr, cg, cb, pad;
 };
 
 struct __attribute__((aligned(16))) TriVsSkin {
@@ -254,7 +256,21 @@ struct TriFrameParams {
     // imported white): the fragment stage takes the colour from here instead of three gathers and an interpolation
     uint32_t obj_ucol;
     float ucol[3];
+    // obj48 (frames outside the ONE instantiation — several draws, textures, the shadow pre-pass — whose every
+    // active draw is affine, unskinned, with a conformal normal matrix and an identity texture transform, over unit
+    // object normals, at most TRI_OBJ48_DRAWS draws): object-space varyings as well. k_vertex writes no varyings; the
+    // fragment stage gathers each vertex's 48-B input record {pos, n.x}{n.yz, colour.rg}{colour.b, uv} (TriVsIn,
+    // uploaded with the geometry) at slot + vdelta[draw] and, when obj48_xform (some draw has a non-identity model),
+    // carries the interpolated position and normal through its draw's model and normal matrices; the clipper writes
+    // its polygon vertices' records in the same layout.
+    uint32_t obj48, obj48_xform;
+    uint32_t vdelta[TRI_OBJ48_DRAWS];  // per draw: base_vertex + min_index - first slot (mod 2^32)
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
+    // Default.frag's AI frame blend (:182-191): on when AiBlendConfig.w > 0 and clamp(AiBlendConfig.x, 0, 1) > 0 (that
+    // clamped weight is ai_wgt); the frame texture is ai_tw x ai_th RGBA8 UNORM (TriDeviceBuffers::ai_frame), sampled at
+    // gl_FragCoord.xy * (ai_sx, ai_sy) = AiBlendConfig.yz
+    uint32_t ai_on, ai_tw, ai_th;
+    float ai_wgt, ai_sx, ai_sy;
     uint32_t shadow_on, s_size, s_nbx, s_nbins;
     uint32_t s_bin_cap;
     float s_hw;    // s_size / 2 (light NDC -> texel, the main pass's viewport transform)

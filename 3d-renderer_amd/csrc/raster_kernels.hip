@@ -176,10 +176,23 @@ struct F3 {
     float x, y, z;
 };
 __device__ __forceinline__ F3 ldF3(TRI_G const F3* p) { return F3{p->x, p->y, p->z}; }
-// Attribute j (0 position, 1 normal, 2 colour) of vertex record vin_base + slot, object space (vary_obj)
-__device__ __forceinline__ F3 vin_attr(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot, int j) {
-    TRI_G const float* q = b.vattr + 9u * (fp.vin_base + slot) + 3 * j;
+__device__ __forceinline__ bool obj48_mode(const TriFrameParams& fp) { return TRI_OBJ48 && fp.obj48; }
+// Attribute j (0 position, 1 normal, 2 colour) of geometry vertex gv's 36-B object record
+__device__ __forceinline__ F3 vattr_at(const TriDeviceBuffers& b, uint32_t gv, int j) {
+    TRI_G const float* q = b.vattr + 9u * gv + 3 * j;
     return F3{q[0], q[1], q[2]};
+}
+// ... of vertex record vin_base + slot, object space (vary_obj)
+__device__ __forceinline__ F3 vin_attr(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t slot, int j) {
+    return vattr_at(b, fp.vin_base + slot, j);
+}
+// obj48: the offset from draw d's vertex slots to its geometry vertices; a wave whose lanes share the draw (the
+// common case) reads it with one scalar load
+__device__ __forceinline__ uint32_t obj_delta(const TriFrameParams& fp, uint32_t d) {
+    d = min(d, (uint32_t)TRI_OBJ48_DRAWS - 1u);
+    const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+    if (__ballot(d != d0) == 0ull) return fp.vdelta[d0];
+    return fp.vdelta[d];
 }
 template <bool ONE = false>
 __device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const TriDeviceBuffers& b) {
@@ -188,6 +201,8 @@ __device__ __forceinline__ FetchBufs fetch_bufs(const TriFrameParams& fp, const 
     f.vary = rec_buf(b.vary, (ONE && TRI_VARY36) ? 36u : 48u, (uint64_t)fp.nslots + fp.ovf_vert_cap);
     f.src = f.vary;
     if (ONE && obj_mode(fp)) f.src = rec_buf(b.vattr + 9u * fp.vin_base, 36u, fp.nslots);
+    // obj48: an unclipped primitive's vertices are its geometry's own 48-B input records (index slot + vdelta)
+    if (!ONE && obj48_mode(fp)) f.src = rec_buf(b.vin, 48u, b.vertex_count);
     f.shade = rec_buf(b.draw_shade, (uint32_t)sizeof(TriDrawShade), fp.ndraws);
     f.shade_base = (const void*)b.draw_shade;
     f.shade_bytes = (uint32_t)sizeof(TriDrawShade) * fp.ndraws;
@@ -346,23 +361,25 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
         if (fp.shadow_on) b.lsnap[slot] = TriSnap{(int32_t)(TRI_OC_BAD << 24), 0, 0.0f, 0.0f};
         return;
     }
-    if (obj_mode(fp)) {  // no varyings to write: the position stream alone (12 B), then the snap
+    if (obj_mode(fp) || obj48_mode(fp)) {  // no varyings to write: the position stream alone (12 B), then the snap
         const Rsrc pr = make_rsrc(b.vpos, 12ull * b.vertex_count);
         const auto q = __builtin_amdgcn_raw_buffer_load_b96(pr, (uint32_t)gi * 12u, 0, 0);
         const float4 world = mat_vec_seq(dr.model, make_float4(__uint_as_float(q[0]), __uint_as_float(q[1]),
                                                                __uint_as_float(q[2]), 1.0f));
         store_snap(fp, b, slot, dr, world);
+        // (obj48 with the pre-pass: the same world position as the input-record path below, so the same map)
+        if (fp.shadow_on) shadow_vertex(fp, b, slot, world);
         return;
     }
     // three 16-byte loads (a plain struct load is split into overlapping per-field loads)
     const Rsrc vr = make_rsrc(b.vin, 48ull * b.vertex_count);
     const uint4 q0 = ld128(vr, (uint32_t)gi * 48u), q1 = ld128(vr, (uint32_t)gi * 48u + 16u),
                 q2 = ld128(vr, (uint32_t)gi * 48u + 32u);
-    TriVsIn in;
+    TriVsIn in;  // {pos, u}{normal, v}{colour, 0}
     in.px = __uint_as_float(q0.x); in.py = __uint_as_float(q0.y); in.pz = __uint_as_float(q0.z);
-    in.nx = __uint_as_float(q0.w); in.ny = __uint_as_float(q1.x); in.nz = __uint_as_float(q1.y);
-    in.cr = __uint_as_float(q1.z); in.cg = __uint_as_float(q1.w); in.cb = __uint_as_float(q2.x);
-    in.u = __uint_as_float(q2.y); in.v = __uint_as_float(q2.z);
+    in.u = __uint_as_float(q0.w); in.nx = __uint_as_float(q1.x); in.ny = __uint_as_float(q1.y);
+    in.nz = __uint_as_float(q1.z); in.v = __uint_as_float(q1.w); in.cr = __uint_as_float(q2.x);
+    in.cg = __uint_as_float(q2.y); in.cb = __uint_as_float(q2.z);
     float4 sp = make_float4(in.px, in.py, in.pz, 1.0f);
     float snx = in.nx, sny = in.ny, snz = in.nz;
     if (dr.bone_count > 0 && b.vskin) {  // Default.vert:64-85
@@ -403,7 +420,7 @@ __device__ __forceinline__ void vertex_slot(const TriFrameParams& fp, const TriD
         vo[0] = F3{world.x, world.y, world.z};
         vo[1] = F3{nnx, nny, nnz};
         vo[2] = F3{in.cr, in.cg, in.cb};
-    } else {
+    } else {  // the input records' layout (TriVsIn), so that obj48 frames read those records with the same code
         float4* vo = b.vary + 3u * slot;
         vo[0] = make_float4(world.x, world.y, world.z, u);
         vo[1] = make_float4(nnx, nny, nnz, v);
@@ -710,22 +727,29 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // Clip primitive `prim` (vertex slots sl[3]) with the whole wave; lanes that set up a fan
 // sub-triangle bin it. Must be reached by the whole wave.
-template <bool LPOS>
+// `draw`: the primitive's draw (wave-uniform), for obj48 frames' object records and model matrix.
+template <bool LPOS, bool ONE>
 __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const TriDeviceBuffers& b, TRI_LDS float* poly,
                                                uint32_t prim, uint32_t sl0, uint32_t sl1, uint32_t sl2, bool cfw,
-                                               uint32_t& nsetup, uint32_t& nentries) {
+                                               uint32_t draw, uint32_t& nsetup, uint32_t& nentries) {
     const uint32_t lane = lanes_below(~0ull);
     const uint64_t below = (lane == 63) ? 0x7FFFFFFFFFFFFFFFull : ((1ull << lane) - 1ull);
     TRI_LDS float* buf[2] = {poly, poly + TRI_MAX_CLIP_VERTS * kClipStride};
+    // object-space records: the ONE frames' (vary_obj: 36-B records at vin_base + slot, never with the pre-pass),
+    // or obj48's (the 48-B input records at slot + vdelta[draw])
+    const bool obj1 = !LPOS && obj_mode(fp), o48 = !ONE && obj48_mode(fp);
+    const uint32_t dl = o48 ? fp.vdelta[min(draw, (uint32_t)TRI_OBJ48_DRAWS - 1u)] : fp.vin_base;
     if (lane < 3) {
         ClipVert v;
         const uint32_t sl = lane == 0 ? sl0 : (lane == 1 ? sl1 : sl2);
         if (cfw && snap_oc(b, b.snap[sl], sl) == 0u) {  // not stored by k_vertex: world.w == 1
             F3 wv;
-            if (!LPOS && obj_mode(fp)) {  // k_vertex's world position, from the record (same operations; never
-                                          // with the shadow pre-pass)
-                const F3 p = vin_attr(fp, b, sl, 0);
-                const float4 w = mat_vec_seq(fp.draw0.model, make_float4(p.x, p.y, p.z, 1.0f));
+            if (obj1 || o48) {  // k_vertex's world position, from the record (same operations)
+                const F3 p = vattr_at(b, dl + sl, 0);
+                float m[16];
+#pragma unroll
+                for (int i = 0; i < 16; ++i) m[i] = o48 ? b.draws[draw].model[i] : fp.draw0.model[i];
+                const float4 w = mat_vec_seq(m, make_float4(p.x, p.y, p.z, 1.0f));
                 wv = F3{w.x, w.y, w.z};
             } else {
                 wv = vary36_mode(fp) ? ldF3(reinterpret_cast<TRI_G const F3*>(b.vary) + 3u * sl)
@@ -799,10 +823,10 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
                 vo[j] = F3{(s.b0 * x.x + s.b1 * y.x) + s.b2 * z.x, (s.b0 * x.y + s.b1 * y.y) + s.b2 * z.y,
                            (s.b0 * x.z + s.b1 * y.z) + s.b2 * z.z};
             }
-        } else {
-            const float4* v0 = b.vary + 3u * sl0;
-            const float4* v1 = b.vary + 3u * sl1;
-            const float4* v2 = b.vary + 3u * sl2;
+        } else {  // 48-B records: the world-space varyings, or (obj48) the input records' own layout
+            const float4* v0 = o48 ? reinterpret_cast<TRI_G const float4*>(b.vin + (dl + sl0)) : b.vary + 3u * sl0;
+            const float4* v1 = o48 ? reinterpret_cast<TRI_G const float4*>(b.vin + (dl + sl1)) : b.vary + 3u * sl1;
+            const float4* v2 = o48 ? reinterpret_cast<TRI_G const float4*>(b.vin + (dl + sl2)) : b.vary + 3u * sl2;
             float4* vo = b.vary + 3u * (sbase + lane);
 #pragma unroll
             for (int j = 0; j < 3; ++j) {
@@ -1208,12 +1232,13 @@ __device__ __forceinline__ void setup_body(const TriFrameParams& fp, const TriDe
                 while (cm) {
                     const int src = __builtin_ctzll(cm);
                     cm &= cm - 1;
-                    clip_prim_wave<WITH_SHADOW>(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
+                    clip_prim_wave<WITH_SHADOW, ONE>(fp, b, poly, (uint32_t)__builtin_amdgcn_readlane((int)p[t], src),
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl0[t], src),
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl1[t], src),
                                                 (uint32_t)__builtin_amdgcn_readlane((int)sl2[t], src),
                                                 (ONE || fp.one_draw) ? fp.draw0.clip_from_world != 0u
                                                             : b.draws[__builtin_amdgcn_readlane(pd[t], src)].clip_from_world != 0u,
+                                                (ONE || fp.one_draw) ? 0u : (uint32_t)__builtin_amdgcn_readlane(pd[t], src),
                                                 nsetup, nentries);
                 }
             }
@@ -2086,7 +2111,8 @@ __device__ __forceinline__ V4 ld_vary(const FetchBufs& fb, uint32_t slot, uint32
         const u32x3v q = rec96<36>(SRC ? fb.src : fb.vary, slot, j * 12u);
         return V4{__uint_as_float(q[0]), __uint_as_float(q[1]), __uint_as_float(q[2]), 0.0f};
     }
-    const uint4 q = rec128<48>(fb.vary, slot, j * 16u);  // plain-float views (HIP vector unions defeat SROA)
+    // plain-float views (HIP vector unions defeat SROA); fb.src is fb.vary unless obj48 (the input records)
+    const uint4 q = rec128<48>(SRC ? fb.src : fb.vary, slot, j * 16u);
     return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
 }
 template <bool ONE = false, bool SRC = false>
@@ -2131,29 +2157,55 @@ __device__ __forceinline__ ShadeRec load_shade(const FetchBufs& fb, uint32_t d) 
 
 // The varyings at weights (w0, w1, w2), the draw d's texture sample and tint: Frag fields 0..18 through
 // `put`.
-template <bool EXACT, bool ONE, typename Put>
-__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const FetchBufs& fb, const Taps& t, uint32_t d,
-                                            float w0, float w1, float w2, const float* lut, Put&& put) {
+// XF48: the instantiation may apply obj48's per-draw model and normal matrices (not the shadow instantiation: the
+// host keeps frames with the pre-pass and a non-identity obj48 draw on world-space varyings, so that kernel carries
+// none of this code's registers)
+template <bool EXACT, bool ONE, bool XF48, typename Put>
+__device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const TriDeviceBuffers& b, const FetchBufs& fb,
+                                            const Taps& t, uint32_t d, float w0, float w1, float w2, const float* lut,
+                                            Put&& put) {
     auto ip = [&](float x0, float x1, float x2) {
         return EXACT ? interp_exact(w0, w1, w2, x0, x1, x2) : interp_fast(w0, w1, w2, x0, x1, x2);
     };
     const V4 &a0 = t.a0, &a1 = t.a1, &a2 = t.a2, &b0 = t.b0, &b1 = t.b1, &b2 = t.b2, &c0 = t.c0, &c1 = t.c1, &c2 = t.c2;
     // field-wise stores (a struct-valued f3 store is ABI-coerced to <2 x float> + float, which
     // keeps the pixel-pair path's fragments from being promoted to registers)
+    auto row = [](float c0v, float c1v, float c2v, float x, float y, float z, float w) {
+        return __builtin_fmaf(c0v, x, __builtin_fmaf(c1v, y, __builtin_fmaf(c2v, z, w)));
+    };
     if (ONE && obj_mode(fp) && fp.obj_xform) {  // object-space position and normal: the model / normal matrices
         const float px = ip(a0.x, b0.x, c0.x), py = ip(a0.y, b0.y, c0.y), pz = ip(a0.z, b0.z, c0.z);
         const float nx = ip(a1.x, b1.x, c1.x), ny = ip(a1.y, b1.y, c1.y), nz = ip(a1.z, b1.z, c1.z);
         const float* m = fp.draw0.model;  // column-major, affine (vary_obj)
         const float* n = fp.draw0.nm;     // NM[c*3+r]
-        auto row = [](float c0v, float c1v, float c2v, float x, float y, float z, float w) {
-            return __builtin_fmaf(c0v, x, __builtin_fmaf(c1v, y, __builtin_fmaf(c2v, z, w)));
-        };
         put(0, row(m[0], m[4], m[8], px, py, pz, m[12]));
         put(1, row(m[1], m[5], m[9], px, py, pz, m[13]));
         put(2, row(m[2], m[6], m[10], px, py, pz, m[14]));
         put(3, row(n[0], n[3], n[6], nx, ny, nz, 0.0f));
         put(4, row(n[1], n[4], n[7], nx, ny, nz, 0.0f));
         put(5, row(n[2], n[5], n[8], nx, ny, nz, 0.0f));
+    } else if (!ONE && XF48 && obj48_mode(fp) && fp.obj48_xform) {
+        // obj48: the fragment's own draw's matrices, one draw of the wave at a time (a waterfall: usually one
+        // pass), read with scalar loads, so they live in SGPRs
+        const float px = ip(a0.x, b0.x, c0.x), py = ip(a0.y, b0.y, c0.y), pz = ip(a0.z, b0.z, c0.z);
+        const float nx = ip(a1.x, b1.x, c1.x), ny = ip(a1.y, b1.y, c1.y), nz = ip(a1.z, b1.z, c1.z);
+        float o[6];
+        for (;;) {
+            const uint32_t d0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)d);
+            if (d == d0) {
+                TRI_G const TriDrawDev& dr = b.draws[d0];
+                TRI_G const float* m = dr.model;
+                TRI_G const float* n = dr.nm;
+                o[0] = row(m[0], m[4], m[8], px, py, pz, m[12]);
+                o[1] = row(m[1], m[5], m[9], px, py, pz, m[13]);
+                o[2] = row(m[2], m[6], m[10], px, py, pz, m[14]);
+                o[3] = row(n[0], n[3], n[6], nx, ny, nz, 0.0f);
+                o[4] = row(n[1], n[4], n[7], nx, ny, nz, 0.0f);
+                o[5] = row(n[2], n[5], n[8], nx, ny, nz, 0.0f);
+                break;
+            }
+        }
+        for (int i = 0; i < 6; ++i) put(i, o[i]);
     } else {
         put(0, ip(a0.x, b0.x, c0.x)); put(1, ip(a0.y, b0.y, c0.y)); put(2, ip(a0.z, b0.z, c0.z));
         put(3, ip(a1.x, b1.x, c1.x)); put(4, ip(a1.y, b1.y, c1.y)); put(5, ip(a1.z, b1.z, c1.z));
@@ -2209,7 +2261,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     const FetchBufs fb = fetch_bufs<ONE>(fp, b);
     uint32_t sl[3] = {0, 0, 0}, d = 0;
     TriSnap a0{}, a1{}, a2{};
-    uint32_t v0 = 0, v1 = 0, v2 = 0;
+    uint32_t v0 = 0, v1 = 0, v2 = 0, dl = 0;
     Taps taps;
     if (CLIPM != 2) {
         prim_slots<ONE>(fp, b, prim, sl, d);
@@ -2218,9 +2270,11 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         // too, unused: its sub-triangle's record names its slots).
         a0 = ld_snap_xyw(fb, sl[0]); a1 = ld_snap_xyw(fb, sl[1]); a2 = ld_snap_xyw(fb, sl[2]);
         v0 = sl[0]; v1 = sl[2]; v2 = sl[1];  // set-up orientation (rec_from_snaps swaps v1 and v2)
+        // obj48: the geometry's input records at slot + vdelta[draw]
+        if (!ONE) dl = obj_delta(fp, d);  // (0 unless obj48: the host zeroes vdelta)
         // the varyings are gathered before the (rare) clipped branch: its record loads are waited for inside
         // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
-        taps = load_taps<ONE, true>(fb, v0, v1, v2);
+        taps = load_taps<ONE, true>(fb, v0 + dl, v1 + dl, v2 + dl);
     } else if (!ONE) {
         prim_slots<ONE>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
     }
@@ -2240,6 +2294,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         L0 = rec128<16>(lr, v0, 0u); L1 = rec128<16>(lr, v1, 0u); L2 = rec128<16>(lr, v2, 0u);
     }
     const TriRec r = from_rec ? rc : rec_from_snaps(prim, sl, a0, a1, a2);
+    // obj48: past the light-space gathers (slot-indexed) an unclipped primitive's vertices are only needed as
+    // input-record indices (one register each instead of the slot and the offset)
+    if (!ONE && !from_rec) { v0 += dl; v1 += dl; v2 += dl; }
     float w0, w1, w2;
     // exact int64 edge functions, IEEE divides (oracle order). The shadow lookup needs these weights in both
     // builds (TRI_SHADOW_SHARED_WEIGHTS: the fast build shades with them too instead of forming its own)
@@ -2255,13 +2312,15 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     } else if (ONE && TRI_VARY_OBJ && obj_mode(fp) && fp.obj_ucol) {
         // one colour for every vertex: fetch_attrs takes it from the frame arguments
     } else if (TRI_COLOUR_LATE) {
-        if (ONE && !from_rec) {  // an unclipped primitive's vertices (with CLIPM 0 a per-lane choice: both masked)
+        if (!from_rec) {  // an unclipped primitive's vertices: fb.src (fb.vary unless ONE or obj48; with CLIPM 0 a
+                          // per-lane choice: both masked)
             taps.a2 = ld_vary<ONE, true>(fb, v0, 2); taps.b2 = ld_vary<ONE, true>(fb, v1, 2);
             taps.c2 = ld_vary<ONE, true>(fb, v2, 2);
         } else {
             taps.a2 = ld_vary<ONE>(fb, v0, 2); taps.b2 = ld_vary<ONE>(fb, v1, 2); taps.c2 = ld_vary<ONE>(fb, v2, 2);
         }
     }
+
     float vis = 1.0f;
     if constexpr (kInlineVis && !(kAblate & 2048)) {  // light-space position at the pixel with the oracle's weights,
                                                        // then the compare (diagnostics: 2048 = no lookup)
@@ -2274,7 +2333,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         vis = shadow_vis(fp, b.shadow_map, ix(L0.x, L1.x, L2.x), ix(L0.y, L1.y, L2.y), ix(L0.z, L1.z, L2.z));
     }
     put(19, vis);
-    fetch_attrs<EXACT, ONE>(fp, fb, taps, d, w0, w1, w2, lut, put);
+    fetch_attrs<EXACT, ONE, !SHADOW>(fp, b, fb, taps, d, w0, w1, w2, lut, put);
 }
 
 template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0>
@@ -2519,14 +2578,56 @@ __device__ __forceinline__ void cov_row(const CovEntry& c, uint32_t r, uint64_t*
     }
 }
 
-// Default.frag for one fragment, stored as B8G8R8A8_UNORM
-template <bool EXACT, bool ONE>
-__device__ __forceinline__ uint32_t shade_bgra(const TriFrameParams& fp, const Frag& f) {
+// texture(AiBlendTexture, gl_FragCoord.xy * AiBlendConfig.yz) (Default.frag:186-188): R8G8B8A8_UNORM (the UNORM
+// decode b / 255, no sRGB), LINEAR, CLAMP_TO_EDGE, level 0 (the sampler of EnsureAiTextureResources,
+// Renderer.cpp:1462-1470). Same float operations as the oracle's ai_sample.
+__device__ __forceinline__ float4 sample_ai(const TriFrameParams& fp, const TriDeviceBuffers& b, int32_t px, int32_t py) {
+    const float u = ((float)px + 0.5f) * fp.ai_sx, v = ((float)py + 0.5f) * fp.ai_sy;
+    const float x = u * (float)fp.ai_tw - 0.5f, y = v * (float)fp.ai_th - 0.5f;
+    const float fx = floorf(x), fy = floorf(y);
+    const float a = x - fx, bb = y - fy;
+    const int32_t i0 = (int32_t)fminf(fmaxf(fx, -1.0f), 1.0e9f), j0 = (int32_t)fminf(fmaxf(fy, -1.0f), 1.0e9f);
+    const int32_t tw = (int32_t)fp.ai_tw, th = (int32_t)fp.ai_th;
+    const int32_t xa = min(max(i0, 0), tw - 1), xb = min(max(i0 + 1, 0), tw - 1);
+    const int32_t ya = min(max(j0, 0), th - 1), yb = min(max(j0 + 1, 0), th - 1);
+    TRI_G const uint32_t* t = b.ai_frame;
+    const uint32_t p00 = t[(size_t)ya * tw + xa], p10 = t[(size_t)ya * tw + xb];
+    const uint32_t p01 = t[(size_t)yb * tw + xa], p11 = t[(size_t)yb * tw + xb];
+    float r[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        auto ch = [&](uint32_t q) { return (float)((q >> (8 * c)) & 0xFFu) / 255.0f; };
+        const float t00 = ch(p00), t10 = ch(p10), t01 = ch(p01), t11 = ch(p11);
+        const float l0 = t00 + a * (t10 - t00), l1 = t01 + a * (t11 - t01);
+        r[c] = l0 + bb * (l1 - l0);
+    }
+    return make_float4(r[0], r[1], r[2], r[3]);
+}
+// mix(x, y, a) = x * (1 - a) + y * a (GLSL)
+__device__ __forceinline__ float mix_ai(float x, float y, float w) { return x * (1.0f - w) + y * w; }
+
+// Default.frag for one fragment at pixel (px, py), stored as B8G8R8A8_UNORM. AI: the instantiation for frames with
+// the AI frame blend (k_raster_ai; the other kernels carry none of its registers)
+template <bool EXACT, bool ONE, bool AI>
+__device__ __forceinline__ uint32_t shade_bgra(const TriFrameParams& fp, const TriDeviceBuffers& b, const Frag& f,
+                                               int32_t px, int32_t py) {
     if (EXACT) {
-        const float4 c = fs_exact(fp, f);
+        float4 c = fs_exact(fp, f);
+        if (AI && fp.ai_on) {  // (an AI frame-generation model is loaded) the blend with the AI frame's sample
+            const float4 ai = sample_ai(fp, b, px, py);
+            const float w = fp.ai_wgt;
+            c = make_float4(mix_ai(c.x, ai.x, w), mix_ai(c.y, ai.y, w), mix_ai(c.z, ai.z, w), mix_ai(c.w, ai.w, w));
+        }
         return unorm8(c.z) | (unorm8(c.y) << 8) | (unorm8(c.x) << 16) | (unorm8(c.w) << 24);
     }
-    const float4 c = fs_fast<ONE>(fp.sc, f);
+    float4 c = fs_fast<ONE>(fp.sc, f);
+    if (AI && fp.ai_on) {  // the fast build's channels are already scaled by 255 (tone_out): mix there
+        const float4 ai = sample_ai(fp, b, px, py);
+        const float w = fp.ai_wgt;
+        const float alpha = ONE ? fp.sc.sbt[3] : c.w;
+        return fast_bgra(mix_ai(c.x, 255.0f * ai.x, w), mix_ai(c.y, 255.0f * ai.y, w), mix_ai(c.z, 255.0f * ai.z, w),
+                         unorm8(mix_ai(alpha, ai.w, w)));
+    }
     return fast_bgra(c.x, c.y, c.z, ONE ? fp.sc.a8 : unorm8(c.w));  // ONE: the uniform alpha byte, host-folded
 }
 
@@ -2535,7 +2636,7 @@ __device__ __forceinline__ uint32_t shade_bgra(const TriFrameParams& fp, const F
 #endif
 
 // One bin: coverage into the LDS key tile, then shading and stores. Reached by the whole workgroup.
-template <bool EXACT, int BL, bool SHADOW, bool ONE = false>
+template <bool EXACT, int BL, bool SHADOW, bool ONE = false, bool AI = false>
 __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDeviceBuffers& b, const int bin) {
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
@@ -2783,7 +2884,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             } else {
                 fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f);
             }
-            out = shade_bgra<EXACT, ONE>(fp, f);
+            out = shade_bgra<EXACT, ONE, AI>(fp, b, f, px, py);
         }
         const size_t o = (size_t)(py - fp.y0) * fp.W + px;
         b.color[o] = out;
@@ -2799,7 +2900,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             Frag f;
             fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f);
             const size_t o = (size_t)(py - fp.y0) * fp.W + px;
-            b.color[o] = shade_bgra<EXACT, ONE>(fp, f);
+            b.color[o] = shade_bgra<EXACT, ONE, AI>(fp, b, f, px, py);
             if (fp.write_depth) b.depth[o] = __uint_as_float((uint32_t)(key >> 32));
         }
     }
@@ -2855,6 +2956,13 @@ template <bool EXACT, int BL, bool ONE>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? ((ONE && !EXACT) ? TRI_RASTER_WAVES_PLAIN_ONE : TRI_RASTER_WAVES_PLAIN) : 3))) void k_raster_plain(TRI_KARGS) {
     TRI_BIND_ARGS;
     raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
+}
+// Frames with Default.frag's AI frame blend (AiBlendConfig.w > 0, an uploaded AI frame; never with the shadow
+// pre-pass, which the reference does not have): the general instantiation plus the blend
+template <bool EXACT, int BL>
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? TRI_RASTER_WAVES_PLAIN : 3))) void k_raster_ai(TRI_KARGS) {
+    TRI_BIND_ARGS;
+    raster_bin<EXACT, BL, false, false, true>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -3128,6 +3236,11 @@ const void* tri_raster_plain_kernel(const TriFrameParams& fp) {
     const int bl = fp.bin_log2 == 5 ? 5 : fp.bin_log2 == 4 ? 4 : 6;
     const int sel = (fp.exact_shading ? 1 : 0) | (one ? 2 : 0);
     auto f = [](auto kernel) { return reinterpret_cast<const void*>(kernel); };
+    if (fp.ai_on) {  // (the host keeps such frames off the ONE instantiation's 36-B varyings)
+        if (bl == 5) return fp.exact_shading ? f(k_raster_ai<true, 5>) : f(k_raster_ai<false, 5>);
+        if (bl == 4) return fp.exact_shading ? f(k_raster_ai<true, 4>) : f(k_raster_ai<false, 4>);
+        return fp.exact_shading ? f(k_raster_ai<true, 6>) : f(k_raster_ai<false, 6>);
+    }
     if (bl == 5) {
         if (sel == 0) return f(k_raster_plain<false, 5, false>); if (sel == 1) return f(k_raster_plain<true, 5, false>);
         if (sel == 2) return f(k_raster_plain<false, 5, true>); return f(k_raster_plain<true, 5, true>);

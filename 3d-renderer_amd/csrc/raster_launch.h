@@ -28,6 +28,10 @@
 #ifndef TRI_UCOL
 #define TRI_UCOL 1
 #endif
+// TRI_OBJ48: object-space varyings outside the ONE instantiation (TriFrameParams::obj48); 0 keeps world-space varyings
+#ifndef TRI_OBJ48
+#define TRI_OBJ48 1
+#endif
 
 struct TriDeviceBuffers {
     TRI_G const TriVsIn* vin;
@@ -68,6 +72,7 @@ struct TriDeviceBuffers {
     TRI_G uint32_t* sbin_count;        // s_nbins shadow-map bin counters (zeroed by k_shadow_raster)
     TRI_G uint32_t* sbin_list;         // s_nbins * s_bin_cap primitive ids
     TRI_G uint32_t* shadow_map;        // s_size * s_size float32 depth bits
+    TRI_G const uint32_t* ai_frame;    // the AI blend's RGBA8 UNORM frame (only when TriFrameParams::ai_on)
 };
 
 // One frame's arguments (DESIGN.md §2 "launch cost"). The frame's first kernel (k_vertex, k_vertex_band or

@@ -295,6 +295,9 @@ int tri_group_upload_texture(tri_group* g, uint32_t slot, const uint8_t* rgba, u
 int tri_group_upload_bone_palette(tri_group* g, const float* m, uint32_t n) {
     return each(g, [&](tri_ctx* c) { return tri_upload_bone_palette(c, m, n); });
 }
+int tri_group_upload_ai_frame(tri_group* g, const uint8_t* rgba8, uint32_t w, uint32_t h) {
+    return each(g, [&](tri_ctx* c) { return tri_upload_ai_frame(c, rgba8, w, h); });
+}
 int tri_group_upload_skybox(tri_group* g, const uint8_t* faces, uint32_t size) {
     return each(g, [&](tri_ctx* c) { return tri_upload_skybox(c, faces, size); });
 }

@@ -122,6 +122,8 @@ struct tri_ctx {
 
     float* d_bones = nullptr; size_t cap_bones = 0;
     uint32_t* d_sky = nullptr; size_t cap_sky = 0;
+    uint32_t* d_ai = nullptr; size_t cap_ai = 0;  // the AI blend's RGBA8 UNORM frame (tri_upload_ai_frame)
+    uint32_t ai_w = 0, ai_h = 0;
     uint32_t sky_size = 0;
     bool sky_uniform = false;  // every texel of the cubemap equal (e.g. the solid fallback)
     uint32_t sky_uniform_bgra = 0;
@@ -152,6 +154,9 @@ struct tri_ctx {
     bool draw0_obj = false;    // draw0 may keep object-space varyings (draw_obj_ok)
     bool draw0_xform = false;  // ... and its model matrix is not the identity
     bool draw0_ucol = false;   // ... and every vertex of its geometry has one colour
+    bool obj48 = false;        // every active draw may keep object-space varyings (TriFrameParams::obj48)
+    bool obj48_xform = false;  // ... and some draw's model matrix is not the identity
+    uint32_t vdelta[TRI_OBJ48_DRAWS] = {};  // per draw: base_vertex + min_index - first slot
 
     // work buffers
     float4* d_clip = nullptr; size_t cap_clip = 0;
@@ -501,6 +506,19 @@ int resolve_draws(tri_ctx* c) {
     c->draw0_obj = n == 1 && draw_obj_ok(*c->geom, dd[0]);
     c->draw0_xform = c->draw0_obj && !identity_model(dd[0].model);
     c->draw0_ucol = c->draw0_obj && c->geom->uni_col;
+    // object-space varyings for any draw list (obj48): every active draw affine, unskinned, conformal, with an
+    // identity texture transform (uv * scale * tiling + offset == uv bit for bit), at most TRI_OBJ48_DRAWS of them
+    c->obj48 = n >= 1 && n <= TRI_OBJ48_DRAWS && !skin;
+    c->obj48_xform = false;
+    for (uint32_t d = 0; d < n && c->obj48; ++d) {
+        const TriDrawDev& o = dd[d];
+        c->vdelta[d] = (uint32_t)((int64_t)o.base_vertex + (int64_t)o.min_index - (int64_t)vb[d]);
+        if (o.vert_count == 0) continue;  // inactive: no slots, no primitives
+        const bool uv_id = o.tex_scale[0] == 1.0f && o.tex_scale[1] == 1.0f && o.tiling == 1.0f &&
+                           o.tex_offset[0] == 0.0f && o.tex_offset[1] == 0.0f;
+        c->obj48 = uv_id && draw_obj_ok(*c->geom, o);
+        c->obj48_xform = c->obj48_xform || !identity_model(o.model);
+    }
     c->nslots = (uint32_t)vslots;
     c->nprims = (uint32_t)prims;
     c->ncl_total = (uint32_t)ncl;
@@ -889,7 +907,7 @@ int tri_destroy(tri_ctx* c) {
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     auto f = [](void* p) { if (p) (void)hipFree(p); };
     free_geometry(c->own_geom);
-    f(c->d_lut); f(c->d_bones); f(c->d_sky);
+    f(c->d_lut); f(c->d_bones); f(c->d_sky); f(c->d_ai);
     for (auto& t : c->d_tex) f(t);
     f(c->d_draws); f(c->d_draw_shade); f(c->d_vbase); f(c->d_pbase); f(c->d_cbase); f(c->d_cvis);
     f(c->d_clip); f(c->d_snap); f(c->d_oc); f(c->d_vary); f(c->d_recs); f(c->d_clip_slot); f(c->d_prim_vs); f(c->d_setup_stats);
@@ -1058,6 +1076,27 @@ int tri_upload_skybox(tri_ctx* c, const uint8_t* faces, uint32_t n) {
     return TRI_OK;
 }
 
+// The AI frame-generation texture (EnsureAiTextureResources, Renderer.cpp:1390-1500; UploadAiInterpolationToGpu,
+// :1560-1700): R8G8B8A8_UNORM, the extent of the frame it was generated for.
+int tri_upload_ai_frame(tri_ctx* c, const uint8_t* rgba8, uint32_t w, uint32_t h) {
+    if (!c) return fail(TRI_E_INVALID, "tri_upload_ai_frame: null context");
+    if (!rgba8 || w == 0 || h == 0) {  // DestroyAiResources: no texture, no blend
+        c->ai_w = c->ai_h = 0;
+        return TRI_OK;
+    }
+    if (w > TRI_MAX_DIM || h > TRI_MAX_DIM)
+        return fail(TRI_E_INVALID, "tri_upload_ai_frame: extent %ux%u outside 1..%d", w, h, TRI_MAX_DIM);
+    int rc = make_current(c);
+    if (rc) return rc;
+    HIP_TRY(hipStreamSynchronize(c->stream));  // no queued frame still samples the previous texture
+    if ((rc = grow(c->d_ai, c->cap_ai, (size_t)w * h))) return rc;
+    HIP_TRY(hipMemcpy(c->d_ai, rgba8, (size_t)w * h * 4, hipMemcpyHostToDevice));
+    HIP_TRY(hipStreamSynchronize(nullptr));  // complete before the next frame on the non-blocking stream
+    c->ai_w = w;
+    c->ai_h = h;
+    return TRI_OK;
+}
+
 int tri_set_shadow(tri_ctx* c, const tri_shadow_config* cfg) {
     if (!c) return fail(TRI_E_INVALID, "tri_set_shadow: null context");
     if (!cfg || cfg->size == 0) {
@@ -1109,8 +1148,6 @@ int tri_read_shadow_map(tri_ctx* c, uint32_t* out) {
 
 int tri_set_frame(tri_ctx* c, const tri_global_ubo* ubo, const float clear[4]) {
     if (!c || !ubo) return fail(TRI_E_INVALID, "tri_set_frame: null argument");
-    if (ubo->ai_blend_config[3] > 0.0f && ubo->ai_blend_config[0] > 0.0f)
-        return fail(TRI_E_UNSUPPORTED, "tri_set_frame: AI frame blend (AiBlendConfig.w > 0) is outside the hot path");
     c->ubo = *ubo;
     mat4_mul(ubo->projection, ubo->view, c->pv);  // (P*V), Default.vert:104
     if (clear)
@@ -1127,6 +1164,8 @@ int tri_frame_alpha(tri_ctx* c, int32_t* alpha) {
     if (!c || !alpha) return fail(TRI_E_INVALID, "tri_frame_alpha: null argument");
     int32_t a = (int32_t)(c->clear_bgra >> 24);
     bool uniform = !c->sky_size || a == 255;
+    // the AI frame blend mixes every mesh fragment's alpha with the AI frame's (not proven uniform here)
+    if (c->ubo.ai_blend_config[3] > 0.0f && c->ubo.ai_blend_config[0] > 0.0f && !c->draws.empty()) uniform = false;
     for (const tri_draw& d : c->draws) {
         if (!uniform) break;
         int32_t slot = d.pc.texture_slot;
@@ -1235,13 +1274,33 @@ int tri_render(tri_ctx* c) {
     if (fp.one_draw) fp.draw0 = c->draw0;
     fp.shade_solid = (fp.one_draw && c->shade0.tex.w == 1 && c->shade0.tex.h == 1) ? 1u : 0u;
     // the frames k_raster_plain<.., ONE> shades keep 36-B varyings (no texture coordinates)
-    fp.vary36 = (fp.shade_solid && !c->shadow.size) ? 1u : 0u;
+    // Default.frag's AI frame blend (:182-191): on when AiBlendConfig.w > 0 and its clamped weight is positive; its
+    // frames take k_raster_ai (the general instantiation: world-space or obj48 varyings, never the ONE 36-B records)
+    const float ai_wgt = std::fmin(std::fmax(c->ubo.ai_blend_config[0], 0.0f), 1.0f);
+    fp.ai_on = (c->ubo.ai_blend_config[3] > 0.0f && ai_wgt > 0.0f) ? 1u : 0u;
+    if (fp.ai_on) {
+        if (!c->ai_w) return fail(TRI_E_STATE, "tri_render: AiBlendConfig.w > 0 but no AI frame uploaded (tri_upload_ai_frame)");
+        if (c->shadow.size)
+            return fail(TRI_E_UNSUPPORTED, "tri_render: the AI frame blend with the shadow pre-pass (the reference has no shadow pass)");
+        fp.ai_wgt = ai_wgt;
+        fp.ai_sx = c->ubo.ai_blend_config[1];
+        fp.ai_sy = c->ubo.ai_blend_config[2];
+        fp.ai_tw = c->ai_w;
+        fp.ai_th = c->ai_h;
+    }
+    fp.vary36 = (fp.shade_solid && !c->shadow.size && !fp.ai_on) ? 1u : 0u;
     fp.vary_obj = fp.vary36 && c->draw0_obj ? 1u : 0u;
     fp.obj_xform = fp.vary_obj && c->draw0_xform ? 1u : 0u;
     fp.vin_base = fp.vary_obj ? (uint32_t)((int64_t)c->draw0.base_vertex + (int64_t)c->draw0.min_index) : 0u;
     fp.obj_ucol = TRI_UCOL && fp.vary_obj && c->draw0_ucol ? 1u : 0u;
     if (fp.obj_ucol) std::memcpy(fp.ucol, c->geom->ucol, sizeof fp.ucol);
-    c->last_path = (fp.shade_solid ? TRI_PATH_ONE_DRAW : 0u) | (fp.vary_obj ? TRI_PATH_VARY_OBJ : 0u) |
+    // object-space varyings for the other instantiations (the ONE frames keep vary_obj's 36-B records)
+    // (not with the pre-pass over a transformed draw: the shadow instantiation carries no per-draw transform)
+    fp.obj48 = (TRI_OBJ48 && !fp.vary36 && c->obj48 && !(c->shadow.size && c->obj48_xform)) ? 1u : 0u;
+    fp.obj48_xform = fp.obj48 && c->obj48_xform ? 1u : 0u;
+    if (fp.obj48) std::memcpy(fp.vdelta, c->vdelta, sizeof fp.vdelta);  // (zero otherwise: world-space records
+                                                                          // at the slots themselves)
+    c->last_path = (fp.obj48 ? TRI_PATH_OBJ48 : 0u) | (fp.shade_solid ? TRI_PATH_ONE_DRAW : 0u) | (fp.vary_obj ? TRI_PATH_VARY_OBJ : 0u) |
                    (fp.obj_xform ? TRI_PATH_OBJ_XFORM : 0u) | (fp.obj_ucol ? TRI_PATH_OBJ_UCOL : 0u) |
                    (c->shadow.size ? TRI_PATH_SHADOW : 0u);
     fp.ovf_rec_cap = c->ovf_rec_cap;
@@ -1316,6 +1375,7 @@ int tri_render(tri_ctx* c) {
     b.draw_pbase = c->d_pbase;
     b.srgb_lut = c->d_lut;
     b.sky = c->d_sky;
+    b.ai_frame = fp.ai_on ? c->d_ai : nullptr;
     b.clip = c->d_clip;
     b.snap = c->d_snap;
     b.oc = c->d_oc;

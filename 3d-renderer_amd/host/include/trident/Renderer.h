@@ -65,6 +65,16 @@ public:
     size_t GetOrCreatePrimitiveMeshIndex(MeshComponent::PrimitiveType primitiveType);
 
     void SetClearColor(const glm::vec4& color) { m_ClearColor = color; }
+    // The AI frame blend of Default.frag (:182-191). SetAiBlendStrength clamps to [0, 1] (Renderer.cpp:2533-2538,
+    // default 0.35, Renderer.h:508). SubmitAiInterpolation takes a generated frame the way UploadAiInterpolationToGpu
+    // does (Renderer.cpp:1560-1700): width * height * channels floats, each clamped to [0, 1] and rounded to a UNORM8
+    // byte, alpha 1 when the frame has fewer than four channels; every viewport then blends with it (UpdateUniformBuffer
+    // packs AiBlendConfig = (strength, 1 / width, 1 / height, 1) while a frame is held, :5916-5921). nullptr or an
+    // empty frame drops it (the blend is off again). The frame generator (ONNX Runtime) itself stays outside.
+    void SetAiBlendStrength(float blendStrength) { m_AiBlendStrength = std::min(std::max(blendStrength, 0.0f), 1.0f); }
+    float GetAiBlendStrength() const { return m_AiBlendStrength; }
+    bool SubmitAiInterpolation(const float* pixels, uint32_t width, uint32_t height, uint32_t channels);
+    bool HasAiFrame() const { return m_AiWidth != 0 && m_AiHeight != 0; }
     // Replaces the skybox cubemap (CreateSkyboxCubemap, Renderer.cpp:3818-4110). Init installs the
     // reference's fallback, a solid 0x808080 cubemap (:3925-3926). An invalid cubemap is rejected
     // and logged; returns false in that case.
@@ -166,6 +176,7 @@ private:
         tri_group* m_Group = nullptr;  // multi-device viewport (SetDeviceCount > 1)
         uint32_t m_Width = 0, m_Height = 0;
         uint64_t m_GeometryGeneration = 0, m_TextureGeneration = 0, m_MaterialGeneration = 0, m_SkyboxGeneration = 0;
+        uint64_t m_AiGeneration = 0;
         std::vector<float> m_BonePalette;  // the palette last uploaded to this viewport's context
         tri_shadow_config m_Shadow{};      // the pre-pass configuration last set on this context
         tri_image m_Image{};               // GetViewportTexture's handle (after the first frame)
@@ -226,6 +237,10 @@ private:
     std::string m_AssetsDirectory = "Assets";
     std::string m_SkyboxSource;
     uint64_t m_SkyboxGeneration = 1;
+    std::vector<uint8_t> m_AiFrame;  // the AI frame's R8G8B8A8_UNORM bytes (SubmitAiInterpolation)
+    uint32_t m_AiWidth = 0, m_AiHeight = 0;
+    float m_AiBlendStrength = 0.35f;
+    uint64_t m_AiGeneration = 1;
 
     struct TextureSlot {
         std::string m_SourcePath;

@@ -106,6 +106,10 @@ int trident_app_entity_count(trident_app* app, uint32_t* count);
 /* Renderer::SetPresentExtent: DrawFrame then blits the active (last SetViewport) viewport onto a
  * width x height present image (VK_FILTER_LINEAR); 0 x 0 disables. */
 int trident_app_set_present_extent(trident_app* app, uint32_t width, uint32_t height);
+/* Renderer::SetAiBlendStrength / SubmitAiInterpolation (Default.frag's AI frame blend): width * height * channels
+ * floats in [0, 1] (NULL or a zero extent drops the frame). */
+int trident_app_set_ai_blend_strength(trident_app* app, float strength);
+int trident_app_submit_ai_frame(trident_app* app, const float* pixels, uint32_t width, uint32_t height, uint32_t channels);
 int trident_app_read_present(trident_app* app, uint8_t* rgba, uint32_t width, uint32_t height);
 
 int trident_app_draw_frame(trident_app* app);

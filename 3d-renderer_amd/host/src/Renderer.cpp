@@ -170,6 +170,9 @@ struct Target {
         return g ? tri_group_upload_materials(g, r, n) : tri_upload_materials(c, r, n);
     }
     int Skybox(const uint8_t* f, uint32_t n) const { return g ? tri_group_upload_skybox(g, f, n) : tri_upload_skybox(c, f, n); }
+    int AiFrame(const uint8_t* p, uint32_t w, uint32_t h) const {
+        return g ? tri_group_upload_ai_frame(g, p, w, h) : tri_upload_ai_frame(c, p, w, h);
+    }
     int Texture(uint32_t slot, const uint8_t* p, uint32_t w, uint32_t h) const {
         return g ? tri_group_upload_texture(g, slot, p, w, h) : tri_upload_texture(c, slot, p, w, h);
     }
@@ -716,7 +719,38 @@ void Renderer::UpdateUniformBuffer(const Camera* camera, tri_global_ubo& g) cons
     g.directional_light_color[2] = color.z; g.directional_light_color[3] = intensity;
     g.light_counts[0] = (ndir > 0 || fallback) ? 1u : 0u;
     g.light_counts[1] = npt;
-    // AiBlendConfig stays 0: the AI frame blend is outside the hot path (Renderer.cpp:5916-5925)
+    // AiBlendConfig (Renderer.cpp:5916-5925): (strength, 1 / width, 1 / height, 1) while an AI frame is held, else 0
+    if (m_AiWidth && m_AiHeight) {
+        g.ai_blend_config[0] = m_AiBlendStrength;
+        g.ai_blend_config[1] = 1.0f / (float)std::max<uint32_t>(m_AiWidth, 1);
+        g.ai_blend_config[2] = 1.0f / (float)std::max<uint32_t>(m_AiHeight, 1);
+        g.ai_blend_config[3] = 1.0f;
+    } else {
+        std::memset(g.ai_blend_config, 0, sizeof g.ai_blend_config);
+    }
+}
+
+bool Renderer::SubmitAiInterpolation(const float* pixels, uint32_t width, uint32_t height, uint32_t channels) {
+    ++m_AiGeneration;
+    if (!pixels || width == 0 || height == 0 || channels == 0) {  // no frame: the texture is not ready, no blend
+        m_AiFrame.clear();
+        m_AiWidth = m_AiHeight = 0;
+        return true;
+    }
+    // UploadAiInterpolationToGpu's packing (Renderer.cpp:1572-1590)
+    const size_t n = (size_t)width * height;
+    m_AiFrame.resize(n * 4);
+    for (size_t p = 0; p < n; ++p)
+        for (uint32_t ch = 0; ch < 4; ++ch) {
+            float v = 0.0f;
+            if (ch < channels) v = pixels[p * channels + ch];
+            else if (ch == 3) v = 1.0f;  // opaque when the network omits alpha
+            v = std::min(std::max(v, 0.0f), 1.0f);
+            m_AiFrame[p * 4 + ch] = (uint8_t)std::round(v * 255.0f);
+        }
+    m_AiWidth = width;
+    m_AiHeight = height;
+    return true;
 }
 
 bool Renderer::BuildShadowConfig(tri_shadow_config& out) {
@@ -844,6 +878,7 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
         vc.m_Width = w;
         vc.m_Height = h;
         vc.m_GeometryGeneration = vc.m_TextureGeneration = vc.m_MaterialGeneration = vc.m_SkyboxGeneration = 0;
+        vc.m_AiGeneration = 0;
         vc.m_Shadow = tri_shadow_config{};  // a fresh context starts without the pre-pass and bones
         vc.m_BonePalette.clear();
     }
@@ -897,6 +932,13 @@ bool Renderer::PrepareViewport(ViewportContext& vc) {
             return false;
         }
         vc.m_SkyboxGeneration = m_SkyboxGeneration;
+    }
+    if (vc.m_AiGeneration != m_AiGeneration) {  // the AI frame texture (UploadAiInterpolationToGpu)
+        if (t.AiFrame(m_AiWidth ? m_AiFrame.data() : nullptr, m_AiWidth, m_AiHeight) != TRI_OK) {
+            LogError("AI frame texture", tri_last_error());
+            return false;
+        }
+        vc.m_AiGeneration = m_AiGeneration;
     }
     if (vc.m_TextureGeneration != m_TextureGeneration) {
         for (size_t s = 0; s < m_TextureSlots.size(); ++s) {

@@ -486,6 +486,20 @@ int trident_app_set_present_extent(trident_app* app, uint32_t width, uint32_t he
     });
 }
 
+int trident_app_set_ai_blend_strength(trident_app* app, float strength) {
+    return Guard(app, [&] {
+        app->renderer.SetAiBlendStrength(strength);
+        return TRI_OK;
+    });
+}
+
+int trident_app_submit_ai_frame(trident_app* app, const float* pixels, uint32_t width, uint32_t height, uint32_t channels) {
+    return Guard(app, [&] {
+        if (width > TRI_MAX_DIM || height > TRI_MAX_DIM || channels > 4) return TRI_E_INVALID;
+        return app->renderer.SubmitAiInterpolation(pixels, width, height, channels) ? TRI_OK : TRI_E_INVALID;
+    });
+}
+
 int trident_app_read_present(trident_app* app, uint8_t* rgba, uint32_t width, uint32_t height) {
     return Guard(app, [&] {
         if (!rgba) return TRI_E_INVALID;

@@ -142,8 +142,13 @@ class TriFrameStats(C.Structure):
         ("bins_x", C.c_uint32),
         ("bins_y", C.c_uint32),
         ("bin_size", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("path", C.c_uint32),
     ]
+
+
+# tri_frame_stats.path bits (include/tri_raster.h)
+TRI_PATH_ONE_DRAW, TRI_PATH_VARY_OBJ, TRI_PATH_OBJ_XFORM, TRI_PATH_OBJ_UCOL, TRI_PATH_SHADOW = 0x1, 0x2, 0x4, 0x8, 0x10
+TRI_PATH_OBJ48 = 0x20
 
 
 class TriShadowConfig(C.Structure):
@@ -210,6 +215,7 @@ CABI_FUNCTIONS = [
     ("tri_upload_texture", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_upload_bone_palette", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("tri_upload_skybox", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("tri_upload_ai_frame", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_set_frame", C.c_int, [C.c_void_p, C.POINTER(TriGlobalUbo), C.POINTER(C.c_float * 4)]),
     ("tri_set_draws", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("tri_bind_output", C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
@@ -243,6 +249,7 @@ CABI_FUNCTIONS = [
     ("tri_group_upload_texture", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_group_upload_bone_palette", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("tri_group_upload_skybox", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    ("tri_group_upload_ai_frame", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_group_set_shadow", C.c_int, [C.c_void_p, C.POINTER(TriShadowConfig)]),
     ("tri_group_set_frame", C.c_int, [C.c_void_p, C.POINTER(TriGlobalUbo), C.POINTER(C.c_float * 4)]),
     ("tri_group_set_draws", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),

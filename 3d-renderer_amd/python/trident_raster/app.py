@@ -66,6 +66,8 @@ _APP_FUNCTIONS = [
     ("trident_app_entity_mesh", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(C.c_uint64)]),
     ("trident_app_entity_count", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     ("trident_app_set_present_extent", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32]),
+    ("trident_app_set_ai_blend_strength", C.c_int, [C.c_void_p, C.c_float]),
+    ("trident_app_submit_ai_frame", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32]),
     ("trident_app_read_present", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
 ]
 
@@ -310,6 +312,19 @@ class TridentApp:
     # ---- presentation: active viewport -> swapchain-sized image ----
     def set_present_extent(self, width, height):
         _check(self._lib.trident_app_set_present_extent(self._h, width, height), "set_present_extent")
+
+    # ---- Default.frag's AI frame blend (SetAiBlendStrength / UploadAiInterpolationToGpu) ----
+    def set_ai_blend_strength(self, strength):
+        _check(self._lib.trident_app_set_ai_blend_strength(self._h, strength), "set_ai_blend_strength")
+
+    def submit_ai_frame(self, pixels):
+        """pixels: float32 [h, w, channels] in [0, 1] (the frame generator's output), or None to drop it."""
+        if pixels is None:
+            _check(self._lib.trident_app_submit_ai_frame(self._h, None, 0, 0, 0), "submit_ai_frame")
+            return
+        p = np.ascontiguousarray(pixels, np.float32)
+        _check(self._lib.trident_app_submit_ai_frame(self._h, p.ctypes.data, p.shape[1], p.shape[0], p.shape[2]),
+               "submit_ai_frame")
 
     def read_present(self, width, height):
         out = np.zeros((height, width, 4), np.uint8)

@@ -33,8 +33,14 @@ def load_library(path=None):
     if not os.path.exists(path):
         raise ImportError(f"HIP rasterizer library not built: {path} (run __graft_entry__.build())")
     lib = C.CDLL(path)
+    variant = os.path.abspath(path) != os.path.abspath(LIB_PATH)
     for name, res, args in abi.CABI_FUNCTIONS:
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if not variant:  # the product library exports every entry point include/tri_raster.h declares
+                raise
+            continue  # an older A/B variant: entry points added since are absent there
         fn.restype = res
         fn.argtypes = args
     if lib.tri_abi_version() != abi.TRI_RASTER_ABI_VERSION:
@@ -120,6 +126,16 @@ class TriRaster:
     def upload_bone_palette(self, mats):
         m = np.ascontiguousarray(mats, dtype=np.float32).reshape(-1, 16)
         _check(_lib.tri_upload_bone_palette(self._ctx, _ptr(m), m.shape[0]))
+
+    def upload_ai_frame(self, rgba):
+        """rgba: uint8 [h, w, 4] R8G8B8A8_UNORM AI frame (Default.frag's blend), or None to remove it."""
+        if rgba is None:
+            _check(_lib.tri_upload_ai_frame(self._ctx, None, 0, 0))
+            return
+        f = np.ascontiguousarray(rgba, dtype=np.uint8)
+        if f.ndim != 3 or f.shape[2] != 4:
+            raise ValueError("AI frame must be uint8 [h, w, 4]")
+        _check(_lib.tri_upload_ai_frame(self._ctx, _ptr(f), f.shape[1], f.shape[0]))
 
     def upload_skybox(self, faces):
         """faces: uint8 [6, n, n, 4] sRGB (+X,-X,+Y,-Y,+Z,-Z), or None to remove the skybox."""
@@ -321,6 +337,13 @@ class TriGroup:
     def upload_bone_palette(self, mats):
         m = np.ascontiguousarray(mats, dtype=np.float32).reshape(-1, 16)
         _check(_lib.tri_group_upload_bone_palette(self._g, _ptr(m), m.shape[0]))
+
+    def upload_ai_frame(self, rgba):
+        if rgba is None:
+            _check(_lib.tri_group_upload_ai_frame(self._g, None, 0, 0))
+            return
+        f = np.ascontiguousarray(rgba, dtype=np.uint8)
+        _check(_lib.tri_group_upload_ai_frame(self._g, _ptr(f), f.shape[1], f.shape[0]))
 
     def upload_skybox(self, faces):
         if faces is None:

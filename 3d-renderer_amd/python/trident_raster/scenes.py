@@ -304,6 +304,7 @@ class Scene:
     bones: np.ndarray = None
     skybox: np.ndarray = None  # uint8 [6, n, n, 4] sRGB cubemap (+X,-X,+Y,-Y,+Z,-Z), None = no skybox pass
     shadow: abi.TriShadowConfig = None  # shadow-map pre-pass (tri_set_shadow), None = off
+    ai_frame: np.ndarray = None  # uint8 [h, w, 4] R8G8B8A8_UNORM AI frame (tri_upload_ai_frame), None = none
 
     @property
     def triangles(self):
@@ -499,5 +500,20 @@ def load_scene(rast, scene, geometry=None):
     if scene.skybox is not None:
         rast.upload_skybox(scene.skybox)
     rast.set_shadow(scene.shadow)
+    if scene.ai_frame is not None:
+        rast.upload_ai_frame(scene.ai_frame)
     rast.set_frame(scene.ubo, scene.clear)
     rast.set_draws(scene.draws)
+
+
+def with_ai_blend(scene, strength=0.35, ai_frame=None, seed=0xA1):
+    """Default.frag's AI frame blend (:182-191) on a scene: an R8G8B8A8_UNORM frame of the scene's extent (seeded
+    noise unless given) and the UBO's AiBlendConfig as UpdateUniformBuffer packs it while the AI texture is ready,
+    (strength, 1 / width, 1 / height, 1) (Renderer.cpp:5916-5921; SetAiBlendStrength's default 0.35, Renderer.h:508)."""
+    if ai_frame is None:
+        rng = np.random.default_rng(seed)
+        ai_frame = rng.integers(0, 256, size=(scene.height, scene.width, 4), dtype=np.uint8)
+    h, w = ai_frame.shape[:2]
+    scene.ai_frame = ai_frame
+    scene.ubo.ai_blend_config = (abi.C.c_float * 4)(strength, F(1) / F(max(w, 1)), F(1) / F(max(h, 1)), 1.0)
+    return scene

@@ -36,7 +36,7 @@ extern "C" {
 #define TRI_E_OOM (-3)         /* device allocation failed                                      */
 #define TRI_E_OVERFLOW (-4)    /* a frame overflowed an internal bin/clip buffer; buffers were   *
                                 * grown, re-render the frame                                    */
-#define TRI_E_UNSUPPORTED (-5) /* feature outside the hot path (AI frame blend)                 */
+#define TRI_E_UNSUPPORTED (-5) /* combination outside the path (AI blend + shadow pre-pass)     */
 #define TRI_E_STATE (-6)       /* call order violated (e.g. render before geometry upload)      */
 
 /* ---- limits mirrored from the reference ----------------------------------------------- */
@@ -166,6 +166,7 @@ typedef struct tri_frame_stats {
 #define TRI_PATH_OBJ_XFORM  0x4u  /* ... carried through a non-identity model / normal matrix per pixel     */
 #define TRI_PATH_OBJ_UCOL   0x8u  /* ... one vertex colour for the whole geometry                           */
 #define TRI_PATH_SHADOW    0x10u  /* the shadow-map pre-pass ran                                            */
+#define TRI_PATH_OBJ48     0x20u  /* object-space varyings outside the single-draw solid instantiation      */
 
 /* Shadow-map pre-pass (BASELINE.json config 5). The reference reserves the switch
  * (LightComponent::m_ShadowCaster, Trident/src/ECS/Components/LightComponent.h:33) but renders no shadow
@@ -239,6 +240,16 @@ int tri_upload_bone_palette(tri_ctx* ctx, const float* matrices, uint32_t matrix
  * LEQUAL without writes) then gives every uncovered pixel its sky colour instead of the clear colour.
  * faces = NULL or size = 0 removes the skybox. */
 int tri_upload_skybox(tri_ctx* ctx, const uint8_t* faces_rgba8_srgb, uint32_t size);
+
+/* Default.frag's AI frame-generation blend (Default.frag:182-191). The texture is what UploadAiInterpolationToGpu
+ * (Renderer.cpp:1560-1700) fills and EnsureAiTextureResources (:1390-1500) creates: width x height R8G8B8A8_UNORM
+ * texels (no sRGB decode), rows top to bottom, sampled LINEAR with CLAMP_TO_EDGE at level 0. A frame whose UBO has
+ * AiBlendConfig.w > 0 and w' = clamp(AiBlendConfig.x, 0, 1) > 0 (UpdateUniformBuffer packs (strength, 1 / width,
+ * 1 / height, 1) while the texture is ready, Renderer.cpp:5916-5925) replaces every mesh fragment's output c by
+ * mix(c, texture(ai, gl_FragCoord.xy * AiBlendConfig.yz), w') before the UNORM store; the skybox pass does not
+ * blend. rgba8 = NULL or a zero extent removes the texture (DestroyAiResources). Rendering a blending frame
+ * without a texture is TRI_E_STATE; with the shadow pre-pass (not part of the reference) TRI_E_UNSUPPORTED. */
+int tri_upload_ai_frame(tri_ctx* ctx, const uint8_t* rgba8_unorm, uint32_t width, uint32_t height);
 
 /* Shadow-map pre-pass for the directional light (see tri_shadow_config). NULL or size 0 disables it
  * (the default: C1-C3 frames are exactly the reference's). size <= TRI_MAX_DIM. */
@@ -362,6 +373,7 @@ int tri_group_upload_texture(tri_group* group, uint32_t slot, const uint8_t* rgb
                              uint32_t height);
 int tri_group_upload_bone_palette(tri_group* group, const float* matrices, uint32_t matrix_count);
 int tri_group_upload_skybox(tri_group* group, const uint8_t* faces_rgba8_srgb, uint32_t size);
+int tri_group_upload_ai_frame(tri_group* group, const uint8_t* rgba8_unorm, uint32_t width, uint32_t height);
 int tri_group_set_shadow(tri_group* group, const tri_shadow_config* config);
 int tri_group_set_frame(tri_group* group, const tri_global_ubo* ubo, const float clear_rgba[4]);
 int tri_group_set_draws(tri_group* group, const tri_draw* draws, uint32_t draw_count);

@@ -34,6 +34,7 @@ class OracleScene(C.Structure):
         ("clear_rgba", C.c_float * 4),
         ("sky_faces", C.c_void_p), ("sky_size", C.c_uint32), ("sky_reserved", C.c_uint32),
         ("shadow", C.POINTER(abi.TriShadowConfig)), ("out_shadow_map", C.c_void_p),
+        ("ai_frame", C.c_void_p), ("ai_width", C.c_uint32), ("ai_height", C.c_uint32),
     ]
 
 
@@ -207,6 +208,11 @@ def render(scene, band=None, threads=None, shadow_map_out=None):
         sky = np.ascontiguousarray(sky, np.uint8)  # [6, n, n, 4]
         keep.append(sky)
         sc.sky_faces, sc.sky_size = sky.ctypes.data, sky.shape[1]
+    ai = getattr(scene, "ai_frame", None)
+    if ai is not None:  # the AI frame blend's R8G8B8A8_UNORM texture (Default.frag:182-191)
+        ai = np.ascontiguousarray(ai, np.uint8)
+        keep.append(ai)
+        sc.ai_frame, sc.ai_width, sc.ai_height = ai.ctypes.data, ai.shape[1], ai.shape[0]
     shadow = getattr(scene, "shadow", None)
     if shadow is not None:
         sc.shadow = C.pointer(shadow)

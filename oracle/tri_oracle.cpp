@@ -685,6 +685,27 @@ float shadow_visibility(const ShadowMap& sm, vec3 l) {
     return lerpf(lerpf(c00, c10, a), lerpf(c01, c11, a), b);
 }
 
+// Default.frag:186-188: texture(AiBlendTexture, gl_FragCoord.xy * AiBlendConfig.yz) on the AI texture of
+// EnsureAiTextureResources (Renderer.cpp:1406-1470): R8G8B8A8_UNORM (decode b / 255), LINEAR, CLAMP_TO_EDGE, level 0,
+// Vulkan's unnormalized coordinates u * width - 0.5, floor and fraction.
+vec4 ai_sample(const uint8_t* tex, int32_t tw, int32_t th, float sx, float sy, int32_t px, int32_t py) {
+    const float u = ((float)px + 0.5f) * sx, v = ((float)py + 0.5f) * sy;
+    const float x = u * (float)tw - 0.5f, y = v * (float)th - 0.5f;
+    const float fx = std::floor(x), fy = std::floor(y);
+    const float a = x - fx, b = y - fy;
+    const int32_t i0 = (int32_t)std::fmin(std::fmax(fx, -1.0f), 1.0e9f), j0 = (int32_t)std::fmin(std::fmax(fy, -1.0f), 1.0e9f);
+    const int32_t xa = std::min(std::max(i0, 0), tw - 1), xb = std::min(std::max(i0 + 1, 0), tw - 1);
+    const int32_t ya = std::min(std::max(j0, 0), th - 1), yb = std::min(std::max(j0 + 1, 0), th - 1);
+    float r[4];
+    for (int c = 0; c < 4; ++c) {
+        auto t = [&](int32_t i, int32_t j) { return (float)tex[((size_t)j * tw + i) * 4 + c] / 255.0f; };
+        r[c] = lerpf(lerpf(t(xa, ya), t(xb, ya), a), lerpf(t(xa, yb), t(xb, yb), a), b);
+    }
+    return {r[0], r[1], r[2], r[3]};
+}
+// GLSL mix(x, y, a) = x * (1 - a) + y * a
+inline float mixf(float x, float y, float a) { return x * (1.0f - a) + y * a; }
+
 inline uint32_t unorm8(float c) {
     const float cc = std::fmin(std::fmax(c, 0.0f), 1.0f);  // NaN -> 0
     return (uint32_t)(int)(cc * 255.0f + 0.5f);
@@ -904,6 +925,9 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
     //      fragment's colour is the pixel colour) ----
     const uint32_t clear = pack_bgra({sc->clear_rgba[0], sc->clear_rgba[1], sc->clear_rgba[2], sc->clear_rgba[3]});
     const bool has_sky = sc->sky_faces != nullptr && sc->sky_size > 0;
+    // AiBlendConfig: w > 0 switches the blend on; the weight is clamp(x, 0, 1) and must be positive (Default.frag:182-185)
+    const float ai_w = std::fmin(std::fmax(g.ai_blend_config[0], 0.0f), 1.0f);
+    const bool ai_on = g.ai_blend_config[3] > 0.0f && ai_w > 0.0f && sc->ai_frame && sc->ai_width && sc->ai_height;
     const SkyConst skk = sky_constants(g);
     const Sky sky{sc->sky_faces, (int32_t)sc->sky_size};
     std::atomic<uint32_t> next_row{0};
@@ -955,7 +979,12 @@ extern "C" int oracle_render(const oracle_scene* sc, uint32_t W, uint32_t H, uin
                 if (shadow_on && g.light_counts[0] > 0u)
                     vis = shadow_visibility(sm, {ip(v0.lpos.x, v1.lpos.x, v2.lpos.x), ip(v0.lpos.y, v1.lpos.y, v2.lpos.y),
                                                  ip(v0.lpos.z, v1.lpos.z, v2.lpos.z)});
-                const vec4 c = fragment_shader(f, pc, g, mat0, texs[tidx], vis);
+                vec4 c = fragment_shader(f, pc, g, mat0, texs[tidx], vis);
+                if (ai_on) {  // Default.frag:182-191
+                    const vec4 ai = ai_sample(sc->ai_frame, (int32_t)sc->ai_width, (int32_t)sc->ai_height,
+                                              g.ai_blend_config[1], g.ai_blend_config[2], (int32_t)px, py);
+                    c = {mixf(c.x, ai.x, ai_w), mixf(c.y, ai.y, ai_w), mixf(c.z, ai.z, ai_w), mixf(c.w, ai.w, ai_w)};
+                }
                 if (out_bgra) out_bgra[idx] = pack_bgra(c);
             }
         }

@@ -54,6 +54,10 @@ typedef struct oracle_scene {
      * out_shadow_map (nullable) receives the size*size map (float32 depth bits). */
     const tri_shadow_config* shadow;
     uint32_t* out_shadow_map;
+    /* AI frame blend (Default.frag:182-191, tri_upload_ai_frame): ai_width x ai_height R8G8B8A8_UNORM texels,
+     * rows top to bottom; blends when the UBO's AiBlendConfig asks for it. NULL = no texture. */
+    const uint8_t* ai_frame;
+    uint32_t ai_width, ai_height;
 } oracle_scene;
 
 typedef struct oracle_stats {

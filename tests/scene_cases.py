@@ -257,3 +257,36 @@ def shadow_scene(oracle, w=480, h=320, size=256, sun=(-0.45, -1.0, -0.35), bias=
                      oracle.pack_ubo(view, proj, cam, lights), materials=[((0.9, 0.85, 0.8, 1.0), (0.1, 0.6, 1.0, 0.0))],
                      skybox=SOLID_0x808080)
     return scenes.with_shadow(s, size, bias, slope)
+
+
+def near_clip_multi(w=640, h=480, n=60, identity=False, shadow=False):
+    """near_clip_grid as two textured draws (the grid's index halves, each with its own sRGB slot): clipped primitives
+    on a frame outside the single-draw solid instantiation (obj48's object records through the clipper). identity:
+    the ground-plane rotation baked into the vertices, so both draws have identity models (the C5 case); otherwise
+    the second draw carries its own translation on top of the rotation (a per-draw transform per pixel)."""
+    s = near_clip_grid(w, h, n)
+    model = np.array(s.draws[0].pc.model, F).reshape(4, 4)  # [col][row]
+    if identity:
+        v = s.vertices.copy()
+        p = v["position"].astype(F)
+        nn = v["normal"].astype(F)
+        v["position"] = (p @ model[:3, :3] + model[3, :3]).astype(F)
+        v["normal"] = (nn @ model[:3, :3]).astype(F)
+        s.vertices = v
+        m0 = m1 = np.eye(4, dtype=F)
+    else:
+        m0 = model
+        m1 = scenes.compose_transform((0.4, 0.05, -5.3), (-90.0, 0.0, 0.0), (1.0, 1.0, 1.0))
+    half = (s.indices.size // 6) * 3
+    s.meshes = np.array([(0, half, 0, 0), (half, s.indices.size - half, 0, 0)], abi.MESH_RANGE_DTYPE)
+    s.textures = [(1, checker_texture(16, 8, 3)), (2, checker_texture(8, 16, 4))]
+    s.draws = [abi.make_draw(0, m0, texture_slot=1, material_index=0),
+               abi.make_draw(1, m1, texture_slot=2, material_index=0)]
+    s.ubo = scenes.pack_ubo(*scenes.editor_camera((0.0, 0.35, 0.0), (-28.0, 12.0, 0.0), 70.0, (w, h), 0.1, 40.0),
+                            (0.0, 0.35, 0.0), [{"type": "directional", "direction": (-0.3, -1.0, -0.2), "intensity": 3.0},
+                                               {"type": "point", "position": (0.5, 1.0, -2.0), "range": 6.0,
+                                                "intensity": 8.0}])
+    s.name = f"near_clip_multi{'_id' if identity else ''}{'_shadow' if shadow else ''}"
+    if shadow:
+        scenes.with_shadow(s, 512)
+    return s
