@@ -72,6 +72,243 @@ __global__ __launch_bounds__(kCodecBlock) void k_unpack_bgr24(const uint8_t* __r
     }
 }
 
+// ---- the delta bit-plane codec: a band as a 1-D pixel stream, 4096 pixels per fixed-size slot -------
+// Each wave codes one 1024-pixel segment as 16 blocks of 64 pixels, lane = pixel. Per block and channel (B, G, R) the
+// pixel-to-pixel difference (mod 256, the segment's first pixel stored whole in the slot header and coded as a zero
+// difference) is zigzag-mapped, the block's bit width w (0..8) is the width of the wave maximum, and the block stores w
+// bit planes, each a 64-bit ballot (lane i = bit i). Shaded frames are smooth between neighbours (C3: 1.42 B/pixel on
+// average, at most 1.59 in any slot; C5 with its textures 2.0 / 2.11), so a slot of S bytes carries 4096 pixels in far
+// fewer than the 3-byte format's 12288. Slot layout (S bytes, a multiple of 16):
+//   [0, 4)      the payload bytes P of the 64 blocks (the decoder's bound; P + 160 > S marks an overflowed slot)
+//   [16, 160)   4 segment headers of 36 B: the first pixel (B, G, R, 0) and 16 block widths w_b | w_g << 4 | w_r << 8
+//   [160, +P)   the blocks' planes in order, channel B's w_b planes, then G's, then R's
+// Both kernels run one 1024-thread workgroup per slot, wave w on blocks 4w..4w+3 (lane = pixel), with no serial chain.
+// They are VALU-issue-bound, so every step is counted in wave instructions per 64-pixel block:
+//   k_dbp_pack    a block's differences need only the pixel before it (a second, cached load); the three channels'
+//                 byte differences and zigzag maps are computed together in one 32-bit word (SWAR, ~12 ops), one DPP
+//                 OR-scan gives the three widths, and each plane that exists costs a bit test, a ballot and two
+//                 bit-field inserts (plane j parked in lane j). One wave's DPP prefix sum over the 64 blocks' plane counts
+//                 places every block; each lane < w stores plane `lane` of its channel (contiguous 8-B stores).
+//   k_dbp_unpack  the slot (header + payload, <= 12448 B) is copied to LDS with 16-B loads; every wave sums the 64
+//                 blocks' widths (lane = block, DPP scan) to find its blocks' planes. A plane costs one LDS read (lanes
+//                 0-31 read its low word, 32-63 its high word) and two ops (bit extract, shift-or into the packed
+//                 zigzag word); the zigzag inverse is SWAR over the three channels, and the differences are summed by
+//                 two DPP wave scans (B and R share one in 16-bit fields, G the other: only the sums mod 256 matter).
+//                 The blocks' totals meet in LDS; each block adds the totals of the blocks before it in its segment
+//                 (plus the segment's first pixel), wave-uniform arithmetic. One launch decodes up to
+//                 TRI_DBP_MAX_BANDS bands (the display GPU's remote bands), a workgroup per slot of any of them.
+// Lossless whenever no slot overflows; an overflow (a slot whose pixels need more than S bytes) sets flags[0] bit 1
+// and leaves the slot's pixels undecoded, so the caller grows S and sends the frame again (the bin-queue overflow
+// protocol). A slot whose widths do not add up to its payload count is not decoded either (not this format).
+constexpr uint32_t kDbpSlotPixels = 4096, kDbpHeader = 160, kDbpBlocks = 64, kDbpThreads = 1024;
+constexpr uint32_t kDbpMaxPayload = kDbpBlocks * 24u * 8u;  // 12288 B: 8 planes per channel in every block
+
+// v[lane - k] within the lane's row of 16 (CTRL row_shr:k), or row_bcast:15 / :31 onto the rows in ROW_MASK; 0 elsewhere
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp0(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += dpp0<0x111>(v);
+    v += dpp0<0x112>(v);
+    v += dpp0<0x114>(v);
+    v += dpp0<0x118>(v);
+    v += dpp0<0x142, 0xa>(v);
+    v += dpp0<0x143, 0xc>(v);
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_or(uint32_t v) {  // the OR over the wave (uniform)
+    v |= dpp0<0x111>(v);
+    v |= dpp0<0x112>(v);
+    v |= dpp0<0x114>(v);
+    v |= dpp0<0x118>(v);
+    v |= dpp0<0x142, 0xa>(v);
+    v |= dpp0<0x143, 0xc>(v);
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+// B, G, R bytes of (v - p) mod 256, each zigzag-mapped (0, -1, 1, -2, ... -> 0, 1, 2, 3, ...); alpha byte 0
+__device__ __forceinline__ uint32_t zigzag_diff3(uint32_t v, uint32_t p) {
+    constexpr uint32_t H = 0x00808080u, L = 0x007F7F7Fu;
+    const uint32_t d = (((v | H) - (p & L)) ^ ((v ^ ~p) & H)) & 0x00FFFFFFu;  // bytewise subtraction, no borrows
+    const uint32_t neg = (d >> 7) & 0x00010101u;                                // each byte's sign
+    return ((d << 1) & 0x00FEFEFEu) ^ (neg * 0xFFu);                            // (d << 1) ^ (d >> 7), per byte
+}
+__device__ __forceinline__ uint32_t width8(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
+// planes J..wc-1 of channel C of the wave's zigzag words: plane j (a ballot, in SGPRs) parked in lane j of l (low
+// word) and h (high word) by an and-or with the lane's mask lm[j] (all ones in lane j): one v_and_or per word,
+// an operation the compiler sees (a v_writelane in inline asm would not survive its copies under partial exec masks)
+template <uint32_t C, uint32_t J>
+__device__ __forceinline__ void park_planes(uint32_t zz, uint32_t wc, const uint32_t (&lm)[8], uint32_t& l, uint32_t& h) {
+    if constexpr (J < 8) {
+        if (J < wc) {
+            const uint64_t pl = __ballot((zz >> (8 * C + J)) & 1u);
+            // l and h start at 0 and every lane is written once: (lm & plane) | l, one v_and_or each (a plain
+            // per-lane operation; the compiler splits it into an and and an or with an SGPR operand). The ballot's
+            // SGPRs were just written by a VALU compare: two wait states before a VALU reads them (the compiler
+            // inserts them for its own code, not for inline assembly)
+            asm("s_nop 1\n\tv_and_or_b32 %0, %1, %2, %0" : "+v"(l) : "v"(lm[J]), "s"((uint32_t)pl));
+            asm("v_and_or_b32 %0, %1, %2, %0" : "+v"(h) : "v"(lm[J]), "s"((uint32_t)(pl >> 32)));
+            park_planes<C, J + 1>(zz, wc, lm, l, h);
+        }
+    }
+}
+
+__global__ __launch_bounds__(kDbpThreads) void k_dbp_pack(const uint32_t* __restrict__ src, uint64_t n, uint32_t alpha,
+                                                          uint8_t* __restrict__ dst, uint32_t slot_bytes,
+                                                          uint32_t* __restrict__ flags) {
+    __shared__ uint32_t hdr[kDbpHeader / 4];
+    __shared__ uint32_t cnt[kDbpBlocks];
+    __shared__ uint32_t offs[kDbpBlocks + 1];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t slot0 = (uint64_t)blockIdx.x * kDbpSlotPixels;
+    uint32_t lo[4][3], hi[4][3], wd[4], lm[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        lm[j] = lane == j ? ~0u : 0u;
+        asm volatile("" : "+v"(lm[j]));  // an opaque vector value: kept as a VGPR operand, not turned into lane masks
+    }
+    bool bad = false;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t b = 4u * w + q;
+        const uint64_t i = slot0 + 64u * b + lane;
+        // pixels past the band repeat its last one (zero differences); a segment's first pixel is its own predecessor
+        const bool seg_first = (b & 15u) == 0 && lane == 0;
+        const uint64_t ip = seg_first ? i : i - 1;
+        const uint32_t v = src[i < n ? i : n - 1];
+        const uint32_t p = src[ip < n ? ip : n - 1];
+        bad |= i < n && (v >> 24) != alpha;
+        const uint32_t zz = zigzag_diff3(v, p);
+        const uint32_t any = wave_or(zz);
+        const uint32_t w0 = width8(any & 0xFFu), w1 = width8((any >> 8) & 0xFFu), w2 = width8((any >> 16) & 0xFFu);
+        const uint32_t wq = w0 | (w1 << 4) | (w2 << 8);
+        lo[q][0] = hi[q][0] = lo[q][1] = hi[q][1] = lo[q][2] = hi[q][2] = 0;
+        park_planes<0, 0>(zz, w0, lm, lo[q][0], hi[q][0]);
+        park_planes<1, 0>(zz, w1, lm, lo[q][1], hi[q][1]);
+        park_planes<2, 0>(zz, w2, lm, lo[q][2], hi[q][2]);
+        wd[q] = wq;
+        if (lane == 0) {
+            reinterpret_cast<uint16_t*>(hdr + 4 + 9 * (b >> 4) + 1)[b & 15u] = (uint16_t)wq;
+            cnt[b] = (wq & 15u) + ((wq >> 4) & 15u) + (wq >> 8);
+            if ((b & 15u) == 0) hdr[4 + 9 * (b >> 4)] = i < n ? v & 0x00FFFFFFu : 0u;
+        }
+    }
+    if (__ballot(bad) != 0ull && lane == 0 && flags) atomicOr(flags, 1u);
+    __syncthreads();
+    if (w == 0) {
+        const uint32_t c = cnt[lane];
+        const uint32_t incl = wave_incl_sum(c);
+        offs[lane] = incl - c;
+        if (lane == 63) offs[kDbpBlocks] = incl;
+    }
+    __syncthreads();
+    const uint32_t total = offs[kDbpBlocks];
+    const uint32_t bytes = kDbpHeader + 8u * total;
+    uint8_t* slot = dst + (size_t)blockIdx.x * slot_bytes;
+    if (threadIdx.x == 0 && flags) {
+        atomicMax(flags + 1, bytes);
+        if (bytes > slot_bytes) atomicOr(flags, 2u);
+    }
+    if (bytes > slot_bytes) {  // overflow: only the payload count (the decoder leaves the slot alone)
+        if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(slot) = 8u * total;
+        return;
+    }
+    if (threadIdx.x < kDbpHeader / 4)
+        reinterpret_cast<uint32_t*>(slot)[threadIdx.x] = threadIdx.x == 0 ? 8u * total : threadIdx.x < 4 ? 0u : hdr[threadIdx.x];
+    uint2* pay = reinterpret_cast<uint2*>(slot + kDbpHeader);
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        uint32_t o = offs[4u * w + q];
+#pragma unroll
+        for (int c = 0; c < 3; ++c) {
+            const uint32_t wc = (wd[q] >> (4 * c)) & 15u;
+            if (lane < wc) pay[o + lane] = make_uint2(lo[q][c], hi[q][c]);
+            o += wc;
+        }
+    }
+}
+
+struct DbpBands {  // the bands one k_dbp_unpack launch decodes (kernel argument)
+    const uint8_t* src[TRI_DBP_MAX_BANDS];
+    uint32_t* dst[TRI_DBP_MAX_BANDS];
+    uint64_t n[TRI_DBP_MAX_BANDS];
+    uint32_t first[TRI_DBP_MAX_BANDS + 1];  // first slot (workgroup) of each band; first[count] = the grid
+    uint32_t count;
+};
+
+__global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint32_t alpha, uint32_t slot_bytes) {
+    __shared__ uint4 lds[(kDbpHeader + kDbpMaxPayload) / 16 + 8];  // + 128 B: a block's last channel reads 8 planes
+    __shared__ uint32_t tot[kDbpBlocks][2];
+    uint32_t band = 0;  // the band this slot belongs to (wave-uniform search over <= 16 entries)
+    while (band + 1 < bands.count && blockIdx.x >= bands.first[band + 1]) ++band;
+    const uint64_t n = bands.n[band];
+    uint32_t* __restrict__ dst = bands.dst[band];
+    const uint32_t sl = blockIdx.x - bands.first[band];
+    const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+    const uint64_t slot0 = (uint64_t)sl * kDbpSlotPixels;
+    const uint8_t* slot = bands.src[band] + (size_t)sl * slot_bytes;
+    const uint32_t payload = *reinterpret_cast<const uint32_t*>(slot);
+    // an overflowed slot (the sender flagged the frame), or more payload than the format has: left alone
+    if (kDbpHeader + payload > slot_bytes || payload > kDbpMaxPayload) return;
+    if (16u * threadIdx.x < kDbpHeader + payload)
+        lds[threadIdx.x] = reinterpret_cast<const uint4*>(slot)[threadIdx.x];
+    __syncthreads();
+    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(lds);
+    // lane l: block l's widths and plane count; the inclusive sum places every block's planes
+    const uint32_t wl = reinterpret_cast<const uint16_t*>(hdr + 4 + 9 * (lane >> 4) + 1)[lane & 15u];
+    const uint32_t cl = (wl & 15u) + ((wl >> 4) & 15u) + ((wl >> 8) & 15u);
+    const uint32_t incl = wave_incl_sum(cl);
+    if (8u * (uint32_t)__builtin_amdgcn_readlane((int)incl, 63) != payload) return;  // not a dbp slot (uniform)
+    // this lane's word of every plane: the low word for lanes 0-31, the high word for 32-63
+    const uint32_t* planes = hdr + kDbpHeader / 4 + (lane >> 5);
+    const uint32_t sh = lane & 31u;
+    uint32_t s0[4], s1[4];  // inclusive sums: B | R << 16, and G
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t b = 4u * w + q;
+        const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)wl, (int)b);
+        uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)(incl - cl), (int)b);
+        uint32_t zz = 0;  // the three zigzag values, one per byte
+#pragma unroll
+        for (uint32_t c = 0; c < 3; ++c) {
+            // all 8 candidate planes at once (independent LDS reads, paired by the compiler; the ones past the
+            // channel's width belong to the next channel or block and are masked off): no branch and no wait per plane
+            const uint32_t wc = (wb >> (4 * c)) & 15u;
+            uint32_t z = 0;
+#pragma unroll
+            for (uint32_t j = 0; j < 8; ++j) z |= ((planes[2 * (o + j)] >> sh) & 1u) << j;
+            zz |= (z & ((1u << wc) - 1u)) << (8 * c);
+            o += wc;
+        }
+        // zigzag back to the differences (mod 256), per byte
+        const uint32_t d = ((zz >> 1) & 0x007F7F7Fu) ^ ((zz & 0x00010101u) * 0xFFu);
+        s0[q] = wave_incl_sum(d & 0x00FF00FFu);
+        s1[q] = wave_incl_sum((d >> 8) & 0xFFu);
+        if (lane == 63) {
+            tot[b][0] = s0[q];
+            tot[b][1] = s1[q];
+        }
+    }
+    __syncthreads();
+    // the carry into this wave's first block: its segment's first pixel plus the totals of the blocks before it
+    const uint32_t seg = w >> 2, b0 = 4u * w;
+    const uint32_t first = hdr[4 + 9 * seg];
+    uint32_t c0 = first & 0x00FF00FFu, c1 = (first >> 8) & 0xFFu;
+    for (uint32_t k = 16u * seg; k < b0; ++k) {
+        c0 = (c0 + tot[k][0]) & 0x00FF00FFu;
+        c1 = (c1 + tot[k][1]) & 0xFFu;
+    }
+    const uint32_t a = alpha << 24;
+#pragma unroll
+    for (uint32_t q = 0; q < 4; ++q) {
+        const uint32_t x0 = c0 + s0[q], x1 = c1 + s1[q];
+        const uint64_t i = slot0 + 64u * (b0 + q) + lane;
+        if (i < n) dst[i] = a | (x0 & 0x00FF00FFu) | ((x1 & 0xFFu) << 8);
+        c0 = (c0 + tot[b0 + q][0]) & 0x00FF00FFu;
+        c1 = (c1 + tot[b0 + q][1]) & 0xFFu;
+    }
+}
+
 dim3 codec_grid(uint64_t n) { return dim3((uint32_t)((n + 4ull * kCodecBlock - 1) / (4ull * kCodecBlock))); }
 bool vec_ok(const void* four, const void* three) { return ((uintptr_t)four & 15u) == 0 && ((uintptr_t)three & 3u) == 0; }
 
@@ -92,7 +329,86 @@ hipError_t tri_launch_unpack_bgr24(const uint8_t* src, uint32_t* dst, uint64_t n
     return hipGetLastError();
 }
 
+uint64_t tri_dbp_stream_bytes(uint64_t pixels, uint32_t slot_bytes) {
+    return (pixels + kDbpSlotPixels - 1) / kDbpSlotPixels * (uint64_t)slot_bytes;
+}
+
+hipError_t tri_launch_dbp_pack(const uint32_t* src, uint64_t n, uint32_t alpha, uint8_t* dst, uint32_t slot_bytes,
+                               uint32_t* flags, hipStream_t stream) {
+    if (n == 0) return hipSuccess;
+    const dim3 g((uint32_t)((n + kDbpSlotPixels - 1) / kDbpSlotPixels));
+    hipLaunchKernelGGL(k_dbp_pack, g, dim3(kDbpThreads), 0, stream, src, n, alpha, dst, slot_bytes, flags);
+    return hipGetLastError();
+}
+
+hipError_t tri_launch_dbp_unpack_bands(const uint8_t* const* src, uint32_t* const* dst, const uint64_t* n, uint32_t count,
+                                       uint32_t alpha, uint32_t slot_bytes, hipStream_t stream) {
+    DbpBands b{};
+    uint32_t grid = 0;
+    for (uint32_t k = 0; k < count; ++k) {
+        b.src[b.count] = src[k];
+        b.dst[b.count] = dst[k];
+        b.n[b.count] = n[k];
+        b.first[b.count] = grid;
+        grid += (uint32_t)((n[k] + kDbpSlotPixels - 1) / kDbpSlotPixels);
+        if (n[k]) ++b.count;  // empty bands take no slot
+    }
+    b.first[b.count] = grid;
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_dbp_unpack, dim3(grid), dim3(kDbpThreads), 0, stream, b, alpha, slot_bytes);
+    return hipGetLastError();
+}
+
+hipError_t tri_launch_dbp_unpack(const uint8_t* src, uint64_t n, uint32_t alpha, uint32_t slot_bytes, uint32_t* dst,
+                                 hipStream_t stream) {
+    return tri_launch_dbp_unpack_bands(&src, &dst, &n, 1, alpha, slot_bytes, stream);
+}
+
 extern "C" {
+
+int tri_dbp_pack(const void* bgra, uint64_t pixels, uint32_t alpha, void* stream_out, uint32_t slot_bytes, uint32_t* flags,
+                 void* stream) {
+    if ((pixels && (!bgra || !stream_out)) || alpha > 255u || slot_bytes < TRI_DBP_MIN_SLOT || slot_bytes % 16u)
+        return tri_internal_fail(TRI_E_INVALID, "tri_dbp_pack: bad argument");
+    if (((uintptr_t)bgra & 3u) || ((uintptr_t)stream_out & 15u))
+        return tri_internal_fail(TRI_E_INVALID, "tri_dbp_pack: misaligned buffer");
+    const hipError_t e = tri_launch_dbp_pack(static_cast<const uint32_t*>(bgra), pixels, alpha,
+                                             static_cast<uint8_t*>(stream_out), slot_bytes, flags,
+                                             static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TRI_OK : tri_internal_fail(TRI_E_HIP, hipGetErrorString(e));
+}
+
+int tri_dbp_unpack(const void* stream_in, uint64_t pixels, uint32_t alpha, uint32_t slot_bytes, void* bgra, void* stream) {
+    if ((pixels && (!bgra || !stream_in)) || alpha > 255u || slot_bytes < TRI_DBP_MIN_SLOT || slot_bytes % 16u)
+        return tri_internal_fail(TRI_E_INVALID, "tri_dbp_unpack: bad argument");
+    if (((uintptr_t)bgra & 3u) || ((uintptr_t)stream_in & 15u))
+        return tri_internal_fail(TRI_E_INVALID, "tri_dbp_unpack: misaligned buffer");
+    const hipError_t e = tri_launch_dbp_unpack(static_cast<const uint8_t*>(stream_in), pixels, alpha, slot_bytes,
+                                               static_cast<uint32_t*>(bgra), static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TRI_OK : tri_internal_fail(TRI_E_HIP, hipGetErrorString(e));
+}
+
+uint64_t tri_dbp_bytes(uint64_t pixels, uint32_t slot_bytes) { return tri_dbp_stream_bytes(pixels, slot_bytes); }
+
+int tri_dbp_unpack_bands(const void* const* streams, void* const* bgra, const uint64_t* pixels, uint32_t count,
+                         uint32_t alpha, uint32_t slot_bytes, void* stream) {
+    if ((count && (!streams || !bgra || !pixels)) || count > TRI_DBP_MAX_BANDS || alpha > 255u ||
+        slot_bytes < TRI_DBP_MIN_SLOT || slot_bytes % 16u)
+        return tri_internal_fail(TRI_E_INVALID, "tri_dbp_unpack_bands: bad argument");
+    const uint8_t* src[TRI_DBP_MAX_BANDS];
+    uint32_t* dst[TRI_DBP_MAX_BANDS];
+    for (uint32_t k = 0; k < count; ++k) {
+        if (pixels[k] && (!streams[k] || !bgra[k]))
+            return tri_internal_fail(TRI_E_INVALID, "tri_dbp_unpack_bands: null buffer");
+        if (((uintptr_t)bgra[k] & 3u) || ((uintptr_t)streams[k] & 15u))
+            return tri_internal_fail(TRI_E_INVALID, "tri_dbp_unpack_bands: misaligned buffer");
+        src[k] = static_cast<const uint8_t*>(streams[k]);
+        dst[k] = static_cast<uint32_t*>(bgra[k]);
+    }
+    const hipError_t e = tri_launch_dbp_unpack_bands(src, dst, pixels, count, alpha, slot_bytes,
+                                                     static_cast<hipStream_t>(stream));
+    return e == hipSuccess ? TRI_OK : tri_internal_fail(TRI_E_HIP, hipGetErrorString(e));
+}
 
 int tri_pack_bgr24(const void* bgra, void* bgr, uint64_t pixels, uint32_t alpha, uint32_t* flag, void* stream) {
     if ((pixels && (!bgra || !bgr)) || alpha > 255u) return tri_internal_fail(TRI_E_INVALID, "tri_pack_bgr24: bad argument");

@@ -126,6 +126,13 @@ hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* 
 hipError_t tri_launch_pack_bgr24(const uint32_t* src, uint8_t* dst, uint64_t n, uint32_t alpha, uint32_t* flag,
                                  hipStream_t stream);
 hipError_t tri_launch_unpack_bgr24(const uint8_t* src, uint32_t* dst, uint64_t n, uint32_t alpha, hipStream_t stream);
+hipError_t tri_launch_dbp_pack(const uint32_t* src, uint64_t n, uint32_t alpha, uint8_t* dst, uint32_t slot_bytes,
+                               uint32_t* flags, hipStream_t stream);
+hipError_t tri_launch_dbp_unpack(const uint8_t* src, uint64_t n, uint32_t alpha, uint32_t slot_bytes, uint32_t* dst,
+                                 hipStream_t stream);
+uint64_t tri_dbp_stream_bytes(uint64_t pixels, uint32_t slot_bytes);
+hipError_t tri_launch_dbp_unpack_bands(const uint8_t* const* src, uint32_t* const* dst, const uint64_t* n, uint32_t count,
+                                       uint32_t alpha, uint32_t slot_bytes, hipStream_t stream);
 
 // Internal accessors for the group layer (tri_group.hip): a context's stream and device.
 hipStream_t tri_internal_stream(tri_ctx* ctx);

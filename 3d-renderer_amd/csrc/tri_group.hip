@@ -43,10 +43,14 @@ struct tri_group {
     std::vector<hipEvent_t> band_done;   // per band: its render of the current frame finished
     std::vector<hipEvent_t> asm_done[2]; // per buffer parity, per distinct device: that frame's assembly finished
     std::vector<uint32_t*> band_buf[2];  // per buffer parity, per band on a non-display device: its colour band
-    std::vector<uint8_t*> band_pack[2];  // ... the band as 3-byte pixels (band_codec.hip), on the band's device
-    std::vector<uint8_t*> rx[2];         // ... its 3-byte pixels received on the display device
-    std::vector<uint32_t*> flag;         // per remote band, on its device: the packer's alpha check (0 = lossless)
-    bool packed_last = false;            // the most recent frame travelled as 3-byte pixels
+    std::vector<uint8_t*> band_pack[2];  // ... the band packed (band_codec.hip: 3-byte or dbp), on the band's device
+    std::vector<uint8_t*> rx[2];         // ... its packed bytes received on the display device
+    // per remote band, on its device: [0] the packer's sticky flags (1 alpha differs, 2 a dbp slot overflowed;
+    // 0 = lossless), [1] the largest dbp slot its frames needed since the last tri_group_synchronize
+    std::vector<uint32_t*> flag;
+    uint32_t slot = TRI_DBP_MAX_SLOT;    // the dbp slot size the next frame uses (refitted at synchronize)
+    uint32_t fmt_last = TRI_GROUP_FMT_BGRA32, slot_last = 0;  // the most recent frame's transfer
+    uint64_t inbound_last = 0;
     uint32_t* frame[2] = {nullptr, nullptr};  // W*H on the display device
     hipEvent_t present_done[2] = {nullptr, nullptr};  // consumer fence per buffer (tri_group_present)
     bool present_armed[2] = {false, false};
@@ -95,6 +99,17 @@ int each(tri_group* g, F&& f) {
         if (rc) return rc;
     }
     return TRI_OK;
+}
+
+// Bytes a packed band of px pixels may take: the 3-byte format, or the delta bit-plane format at its largest slot.
+size_t packed_capacity(size_t px) {
+    return std::max(px * 3, (size_t)tri_dbp_stream_bytes(px, TRI_DBP_MAX_SLOT));
+}
+
+// The transfer format of a frame whose alpha tri_frame_alpha returned (-1: not proven uniform).
+uint32_t frame_format(const tri_group* g, int32_t alpha) {
+    if ((g->gflags & TRI_GROUP_NO_PACK) || alpha < 0) return TRI_GROUP_FMT_BGRA32;
+    return (g->gflags & TRI_GROUP_PACK_BGR24) ? TRI_GROUP_FMT_BGR24 : TRI_GROUP_FMT_DBP;
 }
 
 // Buffer parity of the most recent frame (the one tri_group_frame / readback / present refer to).
@@ -209,18 +224,18 @@ int tri_group_create(const tri_group_config* cfg, tri_group** out) {
             const size_t px = (size_t)(g->y1[r] - g->y0[r]) * g->W;
             for (int p = 0; p < 2; ++p)
                 if (hipMalloc(&g->band_buf[p][r], px * 4) != hipSuccess ||
-                    (!(g->gflags & TRI_GROUP_NO_PACK) && hipMalloc(&g->band_pack[p][r], px * 3) != hipSuccess))
+                    (!(g->gflags & TRI_GROUP_NO_PACK) && hipMalloc(&g->band_pack[p][r], packed_capacity(px)) != hipSuccess))
                     return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: band buffer allocation failed"));
             if (!(g->gflags & TRI_GROUP_NO_PACK)) {
                 // zeroed on the band context's own stream: its packer runs on that stream, so the clear is ordered
                 // before every pack (a null-stream memset is not ordered with a non-blocking stream)
-                if (hipMalloc(&g->flag[r], 4) != hipSuccess ||
-                    hipMemsetAsync(g->flag[r], 0, 4, tri_internal_stream(g->ctx[r])) != hipSuccess)
+                if (hipMalloc(&g->flag[r], 8) != hipSuccess ||
+                    hipMemsetAsync(g->flag[r], 0, 8, tri_internal_stream(g->ctx[r])) != hipSuccess)
                     return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: flag allocation failed"));
                 if (hipSetDevice(ddev) != hipSuccess)
                     return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: hipSetDevice failed"));
                 for (int p = 0; p < 2; ++p)
-                    if (hipMalloc(&g->rx[p][r], px * 3) != hipSuccess)
+                    if (hipMalloc(&g->rx[p][r], packed_capacity(px)) != hipSuccess)
                         return bail(tri_internal_fail(TRI_E_OOM, "tri_group_create: receive buffer allocation failed"));
                 if (hipSetDevice(g->dev[r]) != hipSuccess)
                     return bail(tri_internal_fail(TRI_E_HIP, "tri_group_create: hipSetDevice failed"));
@@ -315,14 +330,17 @@ int tri_group_render(tri_group* g) {
     if (!g) return tri_internal_fail(TRI_E_INVALID, "tri_group_render: null group");
     const int32_t ddev = g->dev[g->display];
     const uint32_t p = (uint32_t)(g->frames & 1u);
-    // 3-byte transfer when every pixel's alpha is provably one value (every band context holds the same
+    // a packed transfer when every pixel's alpha is provably one value (every band context holds the same
     // frame state: tri_group_set_* broadcasts it)
     int32_t alpha = -1;
     if (!(g->gflags & TRI_GROUP_NO_PACK)) {
         const int rc = tri_frame_alpha(g->ctx[g->display], &alpha);
         if (rc) return rc;
     }
-    const bool pack = alpha >= 0;
+    const uint32_t fmt = frame_format(g, alpha);
+    const bool pack = fmt != TRI_GROUP_FMT_BGRA32, dbp = fmt == TRI_GROUP_FMT_DBP;
+    const uint32_t slot = g->slot;  // this frame's dbp slot size (both ends of every band use it)
+    auto pixels = [&](uint32_t r) { return (uint64_t)(g->y1[r] - g->y0[r]) * g->W; };
     for (uint32_t r = 0; r < g->n; ++r) {
         GH(hipSetDevice(g->dev[r]));
         hipStream_t s = tri_internal_stream(g->ctx[r]);
@@ -340,9 +358,12 @@ int tri_group_render(tri_group* g) {
         int rc = tri_bind_output(g->ctx[r], out_ptr, nullptr);  // depth stays in the band context
         if (rc) return rc;
         if ((rc = tri_render(g->ctx[r]))) return rc;
-        if (pack && travels(g, r))  // B, G, R bytes only, behind the band's raster on its stream
-            GH(tri_launch_pack_bgr24(g->band_buf[p][r], g->band_pack[p][r], (uint64_t)(g->y1[r] - g->y0[r]) * g->W,
-                                     (uint32_t)alpha, g->flag[r], s));
+        if (pack && travels(g, r)) {  // behind the band's raster on its stream
+            if (dbp)
+                GH(tri_launch_dbp_pack(g->band_buf[p][r], pixels(r), (uint32_t)alpha, g->band_pack[p][r], slot, g->flag[r], s));
+            else
+                GH(tri_launch_pack_bgr24(g->band_buf[p][r], g->band_pack[p][r], pixels(r), (uint32_t)alpha, g->flag[r], s));
+        }
         GH(hipEventRecord(g->band_done[r], s));
     }
     const int disp = g->urank[g->display];
@@ -361,7 +382,9 @@ int tri_group_render(tri_group* g) {
     auto source = [&](uint32_t r) -> const void* {
         return pack ? static_cast<const void*>(g->band_pack[p][r]) : static_cast<const void*>(g->band_buf[p][r]);
     };
-    auto bytes = [&](uint32_t r) { return (size_t)(g->y1[r] - g->y0[r]) * g->W * (pack ? 3u : 4u); };
+    auto bytes = [&](uint32_t r) -> size_t {
+        return dbp ? (size_t)tri_dbp_stream_bytes(pixels(r), slot) : (size_t)pixels(r) * (pack ? 3u : 4u);
+    };
     if (!g->comm.empty()) {
         GN(ncclGroupStart());
         for (uint32_t r = 0; r < g->n; ++r) {
@@ -375,11 +398,22 @@ int tri_group_render(tri_group* g) {
     for (uint32_t r = 0; r < g->n; ++r)  // staged bands on the display device itself: a device-local copy
         if (travels(g, r) && g->dev[r] == ddev)
             GH(hipMemcpyAsync(landing(r), source(r), bytes(r), hipMemcpyDeviceToDevice, g->astream[disp]));
-    if (pack)  // restore the 4-byte pixels with the proven alpha, behind the receives
+    if (pack) {  // restore the 4-byte pixels with the proven alpha, behind the receives
+        std::vector<const uint8_t*> from;
+        std::vector<uint32_t*> to;
+        std::vector<uint64_t> npx;
         for (uint32_t r = 0; r < g->n; ++r)
-            if (travels(g, r))
-                GH(tri_launch_unpack_bgr24(g->rx[p][r], g->frame[p] + (size_t)g->y0[r] * g->W,
-                                           (uint64_t)(g->y1[r] - g->y0[r]) * g->W, (uint32_t)alpha, g->astream[disp]));
+            if (travels(g, r)) {
+                from.push_back(g->rx[p][r]);
+                to.push_back(g->frame[p] + (size_t)g->y0[r] * g->W);
+                npx.push_back(pixels(r));
+                if (!dbp) GH(tri_launch_unpack_bgr24(from.back(), to.back(), npx.back(), (uint32_t)alpha, g->astream[disp]));
+            }
+        for (size_t k = 0; dbp && k < from.size(); k += TRI_DBP_MAX_BANDS)  // every remote band in one launch
+            GH(tri_launch_dbp_unpack_bands(from.data() + k, to.data() + k, npx.data() + k,
+                                           (uint32_t)std::min<size_t>(TRI_DBP_MAX_BANDS, from.size() - k),
+                                           (uint32_t)alpha, slot, g->astream[disp]));
+    }
     for (size_t u = 0; u < g->udev.size(); ++u) {
         GH(hipSetDevice(g->udev[u]));
         GH(hipEventRecord(g->asm_done[p][u], g->astream[u]));
@@ -387,7 +421,11 @@ int tri_group_render(tri_group* g) {
     g->asm_recorded[p] = true;
     g->present_armed[p] = false;  // waited for; the consumer re-arms it for this frame
     g->blit_armed[p] = false;
-    g->packed_last = pack;
+    g->fmt_last = fmt;
+    g->slot_last = dbp ? slot : 0u;
+    g->inbound_last = 0;
+    for (uint32_t r = 0; r < g->n; ++r)
+        if (g->dev[r] != ddev) g->inbound_last += bytes(r);
     ++g->frames;
     return TRI_OK;
 }
@@ -415,28 +453,59 @@ int tri_group_synchronize(tri_group* g) {
         GH(hipSetDevice(g->udev[u]));
         GH(hipStreamSynchronize(g->astream[u]));
     }
-    for (uint32_t r = 0; r < g->n && status == TRI_OK; ++r) {  // every packed band kept the proven alpha
+    // every packed band kept the proven alpha and fitted its dbp slots; the dbp slot is refitted to the largest
+    // slot the frames since the previous synchronize needed (+ 1/16)
+    uint32_t need = 0;
+    bool alpha_bad = false, overflow = false;
+    for (uint32_t r = 0; r < g->n; ++r) {
         if (!g->flag[r]) continue;
-        uint32_t f = 0;
+        uint32_t f[2] = {0, 0};
         GH(hipSetDevice(g->dev[r]));
-        GH(hipMemcpy(&f, g->flag[r], 4, hipMemcpyDeviceToHost));
-        if (f) {
+        GH(hipMemcpy(f, g->flag[r], 8, hipMemcpyDeviceToHost));
+        if (f[0] || f[1])
             // reported once: cleared on the band's stream (idle here), so a later lossless frame synchronises clean.
             // Frames handed out (tri_group_frame / get_output / blit) without a synchronize are not checked.
-            GH(hipMemsetAsync(g->flag[r], 0, 4, tri_internal_stream(g->ctx[r])));
-            status = tri_internal_fail(TRI_E_STATE, "tri_group: a band's alpha was not the proven value (lossy 3-byte transfer)");
-        }
+            GH(hipMemsetAsync(g->flag[r], 0, 8, tri_internal_stream(g->ctx[r])));
+        alpha_bad |= (f[0] & 1u) != 0;
+        overflow |= (f[0] & 2u) != 0;
+        need = std::max(need, f[1]);
     }
+    if (need) {
+        const uint32_t fit = (need + need / 16u + 15u) / 16u * 16u;
+        g->slot = std::min<uint32_t>(TRI_DBP_MAX_SLOT, std::max<uint32_t>(TRI_DBP_MIN_SLOT, fit));
+    }
+    if (status == TRI_OK && alpha_bad)
+        status = tri_internal_fail(TRI_E_STATE, "tri_group: a band's alpha was not the proven value (lossy packed transfer)");
+    if (status == TRI_OK && overflow)
+        status = tri_internal_fail(TRI_E_OVERFLOW, "tri_group: a band outgrew its dbp slots (slot refitted: render the frame again)");
     return status;
 }
 
 int tri_group_transfer_info(tri_group* g, uint32_t* bytes_per_pixel, uint64_t* inbound_bytes) {
     if (!g || !bytes_per_pixel || !inbound_bytes) return tri_internal_fail(TRI_E_INVALID, "tri_group_transfer_info: null argument");
-    *bytes_per_pixel = g->packed_last ? 3u : 4u;
-    uint64_t in = 0;
+    uint64_t px = 0, bytes = 0;  // every band that travelled (staged bands too), for the bytes per pixel
     for (uint32_t r = 0; r < g->n; ++r)
-        if (g->dev[r] != g->dev[g->display]) in += (uint64_t)(g->y1[r] - g->y0[r]) * g->W * *bytes_per_pixel;
-    *inbound_bytes = in;
+        if (travels(g, r)) {
+            const uint64_t n = (uint64_t)(g->y1[r] - g->y0[r]) * g->W;
+            px += n;
+            bytes += g->fmt_last == TRI_GROUP_FMT_DBP ? tri_dbp_stream_bytes(n, g->slot_last)
+                                                       : n * (g->fmt_last == TRI_GROUP_FMT_BGR24 ? 3u : 4u);
+        }
+    *bytes_per_pixel = g->fmt_last == TRI_GROUP_FMT_DBP ? (uint32_t)((bytes + px - 1) / std::max<uint64_t>(px, 1))
+                                                        : (g->fmt_last == TRI_GROUP_FMT_BGR24 ? 3u : 4u);
+    *inbound_bytes = g->inbound_last;
+    return TRI_OK;
+}
+
+int tri_group_transfer_format(tri_group* g, uint32_t* format, uint32_t* slot_bytes) {
+    if (!g || !format || !slot_bytes) return tri_internal_fail(TRI_E_INVALID, "tri_group_transfer_format: null argument");
+    if (g->frames) {
+        *format = g->fmt_last;
+        *slot_bytes = g->slot_last;
+    } else {  // what the next frame would use with a proven alpha
+        *format = frame_format(g, 0);
+        *slot_bytes = *format == TRI_GROUP_FMT_DBP ? g->slot : 0u;
+    }
     return TRI_OK;
 }
 

@@ -150,6 +150,9 @@ class TriFrameStats(C.Structure):
 TRI_PATH_ONE_DRAW, TRI_PATH_VARY_OBJ, TRI_PATH_OBJ_XFORM, TRI_PATH_OBJ_UCOL, TRI_PATH_SHADOW = 0x1, 0x2, 0x4, 0x8, 0x10
 TRI_PATH_OBJ48 = 0x20
 
+# the delta bit-plane band format (include/tri_raster.h)
+TRI_DBP_SLOT_PIXELS, TRI_DBP_MIN_SLOT, TRI_DBP_MAX_SLOT, TRI_DBP_MAX_BANDS = 4096, 176, 12448, 16
+
 
 class TriShadowConfig(C.Structure):
     _fields_ = [
@@ -197,6 +200,8 @@ class TriGroupConfig(C.Structure):
 
 TRI_GROUP_NO_PACK = 0x1
 TRI_GROUP_STAGE_BANDS = 0x2
+TRI_GROUP_PACK_BGR24 = 0x4
+TRI_GROUP_FMT_BGRA32, TRI_GROUP_FMT_BGR24, TRI_GROUP_FMT_DBP = 0, 1, 2
 
 for _s, _n in ((TriImage, 32), (TriGroupConfig, 32), (TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
                (TriShadowConfig, 80)):
@@ -227,6 +232,11 @@ CABI_FUNCTIONS = [
     ("tri_frame_alpha", C.c_int, [C.c_void_p, C.POINTER(C.c_int32)]),
     ("tri_pack_bgr24", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("tri_unpack_bgr24", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]),
+    ("tri_dbp_pack", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("tri_dbp_unpack", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    ("tri_dbp_bytes", C.c_uint64, [C.c_uint64, C.c_uint32]),
+    ("tri_dbp_unpack_bands", C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_uint32,
+                                       C.c_uint32, C.c_uint32, C.c_void_p]),
     ("tri_set_timing", C.c_int, [C.c_void_p, C.c_int]),
     ("tri_get_timing", C.c_int, [C.c_void_p, C.POINTER(TriTiming)]),
     ("tri_get_frame_stats", C.c_int, [C.c_void_p, C.POINTER(TriFrameStats)]),
@@ -263,6 +273,7 @@ CABI_FUNCTIONS = [
     ("tri_group_blit_linear", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32]),
     ("tri_group_read_present", C.c_int, [C.c_void_p, C.c_void_p]),
     ("tri_group_transfer_info", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint64)]),
+    ("tri_group_transfer_format", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32), C.POINTER(C.c_uint32)]),
 ]
 
 

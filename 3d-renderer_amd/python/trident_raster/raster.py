@@ -274,6 +274,36 @@ def unpack_bgr24(src_ptr, dst_ptr, pixels, alpha, stream_ptr=None):
                                  C.c_void_p(stream_ptr) if stream_ptr else None))
 
 
+def dbp_pack(src_ptr, pixels, alpha, dst_ptr, slot_bytes, flags_ptr=None, stream_ptr=None):
+    """tri_dbp_pack: B8G8R8A8 -> the delta bit-plane stream (slots of slot_bytes), stream-ordered; flags: device
+    uint32[2] (bit 1 alpha mismatch, bit 2 slot overflow; the largest slot's bytes)."""
+    load_library()
+    _check(_lib.tri_dbp_pack(C.c_void_p(src_ptr), pixels, alpha, C.c_void_p(dst_ptr), slot_bytes,
+                             C.c_void_p(flags_ptr) if flags_ptr else None, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
+def dbp_unpack(src_ptr, pixels, alpha, slot_bytes, dst_ptr, stream_ptr=None):
+    """tri_dbp_unpack: the delta bit-plane stream -> B8G8R8A8 with the given alpha, stream-ordered."""
+    load_library()
+    _check(_lib.tri_dbp_unpack(C.c_void_p(src_ptr), pixels, alpha, slot_bytes, C.c_void_p(dst_ptr),
+                               C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
+def dbp_unpack_bands(src_ptrs, dst_ptrs, pixels, alpha, slot_bytes, stream_ptr=None):
+    """tri_dbp_unpack_bands: several delta bit-plane streams (one slot size) -> their B8G8R8A8 bands, one launch."""
+    load_library()
+    k = len(src_ptrs)
+    srcs = (C.c_void_p * max(k, 1))(*src_ptrs)
+    dsts = (C.c_void_p * max(k, 1))(*dst_ptrs)
+    npx = (C.c_uint64 * max(k, 1))(*pixels)
+    _check(_lib.tri_dbp_unpack_bands(srcs, dsts, npx, k, alpha, slot_bytes, C.c_void_p(stream_ptr) if stream_ptr else None))
+
+
+def dbp_bytes(pixels, slot_bytes):
+    load_library()
+    return int(_lib.tri_dbp_bytes(pixels, slot_bytes))
+
+
 def copy_device_to_host(ptr, nbytes, device=0):
     """hipMemcpy of `nbytes` at a device pointer (a tri_image handle) into a numpy byte array."""
     hip = C.CDLL("libamdhip64.so")
@@ -425,3 +455,9 @@ class TriGroup:
         bpp, inbound = C.c_uint32(), C.c_uint64()
         _check(_lib.tri_group_transfer_info(self._g, C.byref(bpp), C.byref(inbound)))
         return bpp.value, inbound.value
+
+    def transfer_format(self):
+        """tri_group_transfer_format: (TRI_GROUP_FMT_*, dbp slot bytes or 0) of the last frame."""
+        fmt, slot = C.c_uint32(), C.c_uint32()
+        _check(_lib.tri_group_transfer_format(self._g, C.byref(fmt), C.byref(slot)))
+        return fmt.value, slot.value

@@ -84,53 +84,204 @@ class _Works:
             w.wait()
 
 
-class BandCodec:
-    """Lossless 3-byte/pixel band transfer: a band whose alpha bytes all equal `alpha`
-    (tri_frame_alpha proves it from the context's state) travels as its B, G, R bytes and is restored on
-    arrival. On the GPU the HIP kernels tri_pack_bgr24 / tri_unpack_bgr24 run on torch's current stream; on
-    the CPU (gloo tests) the same byte shuffle runs in torch. An alpha byte that differs sets `flag` (the
-    sender's check that the transfer stayed lossless); check() raises on it."""
+DBP_SLOT_PIXELS, DBP_HEADER, DBP_MAX_SLOT = 4096, 160, 12448  # include/tri_raster.h TRI_DBP_*
+_BITLEN = None
 
-    def __init__(self, alpha, device):
+
+def _dbp_encode_np(px, slot):
+    """The delta bit-plane format (band_codec.hip) in numpy, vectorised: the CPU (gloo) side of BandCodec. px: uint32[n]
+    B8G8R8A8 words -> (uint8[nslots * slot] stream, largest slot's bytes)."""
+    import numpy as np
+
+    global _BITLEN
+    if _BITLEN is None:
+        _BITLEN = np.array([int(i).bit_length() for i in range(256)], np.uint32)
+    n = px.size
+    nslots = (n + DBP_SLOT_PIXELS - 1) // DBP_SLOT_PIXELS
+    p = np.empty(nslots * DBP_SLOT_PIXELS, np.int64)
+    p[:n] = px
+    p[n:] = px[-1] if n else 0
+    seg = p.reshape(nslots * 4, 1024)
+    first = (seg[:, 0] & 0x00FFFFFF).astype(np.uint32)
+    first[np.arange(nslots * 4) * 1024 >= n] = 0  # a segment past the band: empty
+    prev = np.concatenate([seg[:, :1], seg[:, :-1]], axis=1)
+    z = np.empty((nslots * 4, 1024, 3), np.uint32)
+    for c in range(3):
+        d = ((seg >> (8 * c)) - (prev >> (8 * c))) & 0xFF
+        d = np.where(d >= 128, d - 256, d)
+        z[..., c] = np.where(d >= 0, 2 * d, -2 * d - 1)
+    z = z.reshape(nslots * 4, 16, 64, 3)
+    widths = _BITLEN[z.max(axis=2)]  # [segments, 16, 3]
+    lanes = np.arange(64, dtype=np.uint64)
+    planes = np.stack([(((z >> j) & 1).astype(np.uint64) << lanes[None, None, :, None]).sum(axis=2, dtype=np.uint64)
+                       for j in range(8)], axis=-1)  # [segments, 16, 3, 8]
+    used = np.arange(8)[None, None, None, :] < widths[..., None]
+    packed = (widths[..., 0] | (widths[..., 1] << 4) | (widths[..., 2] << 8)).astype(np.uint16)  # [segments, 16]
+    out = np.zeros(nslots * slot, np.uint8)
+    maxb = 0
+    for sl in range(nslots):
+        segs = slice(4 * sl, 4 * sl + 4)
+        pay = planes[segs][used[segs]]
+        hdr = np.zeros(DBP_HEADER // 4, np.uint32)
+        hdr[0] = 8 * pay.size
+        for w in range(4):
+            hdr[4 + 9 * w] = first[4 * sl + w]
+            hdr[4 + 9 * w + 1: 4 + 9 * w + 9] = packed[4 * sl + w].view(np.uint32)
+        nb = DBP_HEADER + 8 * pay.size
+        maxb = max(maxb, nb)
+        o = out[sl * slot:(sl + 1) * slot]
+        if nb > slot:
+            o[:4] = hdr[:1].view(np.uint8)
+            continue
+        o[:DBP_HEADER] = hdr.view(np.uint8)
+        o[DBP_HEADER:nb] = pay.view(np.uint8)
+    return out, maxb
+
+
+def _dbp_decode_np(stream, n, alpha, slot):
+    """The inverse of _dbp_encode_np: uint32[n] with alpha restored (an overflowed slot's pixels stay 0)."""
+    import numpy as np
+
+    nslots = (n + DBP_SLOT_PIXELS - 1) // DBP_SLOT_PIXELS
+    out = np.zeros(nslots * DBP_SLOT_PIXELS, np.uint32)
+    lanes = np.arange(64, dtype=np.uint64)
+    for sl in range(nslots):
+        o = stream[sl * slot:(sl + 1) * slot]
+        hdr = o[:DBP_HEADER].view(np.uint32)
+        if DBP_HEADER + int(hdr[0]) > slot:
+            continue
+        pay = o[DBP_HEADER:DBP_HEADER + int(hdr[0])].view(np.uint64)
+        k = 0
+        for w in range(4):
+            widths = hdr[4 + 9 * w + 1: 4 + 9 * w + 9].view(np.uint16).astype(np.int64)
+            carry = int(hdr[4 + 9 * w])
+            base = (4 * sl + w) * 1024
+            for b in range(16):
+                val = np.full(64, alpha << 24, np.int64)
+                for c in range(3):
+                    wc = (int(widths[b]) >> (4 * c)) & 15
+                    zz = np.zeros(64, np.int64)
+                    for j in range(wc):
+                        zz |= ((pay[k] >> lanes) & np.uint64(1)).astype(np.int64) << j
+                        k += 1
+                    d = np.where(zz & 1, -((zz + 1) >> 1), zz >> 1)
+                    val |= ((np.cumsum(d) + ((carry >> (8 * c)) & 0xFF)) & 0xFF) << (8 * c)
+                out[base + 64 * b: base + 64 * b + 64] = val.astype(np.uint32)
+                carry = int(val[63]) & 0x00FFFFFF
+    return out[:n]
+
+
+class BandCodec:
+    """Lossless band transfer formats for a band whose alpha bytes all equal `alpha` (tri_frame_alpha
+    proves it from the context's state):
+      "bgr24": its B, G, R bytes (3 B per pixel; tri_pack_bgr24 / tri_unpack_bgr24);
+      "dbp":   the delta bit-plane format (tri_dbp_pack / tri_dbp_unpack: per 64-pixel block and channel the bit planes
+               of the zigzag-mapped pixel differences, in fixed slots of `slot_bytes` per 4096 pixels — C3's bands need
+               about 1.6 B per pixel). Every rank uses the same slot size, agreed before the timed region
+               (agree_slot), so each band's message size is known to both sides.
+    On the GPU the HIP kernels run on torch's current stream; on the CPU (gloo tests) the same formats run in torch /
+    numpy. The sender's flags: an alpha byte that differs (1), a slot that overflowed (2, "dbp" only); check() raises on
+    either (the transfer was lossy)."""
+
+    def __init__(self, alpha, device, mode="bgr24", slot_bytes=DBP_MAX_SLOT):
         import torch
 
         self.alpha = int(alpha)
-        self.flag = torch.zeros(1, dtype=torch.int32, device=device)
+        self.mode = mode
+        self.slot = int(slot_bytes)
+        self.flag = torch.zeros(2, dtype=torch.int32, device=device)
         self.gpu = device.type == "cuda"
 
+    def bytes_for(self, n):
+        """The message size of an n-pixel band."""
+        if self.mode == "dbp":
+            return (n + DBP_SLOT_PIXELS - 1) // DBP_SLOT_PIXELS * self.slot
+        return 3 * n
+
+    def max_slot_bytes(self, band):
+        """dbp: the largest slot this band needs (packed once into a scratch stream at the format's maximum slot)."""
+        import numpy as np
+        import torch
+
+        n = band.numel()
+        if not self.gpu:
+            return _dbp_encode_np(band.numpy().view(np.uint32), DBP_MAX_SLOT)[1]
+        from trident_raster import raster
+
+        scratch = torch.empty((n + DBP_SLOT_PIXELS - 1) // DBP_SLOT_PIXELS * DBP_MAX_SLOT, dtype=torch.uint8,
+                              device=band.device)
+        fl = torch.zeros(2, dtype=torch.int32, device=band.device)
+        raster.dbp_pack(band.data_ptr(), n, self.alpha, scratch.data_ptr(), DBP_MAX_SLOT, fl.data_ptr(),
+                        torch.cuda.current_stream().cuda_stream)
+        return int(fl[1].item())
+
     def pack(self, band, out):
-        """band: int32[n] (B8G8R8A8) -> out: uint8[3n]."""
+        """band: int32[n] (B8G8R8A8) -> out: uint8[bytes_for(n)]."""
+        import numpy as np
         import torch
 
         n = band.numel()
         if self.gpu:
             from trident_raster import raster
 
-            raster.pack_bgr24(band.data_ptr(), out.data_ptr(), n, self.alpha, self.flag.data_ptr(),
-                              torch.cuda.current_stream().cuda_stream)
+            cs = torch.cuda.current_stream().cuda_stream
+            if self.mode == "dbp":
+                raster.dbp_pack(band.data_ptr(), n, self.alpha, out.data_ptr(), self.slot, self.flag.data_ptr(), cs)
+            else:
+                raster.pack_bgr24(band.data_ptr(), out.data_ptr(), n, self.alpha, self.flag.data_ptr(), cs)
             return
         b = band.view(torch.uint8).view(n, 4)
-        out.view(n, 3).copy_(b[:, :3])
         if bool((b[:, 3] != self.alpha).any()):
-            self.flag.fill_(1)
+            self.flag[0] |= 1
+        if self.mode == "dbp":
+            st, maxb = _dbp_encode_np(band.numpy().view(np.uint32), self.slot)
+            out.copy_(torch.from_numpy(st))
+            if maxb > self.slot:
+                self.flag[0] |= 2
+            return
+        out.view(n, 3).copy_(b[:, :3])
 
     def unpack(self, src, band):
-        """src: uint8[3n] -> band: int32[n] with alpha restored."""
+        """src: uint8[bytes_for(n)] -> band: int32[n] with alpha restored."""
+        import numpy as np
         import torch
 
         n = band.numel()
         if self.gpu:
             from trident_raster import raster
 
-            raster.unpack_bgr24(src.data_ptr(), band.data_ptr(), n, self.alpha, torch.cuda.current_stream().cuda_stream)
+            cs = torch.cuda.current_stream().cuda_stream
+            if self.mode == "dbp":
+                raster.dbp_unpack(src.data_ptr(), n, self.alpha, self.slot, band.data_ptr(), cs)
+            else:
+                raster.unpack_bgr24(src.data_ptr(), band.data_ptr(), n, self.alpha, cs)
+            return
+        if self.mode == "dbp":
+            band.copy_(torch.from_numpy(_dbp_decode_np(src.numpy(), n, self.alpha, self.slot).view(np.int32)))
             return
         b = band.view(torch.uint8).view(n, 4)
         b[:, :3].copy_(src.view(n, 3))
         b[:, 3].fill_(self.alpha)
 
+    def unpack_many(self, srcs, bands):
+        """unpack of several bands; "dbp" on the GPU decodes them all in one launch (tri_dbp_unpack_bands)."""
+        if self.gpu and self.mode == "dbp" and len(srcs) > 1:
+            import torch
+            from trident_raster import raster
+
+            raster.dbp_unpack_bands([s.data_ptr() for s in srcs], [b.data_ptr() for b in bands],
+                                    [b.numel() for b in bands], self.alpha, self.slot,
+                                    torch.cuda.current_stream().cuda_stream)
+            return
+        for src, band in zip(srcs, bands):
+            self.unpack(src, band)
+
     def check(self):
-        if int(self.flag.item()):
-            raise RuntimeError("a band's alpha was not the promised uniform value: the 3-byte transfer was lossy")
+        f = int(self.flag[0].item())
+        if f & 1:
+            raise RuntimeError("a band's alpha was not the promised uniform value: the band transfer was lossy")
+        if f & 2:
+            raise RuntimeError(f"a band needed more than the agreed {self.slot}-B slots: the dbp transfer was lossy")
 
 
 class _Unpacked:
@@ -190,9 +341,8 @@ def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=
             asm = asm_stream or torch.cuda.current_stream()
             with torch.cuda.stream(asm):
                 work.wait()  # the assembly stream waits for the receives
-                for r in range(world):
-                    if r != dst:
-                        codec.unpack(stage[r], frame.narrow(0, *spans[r]))
+                remote = [r for r in range(world) if r != dst]
+                codec.unpack_many([stage[r] for r in remote], [frame.narrow(0, *spans[r]) for r in remote])
                 ev = torch.cuda.Event()
                 ev.record(asm)
             work = _Unpacked(ev)
@@ -206,6 +356,15 @@ def gather_bands(frame, band, world, async_op=False, mode="gather", rank=0, dst=
         return work
     work.wait()
     return frame if rank == dst else None
+
+
+def agree_dbp_slot(codec, band, dist_on, margin=1.02):
+    """The "dbp" slot size every rank uses: the largest slot any rank's band needs (a max over ranks), with a margin
+    for frame-to-frame variation, rounded up to 16 B and capped at the format's maximum (which never overflows).
+    Every rank calls it at the same point (the max is a collective)."""
+    need = max_over_ranks(float(codec.max_slot_bytes(band)), band.device, dist_on)
+    codec.slot = int(min(DBP_MAX_SLOT, (int(need * margin) + 15) // 16 * 16))
+    return codec.slot
 
 
 def max_over_ranks(value, device, dist_on):
@@ -246,13 +405,14 @@ class GatherRing:
         if self.codec is not None:  # 3-byte staging per slot: the sender's packed band, the receiver's per rank
             sp = spans or [(r * band_elems, band_elems) for r in range(world)]
             if rank == dst:
-                self.stage = [{r: make_bytes(3 * sp[r][1]) for r in range(world) if r != dst} for _ in range(self.nbuf)]
+                self.stage = [{r: make_bytes(self.codec.bytes_for(sp[r][1])) for r in range(world) if r != dst}
+                              for _ in range(self.nbuf)]
                 if self.frames[0].is_cuda:
                     import torch
 
                     self.asm_stream = torch.cuda.Stream(self.frames[0].device)
             else:
-                self.stage = [make_bytes(3 * sp[rank][1]) for _ in range(self.nbuf)]
+                self.stage = [make_bytes(self.codec.bytes_for(sp[rank][1])) for _ in range(self.nbuf)]
 
     @property
     def inbound_bytes(self):
@@ -260,8 +420,8 @@ class GatherRing:
         if self.world == 1 or self.rank != self.dst or self.mode != "gather":
             return 0
         sp = self.spans or [(r * self.bands[0].numel(), self.bands[0].numel()) for r in range(self.world)]
-        per = 3 if self.codec is not None else 4
-        return sum(per * sp[r][1] for r in range(self.world) if r != self.dst)
+        nbytes = (lambda n: 4 * n) if self.codec is None else self.codec.bytes_for
+        return sum(nbytes(sp[r][1]) for r in range(self.world) if r != self.dst)
 
     def acquire(self):
         """The band buffer frame k renders into (after frame k-2's gather released it)."""
@@ -338,25 +498,44 @@ class BandRenderer:
             self.rs.append(r)
             self.streams.append(st)
         self.r = self.rs[0]
-        # 3-byte band transfer when every pixel's alpha is provably one value (every rank proves the same
-        # from the same scene, so sender and receiver agree without a message)
+        # a compact band format when every pixel's alpha is provably one value (every rank proves the same from the
+        # same scene, so sender and receiver agree without a message): the delta bit-plane format by default ("auto"),
+        # or the 3-byte one
         self.alpha = self.r.frame_alpha()
-        self.codec = BandCodec(self.alpha, self.dev) if (pack == "auto" and self.alpha >= 0 and world > 1 and
-                                                         assembly == "gather") else None
+        mode = {"auto": "dbp", "dbp": "dbp", "bgr24": "bgr24"}.get(pack)
+        self.codec = BandCodec(self.alpha, self.dev, mode) if (mode and self.alpha >= 0 and world > 1 and
+                                                                 assembly == "gather") else None
+        self._lib = raster.load_library()
+        self._raster = raster
+        self.pack = pack
+        if self.codec is not None and self.codec.mode == "dbp":  # the slot size every rank's band fits (collective)
+            agree_dbp_slot(self.codec, self.probe_band(), world > 1)
         self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
                                mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1), spans=spans,
                                codec=self.codec, make_bytes=lambda n: torch.empty(n, dtype=torch.uint8, device=self.dev))
         # the per-frame calls with their ctypes arguments built once (a frame at N = 8 is ~60 us of GPU
         # work, so Python-side marshalling per call would show up in the frame rate)
-        self._lib = raster.load_library()
         self._ctxs = [r._ctx for r in self.rs]
         self._ubo = C.byref(scene.ubo)
         self._clear = C.byref((C.c_float * 4)(*scene.clear))
         self._draws, self._ndraws = abi.draws_array(scene.draws)
         self._band_ptrs = {b.data_ptr(): C.c_void_p(b.data_ptr()) for b in self.ring.bands}
         self._depth_ptrs = [C.c_void_p(d.data_ptr()) for d in self.depth]
-        self._raster = raster
         self.frames = 0
+        self.sim_step = None  # --sim-codec: the band codec's per-frame work, on the frame's stream
+
+    def probe_band(self):
+        """One frame of this rank's band on context 0, into a scratch buffer (synchronised; no collective)."""
+        import ctypes as C
+
+        import torch
+
+        band = torch.empty(self.rows * self.scene.width, dtype=torch.int32, device=self.dev)
+        r = self.rs[0]
+        self._raster._check(self._lib.tri_bind_output(r._ctx, C.c_void_p(band.data_ptr()), C.c_void_p(self.depth[0].data_ptr())))
+        r.render_frame()
+        r.synchronize()
+        return band
 
     def _frame(self, i):
         lib, ctx = self._lib, self._ctxs[i]
@@ -367,13 +546,15 @@ class BandRenderer:
               lib.tri_render(ctx))
         if rc:
             self._raster._check(rc)
+        if self.sim_step is not None:
+            self.sim_step(band)
         self.ring.publish()
 
     def step(self, first_only=False):
         """One frame, on the next context in turn (first_only: always context 0, no overlap)."""
         i = 0 if first_only else self.frames % self.inflight
         self.frames += 1
-        if self.world == 1 and self.inflight == 1:  # no collective, one stream: no torch stream context needed
+        if self.world == 1 and self.inflight == 1 and self.sim_step is None:  # no collective, one stream: no torch stream context needed
             self._frame(i)
             return
         import torch
@@ -443,15 +624,50 @@ class BandRenderer:
         self._sync()
         return (time.perf_counter() - t0) * 1e3 / frames
 
+    def attach_sim_codec(self, mode):
+        """--sim-codec (one GPU, no collective): every frame also runs the band codec's work of its rank at N > 1, on
+        the frame's stream — a sender packs its band; the display rank (sim rank 0) decodes every other band of the
+        split (its own band repeated to each band's size and packed once) — so the frame rate includes the codec's
+        cost and its overlap with the other frames in flight. The link transfer itself is not simulated."""
+        import torch
+
+        band = self.ring.bands[0]
+        codec = BandCodec(max(self.alpha, 0), self.dev, mode)
+        if mode == "dbp":
+            agree_dbp_slot(codec, self.probe_band(), False)
+        if self.rank != 0:
+            stage = torch.empty(codec.bytes_for(band.numel()), dtype=torch.uint8, device=self.dev)
+            self.sim_step = lambda b: codec.pack(b, stage)
+        else:
+            W = self.scene.width
+            remote = [(y1 - y0) * W for y0, y1 in self.bands[1:]]
+            own = self.probe_band()
+            srcs, views, frame = [], [], torch.empty(sum(remote), dtype=torch.int32, device=self.dev)
+            off = 0
+            for n in remote:
+                src = torch.empty(codec.bytes_for(n), dtype=torch.uint8, device=self.dev)
+                codec.pack(own.repeat((n + own.numel() - 1) // own.numel())[:n].contiguous(), src)
+                srcs.append(src)
+                views.append(frame.narrow(0, off, n))
+                off += n
+            self._sync()
+            self.sim_step = lambda b: codec.unpack_many(srcs, views)
+        self.sim_codec = codec
+
     def codec_ms(self, bands_rows, frames=200):
-        """Diagnostics (--sim-world): the 3-byte codec's cost on one GPU: packing this rank's band, and the
-        display rank's unpack of every other band of the split (ms per frame each)."""
+        """Diagnostics (--sim-world): the band codec's cost on one GPU: packing this rank's band, and the display
+        rank's unpack of every other band of the split (ms per frame each). The remote bands' streams are this
+        band's pixels repeated to each band's size and packed (real image content, the agreed slot size)."""
         import torch
 
         W = self.scene.width
-        codec = self.codec or BandCodec(max(self.alpha, 0), self.dev)
         band = self.ring.bands[0]
-        st = torch.empty(3 * band.numel(), dtype=torch.uint8, device=self.dev)
+        codec = self.codec
+        if codec is None:  # one GPU: the format --pack names, its slot agreed on this band alone
+            codec = BandCodec(max(self.alpha, 0), self.dev, "bgr24" if self.pack == "bgr24" else "dbp")
+            if codec.mode == "dbp":
+                agree_dbp_slot(codec, band, False)
+        st = torch.empty(codec.bytes_for(band.numel()), dtype=torch.uint8, device=self.dev)
         self._sync()
         t0 = time.perf_counter()
         for _ in range(frames):
@@ -460,18 +676,25 @@ class BandRenderer:
         pack = (time.perf_counter() - t0) * 1e3 / frames
         remote = [r * W for r in bands_rows[1:]]
         frame = torch.empty(sum(remote) + 16, dtype=torch.int32, device=self.dev)
-        srcs = [torch.empty(3 * n, dtype=torch.uint8, device=self.dev) for n in remote]
+        srcs = []
+        for n in remote:
+            src = torch.empty(codec.bytes_for(n), dtype=torch.uint8, device=self.dev)
+            codec.pack(band.repeat((n + band.numel() - 1) // band.numel())[:n].contiguous(), src)
+            srcs.append(src)
+        views, off = [], 0
+        for n in remote:
+            views.append(frame.narrow(0, off, n))
+            off += n
         self._sync()
         t0 = time.perf_counter()
         for _ in range(frames):
-            off = 0
-            for n, src in zip(remote, srcs):
-                codec.unpack(src, frame.narrow(0, off, n))
-                off += n
+            codec.unpack_many(srcs, views)
         self._sync()
         unpack = (time.perf_counter() - t0) * 1e3 / frames
-        return {"pack_ms_per_band": pack, "unpack_ms_display_all_remote_bands": unpack,
-                "remote_bands": len(remote), "band_pixels": band.numel()}
+        return {"format": codec.mode, "slot_bytes": codec.slot if codec.mode == "dbp" else None,
+                "pack_ms_per_band": pack, "unpack_ms_display_all_remote_bands": unpack,
+                "remote_bands": len(remote), "band_pixels": band.numel(),
+                "bytes_per_pixel": codec.bytes_for(band.numel()) / band.numel()}
 
     def latency_ms(self, frames=20):
         """Per-frame latency without overlap: render + gather + wait, host-synchronised each frame."""
@@ -792,6 +1015,9 @@ def main():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostics (1 GPU, no collective): render only band --sim-rank of an N-way split")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--sim-codec", choices=("none", "bgr24", "dbp"), default="none",
+                    help="with --sim-world: every frame also packs this rank's band (sim rank > 0) or decodes the other "
+                         "ranks' bands (sim rank 0, the display), on the frame's stream")
     ap.add_argument("--sim-display-rows", type=int, default=None,
                     help="diagnostics: the simulated split's display band (rank 0) size, the others sharing the rest")
     ap.add_argument("--inflight", type=int, default=None,
@@ -799,9 +1025,9 @@ def main():
                          "config (DEFAULT_INFLIGHT)")
     ap.add_argument("--assembly", choices=("gather", "allgather"), default="gather",
                     help="N > 1: bands gathered onto the display rank 0 (default) or all-gathered onto every rank")
-    ap.add_argument("--pack", choices=("auto", "off"), default="auto",
-                    help="N > 1 gather: bands travel as 3 bytes per pixel when tri_frame_alpha proves every alpha "
-                         "byte equal (auto), or always as 4 (off)")
+    ap.add_argument("--pack", choices=("auto", "dbp", "bgr24", "off"), default="auto",
+                    help="N > 1 gather: when tri_frame_alpha proves every alpha byte equal, bands travel in the delta "
+                         "bit-plane format (auto, dbp) or as 3 bytes per pixel (bgr24); off: always 4 bytes")
     ap.add_argument("--split", default="auto",
                     help="N > 1 gather: 'auto' (time candidate display-band sizes on the hardware, keep the fastest), "
                          "'equal', or the display rank's row count")
@@ -849,6 +1075,8 @@ def main():
     if args.sim_world and world == 1:
         br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=inflight_for(scene),
                           display_rows=args.sim_display_rows, pack=args.pack)
+        if args.sim_codec != "none":
+            br.attach_sim_codec(args.sim_codec)
     else:
         (display_rows, inflight), split_log = choose_split(scene)
         br = make_renderer(scene, display_rows, inflight)
@@ -866,13 +1094,17 @@ def main():
         asm_ms = max_over_ranks(br.assembly_only_ms(), br.dev, dist_on)
         inbound = br.ring.inbound_bytes if rank == 0 else 0
         assembly = {"render_ms": render_ms, "assembly_ms": asm_ms, "inbound_bytes_per_frame": inbound,
-                    "band_bytes_per_pixel": 3 if br.codec is not None else 4, "frame_alpha": br.alpha,
+                    "band_format": br.codec.mode if br.codec is not None else "bgra32",
+                    "dbp_slot_bytes": br.codec.slot if br.codec is not None and br.codec.mode == "dbp" else None,
+                    "band_bytes_per_pixel": (br.codec.bytes_for(br.rows * W) / (br.rows * W)
+                                             if br.codec is not None else 4), "frame_alpha": br.alpha,
                     "render_bound_fps": 1e3 / render_ms if render_ms > 0 else None,
                     "assembly_bound_fps": 1e3 / asm_ms if asm_ms > 0 else None,
                     "bound": "assembly" if asm_ms > render_ms else "render",
                     "note": "max over ranks; render and assembly each timed alone, back to back, outside the timed region"}
     elif args.sim_world > 1:  # one band of an N-way split on one GPU: the codec's cost per band
         assembly = {"sim_world": args.sim_world, "sim_rank": args.sim_rank, "frame_alpha": br.alpha,
+                    "sim_codec": args.sim_codec,
                     "codec": br.codec_ms([y1 - y0 for y0, y1 in br.bands])}
 
     # roofline of the dominant kernel (k_raster = tile_raster_shade): its algorithmic bytes per

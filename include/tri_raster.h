@@ -323,6 +323,27 @@ int tri_frame_alpha(tri_ctx* ctx, int32_t* alpha);
  * `alpha` into every pixel. */
 int tri_pack_bgr24(const void* bgra8, void* bgr8, uint64_t pixels, uint32_t alpha, uint32_t* flag, void* hip_stream);
 int tri_unpack_bgr24(const void* bgr8, void* bgra8, uint64_t pixels, uint32_t alpha, void* hip_stream);
+/* The delta bit-plane band format (lossless): the band as a 1-D pixel stream in slots of
+ * TRI_DBP_SLOT_PIXELS pixels, each slot_bytes long (a multiple of 16, at least TRI_DBP_MIN_SLOT; TRI_DBP_MAX_SLOT
+ * never overflows). Per 64-pixel block and channel, the bit width of the zigzag-mapped pixel-to-pixel differences and
+ * that many 64-bit bit planes; alpha is dropped and restored as `alpha` (proven uniform, tri_frame_alpha).
+ * tri_dbp_pack: flags[0] |= 1 when a pixel's alpha differs, |= 2 when a slot needed more than slot_bytes (that slot is
+ * not decodable: grow slot_bytes and send again); flags[1] = max(flags[1], the largest slot's bytes) — the size the
+ * next frames need. Both stream-ordered on hip_stream; stream buffers 16-B aligned, pixel buffers 4-B aligned.
+ * tri_dbp_bytes: the stream's size for `pixels` pixels. */
+#define TRI_DBP_SLOT_PIXELS 4096u
+#define TRI_DBP_MIN_SLOT 176u
+#define TRI_DBP_MAX_SLOT 12448u
+int tri_dbp_pack(const void* bgra8, uint64_t pixels, uint32_t alpha, void* stream_out, uint32_t slot_bytes,
+                 uint32_t* flags, void* hip_stream);
+int tri_dbp_unpack(const void* stream_in, uint64_t pixels, uint32_t alpha, uint32_t slot_bytes, void* bgra8,
+                   void* hip_stream);
+uint64_t tri_dbp_bytes(uint64_t pixels, uint32_t slot_bytes);
+/* tri_dbp_unpack of `count` (<= TRI_DBP_MAX_BANDS) streams with one slot size in one launch (the display device's
+ * remote bands: a workgroup per slot of any of them); same alignment rules, bands of 0 pixels are skipped. */
+#define TRI_DBP_MAX_BANDS 16u
+int tri_dbp_unpack_bands(const void* const* streams_in, void* const* bgra8, const uint64_t* pixels, uint32_t count,
+                         uint32_t alpha, uint32_t slot_bytes, void* hip_stream);
 
 /* ---- measurement -------------------------------------------------------------------------- */
 /* enable = N > 0: HIP events around every stage of every N-th frame (1 = all frames; sampling keeps
@@ -354,11 +375,22 @@ typedef struct tri_group_config {
     uint32_t group_flags;   /* TRI_GROUP_* (0 = defaults)                                           */
 } tri_group_config;
 /* Bands travel to the display device as 4-byte pixels even when tri_frame_alpha proves a uniform alpha
- * (default: 3 bytes per pixel then, restored on arrival — lossless, 25 % fewer bytes per link). */
+ * (default: the delta bit-plane format then, TRI_GROUP_FMT_DBP below — lossless, restored on arrival). */
 #define TRI_GROUP_NO_PACK 0x1u
 /* Bands on the display device render into band buffers and travel like remote bands (a device-local copy
  * instead of RCCL): the remote path's buffers, fences and codec on a single GPU (tests, diagnostics). */
 #define TRI_GROUP_STAGE_BANDS 0x2u
+/* With a proven uniform alpha, bands travel as their B, G, R bytes (3 per pixel) instead of the delta bit-plane
+ * format. */
+#define TRI_GROUP_PACK_BGR24 0x4u
+/* Band transfer formats (tri_group_transfer_format). */
+#define TRI_GROUP_FMT_BGRA32 0u /* 4 bytes per pixel                                                  */
+#define TRI_GROUP_FMT_BGR24 1u  /* 3 bytes per pixel, the proven alpha restored on arrival           */
+/* the delta bit-plane format (tri_dbp_pack): fixed slots of slot_bytes per 4096 pixels, sized at every
+ * tri_group_synchronize from the largest slot the frames since the previous one needed (+ 1/16); the first frame
+ * uses TRI_DBP_MAX_SLOT, which always fits. A frame with a slot that outgrew its size is reported by
+ * tri_group_synchronize as TRI_E_OVERFLOW (its slot is then refitted: render the frame again). */
+#define TRI_GROUP_FMT_DBP 2u
 
 int tri_group_create(const tri_group_config* config, tri_group** out_group);
 int tri_group_destroy(tri_group* group);
@@ -407,9 +439,12 @@ int tri_group_bind_geometry(tri_group* group, uint32_t count, tri_geometry* cons
  * own present target: tri_group_read_present then fails with TRI_E_STATE until a blit with dst = NULL. */
 int tri_group_blit_linear(tri_group* group, void* dst, uint32_t width, uint32_t height);
 int tri_group_read_present(tri_group* group, uint8_t* bgra8);
-/* The most recent frame's band transfer: bytes per pixel on the links (3 when tri_frame_alpha proved a
- * uniform alpha and packing is on, else 4) and the bytes the display device received over RCCL. */
+/* The most recent frame's band transfer: bytes per pixel on the links (4, 3, or for the delta bit-plane format
+ * its stream bytes per pixel rounded up) and the bytes the display device received over RCCL (exact). */
 int tri_group_transfer_info(tri_group* group, uint32_t* bytes_per_pixel, uint64_t* inbound_bytes);
+/* The most recent frame's transfer format (TRI_GROUP_FMT_*) and, for TRI_GROUP_FMT_DBP, its slot size in bytes
+ * per 4096 pixels (0 otherwise); before any frame, the format and slot the next frame would use with packing. */
+int tri_group_transfer_format(tri_group* group, uint32_t* format, uint32_t* slot_bytes);
 
 #ifdef __cplusplus
 } /* extern "C" */

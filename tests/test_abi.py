@@ -14,7 +14,7 @@ HEADER = os.path.join(ROOT, "include", "tri_raster.h")
 
 def header_functions():
     text = open(HEADER).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(tri_\w+)\(", text, flags=re.M)))
+    return sorted(set(re.findall(r"^(?:int|const char\*|uint64_t)\s+(tri_\w+)\(", text, flags=re.M)))
 
 
 def test_header_declares_exactly_the_python_mirror():

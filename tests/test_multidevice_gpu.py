@@ -299,12 +299,14 @@ def test_frame_alpha_proof(oracle):
         assert r.frame_alpha() == -1
 
 
-@pytest.mark.parametrize("scene_name,group_flags,bpp", [("grid", 0, 3), ("grid", 1, 4), ("textured", 0, 4)])
-def test_group_staged_bands_packed_transfer(oracle, scene_name, group_flags, bpp):
-    """VERDICT r3 #3 on one GPU: TRI_GROUP_STAGE_BANDS sends every non-display band through the remote path
-    (band buffer, 3-byte pack when the alpha is proven uniform, transfer, unpack into the frame). Four frames
-    with different cameras; each assembled frame equals the single-context frame bit for bit, packing on and
-    off (TRI_GROUP_NO_PACK = 1), and a frame with non-uniform alpha travels as 4 bytes."""
+@pytest.mark.parametrize("scene_name,group_flags,fmt", [("grid", 0, 2), ("grid", 4, 1), ("grid", 1, 0), ("textured", 0, 0)])
+def test_group_staged_bands_packed_transfer(oracle, scene_name, group_flags, fmt):
+    """VERDICT r3 #3 / r4 #5 on one GPU: TRI_GROUP_STAGE_BANDS sends every non-display band through the remote path
+    (band buffer, packed when the alpha is proven uniform — the delta bit-plane format by default, 3-byte pixels
+    with TRI_GROUP_PACK_BGR24 (4) — transfer, unpack into the frame). Four frames with different cameras; each
+    assembled frame equals the single-context frame bit for bit, with every format and with packing off
+    (TRI_GROUP_NO_PACK = 1), and a frame with non-uniform alpha travels as 4 bytes. dbp: the first frame uses the
+    largest slot, later ones the slot refitted at each synchronize (render_frame re-renders after an overflow)."""
     from trident_raster import abi, raster, scenes
 
     cams = [(0.0, 0.0, 3.0), (0.3, 0.2, 3.2), (-0.4, -0.1, 2.8), (0.1, 0.3, 3.5)]
@@ -315,29 +317,65 @@ def test_group_staged_bands_packed_transfer(oracle, scene_name, group_flags, bpp
         s.ubo = scenes.pack_ubo(view, proj, cam, [{"type": "directional"}])
         frames.append(s)
     want = [_render_single(s, 0) for s in frames]
-    gf = abi.TRI_GROUP_STAGE_BANDS | (abi.TRI_GROUP_NO_PACK if group_flags else 0)
+    gf = abi.TRI_GROUP_STAGE_BANDS | group_flags
+    slots = []
     with raster.TriGroup(480, 270, [0] * 4, display=1, group_flags=gf) as g:
         scenes.load_scene(g, frames[0])
         for k, s in enumerate(frames):
             g.set_frame(s.ubo, s.clear)
             g.render_frame()
             col, dep = g.readback()
-            assert g.transfer_info() == (bpp, 0)
+            f, slot = g.transfer_format()
+            bpp, inbound = g.transfer_info()
+            assert f == fmt and inbound == 0
+            assert bpp == {0: 4, 1: 3}.get(fmt, bpp)
+            if fmt == 2:
+                slots.append(slot)
+                assert 1 <= bpp <= (4 if k == 0 else 3) and abi.TRI_DBP_MIN_SLOT <= slot <= abi.TRI_DBP_MAX_SLOT
             assert np.array_equal(dep, want[k][1]), f"frame {k} depth"
             assert np.array_equal(col, want[k][0]), f"frame {k}: {int((col != want[k][0]).any(-1).sum())} pixels differ"
             g.present()
+    if fmt == 2:
+        assert slots[0] == abi.TRI_DBP_MAX_SLOT and max(slots[1:]) < abi.TRI_DBP_MAX_SLOT  # refitted after frame 0
+
+
+def test_group_dbp_slot_overflow_rerenders(oracle):
+    """A dbp slot fitted to a clear-only frame (header-only slots) is outgrown by the next frame's geometry:
+    tri_group_synchronize reports TRI_E_OVERFLOW once and refits the slot, and the frame rendered again equals the
+    single-context frame bit for bit."""
+    from trident_raster import abi, raster, scenes
+
+    s = scenes.scene_c3_grid(480, 270, 40, skybox="solid")  # a solid sky: the geometry-free frame is uniform
+    want = _render_single(s, 0)
+    with raster.TriGroup(480, 270, [0] * 3, display=0, group_flags=abi.TRI_GROUP_STAGE_BANDS) as g:
+        scenes.load_scene(g, s)
+        g.set_draws([])
+        g.render_frame()  # largest slot; synchronize fits the slot to the clear colour's header-only slots
+        assert g.transfer_format() == (abi.TRI_GROUP_FMT_DBP, abi.TRI_DBP_MAX_SLOT)
+        g.set_draws(s.draws)
+        g.render()
+        with pytest.raises(raster.TriError) as e:
+            g.synchronize()
+        assert e.value.code == abi.TRI_E_OVERFLOW
+        assert g.transfer_format() == (abi.TRI_GROUP_FMT_DBP, abi.TRI_DBP_MIN_SLOT)  # the overflowed frame's slot
+        g.render_frame()
+        f, slot = g.transfer_format()
+        assert f == abi.TRI_GROUP_FMT_DBP and abi.TRI_DBP_MIN_SLOT < slot < abi.TRI_DBP_MAX_SLOT
+        col, dep = g.readback()
+        assert np.array_equal(col, want[0]) and np.array_equal(dep, want[1])
 
 
 @pytest.mark.skipif(_hip_device_count() < 2, reason="the RCCL branch of tri_group needs two HIP devices")
 @pytest.mark.parametrize("devices,display", [([0, 1, 0, 1], 0), ([1, 0, 1, 0, 1], 3)])
-@pytest.mark.parametrize("no_pack", [False, True])
-def test_group_distinct_devices_rccl_assembly(oracle, devices, display, no_pack):
+@pytest.mark.parametrize("gflags", [0, 4, 1])
+def test_group_distinct_devices_rccl_assembly(oracle, devices, display, gflags):
     """the cross-device branch of tri_group (ncclCommInitAll, grouped ncclSend/ncclRecv into the
-    rotating frame buffer, band buffers reused after asm_done), with the 3-byte band packing on (the default when
-    the frame's alpha is proven) and off (TRI_GROUP_NO_PACK). Four frames with different cameras; each assembled
-    frame equals the single-context render, the k - 1 buffer stays untouched while frame k renders, and
-    transfer_info reports the bytes per pixel and the display device's inbound bytes of the remote bands.
-    Skipped on a one-GPU box (runs on the driver's multi-GPU node)."""
+    rotating frame buffer, band buffers reused after asm_done), with the band packing in the delta bit-plane format
+    (the default when the frame's alpha is proven), as 3-byte pixels (TRI_GROUP_PACK_BGR24 = 4) and off
+    (TRI_GROUP_NO_PACK = 1). Four frames with different cameras; each assembled frame equals the single-context
+    render, the k - 1 buffer stays untouched while frame k renders, and transfer_info / transfer_format report the
+    format, the bytes per pixel and the display device's inbound bytes of the remote bands. Skipped on a one-GPU box
+    (runs on the driver's multi-GPU node)."""
     from trident_raster import abi, raster, scenes
 
     frames = _camera_frames(oracle, [(0.0, 1.0, 6.0), (0.6, 1.3, 6.5), (-0.7, 0.8, 5.5), (0.2, 1.6, 7.0)])
@@ -345,18 +383,24 @@ def test_group_distinct_devices_rccl_assembly(oracle, devices, display, no_pack)
     with raster.TriRaster(320, 240, device=0) as r:
         scenes.load_scene(r, frames[0])
         alpha = r.frame_alpha()
-    bpp = 4 if (no_pack or alpha < 0) else 3
+    fmt = 0 if (gflags == 1 or alpha < 0) else (1 if gflags == 4 else 2)
     n, H, W = len(devices), 240, 320
-    inbound = sum(((k + 1) * H // n - k * H // n) * W * bpp for k in range(n) if devices[k] != devices[display])
-    with raster.TriGroup(320, 240, devices, display=display,
-                         group_flags=abi.TRI_GROUP_NO_PACK if no_pack else 0) as g:
+    remote = [((k + 1) * H // n - k * H // n) * W for k in range(n) if devices[k] != devices[display]]
+    with raster.TriGroup(320, 240, devices, display=display, group_flags=gflags) as g:
         scenes.load_scene(g, frames[0])
         prev = None
         for k, s in enumerate(frames):
             g.set_frame(s.ubo, s.clear)
             g.render_frame()
             g.synchronize()
-            assert g.transfer_info() == (bpp, inbound)
+            f, slot = g.transfer_format()
+            assert f == fmt
+            if fmt == 2:
+                inbound = sum(raster.dbp_bytes(px, slot) for px in remote)
+                assert g.transfer_info()[1] == inbound
+            else:
+                bpp = 4 if fmt == 0 else 3
+                assert g.transfer_info() == (bpp, sum(px * bpp for px in remote))
             p, dev = g.frame_pointer()
             img = _copy_frame(p, dev, 320, 240)
             assert np.array_equal(img, want[k]), f"frame {k}: {int((img != want[k]).any(-1).sum())} pixels differ"

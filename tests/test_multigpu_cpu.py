@@ -292,8 +292,8 @@ class _FakeBand:
         self.d, self.rank, self.dev = d, rank, torch.device("cpu")
         rows = d if rank == 0 else (H - d) / (world - 1)
         self.cost = 2e-5 * rows * (1.0 if rank == 0 else 3.0)  # remote: transfer 3x slower per row
-        if inflight == 3:  # the model's third frame in flight hides a tenth of the work
-            self.cost *= 0.9
+        if inflight == 3:  # the model's third frame in flight hides a quarter of the work (well above a loaded
+            self.cost *= 0.75  # machine's timing noise: the test runs beside others under pytest -n)
         self.closed = False
 
     def warm(self):
@@ -351,9 +351,10 @@ def test_autotune_split_picks_the_balanced_display_band(tmp_path):
     assert (d, k) == (750, 3), (d, k, cands)  # 1.5 x the equal band: the balance point
 
 
-def _codec_worker(rank, world, port, scene_name, out_dir, display_rows, ring, alpha):
-    """The 3-byte band transfer (bench.BandCodec) over gloo: bands packed by the senders, received as bytes
-    and unpacked into the display rank's frame, one-shot (gather_bands) or through the double buffer."""
+def _codec_worker(rank, world, port, scene_name, out_dir, display_rows, ring, alpha, mode="bgr24", slot=None):
+    """A compact band transfer (bench.BandCodec: "bgr24" or "dbp") over gloo: bands packed by the senders, received
+    as bytes and unpacked into the display rank's frame, one-shot (gather_bands) or through the double buffer. dbp:
+    the slot size is agreed over the ranks (agree_dbp_slot, a max) unless `slot` forces one."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     sys.path.insert(0, ROOT)
     sys.path.insert(0, os.path.join(ROOT, "3d-renderer_amd", "python"))
@@ -372,13 +373,18 @@ def _codec_worker(rank, world, port, scene_name, out_dir, display_rows, ring, al
     spans = [(a * W, (b - a) * W) for a, b in bands]
     col, _, _ = oracle_py.render(scene, band=bands[rank], threads=2)
     mine = torch.from_numpy(np.ascontiguousarray(col).view(np.int32).reshape(-1).copy())
-    codec = bench.BandCodec(alpha, torch.device("cpu"))
+    codec = bench.BandCodec(alpha, torch.device("cpu"), mode)
+    if mode == "dbp":
+        if slot is None:
+            bench.agree_dbp_slot(codec, mine, True)
+        else:
+            codec.slot = slot
     u8 = lambda n: torch.zeros(n, dtype=torch.uint8)  # noqa: E731
     if ring:
         r = bench.GatherRing(world, spans[rank][1], H * W, lambda n: torch.zeros(n, dtype=torch.int32), rank=rank,
                              spans=spans, codec=codec, make_bytes=u8)
         if rank == 0:
-            assert r.inbound_bytes == 3 * sum(n for _, n in spans[1:])
+            assert r.inbound_bytes == sum(codec.bytes_for(n) for _, n in spans[1:])
         for k in range(3):
             band = r.acquire()
             band.copy_(mine if k == 2 else torch.full_like(mine, ((alpha << 24) | k) - (1 << 32)))
@@ -386,7 +392,8 @@ def _codec_worker(rank, world, port, scene_name, out_dir, display_rows, ring, al
         r.drain()
         out = r.frame if rank == 0 else None
     else:
-        stage = {q: u8(3 * spans[q][1]) for q in range(1, world)} if rank == 0 else u8(3 * spans[rank][1])
+        stage = ({q: u8(codec.bytes_for(spans[q][1])) for q in range(1, world)} if rank == 0
+                 else u8(codec.bytes_for(spans[rank][1])))
         out = bench.gather_bands(torch.empty(H * W, dtype=torch.int32), mine, world, rank=rank, spans=spans,
                                  codec=codec, stage=stage)
     try:
@@ -395,26 +402,51 @@ def _codec_worker(rank, world, port, scene_name, out_dir, display_rows, ring, al
     except RuntimeError:
         ok = False
     np.save(os.path.join(out_dir, f"alpha_ok_{rank}.npy"), np.array(ok))
+    np.save(os.path.join(out_dir, f"slot_{rank}.npy"), np.array(codec.slot))
     if out is not None:
         np.save(os.path.join(out_dir, "frame.npy"), out.numpy())
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,display_rows,ring", [(2, None, False), (3, 200, True), (4, None, True), (4, 90, False)])
-def test_packed_bands_assemble_bit_exact(world, display_rows, ring, oracle, tmp_path):
-    """bands sent as 3 bytes per pixel assemble to the same frame as 4-byte bands (the oracle's
-    full frame), when every alpha byte is the promised 255 (grid_c3: opaque material, tint, white texture and
-    clear colour)."""
+@pytest.mark.parametrize("world,display_rows,ring,mode", [(2, None, False, "bgr24"), (3, 200, True, "bgr24"),
+                                                          (4, None, True, "bgr24"), (4, 90, False, "bgr24"),
+                                                          (2, None, False, "dbp"), (3, 200, True, "dbp"),
+                                                          (4, 90, False, "dbp")])
+def test_packed_bands_assemble_bit_exact(world, display_rows, ring, mode, oracle, tmp_path):
+    """bands sent as 3 bytes per pixel (bgr24) or in the delta bit-plane format (dbp)
+    assemble to the same frame as 4-byte bands (the oracle's full frame), when every alpha byte is the promised 255
+    (grid_c3: opaque material, tint, white texture and clear colour). dbp: every rank agreed the same slot size."""
     import torch.multiprocessing as mp
 
     import scene_cases as sc
 
-    mp.start_processes(_codec_worker, args=(world, _free_port(), "grid_c3", str(tmp_path), display_rows, ring, 255),
-                       nprocs=world, join=True, start_method="spawn")
+    mp.start_processes(_codec_worker, args=(world, _free_port(), "grid_c3", str(tmp_path), display_rows, ring, 255,
+                                            mode), nprocs=world, join=True, start_method="spawn")
     col, _, _ = oracle.render(sc.grid_c3(), threads=4)
     assert np.array_equal(np.load(tmp_path / "frame.npy"), np.ascontiguousarray(col).view(np.int32).reshape(-1))
     assert all(bool(np.load(tmp_path / f"alpha_ok_{r}.npy")) for r in range(world))
+    slots = {int(np.load(tmp_path / f"slot_{r}.npy")) for r in range(world)}
+    assert len(slots) == 1
+    if mode == "dbp":
+        assert slots.pop() < 3 * bench_mod().DBP_SLOT_PIXELS  # smaller than the 3-byte format
+
+
+def bench_mod():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    return bench
+
+
+def test_dbp_slot_overflow_is_flagged(oracle, tmp_path):
+    """A dbp slot too small for a band's content sets the sender's overflow flag (check() raises): a lossy
+    transfer cannot pass silently."""
+    import torch.multiprocessing as mp
+
+    mp.start_processes(_codec_worker, args=(2, _free_port(), "grid_c3", str(tmp_path), None, False, 255, "dbp",
+                                            bench_mod().DBP_HEADER + 16), nprocs=2, join=True, start_method="spawn")
+    assert not bool(np.load(tmp_path / "alpha_ok_1.npy"))
 
 
 def test_packing_a_non_uniform_alpha_is_flagged(oracle, tmp_path):
@@ -444,3 +476,10 @@ def test_frame_alpha_proof(hiplib):
     codec.unpack(st, back)
     assert torch.equal(back, band)
     codec.check()
+    dbp = bench.BandCodec(255, torch.device("cpu"), "dbp")  # random pixels: the maximum slot, still lossless
+    st = torch.zeros(dbp.bytes_for(1003), dtype=torch.uint8)
+    dbp.pack(band, st)
+    back = torch.zeros_like(band)
+    dbp.unpack(st, back)
+    assert torch.equal(back, band)
+    dbp.check()
