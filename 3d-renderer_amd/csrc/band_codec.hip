@@ -73,34 +73,38 @@ __global__ __launch_bounds__(kCodecBlock) void k_unpack_bgr24(const uint8_t* __r
 }
 
 // ---- the delta bit-plane codec: a band as a 1-D pixel stream, 4096 pixels per fixed-size slot -------
-// Each wave codes one 1024-pixel segment as 16 blocks of 64 pixels, lane = pixel. Per block and channel (B, G, R) the
-// pixel-to-pixel difference (mod 256, the segment's first pixel stored whole in the slot header and coded as a zero
-// difference) is zigzag-mapped, the block's bit width w (0..8) is the width of the wave maximum, and the block stores w
-// bit planes, each a 64-bit ballot (lane i = bit i). Shaded frames are smooth between neighbours (C3: 1.42 B/pixel on
-// average, at most 1.59 in any slot; C5 with its textures 2.0 / 2.11), so a slot of S bytes carries 4096 pixels in far
-// fewer than the 3-byte format's 12288. Slot layout (S bytes, a multiple of 16):
+// A slot is 4 segments of 1024 pixels, a segment 16 blocks of 64. Per block and channel (B, G, R) the pixel-to-pixel
+// difference (mod 256; a segment's first pixel is stored whole in the slot header and coded as a zero difference) is
+// zigzag-mapped, the block's bit width w (0..8) is the width of the largest value, and the block stores w bit planes,
+// each a 64-bit ballot (bit i = pixel i). Shaded frames are smooth between neighbours (C3: 1.42 B/pixel on average,
+// at most 1.59 in any slot; C5 with its textures 2.0 / 2.11), so a slot of S bytes carries 4096 pixels in far fewer
+// than the 3-byte format's 12288. Slot layout (S bytes, a multiple of 16):
 //   [0, 4)      the payload bytes P of the 64 blocks (the decoder's bound; P + 160 > S marks an overflowed slot)
 //   [16, 160)   4 segment headers of 36 B: the first pixel (B, G, R, 0) and 16 block widths w_b | w_g << 4 | w_r << 8
 //   [160, +P)   the blocks' planes in order, channel B's w_b planes, then G's, then R's
-// Both kernels run one 1024-thread workgroup per slot, wave w on blocks 4w..4w+3 (lane = pixel), with no serial chain.
-// They are VALU-issue-bound, so every step is counted in wave instructions per 64-pixel block:
-//   k_dbp_pack    a block's differences need only the pixel before it (a second, cached load); the three channels'
-//                 byte differences and zigzag maps are computed together in one 32-bit word (SWAR, ~12 ops), one DPP
-//                 OR-scan gives the three widths, and each plane that exists costs a bit test, a ballot and two
-//                 bit-field inserts (plane j parked in lane j). One wave's DPP prefix sum over the 64 blocks' plane counts
-//                 places every block; each lane < w stores plane `lane` of its channel (contiguous 8-B stores).
-//   k_dbp_unpack  the slot (header + payload, <= 12448 B) is copied to LDS with 16-B loads; every wave sums the 64
-//                 blocks' widths (lane = block, DPP scan) to find its blocks' planes. A plane costs one LDS read (lanes
-//                 0-31 read its low word, 32-63 its high word) and two ops (bit extract, shift-or into the packed
-//                 zigzag word); the zigzag inverse is SWAR over the three channels, and the differences are summed by
-//                 two DPP wave scans (B and R share one in 16-bit fields, G the other: only the sums mod 256 matter).
-//                 The blocks' totals meet in LDS; each block adds the totals of the blocks before it in its segment
-//                 (plus the segment's first pixel), wave-uniform arithmetic. One launch decodes up to
-//                 TRI_DBP_MAX_BANDS bands (the display GPU's remote bands), a workgroup per slot of any of them.
+// One workgroup per slot. Both kernels are bound by instruction issue (the VALUs and the CU's one scalar unit), so
+// every step is counted in instructions per 64-pixel block:
+//   k_dbp_pack    1024 threads, wave w on blocks 4w..4w+3 (a one-band launch has about one slot per CU: sixteen
+//                 waves keep it busy). The wave issues its 4 pixel loads at once; a pixel's predecessor comes from
+//                 the lane before it (DPP wave_shr:1; lane 0 takes the previous block's last pixel, a readlane, or
+//                 one scalar load at the wave's first block). The three channels' byte differences and zigzag maps
+//                 are one 32-bit SWAR word and one DPP OR-scan gives the widths; the zigzag words stay in registers.
+//                 After one barrier every wave's prefix sum over the 64 blocks' plane counts places its blocks; each
+//                 plane that exists then costs a bit test, a ballot and two and-ors (plane j parked in lane j), and
+//                 lanes < w store a channel's planes in place (8 B each).
+//   k_dbp_unpack  256 threads, wave w on segment w (the carries never leave the wave; eight slots fit a CU at once).
+//                 Every wave sums the 64 blocks' widths (lane = block, DPP scan) to find its blocks' planes and reads
+//                 each channel's 8 candidate planes with one scalar buffer load (16 SGPRs, the next block's in flight
+//                 while this one is summed; planes past the width are dropped, reads past the slot return 0). A plane
+//                 then costs one VALU op: v_addc with the plane as its carry-in lane mask shifts the lane's bit into
+//                 z (z = 2 z + bit, most significant plane first). The zigzag is inverted per byte (SWAR) and the
+//                 differences summed with two DPP wave scans (B and R share one in 16-bit fields, G the other: only
+//                 the sums mod 256 matter); the block's last pixel is the next block's carry (readlane). One launch
+//                 decodes up to TRI_DBP_MAX_BANDS bands (the display GPU's remote bands), a workgroup per slot.
 // Lossless whenever no slot overflows; an overflow (a slot whose pixels need more than S bytes) sets flags[0] bit 1
 // and leaves the slot's pixels undecoded, so the caller grows S and sends the frame again (the bin-queue overflow
 // protocol). A slot whose widths do not add up to its payload count is not decoded either (not this format).
-constexpr uint32_t kDbpSlotPixels = 4096, kDbpHeader = 160, kDbpBlocks = 64, kDbpThreads = 1024;
+constexpr uint32_t kDbpSlotPixels = 4096, kDbpHeader = 160, kDbpBlocks = 64, kDbpThreads = 256, kDbpSegBlocks = 16;
 constexpr uint32_t kDbpMaxPayload = kDbpBlocks * 24u * 8u;  // 12288 B: 8 planes per channel in every block
 
 // v[lane - k] within the lane's row of 16 (CTRL row_shr:k), or row_bcast:15 / :31 onto the rows in ROW_MASK; 0 elsewhere
@@ -126,6 +130,10 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t v) {  // the OR over the wa
     v |= dpp0<0x143, 0xc>(v);
     return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
+// v of the lane before (DPP wave_shr:1); lane 0 gets `first`
+__device__ __forceinline__ uint32_t lane_before(uint32_t v, uint32_t first) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)first, (int)v, 0x138, 0xf, 0xf, false);
+}
 // B, G, R bytes of (v - p) mod 256, each zigzag-mapped (0, -1, 1, -2, ... -> 0, 1, 2, 3, ...); alpha byte 0
 __device__ __forceinline__ uint32_t zigzag_diff3(uint32_t v, uint32_t p) {
     constexpr uint32_t H = 0x00808080u, L = 0x007F7F7Fu;
@@ -136,16 +144,16 @@ __device__ __forceinline__ uint32_t zigzag_diff3(uint32_t v, uint32_t p) {
 __device__ __forceinline__ uint32_t width8(uint32_t x) { return x ? 32u - (uint32_t)__builtin_clz(x) : 0u; }
 // planes J..wc-1 of channel C of the wave's zigzag words: plane j (a ballot, in SGPRs) parked in lane j of l (low
 // word) and h (high word) by an and-or with the lane's mask lm[j] (all ones in lane j): one v_and_or per word,
-// an operation the compiler sees (a v_writelane in inline asm would not survive its copies under partial exec masks)
+// an ordinary per-lane operation (a v_writelane in inline asm would not survive the compiler's copies of the register
+// under partial exec masks)
 template <uint32_t C, uint32_t J>
 __device__ __forceinline__ void park_planes(uint32_t zz, uint32_t wc, const uint32_t (&lm)[8], uint32_t& l, uint32_t& h) {
     if constexpr (J < 8) {
         if (J < wc) {
             const uint64_t pl = __ballot((zz >> (8 * C + J)) & 1u);
-            // l and h start at 0 and every lane is written once: (lm & plane) | l, one v_and_or each (a plain
-            // per-lane operation; the compiler splits it into an and and an or with an SGPR operand). The ballot's
-            // SGPRs were just written by a VALU compare: two wait states before a VALU reads them (the compiler
-            // inserts them for its own code, not for inline assembly)
+            // l and h start at 0 and every lane is written once: (lm & plane) | l, one v_and_or each (the compiler
+            // splits it into an and and an or with an SGPR operand). The ballot's SGPRs were just written by a VALU
+            // compare: two wait states before a VALU reads them (the compiler inserts them for its own code only)
             asm("s_nop 1\n\tv_and_or_b32 %0, %1, %2, %0" : "+v"(l) : "v"(lm[J]), "s"((uint32_t)pl));
             asm("v_and_or_b32 %0, %1, %2, %0" : "+v"(h) : "v"(lm[J]), "s"((uint32_t)(pl >> 32)));
             park_planes<C, J + 1>(zz, wc, lm, l, h);
@@ -153,56 +161,52 @@ __device__ __forceinline__ void park_planes(uint32_t zz, uint32_t wc, const uint
     }
 }
 
-__global__ __launch_bounds__(kDbpThreads) void k_dbp_pack(const uint32_t* __restrict__ src, uint64_t n, uint32_t alpha,
-                                                          uint8_t* __restrict__ dst, uint32_t slot_bytes,
-                                                          uint32_t* __restrict__ flags) {
+constexpr uint32_t kDbpPackThreads = 1024, kDbpPackBlocks = kDbpBlocks / (kDbpPackThreads / 64);  // 4 per wave
+
+__global__ __launch_bounds__(kDbpPackThreads) void k_dbp_pack(const uint32_t* __restrict__ src, uint64_t n,
+                                                              uint32_t alpha, uint8_t* __restrict__ dst,
+                                                              uint32_t slot_bytes, uint32_t* __restrict__ flags) {
     __shared__ uint32_t hdr[kDbpHeader / 4];
     __shared__ uint32_t cnt[kDbpBlocks];
-    __shared__ uint32_t offs[kDbpBlocks + 1];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t slot0 = (uint64_t)blockIdx.x * kDbpSlotPixels;
-    uint32_t lo[4][3], hi[4][3], wd[4], lm[8];
-#pragma unroll
-    for (uint32_t j = 0; j < 8; ++j) {
-        lm[j] = lane == j ? ~0u : 0u;
-        asm volatile("" : "+v"(lm[j]));  // an opaque vector value: kept as a VGPR operand, not turned into lane masks
-    }
+    const uint32_t b0 = kDbpPackBlocks * w;  // this wave's first block in the slot
+    const uint64_t px0 = (uint64_t)blockIdx.x * kDbpSlotPixels + 64u * b0;
+    // pixels past the band repeat its last one (zero differences)
+    uint32_t zz[kDbpPackBlocks], wq[kDbpPackBlocks];
     bool bad = false;
+    {
+        uint32_t v[kDbpPackBlocks];
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t b = 4u * w + q;
-        const uint64_t i = slot0 + 64u * b + lane;
-        // pixels past the band repeat its last one (zero differences); a segment's first pixel is its own predecessor
-        const bool seg_first = (b & 15u) == 0 && lane == 0;
-        const uint64_t ip = seg_first ? i : i - 1;
-        const uint32_t v = src[i < n ? i : n - 1];
-        const uint32_t p = src[ip < n ? ip : n - 1];
-        bad |= i < n && (v >> 24) != alpha;
-        const uint32_t zz = zigzag_diff3(v, p);
-        const uint32_t any = wave_or(zz);
-        const uint32_t w0 = width8(any & 0xFFu), w1 = width8((any >> 8) & 0xFFu), w2 = width8((any >> 16) & 0xFFu);
-        const uint32_t wq = w0 | (w1 << 4) | (w2 << 8);
-        lo[q][0] = hi[q][0] = lo[q][1] = hi[q][1] = lo[q][2] = hi[q][2] = 0;
-        park_planes<0, 0>(zz, w0, lm, lo[q][0], hi[q][0]);
-        park_planes<1, 0>(zz, w1, lm, lo[q][1], hi[q][1]);
-        park_planes<2, 0>(zz, w2, lm, lo[q][2], hi[q][2]);
-        wd[q] = wq;
-        if (lane == 0) {
-            reinterpret_cast<uint16_t*>(hdr + 4 + 9 * (b >> 4) + 1)[b & 15u] = (uint16_t)wq;
-            cnt[b] = (wq & 15u) + ((wq >> 4) & 15u) + (wq >> 8);
-            if ((b & 15u) == 0) hdr[4 + 9 * (b >> 4)] = i < n ? v & 0x00FFFFFFu : 0u;
+        for (uint32_t k = 0; k < kDbpPackBlocks; ++k) {
+            const uint64_t i = px0 + 64u * k + lane;
+            v[k] = src[i < n ? i : n - 1];
+        }
+        // the pixel before this wave's first: a segment's first pixel is its own predecessor (a zero difference,
+        // the pixel stored whole in the header); otherwise the previous wave's last pixel, one scalar load
+        const bool seg_first = (b0 % kDbpSegBlocks) == 0;
+        uint32_t carry = seg_first ? (uint32_t)__builtin_amdgcn_readlane((int)v[0], 0) : src[px0 - 1 < n ? px0 - 1 : n - 1];
+        if (seg_first && lane == 0) hdr[4 + 9 * (b0 / kDbpSegBlocks)] = px0 < n ? carry & 0x00FFFFFFu : 0u;
+#pragma unroll
+        for (uint32_t k = 0; k < kDbpPackBlocks; ++k) {
+            bad |= px0 + 64u * k + lane < n && (v[k] >> 24) != alpha;
+            zz[k] = zigzag_diff3(v[k], lane_before(v[k], carry));
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)v[k], 63);
+            const uint32_t any = wave_or(zz[k]);
+            wq[k] = width8(any & 0xFFu) | (width8((any >> 8) & 0xFFu) << 4) | (width8((any >> 16) & 0xFFu) << 8);
+            if (lane == 0) {
+                const uint32_t b = b0 + k;
+                reinterpret_cast<uint16_t*>(hdr + 4 + 9 * (b / kDbpSegBlocks) + 1)[b % kDbpSegBlocks] = (uint16_t)wq[k];
+                cnt[b] = (wq[k] & 15u) + ((wq[k] >> 4) & 15u) + (wq[k] >> 8);
+            }
         }
     }
     if (__ballot(bad) != 0ull && lane == 0 && flags) atomicOr(flags, 1u);
     __syncthreads();
-    if (w == 0) {
-        const uint32_t c = cnt[lane];
-        const uint32_t incl = wave_incl_sum(c);
-        offs[lane] = incl - c;
-        if (lane == 63) offs[kDbpBlocks] = incl;
-    }
-    __syncthreads();
-    const uint32_t total = offs[kDbpBlocks];
+    // every wave places the slot's 64 blocks itself (lane = block): no second barrier
+    const uint32_t c = cnt[lane];
+    const uint32_t incl = wave_incl_sum(c);
+    const uint32_t excl = incl - c;
+    const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     const uint32_t bytes = kDbpHeader + 8u * total;
     uint8_t* slot = dst + (size_t)blockIdx.x * slot_bytes;
     if (threadIdx.x == 0 && flags) {
@@ -215,16 +219,25 @@ __global__ __launch_bounds__(kDbpThreads) void k_dbp_pack(const uint32_t* __rest
     }
     if (threadIdx.x < kDbpHeader / 4)
         reinterpret_cast<uint32_t*>(slot)[threadIdx.x] = threadIdx.x == 0 ? 8u * total : threadIdx.x < 4 ? 0u : hdr[threadIdx.x];
+    // each block's planes, parked in lanes and stored straight to their place
+    uint32_t lm[8];
+#pragma unroll
+    for (uint32_t j = 0; j < 8; ++j) {
+        lm[j] = lane == j ? ~0u : 0u;
+        asm volatile("" : "+v"(lm[j]));  // an opaque vector value: kept as a VGPR operand, not turned into lane masks
+    }
     uint2* pay = reinterpret_cast<uint2*>(slot + kDbpHeader);
 #pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        uint32_t o = offs[4u * w + q];
-#pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const uint32_t wc = (wd[q] >> (4 * c)) & 15u;
-            if (lane < wc) pay[o + lane] = make_uint2(lo[q][c], hi[q][c]);
-            o += wc;
-        }
+    for (uint32_t k = 0; k < kDbpPackBlocks; ++k) {
+        const uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)excl, (int)(b0 + k));
+        const uint32_t w0 = wq[k] & 15u, w1 = (wq[k] >> 4) & 15u, w2 = wq[k] >> 8;
+        uint32_t l0 = 0, h0 = 0, l1 = 0, h1 = 0, l2 = 0, h2 = 0;
+        park_planes<0, 0>(zz[k], w0, lm, l0, h0);
+        park_planes<1, 0>(zz[k], w1, lm, l1, h1);
+        park_planes<2, 0>(zz[k], w2, lm, l2, h2);
+        if (lane < w0) pay[o + lane] = make_uint2(l0, h0);
+        if (lane < w1) pay[o + w0 + lane] = make_uint2(l1, h1);
+        if (lane < w2) pay[o + w0 + w1 + lane] = make_uint2(l2, h2);
     }
 }
 
@@ -236,76 +249,81 @@ struct DbpBands {  // the bands one k_dbp_unpack launch decodes (kernel argument
     uint32_t count;
 };
 
+// DBP_ABLATE (diagnostic builds only, tools/codec_ablate.sh): 1 skips the plane decode, 2 the scans, 4 the stores
+#ifndef DBP_ABLATE
+#define DBP_ABLATE 0
+#endif
+typedef uint32_t dbp_u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t dbp_u32x16 __attribute__((ext_vector_type(16)));
+__device__ dbp_u32x16 dbp_s_load16(dbp_u32x4 rsrc, int offset, int aux) __asm("llvm.amdgcn.s.buffer.load.v16i32");
+__device__ uint32_t dbp_s_load1(dbp_u32x4 rsrc, int offset, int aux) __asm("llvm.amdgcn.s.buffer.load.i32");
+
+// z = 2 z + (bit `lane` of the 64-bit plane m): one v_addc with the plane as its carry-in lane mask
+__device__ __forceinline__ uint32_t shift_in_plane(uint32_t z, uint64_t m) {
+    uint64_t carry_out;  // unused (an SGPR pair of its own, so successive ops share no VCC)
+    asm("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(z), "=s"(carry_out) : "v"(z), "s"(m));
+    return z;
+}
+// a channel's zigzag values from its wc (<= 8) planes p[0..7] (16 words from one scalar load), most significant plane
+// first; the planes past wc belong to the next channel or block and are masked off afterwards (one VALU op instead of
+// a scalar select per plane: the CU's one scalar unit, shared by its four SIMDs, is the scarcer issue port here)
+__device__ __forceinline__ uint32_t planes_to_lanes(const dbp_u32x16& p, uint32_t wc) {
+    uint32_t z = 0;
+#pragma unroll
+    for (int j = 7; j >= 0; --j) z = shift_in_plane(z, ((uint64_t)p[2 * j + 1] << 32) | p[2 * j]);
+    return z & ((1u << wc) - 1u);
+}
+
 __global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint32_t alpha, uint32_t slot_bytes) {
-    __shared__ uint4 lds[(kDbpHeader + kDbpMaxPayload) / 16 + 8];  // + 128 B: a block's last channel reads 8 planes
-    __shared__ uint32_t tot[kDbpBlocks][2];
     uint32_t band = 0;  // the band this slot belongs to (wave-uniform search over <= 16 entries)
     while (band + 1 < bands.count && blockIdx.x >= bands.first[band + 1]) ++band;
     const uint64_t n = bands.n[band];
     uint32_t* __restrict__ dst = bands.dst[band];
     const uint32_t sl = blockIdx.x - bands.first[band];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-    const uint64_t slot0 = (uint64_t)sl * kDbpSlotPixels;
     const uint8_t* slot = bands.src[band] + (size_t)sl * slot_bytes;
-    const uint32_t payload = *reinterpret_cast<const uint32_t*>(slot);
+    // the slot as a raw buffer (scalar loads past its end return 0)
+    const uint64_t base = (uint64_t)slot;
+    const dbp_u32x4 r = dbp_u32x4{(uint32_t)base, (uint32_t)(base >> 32) & 0xFFFFu, slot_bytes, 0x00020000u};
+    const uint32_t payload = dbp_s_load1(r, 0, 0);
     // an overflowed slot (the sender flagged the frame), or more payload than the format has: left alone
     if (kDbpHeader + payload > slot_bytes || payload > kDbpMaxPayload) return;
-    if (16u * threadIdx.x < kDbpHeader + payload)
-        lds[threadIdx.x] = reinterpret_cast<const uint4*>(slot)[threadIdx.x];
-    __syncthreads();
-    const uint32_t* hdr = reinterpret_cast<const uint32_t*>(lds);
     // lane l: block l's widths and plane count; the inclusive sum places every block's planes
-    const uint32_t wl = reinterpret_cast<const uint16_t*>(hdr + 4 + 9 * (lane >> 4) + 1)[lane & 15u];
+    const uint32_t wl = reinterpret_cast<const uint16_t*>(slot + 16 + 36 * (lane >> 4) + 4)[lane & 15u];
+    const uint32_t first = dbp_s_load1(r, 16 + 36 * (int)w, 0);
     const uint32_t cl = (wl & 15u) + ((wl >> 4) & 15u) + ((wl >> 8) & 15u);
     const uint32_t incl = wave_incl_sum(cl);
     if (8u * (uint32_t)__builtin_amdgcn_readlane((int)incl, 63) != payload) return;  // not a dbp slot (uniform)
-    // this lane's word of every plane: the low word for lanes 0-31, the high word for 32-63
-    const uint32_t* planes = hdr + kDbpHeader / 4 + (lane >> 5);
-    const uint32_t sh = lane & 31u;
-    uint32_t s0[4], s1[4];  // inclusive sums: B | R << 16, and G
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t b = 4u * w + q;
-        const uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)wl, (int)b);
-        uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)(incl - cl), (int)b);
-        uint32_t zz = 0;  // the three zigzag values, one per byte
-#pragma unroll
-        for (uint32_t c = 0; c < 3; ++c) {
-            // all 8 candidate planes at once (independent LDS reads, paired by the compiler; the ones past the
-            // channel's width belong to the next channel or block and are masked off): no branch and no wait per plane
-            const uint32_t wc = (wb >> (4 * c)) & 15u;
-            uint32_t z = 0;
-#pragma unroll
-            for (uint32_t j = 0; j < 8; ++j) z |= ((planes[2 * (o + j)] >> sh) & 1u) << j;
-            zz |= (z & ((1u << wc) - 1u)) << (8 * c);
-            o += wc;
-        }
-        // zigzag back to the differences (mod 256), per byte
-        const uint32_t d = ((zz >> 1) & 0x007F7F7Fu) ^ ((zz & 0x00010101u) * 0xFFu);
-        s0[q] = wave_incl_sum(d & 0x00FF00FFu);
-        s1[q] = wave_incl_sum((d >> 8) & 0xFFu);
-        if (lane == 63) {
-            tot[b][0] = s0[q];
-            tot[b][1] = s1[q];
-        }
-    }
-    __syncthreads();
-    // the carry into this wave's first block: its segment's first pixel plus the totals of the blocks before it
-    const uint32_t seg = w >> 2, b0 = 4u * w;
-    const uint32_t first = hdr[4 + 9 * seg];
-    uint32_t c0 = first & 0x00FF00FFu, c1 = (first >> 8) & 0xFFu;
-    for (uint32_t k = 16u * seg; k < b0; ++k) {
-        c0 = (c0 + tot[k][0]) & 0x00FF00FFu;
-        c1 = (c1 + tot[k][1]) & 0xFFu;
-    }
+    uint32_t c0 = first & 0x00FF00FFu, c1 = (first >> 8) & 0xFFu;  // the carries: B | R << 16, and G
     const uint32_t a = alpha << 24;
-#pragma unroll
-    for (uint32_t q = 0; q < 4; ++q) {
-        const uint32_t x0 = c0 + s0[q], x1 = c1 + s1[q];
-        const uint64_t i = slot0 + 64u * (b0 + q) + lane;
-        if (i < n) dst[i] = a | (x0 & 0x00FF00FFu) | ((x1 & 0xFFu) << 8);
-        c0 = (c0 + tot[b0 + q][0]) & 0x00FF00FFu;
-        c1 = (c1 + tot[b0 + q][1]) & 0xFFu;
+    const uint64_t seg0 = (uint64_t)sl * kDbpSlotPixels + (uint64_t)w * (kDbpSegBlocks * 64u);
+    // block k's planes: three scalar loads (one per channel), issued one block ahead of their use
+    const uint32_t ol = incl - cl;  // lane l: block l's first plane
+    uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)wl, (int)(kDbpSegBlocks * w));
+    uint32_t o = (uint32_t)__builtin_amdgcn_readlane((int)ol, (int)(kDbpSegBlocks * w));
+    dbp_u32x16 p0 = dbp_s_load16(r, (int)(kDbpHeader + 8u * o), 0);
+    dbp_u32x16 p1 = dbp_s_load16(r, (int)(kDbpHeader + 8u * (o + (wb & 15u))), 0);
+    dbp_u32x16 p2 = dbp_s_load16(r, (int)(kDbpHeader + 8u * (o + (wb & 15u) + ((wb >> 4) & 15u))), 0);
+    for (uint32_t k = 0; k < kDbpSegBlocks; ++k) {
+        const uint32_t zz = (DBP_ABLATE & 1) ? lane * (p0[0] + p1[0] + p2[0])
+                                             : planes_to_lanes(p0, wb & 15u) | (planes_to_lanes(p1, (wb >> 4) & 15u) << 8) |
+                                                   (planes_to_lanes(p2, (wb >> 8) & 15u) << 16);
+        if (k + 1 < kDbpSegBlocks) {  // the next block's planes, in flight during this block's sums and stores
+            const uint32_t nb = kDbpSegBlocks * w + k + 1;
+            wb = (uint32_t)__builtin_amdgcn_readlane((int)wl, (int)nb);
+            o = (uint32_t)__builtin_amdgcn_readlane((int)ol, (int)nb);
+            p0 = dbp_s_load16(r, (int)(kDbpHeader + 8u * o), 0);
+            p1 = dbp_s_load16(r, (int)(kDbpHeader + 8u * (o + (wb & 15u))), 0);
+            p2 = dbp_s_load16(r, (int)(kDbpHeader + 8u * (o + (wb & 15u) + ((wb >> 4) & 15u))), 0);
+        }
+        // zigzag back to the differences (mod 256), per byte; then the running sums from the carry
+        const uint32_t d = ((zz >> 1) & 0x007F7F7Fu) ^ ((zz & 0x00010101u) * 0xFFu);
+        const uint32_t x0 = ((DBP_ABLATE & 2) ? (d & 0x00FF00FFu) : wave_incl_sum(d & 0x00FF00FFu)) + c0;
+        const uint32_t x1 = ((DBP_ABLATE & 2) ? ((d >> 8) & 0xFFu) : wave_incl_sum((d >> 8) & 0xFFu)) + c1;
+        const uint64_t i = seg0 + 64u * k + lane;
+        if (i < n && (!(DBP_ABLATE & 4) || x0 == 0x12345678u)) dst[i] = a | (x0 & 0x00FF00FFu) | ((x1 & 0xFFu) << 8);
+        c0 = (uint32_t)__builtin_amdgcn_readlane((int)x0, 63) & 0x00FF00FFu;
+        c1 = (uint32_t)__builtin_amdgcn_readlane((int)x1, 63) & 0xFFu;
     }
 }
 
@@ -337,7 +355,7 @@ hipError_t tri_launch_dbp_pack(const uint32_t* src, uint64_t n, uint32_t alpha, 
                                uint32_t* flags, hipStream_t stream) {
     if (n == 0) return hipSuccess;
     const dim3 g((uint32_t)((n + kDbpSlotPixels - 1) / kDbpSlotPixels));
-    hipLaunchKernelGGL(k_dbp_pack, g, dim3(kDbpThreads), 0, stream, src, n, alpha, dst, slot_bytes, flags);
+    hipLaunchKernelGGL(k_dbp_pack, g, dim3(kDbpPackThreads), 0, stream, src, n, alpha, dst, slot_bytes, flags);
     return hipGetLastError();
 }
 

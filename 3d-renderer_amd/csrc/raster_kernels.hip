@@ -44,6 +44,11 @@ constexpr uint32_t kAblate = TRI_ABLATE;
 
 // Diagnostics builds only (-DTRI_PHASE_TIMING): k_raster's wave 0 of every workgroup stamps s_memtime at
 // its phase boundaries (start, init, coverage, large triangles, shading, end) for tools/phase_times.py.
+// Diagnostics builds only (-DTRI_PRIM_GROUPS): the shading loop counts, per wave-iteration, the distinct primitives
+// among its shaded lanes (tools/prim_groups.py): {iterations, distinct primitives, shaded lanes}.
+#ifdef TRI_PRIM_GROUPS
+__device__ unsigned long long g_tri_groups[3];
+#endif
 #ifdef TRI_PHASE_TIMING
 constexpr int kPhaseSlots = 65536;
 __device__ unsigned long long g_tri_phase[kPhaseSlots][6];
@@ -2863,6 +2868,25 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
                 if (bg) skyq[base + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
             }
         }
+#ifdef TRI_PRIM_GROUPS
+        {
+            const bool shade = in && !bg;
+            uint64_t m = __ballot(shade);
+            const uint32_t pid = shade ? ((uint32_t)key >> 3) : 0u;
+            const uint32_t active = (uint32_t)__builtin_popcountll(m);
+            uint32_t groups = 0;
+            while (m) {
+                const uint32_t lp = (uint32_t)__shfl((int)pid, (int)__builtin_ctzll(m));
+                m &= ~__ballot(shade && pid == lp);
+                ++groups;
+            }
+            if ((uint32_t)(tid & 63) == (uint32_t)__builtin_ctzll(__ballot(true)) && active) {
+                atomicAdd(&g_tri_groups[0], 1ull);
+                atomicAdd(&g_tri_groups[1], (unsigned long long)groups);
+                atomicAdd(&g_tri_groups[2], (unsigned long long)active);
+            }
+        }
+#endif
         if (!in) continue;
         const int32_t px = ox + lx, py = oy + ly;
         uint32_t out;
@@ -3252,6 +3276,16 @@ const void* tri_raster_plain_kernel(const TriFrameParams& fp) {
     if (sel == 0) return f(k_raster_plain<false, 6, false>); if (sel == 1) return f(k_raster_plain<true, 6, false>);
     if (sel == 2) return f(k_raster_plain<false, 6, true>); return f(k_raster_plain<true, 6, true>);
 }
+#ifdef TRI_PRIM_GROUPS
+extern "C" int tri_debug_prim_groups(unsigned long long* out3, int reset) {  // k_raster_plain's counts
+    if (reset) {
+        const unsigned long long z[3] = {0, 0, 0};
+        return hipMemcpyToSymbol(HIP_SYMBOL(g_tri_groups), z, sizeof(z)) == hipSuccess ? 0 : -1;
+    }
+    return hipMemcpyFromSymbol(out3, HIP_SYMBOL(g_tri_groups), 3 * sizeof(unsigned long long), 0,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef TRI_PHASE_TIMING
 extern "C" int tri_debug_phase_times(unsigned long long* out, int nslots) {  // k_raster_plain's stamps
     const size_t n = (size_t)(nslots < kPhaseSlots ? nslots : kPhaseSlots) * 6 * sizeof(unsigned long long);

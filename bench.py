@@ -720,15 +720,17 @@ DEFAULT_INFLIGHT = {"c3": 3, "c3trs": 3, "c2": 2, "c5": 2, "c1": 2}
 
 
 def split_candidates(height, world, min_rows=32, inflights=(2,)):
-    """(display rows, frames in flight) pairs autotune_split tries: the equal split and display bands up to
-    2.5x it, as long as every other rank keeps at least `min_rows` rows (one bin row), at each frame count
-    in `inflights` (a band's kernels are short at large N, and a third frame in flight keeps more of the
-    GPU busy: N = 8 rank 4 on one GPU 33.4k frames/s with 2, 39.0k with 3, 33.1k with 4)."""
+    """(display rows, frames in flight) pairs autotune_split tries: the equal split, display bands up to 2.5x
+    it (when the links bind, a larger display band shortens every remote band) and down to a quarter of it (when the
+    display GPU's decode of the remote bands binds: a pixel moved off the display band costs it a decode, ~2 us per
+    million pixels, instead of a render, ~20), as long as every band keeps at least `min_rows` rows (one bin
+    row), at each frame count in `inflights` (a band's kernels are short at large N, and a third frame in flight
+    keeps more of the GPU busy: N = 8 rank 4 on one GPU 33.4k frames/s with 2, 39.0k with 3, 33.1k with 4)."""
     base = height / world
     ds = [int(round(base))]  # the equal split always (a small frame or a large world may leave no other)
-    for m in (1.25, 1.5, 2.0, 2.5):
+    for m in (0.25, 0.5, 0.75, 1.25, 1.5, 2.0, 2.5):
         d = int(round(base * m))
-        if height - d >= (world - 1) * min_rows and d not in ds:
+        if d >= min_rows and height - d >= (world - 1) * min_rows and d not in ds:
             ds.append(d)
     return [(d, k) for k in inflights for d in ds]
 

@@ -347,7 +347,7 @@ def test_autotune_split_picks_the_balanced_display_band(tmp_path):
     picks = [np.load(tmp_path / f"pick{r}.npy") for r in range(world)]
     assert np.array_equal(picks[0], picks[1])
     d, k, cands = int(picks[0][0]), int(picks[0][1]), [int(x) for x in picks[0][2:]]
-    assert cands == [500, 625, 750] * 2
+    assert cands == [500, 125, 250, 375, 625, 750] * 2
     assert (d, k) == (750, 3), (d, k, cands)  # 1.5 x the equal band: the balance point
 
 

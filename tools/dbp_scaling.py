@@ -26,7 +26,7 @@ def main():
     cs = torch.cuda.current_stream().cuda_stream
     lines = []
     base = image(270, 3840)
-    for k in (1, 2, 4, 8):
+    for k in tuple(int(x) for x in os.environ.get("DBP_SIZES", "1,2,4,8").split(",")):
         px = np.tile(base, k)
         n = px.size
         src = torch.from_numpy(px.view(np.int32)).to(dev)

@@ -6,7 +6,7 @@ OUT=gpurun_out/prof_codec
 mkdir -p $OUT
 run() {
     local name=$1; shift
-    timeout -k 10 120 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 tools/dbp_scaling.py > $OUT/$name.log 2>&1
+    DBP_SIZES=8 timeout -k 10 120 rocprofv3 "$@" -d $OUT/$name -o $name --output-format csv -- python3 tools/dbp_scaling.py > $OUT/$name.log 2>&1
     local rc=$?; echo "$name rc=$rc"; return $rc
 }
 run trace --kernel-trace --stats || exit $?
@@ -24,11 +24,15 @@ for name in ("sq1", "sq2"):
         k = row["Kernel_Name"]
         if "dbp" not in k:
             continue
-        kk = "pack" if "pack" in k else "unpack"
+        kk = "unpack" if "unpack" in k else "pack"
         acc[kk][row["Counter_Name"]] += float(row["Counter_Value"])
         disp[kk].add(row["Dispatch_Id"])
     for kk, d in acc.items():
         n = len(disp[kk])
         print(name, kk, "dispatches", n, {c: round(v / n) for c, v in sorted(d.items())})
+        if "SQ_WAVES" in d:
+            wv = d["SQ_WAVES"]
+            print("   per wave: VALU %.0f SALU %.0f LDS %.0f; wait_inst/wave_cycles %.2f" % (d["SQ_INSTS_VALU"] / wv,
+                  d["SQ_INSTS_SALU"] / wv, d["SQ_INSTS_LDS"] / wv, d["SQ_WAIT_INST_ANY"] / d["SQ_WAVE_CYCLES"]))
 P
 for f in $(find $OUT/trace -name "*kernel_stats.csv"); do grep -i dbp $f | cut -c1-200; done
