@@ -266,11 +266,16 @@ __device__ __forceinline__ uint32_t shift_in_plane(uint32_t z, uint64_t m) {
 }
 // a channel's zigzag values from its wc (<= 8) planes p[0..7] (16 words from one scalar load), most significant plane
 // first; the planes past wc belong to the next channel or block and are masked off afterwards (one VALU op instead of
-// a scalar select per plane: the CU's one scalar unit, shared by its four SIMDs, is the scarcer issue port here)
+// a scalar select per plane: the CU's one scalar unit, shared by its four SIMDs, is as scarce an issue port). A
+// channel of at most 4 planes (most of them) takes 4 steps: one scalar branch saves 4 VALU ops.
 __device__ __forceinline__ uint32_t planes_to_lanes(const dbp_u32x16& p, uint32_t wc) {
     uint32_t z = 0;
+    if (wc > 4) {
 #pragma unroll
-    for (int j = 7; j >= 0; --j) z = shift_in_plane(z, ((uint64_t)p[2 * j + 1] << 32) | p[2 * j]);
+        for (int j = 7; j >= 4; --j) z = shift_in_plane(z, ((uint64_t)p[2 * j + 1] << 32) | p[2 * j]);
+    }
+#pragma unroll
+    for (int j = 3; j >= 0; --j) z = shift_in_plane(z, ((uint64_t)p[2 * j + 1] << 32) | p[2 * j]);
     return z & ((1u << wc) - 1u);
 }
 
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint
     uint32_t band = 0;  // the band this slot belongs to (wave-uniform search over <= 16 entries)
     while (band + 1 < bands.count && blockIdx.x >= bands.first[band + 1]) ++band;
     const uint64_t n = bands.n[band];
-    uint32_t* __restrict__ dst = bands.dst[band];
+    uint32_t* dst = bands.dst[band];
     const uint32_t sl = blockIdx.x - bands.first[band];
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint8_t* slot = bands.src[band] + (size_t)sl * slot_bytes;
@@ -297,6 +302,11 @@ __global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint
     uint32_t c0 = first & 0x00FF00FFu, c1 = (first >> 8) & 0xFFu;  // the carries: B | R << 16, and G
     const uint32_t a = alpha << 24;
     const uint64_t seg0 = (uint64_t)sl * kDbpSlotPixels + (uint64_t)w * (kDbpSegBlocks * 64u);
+    // the segment's pixels as a raw buffer: stores past the band's end are dropped by the bounds check (no compare,
+    // no 64-bit address arithmetic per block)
+    const uint64_t left = seg0 < n ? n - seg0 : 0;
+    const __amdgpu_buffer_rsrc_t out = __builtin_amdgcn_make_buffer_rsrc(
+        dst + (seg0 < n ? seg0 : 0), (short)0, (int)(uint32_t)(4u * (left < 1024u ? left : 1024u)), 0x00020000);
     // block k's planes: three scalar loads (one per channel), issued one block ahead of their use
     const uint32_t ol = incl - cl;  // lane l: block l's first plane
     uint32_t wb = (uint32_t)__builtin_amdgcn_readlane((int)wl, (int)(kDbpSegBlocks * w));
@@ -320,8 +330,9 @@ __global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint
         const uint32_t d = ((zz >> 1) & 0x007F7F7Fu) ^ ((zz & 0x00010101u) * 0xFFu);
         const uint32_t x0 = ((DBP_ABLATE & 2) ? (d & 0x00FF00FFu) : wave_incl_sum(d & 0x00FF00FFu)) + c0;
         const uint32_t x1 = ((DBP_ABLATE & 2) ? ((d >> 8) & 0xFFu) : wave_incl_sum((d >> 8) & 0xFFu)) + c1;
-        const uint64_t i = seg0 + 64u * k + lane;
-        if (i < n && (!(DBP_ABLATE & 4) || x0 == 0x12345678u)) dst[i] = a | (x0 & 0x00FF00FFu) | ((x1 & 0xFFu) << 8);
+        if (!(DBP_ABLATE & 4) || x0 == 0x12345678u)
+            __builtin_amdgcn_raw_buffer_store_b32(a | (x0 & 0x00FF00FFu) | ((x1 & 0xFFu) << 8), out, (int)(4u * lane),
+                                                  (int)(256u * k), 0);
         c0 = (uint32_t)__builtin_amdgcn_readlane((int)x0, 63) & 0x00FF00FFu;
         c1 = (uint32_t)__builtin_amdgcn_readlane((int)x1, 63) & 0xFFu;
     }
