@@ -201,6 +201,12 @@ class TriGroupConfig(C.Structure):
 TRI_GROUP_NO_PACK = 0x1
 TRI_GROUP_STAGE_BANDS = 0x2
 TRI_GROUP_PACK_BGR24 = 0x4
+TRI_XFER_ID_BYTES = 128
+
+
+class TriXferConfig(C.Structure):
+    _fields_ = [("width", C.c_uint32), ("band_y", C.POINTER(C.c_uint32)), ("display", C.c_uint32),
+                ("format", C.c_uint32), ("slot_bytes", C.c_uint32), ("alpha", C.c_uint32), ("nbuf", C.c_uint32)]
 TRI_GROUP_FMT_BGRA32, TRI_GROUP_FMT_BGR24, TRI_GROUP_FMT_DBP = 0, 1, 2
 
 for _s, _n in ((TriImage, 32), (TriGroupConfig, 32), (TriVertex, 100), (TriPushConstant, 128), (TriDraw, 144), (TriGlobalUbo, 480), (TriMaterialRecord, 32),
@@ -235,6 +241,16 @@ CABI_FUNCTIONS = [
     ("tri_dbp_pack", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("tri_dbp_unpack", C.c_int, [C.c_void_p, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("tri_dbp_bytes", C.c_uint64, [C.c_uint64, C.c_uint32]),
+    ("tri_xfer_unique_id", C.c_int, [C.c_void_p]),
+    ("tri_xfer_comm_create", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int32, C.POINTER(C.c_void_p)]),
+    ("tri_xfer_comm_destroy", C.c_int, [C.c_void_p]),
+    ("tri_xfer_create", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("tri_xfer_destroy", C.c_int, [C.c_void_p]),
+    ("tri_xfer_bind_slot", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
+    ("tri_xfer_frame", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                 C.c_uint32, C.c_uint32]),
+    ("tri_xfer_synchronize", C.c_int, [C.c_void_p]),
+    ("tri_xfer_info", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
     ("tri_dbp_unpack_bands", C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_uint32,
                                        C.c_uint32, C.c_uint32, C.c_void_p]),
     ("tri_set_timing", C.c_int, [C.c_void_p, C.c_int]),

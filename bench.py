@@ -456,6 +456,34 @@ class GatherRing:
         return self.frames[(self.k - 1) % self.nbuf]
 
 
+_XFER_COMM = {}
+
+
+def xfer_comm(lib, world, rank, device_index, dev):
+    """The process's RCCL communicator for tri_xfer (the native band exchange), created once: rank 0 draws the
+    unique id, torch.distributed broadcasts its 128 bytes, and every rank joins (collective). Destroyed at exit."""
+    import atexit
+    import ctypes as C
+
+    import torch
+    import torch.distributed as dist
+    from trident_raster import raster
+
+    if "comm" in _XFER_COMM:
+        return _XFER_COMM["comm"]
+    uid = (C.c_uint8 * 128)()
+    if rank == 0:
+        raster._check(lib.tri_xfer_unique_id(uid))
+    t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
+    dist.broadcast(t, src=0)
+    uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+    comm = C.c_void_p()
+    raster._check(lib.tri_xfer_comm_create(uid, world, rank, device_index, C.byref(comm)))
+    _XFER_COMM["comm"] = comm
+    atexit.register(lambda: lib.tri_xfer_comm_destroy(comm))
+    return comm
+
+
 class BandRenderer:
     """One rank's share of a frame: rows [y0, y1) rendered into torch-owned device buffers, assembled
     by a GatherRing. `inflight` contexts take frames in turn, each on its own stream with its own work
@@ -464,7 +492,7 @@ class BandRenderer:
     (Renderer::DrawFrame waits on the fence of the frame in flight two frames back, Renderer.cpp:752-772)."""
 
     def __init__(self, scene, rank, world, device_index, band_world=None, assembly="gather", inflight=1,
-                 display_rows=None, pack="auto"):
+                 display_rows=None, pack="auto", exchange="native"):
         import ctypes as C
 
         import torch
@@ -521,8 +549,72 @@ class BandRenderer:
         self._draws, self._ndraws = abi.draws_array(scene.draws)
         self._band_ptrs = {b.data_ptr(): C.c_void_p(b.data_ptr()) for b in self.ring.bands}
         self._depth_ptrs = [C.c_void_p(d.data_ptr()) for d in self.depth]
+        # N > 1 gather on the GPU: the exchange runs natively (tri_xfer: one library call per frame renders the band
+        # and sends it, or receives and decodes every remote band, over an RCCL communicator of the library's own);
+        # torch.distributed's point-to-point calls cost the host ~20 us each (tools/p2p_host_cost.py), which at
+        # N = 8 would bind the display rank far below one GPU's frame rate. The GatherRing above stays the
+        # exchange for --exchange torch, the all-gather and the gloo tests.
+        self.xfer, self._kx = None, 0
+        if exchange == "native" and world > 1 and assembly == "gather" and self.dev.type == "cuda":
+            self._attach_xfer(device_index)
         self.frames = 0
         self.sim_step = None  # --sim-codec: the band codec's per-frame work, on the frame's stream
+
+    def _attach_xfer(self, device_index):
+        import ctypes as C
+
+        import torch
+        from trident_raster import abi
+
+        lib, W, H = self._lib, self.scene.width, self.scene.height
+        comm = xfer_comm(lib, self.world, self.rank, device_index, self.dev)
+        self.nbuf = max(self.inflight, 2)
+        n = H * W if self.rank == 0 else self.rows * W
+        self.xbufs = [torch.empty(n, dtype=torch.int32, device=self.dev) for _ in range(self.nbuf)]
+        fmt = {None: abi.TRI_GROUP_FMT_BGRA32, "bgr24": abi.TRI_GROUP_FMT_BGR24, "dbp": abi.TRI_GROUP_FMT_DBP}[
+            self.codec.mode if self.codec is not None else None]
+        band_y = (C.c_uint32 * (self.world + 1))(*([y0 for y0, _ in self.bands] + [H]))
+        cfg = abi.TriXferConfig(W, band_y, 0, fmt, self.codec.slot if fmt == abi.TRI_GROUP_FMT_DBP else 0,
+                                max(self.alpha, 0) if self.codec is not None else 0, self.nbuf)
+        x = C.c_void_p()
+        self._raster._check(lib.tri_xfer_create(comm, C.byref(cfg), C.byref(x)))
+        self.xfer = x
+        for s, b in enumerate(self.xbufs):
+            self._raster._check(lib.tri_xfer_bind_slot(x, s, C.c_void_p(b.data_ptr())))
+
+    def _xframe(self, i, exchange=1, render=True):
+        """One frame through tri_xfer on context i (render=False: the exchange alone)."""
+        slot = self._kx % self.nbuf
+        self._kx += 1
+        rc = self._lib.tri_xfer_frame(self.xfer, slot, self._ctxs[i] if render else None,
+                                      self._depth_ptrs[i] if render else None, self._ubo if render else None,
+                                      self._clear if render else None, self._draws if render else None,
+                                      self._ndraws, exchange)
+        if rc:
+            self._raster._check(rc)
+
+    def check(self):
+        """Every packed band kept the promised alpha and fitted its dbp slots (synchronising); raises if not."""
+        if self.xfer is not None:
+            self._raster._check(self._lib.tri_xfer_synchronize(self.xfer))
+        else:
+            self.ring.check()
+
+    def inbound_bytes(self):
+        """Bytes the display rank receives per frame (0 elsewhere)."""
+        if self.xfer is None:
+            return self.ring.inbound_bytes
+        import ctypes as C
+
+        sent, recv = C.c_uint64(), C.c_uint64()
+        self._raster._check(self._lib.tri_xfer_info(self.xfer, C.byref(sent), C.byref(recv), None))
+        return recv.value
+
+    def assembled_frame(self):
+        """The display rank's most recently assembled frame (int32[H * W], device), after a device synchronisation."""
+        if self.xfer is not None:
+            return self.xbufs[(self._kx - 1) % self.nbuf]
+        return self.ring.frame
 
     def probe_band(self):
         """One frame of this rank's band on context 0, into a scratch buffer (synchronised; no collective)."""
@@ -538,6 +630,9 @@ class BandRenderer:
         return band
 
     def _frame(self, i):
+        if self.xfer is not None:
+            self._xframe(i)
+            return
         lib, ctx = self._lib, self._ctxs[i]
         band = self.ring.acquire()
         rc = (lib.tri_bind_output(ctx, self._band_ptrs[band.data_ptr()], self._depth_ptrs[i]) or
@@ -554,8 +649,8 @@ class BandRenderer:
         """One frame, on the next context in turn (first_only: always context 0, no overlap)."""
         i = 0 if first_only else self.frames % self.inflight
         self.frames += 1
-        if self.world == 1 and self.inflight == 1 and self.sim_step is None:  # no collective, one stream: no torch stream context needed
-            self._frame(i)
+        if self.xfer is not None or (self.world == 1 and self.inflight == 1 and self.sim_step is None):
+            self._frame(i)  # no torch stream context needed (the native exchange orders its own streams)
             return
         import torch
 
@@ -572,11 +667,16 @@ class BandRenderer:
             r.synchronize()
 
     def close(self):
+        if self.xfer is not None:
+            self._lib.tri_xfer_destroy(self.xfer)
+            self.xfer = None
         for r in self.rs:
             r.close()
         self.geometry.close()
 
     def drain(self):
+        if self.xfer is not None:  # stream-ordered already: the caller's device synchronisation waits for it
+            return
         import torch
 
         with torch.cuda.stream(self.streams[0]):
@@ -597,6 +697,9 @@ class BandRenderer:
         t0 = time.perf_counter()
         for k in range(frames):
             i = k % self.inflight
+            if self.xfer is not None:
+                self._xframe(i, exchange=0)
+                continue
             lib, ctx = self._lib, self._ctxs[i]
             band = self.ring.bands[k % len(self.ring.bands)]
             with torch.cuda.stream(self.streams[i]):
@@ -616,6 +719,11 @@ class BandRenderer:
         self.drain()
         self._sync()
         t0 = time.perf_counter()
+        if self.xfer is not None:
+            for _ in range(frames):
+                self._xframe(0, exchange=1, render=False)
+            self._sync()
+            return (time.perf_counter() - t0) * 1e3 / frames
         with torch.cuda.stream(self.streams[0]):
             for _ in range(frames):
                 self.ring.acquire()
@@ -788,6 +896,34 @@ def autotune_split(make, height, world, dist_on, frames=80, rounds=2, warm_secon
         br.close()
     pick = max(range(len(cands)), key=lambda i: (best[i], -cands[i][0], -cands[i][1]))
     return cands[pick], [(d, k, f) for (d, k), f in zip(cands, best)]
+
+
+def verify_assembly(br, scene, dist_on):
+    """N > 1 parity in the bench itself: one frame through the band exchange, and on the display rank the assembled
+    frame against the same frame rendered whole by one context on that GPU (bit for bit: a band context's pixels are
+    the full frame's). Every rank learns the outcome (a max over ranks). Returns a dict for the
+    bench line's assembly object."""
+    import numpy as np
+    import torch
+    from trident_raster import raster, scenes
+
+    br.step()
+    br.drain()
+    torch.cuda.synchronize(br.dev)
+    br.check()
+    bad = 0.0
+    note = "not the display rank"
+    if br.rank == 0:
+        got = br.assembled_frame().cpu().numpy().view(np.uint8).reshape(scene.height, scene.width, 4)
+        with raster.TriRaster(scene.width, scene.height, device=br.dev.index) as r:
+            scenes.load_scene(r, scene)
+            r.render_frame()
+            want, _ = r.readback(depth=False)
+        diff = int((got != want).any(-1).sum())
+        bad = float(diff)
+        note = f"{diff} of {scene.width * scene.height} pixels differ from the one-context frame"
+    bad = max_over_ranks(bad, br.dev, dist_on)
+    return {"bit_exact": bad == 0.0, "detail": note}
 
 
 def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, warm_seconds=0.25):
@@ -1030,6 +1166,9 @@ def main():
     ap.add_argument("--pack", choices=("auto", "dbp", "bgr24", "off"), default="auto",
                     help="N > 1 gather: when tri_frame_alpha proves every alpha byte equal, bands travel in the delta "
                          "bit-plane format (auto, dbp) or as 3 bytes per pixel (bgr24); off: always 4 bytes")
+    ap.add_argument("--exchange", choices=("native", "torch"), default="native",
+                    help="N > 1 gather: the band exchange through the library's own RCCL communicator, one call per frame "
+                         "(native), or through torch.distributed point-to-point calls (torch)")
     ap.add_argument("--split", default="auto",
                     help="N > 1 gather: 'auto' (time candidate display-band sizes on the hardware, keep the fastest), "
                          "'equal', or the display rank's row count")
@@ -1060,7 +1199,7 @@ def main():
 
     def make_renderer(sc, display_rows=None, inflight=None):
         return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=inflight or inflight_for(sc),
-                            display_rows=display_rows, pack=args.pack)
+                            display_rows=display_rows, pack=args.pack, exchange=args.exchange)
 
     def choose_split(sc):
         """((display_rows or None, frames in flight), the autotune log) for a config at this world size."""
@@ -1082,6 +1221,23 @@ def main():
     else:
         (display_rows, inflight), split_log = choose_split(scene)
         br = make_renderer(scene, display_rows, inflight)
+    parity = None
+    if world > 1 and args.assembly == "gather":
+        # the assembled frame must equal the one-GPU frame; the native exchange falls back to torch.distributed's
+        # if it does not (or fails), and the line says so
+        try:
+            parity = verify_assembly(br, scene, dist_on)
+        except Exception as e:  # noqa: BLE001 - any failure of the native path is reported and replaced
+            parity = {"bit_exact": False, "detail": f"{type(e).__name__}: {str(e)[:200]}"}
+            max_over_ranks(1.0, br.dev, dist_on)  # the other ranks' outcome collective
+        if not parity["bit_exact"] and br.xfer is not None:
+            print(f"WARNING: native band exchange failed its parity check ({parity['detail']}); "
+                  "using torch.distributed", file=sys.stderr, flush=True)
+            br.close()
+            args.exchange = "torch"
+            br = make_renderer(scene, display_rows, inflight)
+            parity = verify_assembly(br, scene, dist_on)
+            parity["native_failed"] = True
     dt, timing, n_warm = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing,
                                    warm_seconds=args.warm_seconds)
     fps = args.steps / dt
@@ -1091,11 +1247,13 @@ def main():
     stage = stage_ms(timing)
     assembly = None
     if world > 1:  # what sets the rate: the slowest rank's render alone vs the assembly alone (outside the timed region)
-        br.ring.check()  # every packed band kept its alpha (lossless)
+        br.check()  # every packed band kept its alpha and fitted its slots (lossless)
         render_ms = max_over_ranks(br.render_only_ms(), br.dev, dist_on)
         asm_ms = max_over_ranks(br.assembly_only_ms(), br.dev, dist_on)
-        inbound = br.ring.inbound_bytes if rank == 0 else 0
+        inbound = br.inbound_bytes() if rank == 0 else 0
         assembly = {"render_ms": render_ms, "assembly_ms": asm_ms, "inbound_bytes_per_frame": inbound,
+                    "exchange": "native (tri_xfer)" if br.xfer is not None else "torch.distributed",
+                    "parity_vs_one_gpu_frame": parity,
                     "band_format": br.codec.mode if br.codec is not None else "bgra32",
                     "dbp_slot_bytes": br.codec.slot if br.codec is not None and br.codec.mode == "dbp" else None,
                     "band_bytes_per_pixel": (br.codec.bytes_for(br.rows * W) / (br.rows * W)

@@ -10,7 +10,7 @@ out=$PWD/3d-renderer_amd/lib/variants
 rm -rf $out/obj_$name
 mkdir -p $src/pkg/csrc $src/include $out/obj_$name
 units=""
-for f in raster_kernels.hip raster_plain.hip vertex_stage.hip tri_raster_capi.hip tri_group.hip band_codec.hip \
+for f in raster_kernels.hip raster_plain.hip vertex_stage.hip tri_raster_capi.hip tri_group.hip band_codec.hip tri_xfer.hip \
          raster_common.h raster_launch.h; do
   if git cat-file -e $rev:3d-renderer_amd/csrc/$f 2>/dev/null; then
     git show $rev:3d-renderer_amd/csrc/$f > $src/pkg/csrc/$f
