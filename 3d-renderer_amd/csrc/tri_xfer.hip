@@ -3,19 +3,20 @@
 // The torch.distributed route costs the host ≈ 20 µs per point-to-point operation (torch's P2POp / batch_isend_irecv
 // bookkeeping, measured on an MI355X with tools/p2p_host_cost.py: one send/receive pair 42 µs per frame, seven 218
 // µs), so a display rank that receives seven bands per frame would be host-bound far below one GPU's frame rate. This
-// file drives the same exchange natively: an RCCL communicator of its own (tri_xfer_comm, bootstrapped with a unique
-// id the caller broadcasts once), and one call per frame that renders the rank's band (tri_bind_output +
-// tri_set_frame + tri_set_draws + tri_render on the context's stream), then on a per-exchange stream packs and sends
-// it (a sender) or receives every remote band and decodes it into the frame (the display rank):
+// file drives the same exchange natively, one call per frame: render the rank's band (tri_bind_output +
+// tri_set_frame + tri_set_draws + tri_render on the context's stream), then on that same stream pack and send it (a
+// sender) or receive every remote band and decode it into the frame (the display rank):
 //
-//   context stream: [wait slot free] render ──event──┐
-//   exchange stream:                                   └─ pack ─ ncclSend                    (sender)
-//                                                      └─ ncclRecv × (N-1) ─ decode bands    (display)
-//                                                      ─ event "slot free"
+//   context stream of slot s:  [render frame k] ─ pack ─ ncclSend (comm s)                       (sender)
+//                              [render own band] ─ ncclRecv × (N-1) (comm s) ─ decode bands       (display)
 //
-// Slots: the caller's band (sender) or frame (display) buffers, one per frame in flight; frame k + nbuf renders into
-// the slot only after frame k's exchange has read it (a device-side wait, no host block). Band formats are
-// tri_group's (TRI_GROUP_FMT_*): the delta bit-plane stream with the slot size every rank agreed, 3-byte pixels, or 4.
+// Each slot (one per frame in flight) has its own RCCL communicator (tri_xfer_comm, bootstrapped from a unique id
+// the caller broadcasts once), so every communicator's operations stay on one stream and frame k + nbuf, which
+// reuses the slot's buffers on the same stream, is ordered behind frame k's transfer with no event: HIP event
+// record/wait calls cost the host ≈ 2 µs each (tools/xfer_host_cost.py: a fenced version of this call took 26.8 µs
+// against 16 µs for the render alone). If a slot changes streams (a different context), it is fenced with events.
+// Band formats are tri_group's (TRI_GROUP_FMT_*): the delta bit-plane stream with the slot size every rank agreed,
+// 3-byte pixels, or 4.
 #include "raster_launch.h"
 
 #include <hip/hip_runtime.h>
@@ -35,15 +36,17 @@ struct tri_xfer_comm {
 };
 
 struct tri_xfer {
-    tri_xfer_comm* xc = nullptr;
+    std::vector<tri_xfer_comm*> xc;          // slot s uses xc[s % xc.size()]
+    int32_t device = 0;
+    uint32_t world = 1, rank = 0;
     uint32_t W = 0, display = 0, fmt = TRI_GROUP_FMT_BGRA32, slot_bytes = 0, alpha = 0, nbuf = 0;
     std::vector<uint32_t> y;                 // world + 1 row boundaries
-    hipStream_t xs = nullptr;                // the exchange stream
+    hipStream_t own = nullptr;               // exchange-only frames of a slot that never rendered
     std::vector<uint32_t*> pixels;           // per slot: this rank's band (sender) or the frame (display)
     std::vector<uint8_t*> stage;             // per slot: the sender's packed band
     std::vector<std::vector<uint8_t*>> rx;   // per slot, per rank: the display's received packed bands
-    std::vector<hipEvent_t> rendered, freed; // per slot
-    std::vector<bool> armed;
+    std::vector<hipStream_t> stream;         // per slot: the stream its last frame ran on
+    std::vector<hipEvent_t> freed;           // per slot: fences a change of stream
     uint32_t* flags = nullptr;               // the packer's [sticky flags, largest dbp slot]
 };
 
@@ -117,27 +120,31 @@ int tri_xfer_comm_destroy(tri_xfer_comm* xc) {
 
 int tri_xfer_destroy(tri_xfer* x) {
     if (!x) return TRI_OK;
-    (void)hipSetDevice(x->xc->device);
-    if (x->xs) (void)hipStreamSynchronize(x->xs);
+    (void)hipSetDevice(x->device);
+    for (hipStream_t st : x->stream)
+        if (st) (void)hipStreamSynchronize(st);
     for (uint8_t* p : x->stage)
         if (p) (void)hipFree(p);
     for (auto& v : x->rx)
         for (uint8_t* p : v)
             if (p) (void)hipFree(p);
-    for (hipEvent_t e : x->rendered)
-        if (e) (void)hipEventDestroy(e);
     for (hipEvent_t e : x->freed)
         if (e) (void)hipEventDestroy(e);
     if (x->flags) (void)hipFree(x->flags);
-    if (x->xs) (void)hipStreamDestroy(x->xs);
+    if (x->own) (void)hipStreamDestroy(x->own);
     delete x;
     return TRI_OK;
 }
 
-int tri_xfer_create(tri_xfer_comm* xc, const tri_xfer_config* cfg, tri_xfer** out) {
-    if (!xc || !cfg || !out || !cfg->band_y) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: null argument");
+int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_config* cfg, tri_xfer** out) {
+    if (!comms || ncomm == 0 || !cfg || !out || !cfg->band_y)
+        return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: null argument");
     *out = nullptr;
-    const uint32_t N = xc->world;
+    for (uint32_t i = 0; i < ncomm; ++i)
+        if (!comms[i] || comms[i]->world != comms[0]->world || comms[i]->rank != comms[0]->rank ||
+            comms[i]->device != comms[0]->device)
+            return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: the communicators differ in world, rank or device");
+    const uint32_t N = comms[0]->world;
     if (cfg->display >= N || cfg->nbuf == 0 || cfg->width == 0 || cfg->alpha > 255u ||
         cfg->format > TRI_GROUP_FMT_DBP ||
         (cfg->format == TRI_GROUP_FMT_DBP && (cfg->slot_bytes < TRI_DBP_MIN_SLOT || cfg->slot_bytes % 16u)))
@@ -145,9 +152,12 @@ int tri_xfer_create(tri_xfer_comm* xc, const tri_xfer_config* cfg, tri_xfer** ou
     for (uint32_t r = 0; r < N; ++r)
         if (cfg->band_y[r + 1] <= cfg->band_y[r])
             return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: every band needs at least one row");
-    XH(hipSetDevice(xc->device));
+    XH(hipSetDevice(comms[0]->device));
     tri_xfer* x = new tri_xfer();
-    x->xc = xc;
+    x->xc.assign(comms, comms + ncomm);
+    x->device = comms[0]->device;
+    x->world = N;
+    x->rank = comms[0]->rank;
     x->W = cfg->width;
     x->display = cfg->display;
     x->fmt = cfg->format;
@@ -160,18 +170,16 @@ int tri_xfer_create(tri_xfer_comm* xc, const tri_xfer_config* cfg, tri_xfer** ou
     x->pixels.assign(x->nbuf, nullptr);
     x->stage.assign(x->nbuf, nullptr);
     x->rx.assign(x->nbuf, std::vector<uint8_t*>(N, nullptr));
-    x->rendered.assign(x->nbuf, nullptr);
+    x->stream.assign(x->nbuf, nullptr);
     x->freed.assign(x->nbuf, nullptr);
-    x->armed.assign(x->nbuf, false);
-    if (hipStreamCreateWithFlags(&x->xs, hipStreamNonBlocking) != hipSuccess)
+    if (hipStreamCreateWithFlags(&x->own, hipStreamNonBlocking) != hipSuccess)
         return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: stream creation failed"));
     for (uint32_t s = 0; s < x->nbuf; ++s) {
-        if (hipEventCreateWithFlags(&x->rendered[s], hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&x->freed[s], hipEventDisableTiming) != hipSuccess)
+        if (hipEventCreateWithFlags(&x->freed[s], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: event creation failed"));
         if (!packed || N == 1) continue;
-        if (xc->rank != x->display) {
-            if (hipMalloc(&x->stage[s], band_bytes(x, xc->rank)) != hipSuccess)
+        if (x->rank != x->display) {
+            if (hipMalloc(&x->stage[s], band_bytes(x, x->rank)) != hipSuccess)
                 return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: staging allocation failed"));
         } else {
             for (uint32_t r = 0; r < N; ++r)
@@ -179,8 +187,8 @@ int tri_xfer_create(tri_xfer_comm* xc, const tri_xfer_config* cfg, tri_xfer** ou
                     return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: receive allocation failed"));
         }
     }
-    if (hipMalloc(&x->flags, 8) != hipSuccess || hipMemsetAsync(x->flags, 0, 8, x->xs) != hipSuccess ||
-        hipStreamSynchronize(x->xs) != hipSuccess)
+    if (hipMalloc(&x->flags, 8) != hipSuccess || hipMemsetAsync(x->flags, 0, 8, x->own) != hipSuccess ||
+        hipStreamSynchronize(x->own) != hipSuccess)
         return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: flag allocation failed"));
     *out = x;
     return TRI_OK;
@@ -196,76 +204,77 @@ int tri_xfer_bind_slot(tri_xfer* x, uint32_t slot, void* pixels) {
 int tri_xfer_frame(tri_xfer* x, uint32_t slot, tri_ctx* ctx, void* depth, const tri_global_ubo* ubo,
                    const float clear[4], const tri_draw* draws, uint32_t draw_count, uint32_t exchange) {
     if (!x || slot >= x->nbuf || !x->pixels[slot]) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_frame: bad slot");
-    const tri_xfer_comm* xc = x->xc;
-    const uint32_t me = xc->rank;
+    const uint32_t me = x->rank, N = x->world;
     const bool disp = me == x->display;
-    XH(hipSetDevice(xc->device));
+    XH(hipSetDevice(x->device));
     uint32_t* frame = x->pixels[slot];  // the band (sender) or the frame (display)
+    // the slot's stream: its context's (render and transfer in one stream order), else the last one it ran on
+    hipStream_t s = ctx ? tri_internal_stream(ctx) : (x->stream[slot] ? x->stream[slot] : x->own);
+    if (x->stream[slot] && x->stream[slot] != s) {  // the slot moves to another stream: fence its last frame
+        XH(hipEventRecord(x->freed[slot], x->stream[slot]));
+        XH(hipStreamWaitEvent(s, x->freed[slot], 0));
+    }
+    x->stream[slot] = s;
     if (ctx) {
-        hipStream_t s = tri_internal_stream(ctx);
-        if (x->armed[slot]) XH(hipStreamWaitEvent(s, x->freed[slot], 0));  // frame k - nbuf's exchange read it
         uint32_t* out = disp ? frame + (size_t)x->y[me] * x->W : frame;
         int rc = tri_bind_output(ctx, out, depth);
         if (!rc && ubo) rc = tri_set_frame(ctx, ubo, clear);
         if (!rc && draws) rc = tri_set_draws(ctx, draws, draw_count);
         if (!rc) rc = tri_render(ctx);
         if (rc) return rc;
-        XH(hipEventRecord(x->rendered[slot], s));
-        XH(hipStreamWaitEvent(x->xs, x->rendered[slot], 0));
     }
-    const uint32_t N = xc->world;
-    if (exchange && N > 1) {
-        if (!disp) {
-            const void* src = frame;
-            const uint64_t px = band_pixels(x, me);
-            if (x->fmt == TRI_GROUP_FMT_DBP) {
-                XH(tri_launch_dbp_pack(frame, px, x->alpha, x->stage[slot], x->slot_bytes, x->flags, x->xs));
-                src = x->stage[slot];
-            } else if (x->fmt == TRI_GROUP_FMT_BGR24) {
-                XH(tri_launch_pack_bgr24(frame, x->stage[slot], px, x->alpha, x->flags, x->xs));
-                src = x->stage[slot];
-            }
-            XN(ncclSend(src, band_bytes(x, me), ncclUint8, (int)x->display, xc->comm, x->xs));
-        } else {
-            XN(ncclGroupStart());
-            for (uint32_t r = 0; r < N; ++r) {
-                if (r == me) continue;
-                void* to = x->fmt == TRI_GROUP_FMT_BGRA32 ? static_cast<void*>(frame + (size_t)x->y[r] * x->W)
-                                                          : static_cast<void*>(x->rx[slot][r]);
-                XN(ncclRecv(to, band_bytes(x, r), ncclUint8, (int)r, xc->comm, x->xs));
-            }
-            XN(ncclGroupEnd());
-            if (x->fmt == TRI_GROUP_FMT_DBP) {  // every remote band in one launch (up to TRI_DBP_MAX_BANDS)
-                std::vector<const uint8_t*> from;
-                std::vector<uint32_t*> to;
-                std::vector<uint64_t> npx;
-                for (uint32_t r = 0; r < N; ++r)
-                    if (r != me) {
-                        from.push_back(x->rx[slot][r]);
-                        to.push_back(frame + (size_t)x->y[r] * x->W);
-                        npx.push_back(band_pixels(x, r));
-                    }
-                for (size_t k = 0; k < from.size(); k += TRI_DBP_MAX_BANDS)
-                    XH(tri_launch_dbp_unpack_bands(from.data() + k, to.data() + k, npx.data() + k,
-                                                   (uint32_t)std::min<size_t>(TRI_DBP_MAX_BANDS, from.size() - k), x->alpha,
-                                                   x->slot_bytes, x->xs));
-            } else if (x->fmt == TRI_GROUP_FMT_BGR24) {
-                for (uint32_t r = 0; r < N; ++r)
-                    if (r != me)
-                        XH(tri_launch_unpack_bgr24(x->rx[slot][r], frame + (size_t)x->y[r] * x->W, band_pixels(x, r),
-                                                   x->alpha, x->xs));
+    if (!exchange || N == 1) return TRI_OK;
+    ncclComm_t comm = x->xc[slot % x->xc.size()]->comm;
+    if (!disp) {
+        const void* src = frame;
+        const uint64_t px = band_pixels(x, me);
+        if (x->fmt == TRI_GROUP_FMT_DBP) {
+            XH(tri_launch_dbp_pack(frame, px, x->alpha, x->stage[slot], x->slot_bytes, x->flags, s));
+            src = x->stage[slot];
+        } else if (x->fmt == TRI_GROUP_FMT_BGR24) {
+            XH(tri_launch_pack_bgr24(frame, x->stage[slot], px, x->alpha, x->flags, s));
+            src = x->stage[slot];
+        }
+        XN(ncclSend(src, band_bytes(x, me), ncclUint8, (int)x->display, comm, s));
+        return TRI_OK;
+    }
+    XN(ncclGroupStart());
+    for (uint32_t r = 0; r < N; ++r) {
+        if (r == me) continue;
+        void* to = x->fmt == TRI_GROUP_FMT_BGRA32 ? static_cast<void*>(frame + (size_t)x->y[r] * x->W)
+                                                  : static_cast<void*>(x->rx[slot][r]);
+        XN(ncclRecv(to, band_bytes(x, r), ncclUint8, (int)r, comm, s));
+    }
+    XN(ncclGroupEnd());
+    if (x->fmt == TRI_GROUP_FMT_DBP) {  // every remote band in one launch (up to TRI_DBP_MAX_BANDS)
+        const uint8_t* from[TRI_DBP_MAX_BANDS];
+        uint32_t* to[TRI_DBP_MAX_BANDS];
+        uint64_t npx[TRI_DBP_MAX_BANDS];
+        uint32_t k = 0;
+        for (uint32_t r = 0; r < N; ++r) {
+            if (r == me) continue;
+            from[k] = x->rx[slot][r];
+            to[k] = frame + (size_t)x->y[r] * x->W;
+            npx[k] = band_pixels(x, r);
+            if (++k == TRI_DBP_MAX_BANDS) {
+                XH(tri_launch_dbp_unpack_bands(from, to, npx, k, x->alpha, x->slot_bytes, s));
+                k = 0;
             }
         }
+        if (k) XH(tri_launch_dbp_unpack_bands(from, to, npx, k, x->alpha, x->slot_bytes, s));
+    } else if (x->fmt == TRI_GROUP_FMT_BGR24) {
+        for (uint32_t r = 0; r < N; ++r)
+            if (r != me)
+                XH(tri_launch_unpack_bgr24(x->rx[slot][r], frame + (size_t)x->y[r] * x->W, band_pixels(x, r), x->alpha, s));
     }
-    XH(hipEventRecord(x->freed[slot], x->xs));
-    x->armed[slot] = true;
     return TRI_OK;
 }
 
 int tri_xfer_synchronize(tri_xfer* x) {
     if (!x) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_synchronize: null exchange");
-    XH(hipSetDevice(x->xc->device));
-    XH(hipStreamSynchronize(x->xs));
+    XH(hipSetDevice(x->device));
+    for (hipStream_t st : x->stream)
+        if (st) XH(hipStreamSynchronize(st));
     uint32_t f[2] = {0, 0};
     XH(hipMemcpy(f, x->flags, 8, hipMemcpyDeviceToHost));
     if (f[0] & 1u) return tri_internal_fail(TRI_E_STATE, "tri_xfer: a band's alpha was not the proven value (lossy packed transfer)");
@@ -275,7 +284,7 @@ int tri_xfer_synchronize(tri_xfer* x) {
 
 int tri_xfer_info(tri_xfer* x, uint64_t* sent_bytes, uint64_t* received_bytes, uint32_t* max_slot_bytes) {
     if (!x || !sent_bytes || !received_bytes) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_info: null argument");
-    const uint32_t N = x->xc->world, me = x->xc->rank;
+    const uint32_t N = x->world, me = x->rank;
     *sent_bytes = (N > 1 && me != x->display) ? band_bytes(x, me) : 0u;
     uint64_t in = 0;
     if (N > 1 && me == x->display)
@@ -283,9 +292,9 @@ int tri_xfer_info(tri_xfer* x, uint64_t* sent_bytes, uint64_t* received_bytes, u
             if (r != me) in += band_bytes(x, r);
     *received_bytes = in;
     if (max_slot_bytes) {
+        const int rc = tri_xfer_synchronize(x);
+        if (rc && rc != TRI_E_STATE && rc != TRI_E_OVERFLOW) return rc;
         uint32_t f[2] = {0, 0};
-        XH(hipSetDevice(x->xc->device));
-        XH(hipStreamSynchronize(x->xs));
         XH(hipMemcpy(f, x->flags, 8, hipMemcpyDeviceToHost));
         *max_slot_bytes = f[1];
     }

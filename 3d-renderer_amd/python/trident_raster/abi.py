@@ -244,7 +244,7 @@ CABI_FUNCTIONS = [
     ("tri_xfer_unique_id", C.c_int, [C.c_void_p]),
     ("tri_xfer_comm_create", C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int32, C.POINTER(C.c_void_p)]),
     ("tri_xfer_comm_destroy", C.c_int, [C.c_void_p]),
-    ("tri_xfer_create", C.c_int, [C.c_void_p, C.c_void_p, C.POINTER(C.c_void_p)]),
+    ("tri_xfer_create", C.c_int, [C.POINTER(C.c_void_p), C.c_uint32, C.c_void_p, C.POINTER(C.c_void_p)]),
     ("tri_xfer_destroy", C.c_int, [C.c_void_p]),
     ("tri_xfer_bind_slot", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     ("tri_xfer_frame", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,

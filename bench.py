@@ -456,12 +456,13 @@ class GatherRing:
         return self.frames[(self.k - 1) % self.nbuf]
 
 
-_XFER_COMM = {}
+_XFER_COMMS = []
+XFER_COMMS = 3  # one RCCL communicator per frame in flight (the most the bench uses), each used on one stream
 
 
-def xfer_comm(lib, world, rank, device_index, dev):
-    """The process's RCCL communicator for tri_xfer (the native band exchange), created once: rank 0 draws the
-    unique id, torch.distributed broadcasts its 128 bytes, and every rank joins (collective). Destroyed at exit."""
+def xfer_comms(lib, world, rank, device_index, dev):
+    """The process's RCCL communicators for tri_xfer (the native band exchange), created once: for each, rank 0 draws
+    a unique id, torch.distributed broadcasts its 128 bytes, and every rank joins (collective). Destroyed at exit."""
     import atexit
     import ctypes as C
 
@@ -469,19 +470,20 @@ def xfer_comm(lib, world, rank, device_index, dev):
     import torch.distributed as dist
     from trident_raster import raster
 
-    if "comm" in _XFER_COMM:
-        return _XFER_COMM["comm"]
-    uid = (C.c_uint8 * 128)()
-    if rank == 0:
-        raster._check(lib.tri_xfer_unique_id(uid))
-    t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
-    dist.broadcast(t, src=0)
-    uid = (C.c_uint8 * 128)(*t.cpu().tolist())
-    comm = C.c_void_p()
-    raster._check(lib.tri_xfer_comm_create(uid, world, rank, device_index, C.byref(comm)))
-    _XFER_COMM["comm"] = comm
-    atexit.register(lambda: lib.tri_xfer_comm_destroy(comm))
-    return comm
+    if _XFER_COMMS:
+        return _XFER_COMMS
+    for _ in range(XFER_COMMS):
+        uid = (C.c_uint8 * 128)()
+        if rank == 0:
+            raster._check(lib.tri_xfer_unique_id(uid))
+        t = torch.tensor(list(bytes(uid)), dtype=torch.uint8, device=dev)
+        dist.broadcast(t, src=0)
+        uid = (C.c_uint8 * 128)(*t.cpu().tolist())
+        comm = C.c_void_p()
+        raster._check(lib.tri_xfer_comm_create(uid, world, rank, device_index, C.byref(comm)))
+        _XFER_COMMS.append(comm)
+    atexit.register(lambda: [lib.tri_xfer_comm_destroy(c) for c in _XFER_COMMS])
+    return _XFER_COMMS
 
 
 class BandRenderer:
@@ -567,8 +569,8 @@ class BandRenderer:
         from trident_raster import abi
 
         lib, W, H = self._lib, self.scene.width, self.scene.height
-        comm = xfer_comm(lib, self.world, self.rank, device_index, self.dev)
-        self.nbuf = max(self.inflight, 2)
+        comms = xfer_comms(lib, self.world, self.rank, device_index, self.dev)
+        self.nbuf = self.inflight  # slot i belongs to context i: its frames render and transfer on one stream
         n = H * W if self.rank == 0 else self.rows * W
         self.xbufs = [torch.empty(n, dtype=torch.int32, device=self.dev) for _ in range(self.nbuf)]
         fmt = {None: abi.TRI_GROUP_FMT_BGRA32, "bgr24": abi.TRI_GROUP_FMT_BGR24, "dbp": abi.TRI_GROUP_FMT_DBP}[
@@ -577,15 +579,16 @@ class BandRenderer:
         cfg = abi.TriXferConfig(W, band_y, 0, fmt, self.codec.slot if fmt == abi.TRI_GROUP_FMT_DBP else 0,
                                 max(self.alpha, 0) if self.codec is not None else 0, self.nbuf)
         x = C.c_void_p()
-        self._raster._check(lib.tri_xfer_create(comm, C.byref(cfg), C.byref(x)))
+        carr = (C.c_void_p * len(comms))(*[c.value for c in comms])
+        self._raster._check(lib.tri_xfer_create(carr, len(comms), C.byref(cfg), C.byref(x)))
         self.xfer = x
         for s, b in enumerate(self.xbufs):
             self._raster._check(lib.tri_xfer_bind_slot(x, s, C.c_void_p(b.data_ptr())))
 
     def _xframe(self, i, exchange=1, render=True):
-        """One frame through tri_xfer on context i (render=False: the exchange alone)."""
-        slot = self._kx % self.nbuf
-        self._kx += 1
+        """One frame through tri_xfer on context i, into its slot i (render=False: the exchange alone)."""
+        slot = i % self.nbuf
+        self._kx = slot
         rc = self._lib.tri_xfer_frame(self.xfer, slot, self._ctxs[i] if render else None,
                                       self._depth_ptrs[i] if render else None, self._ubo if render else None,
                                       self._clear if render else None, self._draws if render else None,
@@ -613,7 +616,7 @@ class BandRenderer:
     def assembled_frame(self):
         """The display rank's most recently assembled frame (int32[H * W], device), after a device synchronisation."""
         if self.xfer is not None:
-            return self.xbufs[(self._kx - 1) % self.nbuf]
+            return self.xbufs[self._kx]
         return self.ring.frame
 
     def probe_band(self):
@@ -720,8 +723,8 @@ class BandRenderer:
         self._sync()
         t0 = time.perf_counter()
         if self.xfer is not None:
-            for _ in range(frames):
-                self._xframe(0, exchange=1, render=False)
+            for k in range(frames):
+                self._xframe(k % self.inflight, exchange=1, render=False)
             self._sync()
             return (time.perf_counter() - t0) * 1e3 / frames
         with torch.cuda.stream(self.streams[0]):

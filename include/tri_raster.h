@@ -347,13 +347,13 @@ int tri_dbp_unpack_bands(const void* const* streams_in, void* const* bgra8, cons
 
 /* ---- one rank's band exchange (process per GPU) --------------------------------------------- */
 /* A process-per-GPU caller (bench.py at N > 1) renders one row band per rank and assembles the frame on the
- * display rank. tri_xfer drives that exchange natively over an RCCL communicator of its own: one call per frame
- * renders the band on the context's stream, then packs and sends it (a sender) or receives and decodes every remote
- * band into the frame (the display rank) on the exchange's own stream — no per-operation host bookkeeping in the
- * caller (torch.distributed's point-to-point calls cost ≈ 20 µs of host time each). Bootstrap: rank 0 calls
- * tri_xfer_unique_id and the caller broadcasts the TRI_XFER_ID_BYTES bytes (e.g. over torch.distributed); every
- * rank then calls tri_xfer_comm_create (collective). One communicator serves any number of exchanges used one at a
- * time. */
+ * display rank. tri_xfer drives that exchange natively over RCCL communicators of its own: one call per frame
+ * renders the band on the context's stream, then on the same stream packs and sends it (a sender) or receives and
+ * decodes every remote band into the frame (the display rank) — no per-operation host bookkeeping in the
+ * caller (torch.distributed's point-to-point calls cost ≈ 20 µs of host time each). Bootstrap, once per
+ * communicator: rank 0 calls tri_xfer_unique_id and the caller broadcasts the TRI_XFER_ID_BYTES bytes (e.g. over
+ * torch.distributed); every rank then calls tri_xfer_comm_create (collective). Communicators serve any number of
+ * exchanges used one at a time. */
 #define TRI_XFER_ID_BYTES 128u
 typedef struct tri_xfer_comm tri_xfer_comm;
 typedef struct tri_xfer tri_xfer;
@@ -369,19 +369,22 @@ typedef struct tri_xfer_config {
 int tri_xfer_unique_id(uint8_t* id_out);
 int tri_xfer_comm_create(const uint8_t* id, uint32_t world, uint32_t rank, int32_t device, tri_xfer_comm** out);
 int tri_xfer_comm_destroy(tri_xfer_comm* comm);
-int tri_xfer_create(tri_xfer_comm* comm, const tri_xfer_config* config, tri_xfer** out);
+/* comms: one communicator per slot in flight (slot s uses comms[s % comm_count]; each created with the same world,
+ * rank and device), so that each one's operations stay on one stream (the slot's context stream). */
+int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t comm_count, const tri_xfer_config* config, tri_xfer** out);
 int tri_xfer_destroy(tri_xfer* xfer);
 /* Slot `slot`'s pixel buffer (device, 4-B aligned, caller-owned): this rank's band (a sender) or the whole
  * width × height frame (the display rank, which renders its own band in place at its row offset). */
 int tri_xfer_bind_slot(tri_xfer* xfer, uint32_t slot, void* bgra8);
 /* One frame into slot `slot`: if ctx is not NULL, bind it to the slot (and `depth`, may be NULL), apply the frame
  * state when given (ubo / draws not NULL: tri_set_frame / tri_set_draws) and tri_render; then, if `exchange`, the
- * band's transfer. Frame k + nbuf waits on the device for frame k's transfer before it writes the slot. Every rank
- * must call it with exchange set the same number of times (the transfers match in order). */
+ * band's transfer, on the same stream (the context's; ctx NULL: the slot's last stream). A slot reused on its
+ * stream is ordered behind its previous transfer by stream order; a slot that changes stream is fenced. Every rank
+ * must make the same sequence of exchanging calls per slot (the transfers match in order per communicator). */
 int tri_xfer_frame(tri_xfer* xfer, uint32_t slot, tri_ctx* ctx, void* depth, const tri_global_ubo* ubo,
                    const float clear_rgba[4], const tri_draw* draws, uint32_t draw_count, uint32_t exchange);
-/* Wait for the exchange stream; TRI_E_STATE if a packed band's alpha differed, TRI_E_OVERFLOW if a band outgrew the
- * agreed dbp slot (both lossy). */
+/* Wait for every slot's stream; TRI_E_STATE if a packed band's alpha differed, TRI_E_OVERFLOW if a band outgrew
+ * the agreed dbp slot (both lossy). */
 int tri_xfer_synchronize(tri_xfer* xfer);
 /* Bytes this rank sends and receives per frame; max_slot_bytes (may be NULL; synchronising): the largest dbp slot
  * this rank's packs needed. */

@@ -33,7 +33,7 @@ def _xfer(lib, comm, W, H, fmt, nbuf=2, slot=8192):
     band_y = (C.c_uint32 * 2)(0, H)
     cfg = abi.TriXferConfig(W, band_y, 0, fmt, slot if fmt == abi.TRI_GROUP_FMT_DBP else 0, 255, nbuf)
     x = C.c_void_p()
-    raster._check(lib.tri_xfer_create(comm, C.byref(cfg), C.byref(x)))
+    raster._check(lib.tri_xfer_create((C.c_void_p * 1)(comm.value), 1, C.byref(cfg), C.byref(x)))
     return x
 
 
@@ -69,7 +69,15 @@ def test_xfer_frames_match_the_plain_render(comm, fmt):
             # an exchange-only frame (no context) and a render-only frame are accepted too
             raster._check(lib.tri_xfer_frame(x, 0, None, None, None, None, None, 0, 1))
             raster._check(lib.tri_xfer_frame(x, 1, r._ctx, None, None, None, None, 0, 0))
-            raster._check(lib.tri_xfer_synchronize(x))
+            # slot 0 moves to another context's stream (fenced behind its last frame) and renders the same pixels
+            with raster.TriRaster(W, H) as r2:
+                scenes.load_scene(r2, s)
+                bufs[0].zero_()
+                torch.cuda.synchronize()
+                raster._check(lib.tri_xfer_frame(x, 0, r2._ctx, None, None, None, None, 0, 1))
+                raster._check(lib.tri_xfer_synchronize(x))
+                torch.cuda.synchronize()
+                assert np.array_equal(bufs[0].cpu().numpy().view(np.uint8).reshape(H, W, 4), want)
         finally:
             lib.tri_xfer_destroy(x)
 
@@ -81,12 +89,12 @@ def test_xfer_rejects_bad_arguments(comm):
     band_y = (C.c_uint32 * 2)(0, 16)
     x = C.c_void_p()
     bad = abi.TriXferConfig(64, band_y, 1, 0, 0, 255, 2)  # display rank outside the world
-    assert lib.tri_xfer_create(c, C.byref(bad), C.byref(x)) == abi.TRI_E_INVALID
+    assert lib.tri_xfer_create((C.c_void_p * 1)(c.value), 1, C.byref(bad), C.byref(x)) == abi.TRI_E_INVALID
     bad = abi.TriXferConfig(64, band_y, 0, abi.TRI_GROUP_FMT_DBP, 100, 255, 2)  # slot below the minimum
-    assert lib.tri_xfer_create(c, C.byref(bad), C.byref(x)) == abi.TRI_E_INVALID
+    assert lib.tri_xfer_create((C.c_void_p * 1)(c.value), 1, C.byref(bad), C.byref(x)) == abi.TRI_E_INVALID
     empty = (C.c_uint32 * 2)(5, 5)  # a band without rows
     bad = abi.TriXferConfig(64, empty, 0, 0, 0, 255, 2)
-    assert lib.tri_xfer_create(c, C.byref(bad), C.byref(x)) == abi.TRI_E_INVALID
+    assert lib.tri_xfer_create((C.c_void_p * 1)(c.value), 1, C.byref(bad), C.byref(x)) == abi.TRI_E_INVALID
     x = _xfer(lib, c, 64, 16, 0)
     try:
         assert lib.tri_xfer_frame(x, 0, None, None, None, None, None, 0, 1) == abi.TRI_E_INVALID  # slot not bound

@@ -35,7 +35,7 @@ def main(frames=3000):
     band_y = (C.c_uint32 * 2)(0, rows)
     cfg = abi.TriXferConfig(W, band_y, 0, abi.TRI_GROUP_FMT_DBP, 6400, 255, 3)
     x = C.c_void_p()
-    raster._check(lib.tri_xfer_create(comm, C.byref(cfg), C.byref(x)))
+    raster._check(lib.tri_xfer_create((C.c_void_p * 1)(comm.value), 1, C.byref(cfg), C.byref(x)))
     bufs = [torch.empty(rows * W, dtype=torch.int32, device="cuda:0") for _ in range(3)]
     for k, b in enumerate(bufs):
         raster._check(lib.tri_xfer_bind_slot(x, k, C.c_void_p(b.data_ptr())))
