@@ -974,10 +974,21 @@ struct BinBox {
     uint32_t box[2][2][4];  // per queue set and round parity: min bx, min by, ~max bx, ~max by (LDS atomicMin)
 };
 
+// The wave's minimum (uniform), as a DPP scan: row_shr 1/2/4/8 inside each row of 16, then row_bcast:15 / :31
+// across rows; lane 63 ends with the minimum of all lanes. Lanes whose DPP source is out of range keep ~0 (the
+// identity), so each step is one v_min with a DPP operand instead of a ds_bpermute round trip per step.
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_max_id(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)~0u, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
-    return v;
+    v = min(v, dpp_max_id<0x111>(v));
+    v = min(v, dpp_max_id<0x112>(v));
+    v = min(v, dpp_max_id<0x114>(v));
+    v = min(v, dpp_max_id<0x118>(v));
+    v = min(v, dpp_max_id<0x142, 0xa>(v));
+    v = min(v, dpp_max_id<0x143, 0xc>(v));
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
 }
 
 #ifndef TRI_SETUP_GROUP
