@@ -981,6 +981,20 @@ template <int CTRL, int ROW_MASK = 0xf>
 __device__ __forceinline__ uint32_t dpp_max_id(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)~0u, (int)v, CTRL, ROW_MASK, 0xf, false);
 }
+template <int CTRL, int ROW_MASK = 0xf>
+__device__ __forceinline__ uint32_t dpp_zero_id(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xf, false);
+}
+// Inclusive prefix sum over the wave's lanes, the same DPP scan (out-of-range sources add 0)
+__device__ __forceinline__ uint32_t wave_incl_sum(uint32_t v) {
+    v += dpp_zero_id<0x111>(v);
+    v += dpp_zero_id<0x112>(v);
+    v += dpp_zero_id<0x114>(v);
+    v += dpp_zero_id<0x118>(v);
+    v += dpp_zero_id<0x142, 0xa>(v);
+    v += dpp_zero_id<0x143, 0xc>(v);
+    return v;
+}
 __device__ __forceinline__ uint32_t wave_min(uint32_t v) {
     v = min(v, dpp_max_id<0x111>(v));
     v = min(v, dpp_max_id<0x112>(v));
@@ -2749,12 +2763,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             }
         }
         // exclusive prefix sum of the row counts over the workgroup
-        uint32_t incl = nrows;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t t = (uint32_t)__shfl_up((int)incl, o);
-            if ((int)lane >= o) incl += t;
-        }
+        const uint32_t incl = wave_incl_sum(nrows);
         if (lane == 63) wsum[tid >> 6] = incl;
         __syncthreads();
         uint32_t start = incl - nrows, total = 0;
