@@ -2884,7 +2884,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
                 const uint32_t leader = (uint32_t)__builtin_ctzll(m);
                 uint32_t base = 0;
                 if (lane == leader) base = atomicAdd(&nsky, (uint32_t)__builtin_popcountll(m));
-                base = (uint32_t)__shfl((int)base, (int)leader);
+                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);  // leader: uniform
                 if (bg) skyq[base + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
             }
         }
