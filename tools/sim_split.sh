@@ -3,7 +3,7 @@
 # (bench.py --sim-world 8 --sim-display-rows D --sim-codec dbp): the display rank (0) and a sender (4).
 set -o pipefail
 mkdir -p gpurun_out
-for d in 135 270; do
+for d in ${DROWS:-135 270}; do
   for r in 0 4; do
     timeout -k 10 200 python -u bench.py --steps 400 --warmup 50 --no-secondary --sim-world 8 --sim-rank $r \
       --sim-display-rows $d --sim-codec dbp > gpurun_out/simd_${d}_$r.json 2> gpurun_out/simd_${d}_$r.err || { tail -20 gpurun_out/simd_${d}_$r.err; exit 1; }
