@@ -540,9 +540,14 @@ class BandRenderer:
         self.pack = pack
         if self.codec is not None and self.codec.mode == "dbp":  # the slot size every rank's band fits (collective)
             agree_dbp_slot(self.codec, self.probe_band(), world > 1)
-        self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
-                               mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1), spans=spans,
-                               codec=self.codec, make_bytes=lambda n: torch.empty(n, dtype=torch.uint8, device=self.dev))
+        native = exchange == "native" and world > 1 and assembly == "gather" and self.dev.type == "cuda"
+        if native:  # tri_xfer owns the exchange (below): the ring keeps one band buffer, no frames or staging
+            self.ring = GatherRing(1, rows * W, rows * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev))
+        else:
+            self.ring = GatherRing(world, rows * W, H * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev),
+                                   mode=assembly, rank=rank, nbuf=max(self.inflight, 2 if world > 1 else 1),
+                                   spans=spans, codec=self.codec,
+                                   make_bytes=lambda n: torch.empty(n, dtype=torch.uint8, device=self.dev))
         # the per-frame calls with their ctypes arguments built once (a frame at N = 8 is ~60 us of GPU
         # work, so Python-side marshalling per call would show up in the frame rate)
         self._ctxs = [r._ctx for r in self.rs]
@@ -557,7 +562,7 @@ class BandRenderer:
         # N = 8 would bind the display rank far below one GPU's frame rate. The GatherRing above stays the
         # exchange for --exchange torch, the all-gather and the gloo tests.
         self.xfer, self._kx = None, 0
-        if exchange == "native" and world > 1 and assembly == "gather" and self.dev.type == "cuda":
+        if native:
             self._attach_xfer(device_index)
         self.frames = 0
         self.sim_step = None  # --sim-codec: the band codec's per-frame work, on the frame's stream
