@@ -41,7 +41,8 @@ struct tri_xfer {
     uint32_t world = 1, rank = 0;
     uint32_t W = 0, display = 0, fmt = TRI_GROUP_FMT_BGRA32, slot_bytes = 0, alpha = 0, nbuf = 0;
     std::vector<uint32_t> y;                 // world + 1 row boundaries
-    hipStream_t own = nullptr;               // exchange-only frames of a slot that never rendered
+    std::vector<hipStream_t> own;            // per slot: exchange-only frames of a slot that never rendered (an
+                                             // assemble-only display's frames: slots overlap like render streams)
     std::vector<uint32_t*> pixels;           // per slot: this rank's band (sender) or the frame (display)
     std::vector<uint8_t*> stage;             // per slot: the sender's packed band
     std::vector<std::vector<uint8_t*>> rx;   // per slot, per rank: the display's received packed bands
@@ -131,7 +132,8 @@ int tri_xfer_destroy(tri_xfer* x) {
     for (hipEvent_t e : x->freed)
         if (e) (void)hipEventDestroy(e);
     if (x->flags) (void)hipFree(x->flags);
-    if (x->own) (void)hipStreamDestroy(x->own);
+    for (hipStream_t st : x->own)
+        if (st) (void)hipStreamDestroy(st);
     delete x;
     return TRI_OK;
 }
@@ -149,9 +151,10 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
         cfg->format > TRI_GROUP_FMT_DBP ||
         (cfg->format == TRI_GROUP_FMT_DBP && (cfg->slot_bytes < TRI_DBP_MIN_SLOT || cfg->slot_bytes % 16u)))
         return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: bad configuration");
+    // every band has rows, except that the display's may be empty (it then only assembles the others)
     for (uint32_t r = 0; r < N; ++r)
-        if (cfg->band_y[r + 1] <= cfg->band_y[r])
-            return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: every band needs at least one row");
+        if (cfg->band_y[r + 1] < cfg->band_y[r] || (cfg->band_y[r + 1] == cfg->band_y[r] && (r != cfg->display || N == 1)))
+            return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: every band but the display's needs at least one row");
     XH(hipSetDevice(comms[0]->device));
     tri_xfer* x = new tri_xfer();
     x->xc.assign(comms, comms + ncomm);
@@ -172,9 +175,10 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
     x->rx.assign(x->nbuf, std::vector<uint8_t*>(N, nullptr));
     x->stream.assign(x->nbuf, nullptr);
     x->freed.assign(x->nbuf, nullptr);
-    if (hipStreamCreateWithFlags(&x->own, hipStreamNonBlocking) != hipSuccess)
-        return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: stream creation failed"));
+    x->own.assign(x->nbuf, nullptr);
     for (uint32_t s = 0; s < x->nbuf; ++s) {
+        if (hipStreamCreateWithFlags(&x->own[s], hipStreamNonBlocking) != hipSuccess)
+            return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: stream creation failed"));
         if (hipEventCreateWithFlags(&x->freed[s], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: event creation failed"));
         if (!packed || N == 1) continue;
@@ -187,8 +191,8 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
                     return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: receive allocation failed"));
         }
     }
-    if (hipMalloc(&x->flags, 8) != hipSuccess || hipMemsetAsync(x->flags, 0, 8, x->own) != hipSuccess ||
-        hipStreamSynchronize(x->own) != hipSuccess)
+    if (hipMalloc(&x->flags, 8) != hipSuccess || hipMemsetAsync(x->flags, 0, 8, x->own[0]) != hipSuccess ||
+        hipStreamSynchronize(x->own[0]) != hipSuccess)
         return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: flag allocation failed"));
     *out = x;
     return TRI_OK;
@@ -205,11 +209,13 @@ int tri_xfer_frame(tri_xfer* x, uint32_t slot, tri_ctx* ctx, void* depth, const 
                    const float clear[4], const tri_draw* draws, uint32_t draw_count, uint32_t exchange) {
     if (!x || slot >= x->nbuf || !x->pixels[slot]) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_frame: bad slot");
     const uint32_t me = x->rank, N = x->world;
+    if (ctx && band_pixels(x, me) == 0)
+        return tri_internal_fail(TRI_E_INVALID, "tri_xfer_frame: an assemble-only display (empty band) renders nothing");
     const bool disp = me == x->display;
     XH(hipSetDevice(x->device));
     uint32_t* frame = x->pixels[slot];  // the band (sender) or the frame (display)
     // the slot's stream: its context's (render and transfer in one stream order), else the last one it ran on
-    hipStream_t s = ctx ? tri_internal_stream(ctx) : (x->stream[slot] ? x->stream[slot] : x->own);
+    hipStream_t s = ctx ? tri_internal_stream(ctx) : (x->stream[slot] ? x->stream[slot] : x->own[slot]);
     if (x->stream[slot] && x->stream[slot] != s) {  // the slot moves to another stream: fence its last frame
         XH(hipEventRecord(x->freed[slot], x->stream[slot]));
         XH(hipStreamWaitEvent(s, x->freed[slot], 0));

@@ -54,7 +54,8 @@ def band_split(height, world, display_rows=None):
     time). With display_rows, the display rank 0 takes that many rows and the others share the rest
     (sizes within one row): the display rank's band never crosses a link, so when the gather is the
     bottleneck a larger display band shortens every remote band's transfer (sort-first load balancing;
-    autotune_split picks the size on the hardware)."""
+    autotune_split picks the size on the hardware). display_rows = 0: the display rank renders nothing and only
+    assembles (receives and decodes the other N - 1 bands; the native exchange only)."""
     if world == 1:
         return [(0, height)]
     if display_rows is None:
@@ -62,7 +63,7 @@ def band_split(height, world, display_rows=None):
         sizes = [base + (1 if r < rem else 0) for r in range(world)]
     else:
         d = int(display_rows)
-        if d < 1 or height - d < world - 1:
+        if d < 0 or height - d < world - 1:
             raise ValueError(f"display band of {d} rows leaves no rows for {world - 1} other ranks of {height}")
         base, rem = divmod(height - d, world - 1)
         sizes = [d] + [base + (1 if r < rem else 0) for r in range(world - 1)]
@@ -204,6 +205,8 @@ class BandCodec:
         import torch
 
         n = band.numel()
+        if n == 0:  # an assemble-only display rank sends nothing
+            return 0
         if not self.gpu:
             return _dbp_encode_np(band.numpy().view(np.uint32), DBP_MAX_SLOT)[1]
         from trident_raster import raster
@@ -510,8 +513,15 @@ class BandRenderer:
         self.scene, self.rank, self.world, self.rows = scene, rank, world, rows
         self.dev = torch.device("cuda", device_index)
         self.inflight = max(1, inflight)
+        native = exchange == "native" and world > 1 and assembly == "gather" and self.dev.type == "cuda"
+        if rows == 0 and not (native or world == 1):
+            raise ValueError("an assemble-only display rank (a band of 0 rows) needs the native exchange")
         self.spans = spans = [(y0 * W, (y1 - y0) * W) for y0, y1 in self.bands] if world > 1 else None
-        self.depth = [torch.empty(rows * W, dtype=torch.float32, device=self.dev) for _ in range(self.inflight)]
+        # an assemble-only display rank (0 rows) never renders in the frame loop: its contexts cover one row, for the
+        # frame's state (the proven alpha, statistics)
+        cband = self.band if rows else (0, 1)
+        self.depth = [torch.empty((cband[1] - cband[0]) * W, dtype=torch.float32, device=self.dev)
+                      for _ in range(self.inflight)]
         self.geometry = raster.TriGeometry(device_index)
         self.geometry.upload(scene.vertices, scene.indices, scene.meshes)
         # Each context renders on a dedicated torch stream (a non-zero handle) that is torch's current
@@ -521,7 +531,7 @@ class BandRenderer:
         # as "the context's own non-blocking stream" — unordered with the collective.)
         self.rs, self.streams = [], []
         for _ in range(self.inflight):
-            r = raster.TriRaster(W, H, band=self.band, device=device_index)
+            r = raster.TriRaster(W, H, band=cband, device=device_index)
             st = torch.cuda.Stream(self.dev)
             r.set_stream(st.cuda_stream)
             scenes.load_scene(r, scene, geometry=self.geometry)
@@ -540,7 +550,6 @@ class BandRenderer:
         self.pack = pack
         if self.codec is not None and self.codec.mode == "dbp":  # the slot size every rank's band fits (collective)
             agree_dbp_slot(self.codec, self.probe_band(), world > 1)
-        native = exchange == "native" and world > 1 and assembly == "gather" and self.dev.type == "cuda"
         if native:  # tri_xfer owns the exchange (below): the ring keeps one band buffer, no frames or staging
             self.ring = GatherRing(1, rows * W, rows * W, lambda n: torch.empty(n, dtype=torch.int32, device=self.dev))
         else:
@@ -591,9 +600,11 @@ class BandRenderer:
             self._raster._check(lib.tri_xfer_bind_slot(x, s, C.c_void_p(b.data_ptr())))
 
     def _xframe(self, i, exchange=1, render=True):
-        """One frame through tri_xfer on context i, into its slot i (render=False: the exchange alone)."""
+        """One frame through tri_xfer on context i, into its slot i (render=False, or an assemble-only display rank:
+        the exchange alone)."""
         slot = i % self.nbuf
         self._kx = slot
+        render = render and self.rows > 0
         rc = self._lib.tri_xfer_frame(self.xfer, slot, self._ctxs[i] if render else None,
                                       self._depth_ptrs[i] if render else None, self._ubo if render else None,
                                       self._clear if render else None, self._draws if render else None,
@@ -625,11 +636,21 @@ class BandRenderer:
         return self.ring.frame
 
     def probe_band(self):
-        """One frame of this rank's band on context 0, into a scratch buffer (synchronised; no collective)."""
+        """One frame of this rank's band on context 0, into a scratch buffer (synchronised; no collective). An
+        assemble-only display rank probes the first sender's band instead (a scratch context)."""
         import ctypes as C
 
+        import numpy as np
         import torch
+        from trident_raster import scenes
 
+        if self.rows == 0:
+            with self._raster.TriRaster(self.scene.width, self.scene.height, band=self.bands[1],
+                                        device=self.dev.index) as r:
+                scenes.load_scene(r, self.scene, geometry=self.geometry)
+                r.render_frame()
+                col, _ = r.readback(depth=False)
+            return torch.from_numpy(np.ascontiguousarray(col).view(np.int32).reshape(-1)).to(self.dev)
         band = torch.empty(self.rows * self.scene.width, dtype=torch.int32, device=self.dev)
         r = self.rs[0]
         self._raster._check(self._lib.tri_bind_output(r._ctx, C.c_void_p(band.data_ptr()), C.c_void_p(self.depth[0].data_ptr())))
@@ -643,12 +664,13 @@ class BandRenderer:
             return
         lib, ctx = self._lib, self._ctxs[i]
         band = self.ring.acquire()
-        rc = (lib.tri_bind_output(ctx, self._band_ptrs[band.data_ptr()], self._depth_ptrs[i]) or
-              lib.tri_set_frame(ctx, self._ubo, self._clear) or   # per-frame uniform update
-              lib.tri_set_draws(ctx, self._draws, self._ndraws) or  # per-frame draw list (push constants)
-              lib.tri_render(ctx))
-        if rc:
-            self._raster._check(rc)
+        if self.rows:  # (--sim-world's assemble-only display rank renders nothing)
+            rc = (lib.tri_bind_output(ctx, self._band_ptrs[band.data_ptr()], self._depth_ptrs[i]) or
+                  lib.tri_set_frame(ctx, self._ubo, self._clear) or   # per-frame uniform update
+                  lib.tri_set_draws(ctx, self._draws, self._ndraws) or  # per-frame draw list (push constants)
+                  lib.tri_render(ctx))
+            if rc:
+                self._raster._check(rc)
         if self.sim_step is not None:
             self.sim_step(band)
         self.ring.publish()
@@ -707,6 +729,8 @@ class BandRenderer:
             i = k % self.inflight
             if self.xfer is not None:
                 self._xframe(i, exchange=0)
+                continue
+            if self.rows == 0:
                 continue
             lib, ctx = self._lib, self._ctxs[i]
             band = self.ring.bands[k % len(self.ring.bands)]
@@ -777,7 +801,7 @@ class BandRenderer:
         import torch
 
         W = self.scene.width
-        band = self.ring.bands[0]
+        band = self.ring.bands[0] if self.rows else self.probe_band()
         codec = self.codec
         if codec is None:  # one GPU: the format --pack names, its slot agreed on this band alone
             codec = BandCodec(max(self.alpha, 0), self.dev, "bgr24" if self.pack == "bgr24" else "dbp")
@@ -835,19 +859,24 @@ class BandRenderer:
 DEFAULT_INFLIGHT = {"c3": 3, "c3trs": 3, "c2": 2, "c5": 2, "c1": 2}
 
 
-def split_candidates(height, world, min_rows=32, inflights=(2,)):
+def split_candidates(height, world, min_rows=32, inflights=(2,), assemble_only=False):
     """(display rows, frames in flight) pairs autotune_split tries: the equal split, display bands up to 2.5x
     it (when the links bind, a larger display band shortens every remote band) and down to a quarter of it (when the
     display GPU's decode of the remote bands binds: a pixel moved off the display band costs it a decode, ~2 us per
     million pixels, instead of a render, ~20), as long as every band keeps at least `min_rows` rows (one bin
     row), at each frame count in `inflights` (a band's kernels are short at large N, and a third frame in flight
-    keeps more of the GPU busy: N = 8 rank 4 on one GPU 33.4k frames/s with 2, 39.0k with 3, 33.1k with 4)."""
+    keeps more of the GPU busy: N = 8 rank 4 on one GPU 33.4k frames/s with 2, 39.0k with 3, 33.1k with 4).
+    assemble_only (the native exchange): also a display band of 0 rows — the display GPU renders nothing and only
+    receives and decodes the other N - 1 bands, so it pays no front end of its own (a band's vertex and set-up
+    kernels cost about as much at 67 rows as at 270)."""
     base = height / world
     ds = [int(round(base))]  # the equal split always (a small frame or a large world may leave no other)
     for m in (0.25, 0.5, 0.75, 1.25, 1.5, 2.0, 2.5):
         d = int(round(base * m))
         if d >= min_rows and height - d >= (world - 1) * min_rows and d not in ds:
             ds.append(d)
+    if assemble_only and world > 2 and height >= (world - 1) * min_rows:
+        ds.append(0)
     return [(d, k) for k in inflights for d in ds]
 
 
@@ -1137,6 +1166,24 @@ def stage_ms(timing):
     return {k: timing[k] / n for k in keys}
 
 
+def rendering_rank_stage(br, timing, dist_on):
+    """(stage ms, kernel samples, band rows) of the rank whose kernels the line describes: this rank's own, or, when
+    the display rank 0 only assembles (a band of 0 rows, no kernels of its own), rank 1's, broadcast. Every rank calls
+    it at the same point (the broadcast is a collective)."""
+    stage = stage_ms(timing)
+    samples = int(timing["frames"]) if timing else 0
+    if not dist_on or br.bands[0][1] > br.bands[0][0]:
+        return stage, samples, br.rows
+    import torch
+    import torch.distributed as dist
+
+    keys = list(stage)
+    t = torch.tensor([stage[k] for k in keys] + [samples, br.rows], dtype=torch.float64, device=br.dev)
+    dist.broadcast(t, src=1)
+    v = t.tolist()
+    return dict(zip(keys, v[:len(keys)])), int(v[-2]), int(v[-1])
+
+
 def skybox_name(scene):
     sky = scene.skybox
     if sky is None:
@@ -1215,9 +1262,10 @@ def main():
             return (None, inflight_for(sc)), None
         if args.split != "auto":
             return (int(args.split), inflight_for(sc)), None
+        inflights = tuple(int(k) for k in args.inflight_candidates.split(","))
+        cands = split_candidates(sc.height, world, inflights=inflights, assemble_only=args.exchange == "native")
         return autotune_split(lambda d, k: make_renderer(sc, d, k), sc.height, world, dist_on,
-                              warm_seconds=args.warm_seconds,
-                              inflights=tuple(int(k) for k in args.inflight_candidates.split(",")))
+                              warm_seconds=args.warm_seconds, candidates=cands)
 
     split_log = None
     inflight = inflight_for(scene)
@@ -1243,6 +1291,8 @@ def main():
                   "using torch.distributed", file=sys.stderr, flush=True)
             br.close()
             args.exchange = "torch"
+            if display_rows == 0:  # the torch exchange has no assemble-only display: the equal split
+                display_rows = None
             br = make_renderer(scene, display_rows, inflight)
             parity = verify_assembly(br, scene, dist_on)
             parity["native_failed"] = True
@@ -1252,7 +1302,7 @@ def main():
     W, H = scene.width, scene.height
     stats = br.r.frame_stats()
     latency = br.latency_ms()  # one frame end to end (render + gather), no overlap
-    stage = stage_ms(timing)
+    stage, samples, rrows = rendering_rank_stage(br, timing, dist_on)  # rrows: the band those kernels rendered
     assembly = None
     if world > 1:  # what sets the rate: the slowest rank's render alone vs the assembly alone (outside the timed region)
         br.check()  # every packed band kept its alpha and fitted its slots (lossless)
@@ -1264,11 +1314,12 @@ def main():
                     "parity_vs_one_gpu_frame": parity,
                     "band_format": br.codec.mode if br.codec is not None else "bgra32",
                     "dbp_slot_bytes": br.codec.slot if br.codec is not None and br.codec.mode == "dbp" else None,
-                    "band_bytes_per_pixel": (br.codec.bytes_for(br.rows * W) / (br.rows * W)
+                    "band_bytes_per_pixel": (br.codec.bytes_for(rrows * W) / (rrows * W)
                                              if br.codec is not None else 4), "frame_alpha": br.alpha,
                     "render_bound_fps": 1e3 / render_ms if render_ms > 0 else None,
                     "assembly_bound_fps": 1e3 / asm_ms if asm_ms > 0 else None,
                     "bound": "assembly" if asm_ms > render_ms else "render",
+                    "display_renders": br.bands[0][1] > br.bands[0][0],
                     "note": "max over ranks; render and assembly each timed alone, back to back, outside the timed region"}
     elif args.sim_world > 1:  # one band of an N-way split on one GPU: the codec's cost per band
         assembly = {"sim_world": args.sim_world, "sim_rank": args.sim_rank, "frame_alpha": br.alpha,
@@ -1280,11 +1331,11 @@ def main():
     # divided by its mean duration from HIP events on the render stream (a separate event pass).
     raster_ms = stage["ms_raster"]
     frame_ms = dt / args.steps * 1e3  # whole-frame figure on the throughput clock
-    raster_bytes = 8.0 * W * br.rows
+    raster_bytes = 8.0 * W * rrows
     achieved = raster_bytes / (raster_ms * 1e-3) / 1e9 if raster_ms > 0 else None
-    frame_bytes = scene.algorithmic_bytes(rows=br.rows)
+    frame_bytes = scene.algorithmic_bytes(rows=rrows)
     pmc = pmc_kernel(scene.name, "k_raster")
-    traffic = None if pmc is None or "hbm_bytes_per_launch" not in pmc else pmc["hbm_bytes_per_launch"] * br.rows / H
+    traffic = None if pmc is None or "hbm_bytes_per_launch" not in pmc else pmc["hbm_bytes_per_launch"] * rrows / H
 
     secondary = {}
     if not args.no_secondary and args.config == "c3":
@@ -1300,10 +1351,10 @@ def main():
             n2 = max(args.steps, 200) if key in ("c2", "c3trs") else max(args.steps, 100)
             dt2, t2, _ = timed_run(br2, n2, args.warmup, dist_on, warm_seconds=args.warm_seconds)
             fps2 = n2 / dt2
-            st2 = stage_ms(t2)
+            st2, samples2, rows2 = rendering_rank_stage(br2, t2, dist_on)
             entry = {"frames_per_s": fps2, "mpix_per_s": fps2 * s2.width * s2.height / 1e6, "ms_per_frame": 1e3 / fps2,
-                     "stage_ms": st2, "kernel_samples": int(t2["frames"]) if t2 else 0, "triangles": s2.triangles,
-                     "algorithmic_bytes": s2.algorithmic_bytes(rows=br2.rows)}
+                     "stage_ms": st2, "kernel_samples": samples2, "triangles": s2.triangles,
+                     "algorithmic_bytes": s2.algorithmic_bytes(rows=rows2)}
             entry["frames_in_flight"] = k2
             entry["fragment_path"] = br2.r.frame_stats()["path"]  # tri_frame_stats.path (TRI_PATH_* bits)
             if world > 1:
@@ -1351,10 +1402,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": achieved / HBM_PEAK_GBS if achieved else None, "traffic": traffic,
                          "binding": "valu issue + TA/TD gather path (roofline_valu), not HBM bytes",
-                         "valu_floor_frac": valu_floor_frac(pmc if br.rows == H else None, raster_bytes),
+                         "valu_floor_frac": valu_floor_frac(pmc if rrows == H else None, raster_bytes),
                          "measured_copy_GBs": copy_gbs,
                          "kernel": "k_raster",
-                         "kernel_ms": raster_ms, "kernel_samples": int(timing["frames"]) if timing else 0,
+                         "kernel_ms": raster_ms, "kernel_samples": samples,
                          "algorithmic_bytes": raster_bytes,
                          "traffic_source": (None if traffic is None else
                                             f"profiles/pmc_summary.json k_raster: {pmc.get('hbm_read_method', '2 x FETCH_SIZE')}"
@@ -1362,7 +1413,7 @@ def main():
                                             " known bytes for k_raster's 12-B / 16-B gather shapes in"
                                             " profiles/round3/fetch_calib.json (tools/fetch_calib.sh)")},
             # the PMC count is of a whole frame: no VALU roofline for a band
-            "roofline_valu": valu_roofline(pmc if br.rows == H else None, raster_ms),
+            "roofline_valu": valu_roofline(pmc if rrows == H else None, raster_ms),
             "frame_roofline": {"algorithmic_bytes": frame_bytes, "ms_per_frame": frame_ms,
                                "achieved_GBs": frame_bytes / (frame_ms * 1e-3) / 1e9 if frame_ms > 0 else None,
                                "frac": frame_bytes / (frame_ms * 1e-3) / 1e9 / HBM_PEAK_GBS if frame_ms > 0 else None},

@@ -359,7 +359,9 @@ typedef struct tri_xfer_comm tri_xfer_comm;
 typedef struct tri_xfer tri_xfer;
 typedef struct tri_xfer_config {
     uint32_t width;           /* pixels per row                                                          */
-    const uint32_t* band_y;   /* world + 1 row boundaries: rank r renders rows [band_y[r], band_y[r + 1]) */
+    const uint32_t* band_y;   /* world + 1 row boundaries: rank r renders rows [band_y[r], band_y[r + 1]);
+                                 every band has rows except the display's, which may be empty: the
+                                 display then renders nothing and only assembles (ctx NULL every frame) */
     uint32_t display;         /* the rank that assembles the frame                                       */
     uint32_t format;          /* TRI_GROUP_FMT_*: the bands' transfer format                             */
     uint32_t slot_bytes;      /* TRI_GROUP_FMT_DBP: the slot size every rank agreed                      */
@@ -378,7 +380,8 @@ int tri_xfer_destroy(tri_xfer* xfer);
 int tri_xfer_bind_slot(tri_xfer* xfer, uint32_t slot, void* bgra8);
 /* One frame into slot `slot`: if ctx is not NULL, bind it to the slot (and `depth`, may be NULL), apply the frame
  * state when given (ubo / draws not NULL: tri_set_frame / tri_set_draws) and tri_render; then, if `exchange`, the
- * band's transfer, on the same stream (the context's; ctx NULL: the slot's last stream). A slot reused on its
+ * band's transfer, on the same stream (the context's; ctx NULL: the slot's last stream, or a stream of the slot's
+ * own if it never rendered, so an assemble-only display's slots overlap as render streams do). A slot reused on its
  * stream is ordered behind its previous transfer by stream order; a slot that changes stream is fenced. Every rank
  * must make the same sequence of exchanging calls per slot (the transfers match in order per communicator). */
 int tri_xfer_frame(tri_xfer* xfer, uint32_t slot, tri_ctx* ctx, void* depth, const tri_global_ubo* ubo,

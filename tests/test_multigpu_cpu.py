@@ -226,6 +226,16 @@ def test_band_split_partition():
     assert {k for _, k in bench.split_candidates(2160, 4, inflights=(2, 3))} == {2, 3}
     # a small frame over a large world keeps the equal split (no empty candidate list)
     assert bench.split_candidates(240, 8) == [(30, 2)]
+    # an assemble-only display (0 rows: the native exchange's display renders nothing) is a candidate when asked for
+    # and the other ranks keep at least one bin row each; never at N = 2 (one sender would render the whole frame)
+    bands = bench.band_split(2160, 8, 0)
+    assert bands[0] == (0, 0) and [b - a for a, b in bands[1:]] == [309] * 4 + [308] * 3
+    assert 0 not in [d for d, _ in bench.split_candidates(2160, 8)]
+    assert [d for d, _ in bench.split_candidates(2160, 8, inflights=(2, 3), assemble_only=True)].count(0) == 2
+    assert 0 not in [d for d, _ in bench.split_candidates(2160, 2, assemble_only=True)]
+    assert 0 not in [d for d, _ in bench.split_candidates(200, 8, assemble_only=True)]
+    with pytest.raises(ValueError):
+        bench.band_split(2160, 8, -1)
 
 
 def _uneven_worker(rank, world, port, scene_name, out_dir, display_rows, ring):

@@ -102,3 +102,22 @@ def test_xfer_rejects_bad_arguments(comm):
         assert lib.tri_xfer_bind_slot(x, 0, C.c_void_p(258)) == abi.TRI_E_INVALID  # misaligned
     finally:
         raster._check(lib.tri_xfer_destroy(x))
+
+
+def test_xfer_exchange_only_slots_run_on_their_own_streams(comm):
+    """Slots that never rendered (an assemble-only display rank's, which passes no context) take streams of their
+    own, one per slot; the frames are accepted and synchronise."""
+    import torch
+    from trident_raster import raster
+
+    lib, c = comm
+    x = _xfer(lib, c, 64, 16, 0, nbuf=3)
+    try:
+        bufs = [torch.zeros(64 * 16, dtype=torch.int32, device="cuda:0") for _ in range(3)]
+        for k, b in enumerate(bufs):
+            raster._check(lib.tri_xfer_bind_slot(x, k, C.c_void_p(b.data_ptr())))
+        for k in range(7):
+            raster._check(lib.tri_xfer_frame(x, k % 3, None, None, None, None, None, 0, 1))
+        raster._check(lib.tri_xfer_synchronize(x))
+    finally:
+        raster._check(lib.tri_xfer_destroy(x))
