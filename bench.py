@@ -55,10 +55,15 @@ def band_split(height, world, display_rows=None):
     (sizes within one row): the display rank's band never crosses a link, so when the gather is the
     bottleneck a larger display band shortens every remote band's transfer (sort-first load balancing;
     autotune_split picks the size on the hardware). display_rows = 0: the display rank renders nothing and only
-    assembles (receives and decodes the other N - 1 bands; the native exchange only)."""
+    assembles (receives and decodes the other N - 1 bands; the native exchange only). A list of N row counts gives
+    every band's size (rebalance_split)."""
     if world == 1:
         return [(0, height)]
-    if display_rows is None:
+    if isinstance(display_rows, (list, tuple)):  # explicit per-rank row counts (rebalance_split)
+        sizes = [int(n) for n in display_rows]
+        if len(sizes) != world or sum(sizes) != height or sizes[0] < 0 or min(sizes[1:]) < 1:
+            raise ValueError(f"band sizes {sizes} do not split {height} rows over {world} ranks")
+    elif display_rows is None:
         base, rem = divmod(height, world)
         sizes = [base + (1 if r < rem else 0) for r in range(world)]
     else:
@@ -935,6 +940,70 @@ def autotune_split(make, height, world, dist_on, frames=80, rounds=2, warm_secon
     return cands[pick], [(d, k, f) for (d, k), f in zip(cands, best)]
 
 
+def rebalance_sizes(bands, ms, min_rows=32):
+    """Sender bands re-cut in proportion to their measured row rates (rows / ms of each rank's render alone), the
+    display band kept: the slowest sender sets the whole job's rate, so rows move from slow bands (dense geometry,
+    the bottom of the frame) to fast ones. Every band keeps at least `min_rows` rows; largest remainders round.
+    Deterministic, so every rank computes the same sizes from the same gathered times."""
+    sizes = [b - a for a, b in bands]
+    d, rest = sizes[0], sum(sizes[1:])
+    rates = [sizes[r] / max(float(ms[r]), 1e-9) for r in range(1, len(sizes))]
+    ideal = [rest * x / sum(rates) for x in rates]
+    new = [max(min_rows, int(v)) for v in ideal]
+    order = sorted(range(len(new)), key=lambda i: -(ideal[i] - int(ideal[i])))
+    k = 0
+    while sum(new) != rest and k < 10 * len(new) + rest:  # hand out (or take back) the remaining rows one at a time
+        i = order[k % len(new)]
+        if sum(new) < rest:
+            new[i] += 1
+        elif new[i] > min_rows:
+            new[i] -= 1
+        k += 1
+    return [d] + new if sum(new) == rest else sizes
+
+
+def rebalance_split(make, display_rows, inflight, dist_on, frames=80, rounds=2, warm_seconds=0.25):
+    """One load-balancing step after autotune_split (band heights from the measured per-band time):
+    every rank times its band's render alone, the times are all-gathered, the sender bands are re-cut by
+    rebalance_sizes, and the re-cut split is kept only if it measures faster (max-over-ranks frames/s, interleaved
+    rounds). Returns (display_rows or the list of band sizes, log)."""
+    import torch
+
+    br = make(display_rows, inflight)
+    br.warm()
+    ms = br.render_only_ms(frames=frames)
+    world = len(br.bands)
+    if dist_on:
+        import torch.distributed as dist
+
+        t = [torch.zeros(1, dtype=torch.float64, device=br.dev) for _ in range(world)]
+        dist.all_gather(t, torch.tensor([ms], dtype=torch.float64, device=br.dev))
+        times = [float(x.item()) for x in t]
+    else:
+        times = [ms] * world
+    sizes = rebalance_sizes(br.bands, times)
+    if sizes == [b - a for a, b in br.bands]:
+        br.close()
+        return display_rows, {"render_ms": times, "resplit": None}
+    br2 = make(tuple(sizes), inflight)
+    br2.warm()
+    t_end = time.perf_counter() + warm_seconds
+    while True:
+        for _ in range(20):
+            br.step()
+        br.drain()
+        if max_over_ranks(t_end - time.perf_counter(), br.dev, dist_on) <= 0:
+            break
+    best = [0.0, 0.0]
+    for _ in range(rounds):
+        for i, b in enumerate((br, br2)):
+            best[i] = max(best[i], measure_fps(b, frames, dist_on))
+    br.close()
+    br2.close()
+    log = {"render_ms": times, "resplit": sizes, "fps": {"autotuned": best[0], "resplit": best[1]}}
+    return (tuple(sizes) if best[1] > best[0] else display_rows), log
+
+
 def verify_assembly(br, scene, dist_on):
     """N > 1 parity in the bench itself: one frame through the band exchange, and on the display rank the assembled
     frame against the same frame rendered whole by one context on that GPU (bit for bit: a band context's pixels are
@@ -1264,8 +1333,13 @@ def main():
             return (int(args.split), inflight_for(sc)), None
         inflights = tuple(int(k) for k in args.inflight_candidates.split(","))
         cands = split_candidates(sc.height, world, inflights=inflights, assemble_only=args.exchange == "native")
-        return autotune_split(lambda d, k: make_renderer(sc, d, k), sc.height, world, dist_on,
-                              warm_seconds=args.warm_seconds, candidates=cands)
+        (d, k), log = autotune_split(lambda d, k: make_renderer(sc, d, k), sc.height, world, dist_on,
+                                     warm_seconds=args.warm_seconds, candidates=cands)
+        if world > 2:  # then one rebalancing step of the sender bands from their measured render times
+            d, rlog = rebalance_split(lambda d, k: make_renderer(sc, d, k), d, k, dist_on,
+                                      warm_seconds=args.warm_seconds)
+            log = {"candidates": log, "rebalance": rlog}
+        return (d, k), log
 
     split_log = None
     inflight = inflight_for(scene)
@@ -1291,8 +1365,8 @@ def main():
                   "using torch.distributed", file=sys.stderr, flush=True)
             br.close()
             args.exchange = "torch"
-            if display_rows == 0:  # the torch exchange has no assemble-only display: the equal split
-                display_rows = None
+            if display_rows == 0 or (isinstance(display_rows, tuple) and display_rows[0] == 0):
+                display_rows = None  # the torch exchange has no assemble-only display: the equal split
             br = make_renderer(scene, display_rows, inflight)
             parity = verify_assembly(br, scene, dist_on)
             parity["native_failed"] = True

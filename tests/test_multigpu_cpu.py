@@ -236,6 +236,19 @@ def test_band_split_partition():
     assert 0 not in [d for d, _ in bench.split_candidates(200, 8, assemble_only=True)]
     with pytest.raises(ValueError):
         bench.band_split(2160, 8, -1)
+    # explicit band sizes, and the rebalancing step's re-cut: rows move from the slow bands to the fast ones, the
+    # display band is kept, the rows still cover the frame, equal times change nothing
+    assert bench.band_split(100, 3, (0, 60, 40)) == [(0, 0), (0, 60), (60, 100)]
+    for bad in [(0, 60, 39), (10, 90), (0, 100, 0)]:
+        with pytest.raises(ValueError):
+            bench.band_split(100, 3, bad)
+    new = bench.rebalance_sizes(bands, [0.0, 26.7, 26.5, 26.4, 26.4, 26.6, 26.9, 27.4])
+    assert new[0] == 0 and sum(new) == 2160 and new[7] < 308 and new[4] > 309 and min(new[1:]) >= 32
+    assert bench.band_split(2160, 8, tuple(new))[-1] == (2160 - new[7], 2160)
+    b67 = bench.band_split(2160, 8, 67)
+    assert bench.rebalance_sizes(b67, [30.0] + [26.0] * 7) == [b - a for a, b in b67]
+    tiny = bench.rebalance_sizes(bench.band_split(300, 8, 0), [1.0] * 7 + [100.0])  # a very slow band keeps min_rows
+    assert tiny[7] == 32 and sum(tiny) == 300 and max(tiny[1:7]) - min(tiny[1:7]) <= 1
 
 
 def _uneven_worker(rank, world, port, scene_name, out_dir, display_rows, ring):
