@@ -1280,8 +1280,9 @@ def main():
     ap.add_argument("--sim-codec", choices=("none", "bgr24", "dbp"), default="none",
                     help="with --sim-world: every frame also packs this rank's band (sim rank > 0) or decodes the other "
                          "ranks' bands (sim rank 0, the display), on the frame's stream")
-    ap.add_argument("--sim-display-rows", type=int, default=None,
-                    help="diagnostics: the simulated split's display band (rank 0) size, the others sharing the rest")
+    ap.add_argument("--sim-display-rows", default=None,
+                    help="diagnostics: the simulated split's display band (rank 0) size, the others sharing the rest; "
+                         "or every band's size, comma-separated")
     ap.add_argument("--inflight", type=int, default=None,
                     help="frames in flight per rank (contexts taking frames in turn, one stream each); default per "
                          "config (DEFAULT_INFLIGHT)")
@@ -1345,7 +1346,10 @@ def main():
     inflight = inflight_for(scene)
     if args.sim_world and world == 1:
         br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=inflight_for(scene),
-                          display_rows=args.sim_display_rows, pack=args.pack)
+                          display_rows=(None if args.sim_display_rows is None else
+                                        tuple(int(v) for v in args.sim_display_rows.split(","))
+                                        if "," in args.sim_display_rows else int(args.sim_display_rows)),
+                          pack=args.pack)
         if args.sim_codec != "none":
             br.attach_sim_codec(args.sim_codec)
     else:
