@@ -175,10 +175,8 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
     x->rx.assign(x->nbuf, std::vector<uint8_t*>(N, nullptr));
     x->stream.assign(x->nbuf, nullptr);
     x->freed.assign(x->nbuf, nullptr);
-    x->own.assign(x->nbuf, nullptr);
+    x->own.assign(x->nbuf, nullptr);  // created on first use: a rank that renders every frame never needs them
     for (uint32_t s = 0; s < x->nbuf; ++s) {
-        if (hipStreamCreateWithFlags(&x->own[s], hipStreamNonBlocking) != hipSuccess)
-            return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: stream creation failed"));
         if (hipEventCreateWithFlags(&x->freed[s], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: event creation failed"));
         if (!packed || N == 1) continue;
@@ -191,8 +189,7 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
                     return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: receive allocation failed"));
         }
     }
-    if (hipMalloc(&x->flags, 8) != hipSuccess || hipMemsetAsync(x->flags, 0, 8, x->own[0]) != hipSuccess ||
-        hipStreamSynchronize(x->own[0]) != hipSuccess)
+    if (hipMalloc(&x->flags, 8) != hipSuccess || hipMemset(x->flags, 0, 8) != hipSuccess)
         return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: flag allocation failed"));
     *out = x;
     return TRI_OK;
@@ -215,6 +212,8 @@ int tri_xfer_frame(tri_xfer* x, uint32_t slot, tri_ctx* ctx, void* depth, const 
     XH(hipSetDevice(x->device));
     uint32_t* frame = x->pixels[slot];  // the band (sender) or the frame (display)
     // the slot's stream: its context's (render and transfer in one stream order), else the last one it ran on
+    if (!ctx && !x->stream[slot] && !x->own[slot])  // an exchange-only slot that never rendered: a stream of its own
+        XH(hipStreamCreateWithFlags(&x->own[slot], hipStreamNonBlocking));
     hipStream_t s = ctx ? tri_internal_stream(ctx) : (x->stream[slot] ? x->stream[slot] : x->own[slot]);
     if (x->stream[slot] && x->stream[slot] != s) {  // the slot moves to another stream: fence its last frame
         XH(hipEventRecord(x->freed[slot], x->stream[slot]));
