@@ -1277,6 +1277,9 @@ def main():
     ap.add_argument("--sim-world", type=int, default=0,
                     help="diagnostics (1 GPU, no collective): render only band --sim-rank of an N-way split")
     ap.add_argument("--sim-rank", type=int, default=0)
+    ap.add_argument("--sim-extra-streams", type=int, default=0,
+                    help="diagnostics: streams created (and kept) before the renderer, as a multi-GPU run's "
+                         "collective libraries create theirs (HIP maps streams onto the process's hardware queues)")
     ap.add_argument("--sim-codec", choices=("none", "bgr24", "dbp"), default="none",
                     help="with --sim-world: every frame also packs this rank's band (sim rank > 0) or decodes the other "
                          "ranks' bands (sim rank 0, the display), on the frame's stream")
@@ -1345,6 +1348,7 @@ def main():
     split_log = None
     inflight = inflight_for(scene)
     if args.sim_world and world == 1:
+        extra_streams = [torch.cuda.Stream(torch.device("cuda", local)) for _ in range(args.sim_extra_streams)]
         br = BandRenderer(scene, args.sim_rank, 1, local, band_world=args.sim_world, inflight=inflight_for(scene),
                           display_rows=(None if args.sim_display_rows is None else
                                         tuple(int(v) for v in args.sim_display_rows.split(","))
