@@ -2845,7 +2845,9 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     // queue consumed (every wave's count load has completed: each waited for it, and the barrier's fence
     // covers this workgroup's global accesses): ready for the next frame
     if (tid == 0) {
+#ifndef TRI_DIAG_FRONT  // diagnostics (tri_render): later frames re-raster the first frame's queues
         b.bin_count[bin] = 0;
+#endif
         if (cnt > fp.bin_cap) note_bin_overflow(b, cnt);
     }
     if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(0);
@@ -3352,6 +3354,22 @@ void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan) {
     add(r, dim3(fp.nbins), t, kStageRaster);
 }
 
+#ifdef TRI_DIAG_FRONT
+// Diagnostics build: what the front end costs a frame beside its raster (tri_render): 1 = after a context's first
+// frame only k_raster runs (over that frame's queues, which it keeps), 2 = the same with two empty launches in place
+// of k_vertex and k_setup (the launches and their stream order, without their work)
+__global__ void k_diag_empty(const TriLaunchArgs*) {}
+void tri_diag_front_plan(TriFramePlan& plan) {
+    TriFramePlan q;
+    q.n = 0;
+    for (uint32_t i = 0; i < plan.n; ++i) {
+        if (plan.k[i].stage == kStageRaster) q.k[q.n++] = plan.k[i];
+        else if (TRI_DIAG_FRONT == 2) q.k[q.n++] = TriKernelLaunch{reinterpret_cast<const void*>(k_diag_empty), dim3(1), dim3(64), kStageSetup};
+    }
+    plan = q;
+}
+#endif
+
 hipError_t tri_run_plan(const TriFramePlan& plan, const TriLaunchArgs& args, TriLaunchArgs* d_args,
                         hipStream_t stream, hipEvent_t* ev) {
     hipError_t e = hipSuccess;
@@ -3369,7 +3387,8 @@ hipError_t tri_run_plan(const TriFramePlan& plan, const TriLaunchArgs& args, Tri
         }
         void* first[] = {const_cast<TriLaunchArgs*>(&args), &d_args};
         void* later[] = {&d_args};
-        e = hipLaunchKernel(k.func, k.grid, k.block, i == 0 ? first : later, 0, stream);
+        // the frame's first kernel (k_vertex's stage) takes the arguments by value and publishes them
+        e = hipLaunchKernel(k.func, k.grid, k.block, k.stage == kStageVertex ? first : later, 0, stream);
         if (e != hipSuccess) return e;
     }
     if (ev) (void)hipEventRecord(ev[kStageCount], stream);

@@ -99,6 +99,9 @@ struct TriFramePlan {
     TriKernelLaunch k[4];
 };
 void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan);
+#ifdef TRI_DIAG_FRONT
+void tri_diag_front_plan(TriFramePlan& plan);  // diagnostics build only (raster_kernels.hip)
+#endif
 // k_raster_plain's instantiation for a frame without the shadow pre-pass (raster_plain.hip)
 const void* tri_raster_plain_kernel(const TriFrameParams& fp);
 // The frame's first kernel (vertex_stage.hip): k_vertex, k_vertex_band (row bands with cluster culling) or k_reset

@@ -197,6 +197,9 @@ struct tri_ctx {
     TriLaunchArgs args{};
     TriLaunchArgs* d_args = nullptr;
     bool launched = false;  // a frame was enqueued (tri_set_stream orders the next one behind it)
+#ifdef TRI_DIAG_FRONT
+    uint32_t diag_frames = 0;  // diagnostics build: frames rendered (the first one runs the whole plan)
+#endif
 
     bool timing = false;
     uint32_t timing_period = 1, timing_counter = 0;  // time every timing_period-th frame
@@ -1414,6 +1417,9 @@ int tri_render(tri_ctx* c) {
     ts.shadow = fp.shadow_on != 0;
     TriFramePlan plan;
     tri_plan_frame(fp, plan);
+#ifdef TRI_DIAG_FRONT
+    if (c->diag_frames++ > 0) tri_diag_front_plan(plan);
+#endif
     TRI_HSTAMP(3);
     HIP_TRY(tri_run_plan(plan, ha, c->d_args, c->stream, ev));
     c->launched = true;
