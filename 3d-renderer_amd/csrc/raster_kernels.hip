@@ -3374,6 +3374,7 @@ hipError_t tri_run_plan(const TriFramePlan& plan, const TriLaunchArgs& args, Tri
                         hipStream_t stream, hipEvent_t* ev) {
     hipError_t e = hipSuccess;
     bool setup_stamped = false;
+    if (ev && (plan.n == 0 || plan.k[0].stage != kStageVertex)) (void)hipEventRecord(ev[kStageVertex], stream);
     for (uint32_t i = 0; i < plan.n; ++i) {
         const TriKernelLaunch& k = plan.k[i];
         if (ev) {
