@@ -8,7 +8,9 @@
 #ifndef TRI_SETUP_WAVES
 #define TRI_SETUP_WAVES 6
 #endif
+#ifndef TRI_SETUP_WGS_PER_CU
 #define TRI_SETUP_WGS_PER_CU TRI_SETUP_WAVES
+#endif
 
 // Device pointers in the global address space (device compilation only; the host sees plain pointers of the same
 // size). The later kernels of a frame read these pointers from the device copy of their arguments, not from
