@@ -45,7 +45,7 @@ static_assert(TRI_MAX_CLIP_POLY <= TRI_MAX_CLIP_VERTS, "clip polygon buffers");
 #define TRI_WMIN 1e-5f
 #define TRI_GUARD_BAND_PX 16000.0f
 #ifndef TRI_MAX_PPT
-#define TRI_MAX_PPT 8  // primitives per k_setup thread
+#define TRI_MAX_PPT 16  // primitives per k_setup thread
 #endif
 #define TRI_OBJ48_DRAWS 16  // draws a frame may hold for object-space varyings outside the ONE instantiation
 

@@ -2570,6 +2570,9 @@ __device__ __forceinline__ int xcd_bin(int b, int nb) {
 // Raised wave priority (s_setprio 1) from a 32x32 bin's start to the end of its coverage: the latency-bound
 // init and coverage phases issue ahead of other workgroups' shading waves (C3 k_raster 101.7 -> 99.6 us,
 // round 3 A/B; at 16x16 bins it was slower, so BL == 5 only). Scheduling only: output unchanged.
+#ifndef TRI_RASTER_PRIO  // the rest of the bin (shading, stores) at this priority: above a concurrent frame's front end
+#define TRI_RASTER_PRIO 0
+#endif
 #ifndef TRI_COV_PRIO
 #define TRI_COV_PRIO 1
 #endif
@@ -2681,7 +2684,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ uint32_t nbig, nsky;
     const int tid = threadIdx.x;
     TRI_STAMP(0);
-    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1);  // (TRI_COV_PRIO above)
+    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1 + TRI_RASTER_PRIO);  // (TRI_COV_PRIO above)
     const int bx = bin % fp.nbx, by = bin / fp.nbx;
     const int32_t ox = bx * BIN, oy = fp.y0 + by * BIN;
     const int32_t bw = min(BIN, fp.W - ox), bh = min(BIN, fp.y1 - oy);
@@ -2850,7 +2853,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
 #endif
         if (cnt > fp.bin_cap) note_bin_overflow(b, cnt);
     }
-    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(0);
+    if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(TRI_RASTER_PRIO);
     // shade + store: each wave covers whole BIN-pixel row pieces -> coalesced colour/depth stores.
     // Background pixels go to an LDS queue for the skybox pass below (lane-dense, and its registers
     // are not live during shading).

@@ -11,6 +11,15 @@
 #ifndef TRI_SETUP_WGS_PER_CU
 #define TRI_SETUP_WGS_PER_CU TRI_SETUP_WAVES
 #endif
+// k_setup workgroups per CU for frames without the shadow pre-pass. With frames in flight, one frame's set-up runs
+// beside another frame's k_raster, and every resident set-up workgroup holds wave slots and LDS that the raster's
+// bins cannot use while it waits on its fetch -> atomic -> store chain. Fewer, longer workgroups (more primitives
+// per lane) make the set-up slower alone (C3 27.9 -> 37 us) but the frame rate higher (C3 10.39-10.43k -> 10.55k,
+// C3 under a TRS draw +1 %, C2 unchanged: its set-up is one primitive per lane either way). The shadow set-up bins
+// every primitive twice and keeps the resident round (C5 4.90k -> 4.75k with 2).
+#ifndef TRI_SETUP_WGS_PER_CU_OVERLAP
+#define TRI_SETUP_WGS_PER_CU_OVERLAP 2
+#endif
 
 // Device pointers in the global address space (device compilation only; the host sees plain pointers of the same
 // size). The later kernels of a frame read these pointers from the device copy of their arguments, not from

@@ -1250,13 +1250,16 @@ int tri_render(tri_ctx* c) {
     fp.W = c->W; fp.H = c->H; fp.y0 = c->y0; fp.y1 = c->y1;
     fp.nbx = c->nbx; fp.nby = c->nby; fp.nbins = c->nbins;
     fp.bin_log2 = c->bin_log2;
-    // k_setup grid: a whole frame takes at most one resident round of workgroups (7 per CU at its
+    // k_setup grid: a shadow frame takes at most one resident round of workgroups (6 per CU at its
     // occupancy): a workgroup's fetch -> set-up -> reservation -> store chain is latency, and a partial
-    // second round doubles the kernel (C3: 1953 chunks of 512 -> 977 of 1024, set-up 33 -> 30 us). A band
-    // (cluster culling) keeps 512-primitive chunks: most of them exit at once, and the visible ones keep
-    // one chain each.
+    // second round doubles the kernel (C3: 1953 chunks of 512 -> 977 of 1024, set-up 33 -> 30 us). Other
+    // frames take 2 per CU with more primitives each, leaving wave slots to the raster of the frame in
+    // flight beside them (TRI_SETUP_WGS_PER_CU_OVERLAP, raster_launch.h). A band (cluster culling) keeps
+    // 512-primitive chunks: most of them exit at once, and the visible ones keep one chain each.
     const bool culling = (c->y0 != 0 || c->y1 != c->H || (c->cfg.flags & TRI_FLAG_CLUSTER_CULL)) && c->ncl_total > 0;
-    const uint32_t target_chunks = culling ? 4096u : (uint32_t)c->cu_count * TRI_SETUP_WGS_PER_CU;
+    const uint32_t target_chunks = culling ? 4096u
+                                           : (uint32_t)c->cu_count * (c->shadow.size ? TRI_SETUP_WGS_PER_CU
+                                                                                      : TRI_SETUP_WGS_PER_CU_OVERLAP);
     uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
     // k_setup sets up and bins pairs: an odd count leaves half of its last round idle, which costs more
     // than the extra chunks save (C3: 3 per lane 29.2 us, 4 per lane 28.3 us), except on a frame whose
