@@ -3360,13 +3360,13 @@ void tri_plan_frame(const TriFrameParams& fp, TriFramePlan& plan) {
 #ifdef TRI_DIAG_FRONT
 // Diagnostics build: what the front end costs a frame beside its raster (tri_render): 1 = after a context's first
 // frame only k_raster runs (over that frame's queues, which it keeps), 2 = the same with two empty launches in place
-// of k_vertex and k_setup (the launches and their stream order, without their work)
+// of k_vertex and k_setup (the launches and their stream order, without their work), 3 = k_vertex and k_raster
 __global__ void k_diag_empty(const TriLaunchArgs*) {}
 void tri_diag_front_plan(TriFramePlan& plan) {
     TriFramePlan q;
     q.n = 0;
     for (uint32_t i = 0; i < plan.n; ++i) {
-        if (plan.k[i].stage == kStageRaster) q.k[q.n++] = plan.k[i];
+        if (plan.k[i].stage == kStageRaster || (TRI_DIAG_FRONT == 3 && plan.k[i].stage == kStageVertex)) q.k[q.n++] = plan.k[i];
         else if (TRI_DIAG_FRONT == 2) q.k[q.n++] = TriKernelLaunch{reinterpret_cast<const void*>(k_diag_empty), dim3(1), dim3(64), kStageSetup};
     }
     plan = q;
