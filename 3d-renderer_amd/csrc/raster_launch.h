@@ -17,6 +17,10 @@
 // per lane) make the set-up slower alone (C3 27.9 -> 37 us) but the frame rate higher (C3 10.39-10.43k -> 10.55k,
 // C3 under a TRS draw +1 %, C2 unchanged: its set-up is one primitive per lane either way). The shadow set-up bins
 // every primitive twice and keeps the resident round (C5 4.90k -> 4.75k with 2).
+// k_setup's chunk target for bands (cluster culling): most chunks are culled and exit at once
+#ifndef TRI_SETUP_BAND_CHUNKS
+#define TRI_SETUP_BAND_CHUNKS 4096
+#endif
 #ifndef TRI_SETUP_WGS_PER_CU_OVERLAP
 #define TRI_SETUP_WGS_PER_CU_OVERLAP 2
 #endif

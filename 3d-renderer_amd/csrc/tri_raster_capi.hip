@@ -1257,7 +1257,7 @@ int tri_render(tri_ctx* c) {
     // flight beside them (TRI_SETUP_WGS_PER_CU_OVERLAP, raster_launch.h). A band (cluster culling) keeps
     // 512-primitive chunks: most of them exit at once, and the visible ones keep one chain each.
     const bool culling = (c->y0 != 0 || c->y1 != c->H || (c->cfg.flags & TRI_FLAG_CLUSTER_CULL)) && c->ncl_total > 0;
-    const uint32_t target_chunks = culling ? 4096u
+    const uint32_t target_chunks = culling ? (uint32_t)TRI_SETUP_BAND_CHUNKS
                                            : (uint32_t)c->cu_count * (c->shadow.size ? TRI_SETUP_WGS_PER_CU
                                                                                       : TRI_SETUP_WGS_PER_CU_OVERLAP);
     uint32_t ppt = (c->nprims + target_chunks * TRI_BLOCK - 1) / (target_chunks * TRI_BLOCK);
