@@ -741,8 +741,11 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
     const uint64_t below = (lane == 63) ? 0x7FFFFFFFFFFFFFFFull : ((1ull << lane) - 1ull);
     TRI_LDS float* buf[2] = {poly, poly + TRI_MAX_CLIP_VERTS * kClipStride};
     // object-space records: the ONE frames' (vary_obj: 36-B records at vin_base + slot, never with the pre-pass),
-    // or obj48's (the 48-B input records at slot + vdelta[draw])
-    const bool obj1 = !LPOS && obj_mode(fp), o48 = !ONE && obj48_mode(fp);
+    // or obj48's (the 48-B input records at slot + vdelta[draw]). ONE here is k_setup's single-draw instantiation, not
+    // the raster's: a single draw may be an obj48 frame too (a textured draw, the pre-pass, the AI blend), and then
+    // k_vertex wrote no varyings for the clipper to read (draw is 0 and fp.draw0 is that draw)
+    const bool obj1 = !LPOS && obj_mode(fp), o48 = obj48_mode(fp);
+    const bool one_draw = ONE || fp.one_draw;
     const uint32_t dl = o48 ? fp.vdelta[min(draw, (uint32_t)TRI_OBJ48_DRAWS - 1u)] : fp.vin_base;
     if (lane < 3) {
         ClipVert v;
@@ -753,7 +756,7 @@ __device__ __forceinline__ void clip_prim_wave(const TriFrameParams& fp, const T
                 const F3 p = vattr_at(b, dl + sl, 0);
                 float m[16];
 #pragma unroll
-                for (int i = 0; i < 16; ++i) m[i] = o48 ? b.draws[draw].model[i] : fp.draw0.model[i];
+                for (int i = 0; i < 16; ++i) m[i] = (o48 && !one_draw) ? b.draws[draw].model[i] : fp.draw0.model[i];
                 const float4 w = mat_vec_seq(m, make_float4(p.x, p.y, p.z, 1.0f));
                 wv = F3{w.x, w.y, w.z};
             } else {

@@ -290,3 +290,17 @@ def near_clip_multi(w=640, h=480, n=60, identity=False, shadow=False):
     if shadow:
         scenes.with_shadow(s, 512)
     return s
+
+
+def near_clip_single(w=640, h=480, n=60, shadow=False):
+    """near_clip_grid as ONE textured draw (a non-1x1 sRGB slot, the identity uv transform, the ground-plane rotation
+    as its model): a single-draw frame outside the solid instantiation, so k_setup runs its single-draw form while
+    k_vertex writes no varyings (obj48). The clipper must read the geometry's input records."""
+    s = near_clip_grid(w, h, n)
+    model = np.array(s.draws[0].pc.model, F).reshape(4, 4)
+    s.textures = [(1, checker_texture(16, 8, 3))]
+    s.draws = [abi.make_draw(0, model, texture_slot=1, material_index=0)]
+    s.name = f"near_clip_single{'_shadow' if shadow else ''}"
+    if shadow:
+        scenes.with_shadow(s, 512)
+    return s

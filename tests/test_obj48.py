@@ -55,6 +55,28 @@ def test_obj48_off_for_transformed_draws_with_shadow(oracle, flags):
     assert path & abi.TRI_PATH_SHADOW and not path & abi.TRI_PATH_OBJ48, hex(path)
 
 
+def test_obj48_single_textured_draw_clipped(oracle, flags):
+    """ONE textured draw, near-plane clipped: k_setup's single-draw instantiation on an obj48 frame (its clipper reads
+    the input records, not the varyings k_vertex did not write)."""
+    from trident_raster import abi
+
+    s = sc.near_clip_single()
+    assert_parity(s, oracle, min_covered=10000, flags=flags)
+    path, clipped = frame_path(s, flags)
+    assert path & abi.TRI_PATH_OBJ48 and clipped > 0, (hex(path), clipped)
+
+
+def test_obj48_single_draw_ai_blend_clipped(oracle, flags):
+    """The same single clipped draw on a solid slot with the AI-frame blend (k_raster_ai, obj48)."""
+    from trident_raster import abi, scenes
+
+    s = sc.near_clip_grid()
+    scenes.with_ai_blend(s, strength=0.35)
+    assert_parity(s, oracle, min_covered=10000, flags=flags)
+    path, clipped = frame_path(s, flags)
+    assert path & abi.TRI_PATH_OBJ48 and clipped > 0, (hex(path), clipped)
+
+
 def test_obj48_c5_and_fallbacks(oracle):
     """C5 (4 textured identity draws + the pre-pass) takes obj48; a texture transform, skinning or a non-conformal
     model does not."""
