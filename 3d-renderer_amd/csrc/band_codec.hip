@@ -23,7 +23,8 @@ constexpr uint32_t kCodecBlock = 256;
 // multiple of 4); otherwise every pixel moves by itself (same bytes).
 template <bool VEC>
 __global__ __launch_bounds__(kCodecBlock) void k_pack_bgr24(const uint32_t* __restrict__ src, uint8_t* __restrict__ dst,
-                                                            uint64_t n, uint32_t alpha, uint32_t* __restrict__ flag) {
+                                                            uint64_t n, uint32_t alpha, uint32_t* __restrict__ flag,
+                                                            uint32_t* __restrict__ trailer) {
     const uint64_t q = (uint64_t)blockIdx.x * kCodecBlock + threadIdx.x;  // pixel quad
     const uint64_t p = q * 4;
     if (p >= n) return;
@@ -48,13 +49,16 @@ __global__ __launch_bounds__(kCodecBlock) void k_pack_bgr24(const uint32_t* __re
         }
     }
     if (bad && flag) atomicOr(flag, 1u);
+    if (bad && trailer) atomicOr(trailer, 1u);  // the status that travels with the band (tri_xfer)
 }
 
 template <bool VEC>
 __global__ __launch_bounds__(kCodecBlock) void k_unpack_bgr24(const uint8_t* __restrict__ src, uint32_t* __restrict__ dst,
-                                                              uint64_t n, uint32_t alpha) {
+                                                              uint64_t n, uint32_t alpha, const uint32_t* __restrict__ trailer,
+                                                              uint32_t* __restrict__ flags) {
     const uint64_t q = (uint64_t)blockIdx.x * kCodecBlock + threadIdx.x;
     const uint64_t p = q * 4;
+    if (q == 0 && trailer && flags && (*trailer & 1u)) atomicOr(flags, 1u);  // the sender's alpha check failed
     if (p >= n) return;
     const uint32_t a = alpha << 24;
     if (VEC && p + 4 <= n) {
@@ -168,6 +172,7 @@ __global__ __launch_bounds__(kDbpPackThreads) void k_dbp_pack(const uint32_t* __
                                                               uint32_t slot_bytes, uint32_t* __restrict__ flags) {
     __shared__ uint32_t hdr[kDbpHeader / 4];
     __shared__ uint32_t cnt[kDbpBlocks];
+    __shared__ uint32_t wave_bad[kDbpPackThreads / 64];  // a pixel's alpha differs (the slot's header word 1)
     const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
     const uint32_t b0 = kDbpPackBlocks * w;  // this wave's first block in the slot
     const uint64_t px0 = (uint64_t)blockIdx.x * kDbpSlotPixels + 64u * b0;
@@ -200,7 +205,9 @@ __global__ __launch_bounds__(kDbpPackThreads) void k_dbp_pack(const uint32_t* __
             }
         }
     }
-    if (__ballot(bad) != 0ull && lane == 0 && flags) atomicOr(flags, 1u);
+    const bool wbad = __ballot(bad) != 0ull;
+    if (wbad && lane == 0 && flags) atomicOr(flags, 1u);
+    if (lane == 0) wave_bad[w] = wbad ? 1u : 0u;
     __syncthreads();
     // every wave places the slot's 64 blocks itself (lane = block): no second barrier
     const uint32_t c = cnt[lane];
@@ -213,12 +220,18 @@ __global__ __launch_bounds__(kDbpPackThreads) void k_dbp_pack(const uint32_t* __
         atomicMax(flags + 1, bytes);
         if (bytes > slot_bytes) atomicOr(flags, 2u);
     }
-    if (bytes > slot_bytes) {  // overflow: only the payload count (the decoder leaves the slot alone)
-        if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(slot) = 8u * total;
+    uint32_t slot_bad = 0u;  // (read by the two header threads only)
+    if (threadIdx.x < 2) {
+#pragma unroll
+        for (uint32_t k = 0; k < kDbpPackThreads / 64; ++k) slot_bad |= wave_bad[k];
+    }
+    if (bytes > slot_bytes) {  // overflow: only the payload count and the alpha mark (the decoder leaves the slot alone)
+        if (threadIdx.x < 2) reinterpret_cast<uint32_t*>(slot)[threadIdx.x] = threadIdx.x == 0 ? 8u * total : slot_bad;
         return;
     }
     if (threadIdx.x < kDbpHeader / 4)
-        reinterpret_cast<uint32_t*>(slot)[threadIdx.x] = threadIdx.x == 0 ? 8u * total : threadIdx.x < 4 ? 0u : hdr[threadIdx.x];
+        reinterpret_cast<uint32_t*>(slot)[threadIdx.x] =
+            threadIdx.x == 0 ? 8u * total : threadIdx.x == 1 ? slot_bad : threadIdx.x < 4 ? 0u : hdr[threadIdx.x];
     // each block's planes, parked in lanes and stored straight to their place
     uint32_t lm[8];
 #pragma unroll
@@ -279,7 +292,8 @@ __device__ __forceinline__ uint32_t planes_to_lanes(const dbp_u32x16& p, uint32_
     return z & ((1u << wc) - 1u);
 }
 
-__global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint32_t alpha, uint32_t slot_bytes) {
+__global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint32_t alpha, uint32_t slot_bytes,
+                                                             uint32_t* __restrict__ flags) {
     uint32_t band = 0;  // the band this slot belongs to (wave-uniform search over <= 16 entries)
     while (band + 1 < bands.count && blockIdx.x >= bands.first[band + 1]) ++band;
     const uint64_t n = bands.n[band];
@@ -291,6 +305,12 @@ __global__ __launch_bounds__(kDbpThreads) void k_dbp_unpack(DbpBands bands, uint
     const uint64_t base = (uint64_t)slot;
     const dbp_u32x4 r = dbp_u32x4{(uint32_t)base, (uint32_t)(base >> 32) & 0xFFFFu, slot_bytes, 0x00020000u};
     const uint32_t payload = dbp_s_load1(r, 0, 0);
+    // the sender's status travels in the slot: its alpha mark (header word 1) and an overflow (the payload count), so
+    // the display's own flags report a lossy frame (tri_xfer_synchronize on the display rank)
+    if (flags && threadIdx.x == 0) {
+        const uint32_t st = (dbp_s_load1(r, 4, 0) != 0u ? 1u : 0u) | (kDbpHeader + payload > slot_bytes ? 2u : 0u);
+        if (st) atomicOr(flags, st);
+    }
     // an overflowed slot (the sender flagged the frame), or more payload than the format has: left alone
     if (kDbpHeader + payload > slot_bytes || payload > kDbpMaxPayload) return;
     // lane l: block l's widths and plane count; the inclusive sum places every block's planes
@@ -344,17 +364,22 @@ bool vec_ok(const void* four, const void* three) { return ((uintptr_t)four & 15u
 }  // namespace
 
 hipError_t tri_launch_pack_bgr24(const uint32_t* src, uint8_t* dst, uint64_t n, uint32_t alpha, uint32_t* flag,
-                                 hipStream_t stream) {
+                                 hipStream_t stream, uint32_t* trailer) {
     if (n == 0) return hipSuccess;
-    if (vec_ok(src, dst)) hipLaunchKernelGGL(k_pack_bgr24<true>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha, flag);
-    else hipLaunchKernelGGL(k_pack_bgr24<false>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha, flag);
+    if (vec_ok(src, dst))
+        hipLaunchKernelGGL(k_pack_bgr24<true>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha, flag, trailer);
+    else
+        hipLaunchKernelGGL(k_pack_bgr24<false>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha, flag, trailer);
     return hipGetLastError();
 }
 
-hipError_t tri_launch_unpack_bgr24(const uint8_t* src, uint32_t* dst, uint64_t n, uint32_t alpha, hipStream_t stream) {
+hipError_t tri_launch_unpack_bgr24(const uint8_t* src, uint32_t* dst, uint64_t n, uint32_t alpha, hipStream_t stream,
+                                   const uint32_t* trailer, uint32_t* flags) {
     if (n == 0) return hipSuccess;
-    if (vec_ok(dst, src)) hipLaunchKernelGGL(k_unpack_bgr24<true>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha);
-    else hipLaunchKernelGGL(k_unpack_bgr24<false>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha);
+    if (vec_ok(dst, src))
+        hipLaunchKernelGGL(k_unpack_bgr24<true>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha, trailer, flags);
+    else
+        hipLaunchKernelGGL(k_unpack_bgr24<false>, codec_grid(n), dim3(kCodecBlock), 0, stream, src, dst, n, alpha, trailer, flags);
     return hipGetLastError();
 }
 
@@ -371,7 +396,7 @@ hipError_t tri_launch_dbp_pack(const uint32_t* src, uint64_t n, uint32_t alpha, 
 }
 
 hipError_t tri_launch_dbp_unpack_bands(const uint8_t* const* src, uint32_t* const* dst, const uint64_t* n, uint32_t count,
-                                       uint32_t alpha, uint32_t slot_bytes, hipStream_t stream) {
+                                       uint32_t alpha, uint32_t slot_bytes, hipStream_t stream, uint32_t* flags) {
     DbpBands b{};
     uint32_t grid = 0;
     for (uint32_t k = 0; k < count; ++k) {
@@ -384,7 +409,7 @@ hipError_t tri_launch_dbp_unpack_bands(const uint8_t* const* src, uint32_t* cons
     }
     b.first[b.count] = grid;
     if (grid == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dbp_unpack, dim3(grid), dim3(kDbpThreads), 0, stream, b, alpha, slot_bytes);
+    hipLaunchKernelGGL(k_dbp_unpack, dim3(grid), dim3(kDbpThreads), 0, stream, b, alpha, slot_bytes, flags);
     return hipGetLastError();
 }
 

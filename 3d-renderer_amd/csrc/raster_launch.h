@@ -140,17 +140,21 @@ hipError_t tri_run_plan(const TriFramePlan& plan, const TriLaunchArgs& args, Tri
 hipError_t tri_launch_blit(const uint32_t* src, int32_t w, int32_t h, uint32_t* dst, int32_t dw, int32_t dh,
                            const float* unorm_lut, hipStream_t stream);
 
-// The band codec (band_codec.hip): B8G8R8A8 <-> 3-byte BGR with a known alpha.
+// The band codec (band_codec.hip): B8G8R8A8 <-> 3-byte BGR with a known alpha. The sender's status reaches the
+// display with the band (tri_xfer): pack_bgr24 also ORs its alpha flag into `trailer` (a word after the packed pixels,
+// zero at allocation, sticky like the flags), which unpack_bgr24 ORs into the display's `flags`; a dbp slot carries
+// its own alpha mark (header word 1) and overflow (its payload count), which unpack ORs into `flags` (both nullable).
 hipError_t tri_launch_pack_bgr24(const uint32_t* src, uint8_t* dst, uint64_t n, uint32_t alpha, uint32_t* flag,
-                                 hipStream_t stream);
-hipError_t tri_launch_unpack_bgr24(const uint8_t* src, uint32_t* dst, uint64_t n, uint32_t alpha, hipStream_t stream);
+                                 hipStream_t stream, uint32_t* trailer = nullptr);
+hipError_t tri_launch_unpack_bgr24(const uint8_t* src, uint32_t* dst, uint64_t n, uint32_t alpha, hipStream_t stream,
+                                   const uint32_t* trailer = nullptr, uint32_t* flags = nullptr);
 hipError_t tri_launch_dbp_pack(const uint32_t* src, uint64_t n, uint32_t alpha, uint8_t* dst, uint32_t slot_bytes,
                                uint32_t* flags, hipStream_t stream);
 hipError_t tri_launch_dbp_unpack(const uint8_t* src, uint64_t n, uint32_t alpha, uint32_t slot_bytes, uint32_t* dst,
                                  hipStream_t stream);
 uint64_t tri_dbp_stream_bytes(uint64_t pixels, uint32_t slot_bytes);
 hipError_t tri_launch_dbp_unpack_bands(const uint8_t* const* src, uint32_t* const* dst, const uint64_t* n, uint32_t count,
-                                       uint32_t alpha, uint32_t slot_bytes, hipStream_t stream);
+                                       uint32_t alpha, uint32_t slot_bytes, hipStream_t stream, uint32_t* flags = nullptr);
 
 // Internal accessors for the group layer (tri_group.hip): a context's stream and device.
 hipStream_t tri_internal_stream(tri_ctx* ctx);

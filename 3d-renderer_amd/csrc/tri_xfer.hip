@@ -16,23 +16,69 @@
 // record/wait calls cost the host ≈ 2 µs each (tools/xfer_host_cost.py: a fenced version of this call took 26.8 µs
 // against 16 µs for the render alone). If a slot changes streams (a different context), it is fenced with events.
 // Band formats are tri_group's (TRI_GROUP_FMT_*): the delta bit-plane stream with the slot size every rank agreed,
-// 3-byte pixels, or 4.
+// 3-byte pixels, or 4. A packed band carries its sender's status (an alpha that broke the proof, a dbp slot that
+// overflowed), which the display's decode ORs into its own flags, so tri_xfer_synchronize on the display rank reports a
+// lossy frame as well as the sender's does.
+//
+// Fail-safe waits: tri_xfer_synchronize polls every slot's stream against a deadline (tri_xfer_set_timeout) and each
+// communicator's asynchronous error; on expiry or error it aborts the communicators (ncclCommAbort, which releases
+// kernels stuck in a transfer) and returns TRI_E_TIMEOUT, so a caller process exits instead of hanging its job.
+//
+// Loopback transport (tri_xfer_loopback, tests only): N exchanges of one process on one device stand in for N ranks,
+// because RCCL refuses two ranks on one GPU. A loopback communicator replaces ncclSend/ncclRecv and nothing else: the
+// sender records an event behind its pack and posts {buffer, bytes, event}; the display's receive waits for that event
+// and copies the bytes into the same receive buffer ncclRecv would fill, then records a "consumed" event that the
+// sender's next frame on the slot waits for (ncclSend's rendezvous: a sender's stream does not run past a send until it
+// is received). Everything else — the pack, the receive buffers, the batched decode and an assemble-only display's
+// own streams — is the code the N-GPU run executes. The caller drives the ranks frame by frame, senders before the
+// display (a receive whose send was not posted yet is TRI_E_STATE).
 #include "raster_launch.h"
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
+#include <deque>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 static_assert(sizeof(ncclUniqueId) == TRI_XFER_ID_BYTES, "tri_xfer: RCCL unique id size");
+
+namespace {
+struct LbMsg {  // one posted loopback send
+    const void* src = nullptr;
+    uint64_t bytes = 0;
+    hipEvent_t ready = nullptr, consumed = nullptr;
+    bool received = false;
+    ~LbMsg() {
+        if (ready) (void)hipEventDestroy(ready);
+        if (consumed) (void)hipEventDestroy(consumed);
+    }
+};
+}  // namespace
+
+struct tri_xfer_loopback {
+    uint32_t world = 0;
+    std::vector<uint32_t> made;  // communicators created per rank: the k-th of every rank forms channel k
+    // channel -> sender rank -> posted sends in order
+    std::vector<std::vector<std::deque<std::shared_ptr<LbMsg>>>> chan;
+};
 
 struct tri_xfer_comm {
     ncclComm_t comm = nullptr;
     int32_t device = 0;
     uint32_t world = 0, rank = 0;
+    tri_xfer_loopback* lb = nullptr;  // loopback transport (tests): the hub and this communicator's channel
+    uint32_t channel = 0;
+    bool aborted = false;
+    // a communicator shared by several slots (fewer communicators than frames in flight): its operations are fenced
+    // across streams (the stream of its last operation, and an event recorded after it)
+    hipStream_t last = nullptr;
+    hipEvent_t after = nullptr;
 };
 
 struct tri_xfer {
@@ -48,7 +94,10 @@ struct tri_xfer {
     std::vector<std::vector<uint8_t*>> rx;   // per slot, per rank: the display's received packed bands
     std::vector<hipStream_t> stream;         // per slot: the stream its last frame ran on
     std::vector<hipEvent_t> freed;           // per slot: fences a change of stream
-    uint32_t* flags = nullptr;               // the packer's [sticky flags, largest dbp slot]
+    uint32_t* flags = nullptr;               // [sticky flags, largest dbp slot]: this rank's packs, or on the display
+                                             // its decodes of the senders' status
+    std::vector<std::shared_ptr<LbMsg>> lb_sent;  // loopback: per slot, the last send its next frame waits for
+    uint32_t timeout_ms = 60000;             // tri_xfer_synchronize's deadline (0: none)
 };
 
 namespace {
@@ -77,7 +126,45 @@ uint64_t band_pixels(const tri_xfer* x, uint32_t r) { return (uint64_t)(x->y[r +
 uint64_t band_bytes(const tri_xfer* x, uint32_t r) {
     const uint64_t px = band_pixels(x, r);
     if (x->fmt == TRI_GROUP_FMT_DBP) return tri_dbp_stream_bytes(px, x->slot_bytes);
-    return px * (x->fmt == TRI_GROUP_FMT_BGR24 ? 3u : 4u);
+    // 3-byte bands end in a 16-B aligned status word (the sender's sticky alpha flag), so the display sees it
+    if (x->fmt == TRI_GROUP_FMT_BGR24) return (px * 3u + 15u) / 16u * 16u + 16u;
+    return px * 4u;
+}
+uint64_t bgr24_trailer(uint64_t px) { return (px * 3u + 15u) / 16u * 16u; }
+
+int lb_send(tri_xfer_comm* c, const void* src, uint64_t bytes, uint32_t peer, hipStream_t s, std::shared_ptr<LbMsg>& out) {
+    (void)peer;  // (the display; one receiver per channel)
+    auto m = std::make_shared<LbMsg>();
+    m->src = src;
+    m->bytes = bytes;
+    XH(hipEventCreateWithFlags(&m->ready, hipEventDisableTiming));
+    XH(hipEventCreateWithFlags(&m->consumed, hipEventDisableTiming));
+    XH(hipEventRecord(m->ready, s));
+    c->lb->chan[c->channel][c->rank].push_back(m);
+    out = m;
+    return TRI_OK;
+}
+
+int lb_recv(tri_xfer_comm* c, void* to, uint64_t bytes, uint32_t peer, hipStream_t s) {
+    auto& q = c->lb->chan[c->channel][peer];
+    if (q.empty()) return tri_internal_fail(TRI_E_STATE, "tri_xfer loopback: a sender has not posted this frame's band");
+    std::shared_ptr<LbMsg> m = q.front();
+    q.pop_front();
+    if (m->bytes != bytes) return tri_internal_fail(TRI_E_STATE, "tri_xfer loopback: send and receive sizes differ");
+    XH(hipStreamWaitEvent(s, m->ready, 0));
+    XH(hipMemcpyAsync(to, m->src, bytes, hipMemcpyDeviceToDevice, s));
+    XH(hipEventRecord(m->consumed, s));
+    m->received = true;
+    return TRI_OK;
+}
+
+void abort_comms(tri_xfer* x) {
+    for (tri_xfer_comm* c : x->xc)
+        if (c->comm && !c->aborted) {
+            (void)ncclCommAbort(c->comm);  // releases kernels blocked in a transfer; frees the communicator
+            c->comm = nullptr;
+            c->aborted = true;
+        }
 }
 
 }  // namespace
@@ -115,7 +202,37 @@ int tri_xfer_comm_destroy(tri_xfer_comm* xc) {
     if (!xc) return TRI_OK;
     (void)hipSetDevice(xc->device);
     if (xc->comm) (void)ncclCommDestroy(xc->comm);
+    if (xc->after) (void)hipEventDestroy(xc->after);
     delete xc;
+    return TRI_OK;
+}
+
+int tri_xfer_loopback_create(uint32_t world, tri_xfer_loopback** out) {
+    if (!out || world == 0) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_loopback_create: bad argument");
+    tri_xfer_loopback* lb = new tri_xfer_loopback();
+    lb->world = world;
+    lb->made.assign(world, 0u);
+    *out = lb;
+    return TRI_OK;
+}
+
+int tri_xfer_loopback_destroy(tri_xfer_loopback* lb) {
+    delete lb;
+    return TRI_OK;
+}
+
+int tri_xfer_comm_create_loopback(tri_xfer_loopback* lb, uint32_t rank, int32_t device, tri_xfer_comm** out) {
+    if (!lb || !out || rank >= lb->world) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_comm_create_loopback: bad argument");
+    *out = nullptr;
+    XH(hipSetDevice(device));
+    tri_xfer_comm* xc = new tri_xfer_comm();
+    xc->device = device;
+    xc->world = lb->world;
+    xc->rank = rank;
+    xc->lb = lb;
+    xc->channel = lb->made[rank]++;
+    if (lb->chan.size() <= xc->channel) lb->chan.resize(xc->channel + 1, std::vector<std::deque<std::shared_ptr<LbMsg>>>(lb->world));
+    *out = xc;
     return TRI_OK;
 }
 
@@ -144,8 +261,8 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
     *out = nullptr;
     for (uint32_t i = 0; i < ncomm; ++i)
         if (!comms[i] || comms[i]->world != comms[0]->world || comms[i]->rank != comms[0]->rank ||
-            comms[i]->device != comms[0]->device)
-            return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: the communicators differ in world, rank or device");
+            comms[i]->device != comms[0]->device || (comms[i]->lb == nullptr) != (comms[0]->lb == nullptr))
+            return tri_internal_fail(TRI_E_INVALID, "tri_xfer_create: the communicators differ in world, rank, device or transport");
     const uint32_t N = comms[0]->world;
     if (cfg->display >= N || cfg->nbuf == 0 || cfg->width == 0 || cfg->alpha > 255u ||
         cfg->format > TRI_GROUP_FMT_DBP ||
@@ -176,6 +293,7 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
     x->stream.assign(x->nbuf, nullptr);
     x->freed.assign(x->nbuf, nullptr);
     x->own.assign(x->nbuf, nullptr);  // created on first use: a rank that renders every frame never needs them
+    x->lb_sent.assign(x->nbuf, nullptr);
     for (uint32_t s = 0; s < x->nbuf; ++s) {
         if (hipEventCreateWithFlags(&x->freed[s], hipEventDisableTiming) != hipSuccess)
             return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: event creation failed"));
@@ -191,6 +309,12 @@ int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t ncomm, const tri_xfer_
     }
     if (hipMalloc(&x->flags, 8) != hipSuccess || hipMemset(x->flags, 0, 8) != hipSuccess)
         return bail(tri_internal_fail(TRI_E_OOM, "tri_xfer_create: flag allocation failed"));
+    if (packed && N > 1 && x->fmt == TRI_GROUP_FMT_BGR24 && x->rank != x->display)  // the status words start clear
+        for (uint32_t s = 0; s < x->nbuf; ++s)
+            if (hipMemset(x->stage[s] + bgr24_trailer(band_pixels(x, x->rank)), 0, 16) != hipSuccess)
+                return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: status word initialisation failed"));
+    // the null-stream memsets above are not ordered with the non-blocking streams that pack and decode: complete them
+    if (hipDeviceSynchronize() != hipSuccess) return bail(tri_internal_fail(TRI_E_HIP, "tri_xfer_create: synchronisation failed"));
     *out = x;
     return TRI_OK;
 }
@@ -220,6 +344,12 @@ int tri_xfer_frame(tri_xfer* x, uint32_t slot, tri_ctx* ctx, void* depth, const 
         XH(hipStreamWaitEvent(s, x->freed[slot], 0));
     }
     x->stream[slot] = s;
+    if (x->lb_sent[slot]) {  // loopback: the slot's previous send must be received before its buffers are reused
+        if (!x->lb_sent[slot]->received)
+            return tri_internal_fail(TRI_E_STATE, "tri_xfer loopback: the display has not received this slot's previous frame");
+        XH(hipStreamWaitEvent(s, x->lb_sent[slot]->consumed, 0));
+        x->lb_sent[slot].reset();
+    }
     if (ctx) {
         uint32_t* out = disp ? frame + (size_t)x->y[me] * x->W : frame;
         int rc = tri_bind_output(ctx, out, depth);
@@ -229,7 +359,15 @@ int tri_xfer_frame(tri_xfer* x, uint32_t slot, tri_ctx* ctx, void* depth, const 
         if (rc) return rc;
     }
     if (!exchange || N == 1) return TRI_OK;
-    ncclComm_t comm = x->xc[slot % x->xc.size()]->comm;
+    tri_xfer_comm* xc = x->xc[slot % x->xc.size()];
+    if (xc->aborted) return tri_internal_fail(TRI_E_STATE, "tri_xfer_frame: the communicator was aborted (a timed-out wait)");
+    // fewer communicators than slots: a communicator's operations on another stream are fenced behind its last ones
+    const bool shared = x->xc.size() < x->nbuf;
+    if (shared) {
+        if (!xc->after) XH(hipEventCreateWithFlags(&xc->after, hipEventDisableTiming));
+        if (xc->last && xc->last != s) XH(hipStreamWaitEvent(s, xc->after, 0));
+    }
+    ncclComm_t comm = xc->comm;
     if (!disp) {
         const void* src = frame;
         const uint64_t px = band_pixels(x, me);
@@ -237,53 +375,115 @@ int tri_xfer_frame(tri_xfer* x, uint32_t slot, tri_ctx* ctx, void* depth, const 
             XH(tri_launch_dbp_pack(frame, px, x->alpha, x->stage[slot], x->slot_bytes, x->flags, s));
             src = x->stage[slot];
         } else if (x->fmt == TRI_GROUP_FMT_BGR24) {
-            XH(tri_launch_pack_bgr24(frame, x->stage[slot], px, x->alpha, x->flags, s));
+            XH(tri_launch_pack_bgr24(frame, x->stage[slot], px, x->alpha, x->flags, s,
+                                     reinterpret_cast<uint32_t*>(x->stage[slot] + bgr24_trailer(px))));
             src = x->stage[slot];
         }
-        XN(ncclSend(src, band_bytes(x, me), ncclUint8, (int)x->display, comm, s));
-        return TRI_OK;
-    }
-    XN(ncclGroupStart());
-    for (uint32_t r = 0; r < N; ++r) {
-        if (r == me) continue;
-        void* to = x->fmt == TRI_GROUP_FMT_BGRA32 ? static_cast<void*>(frame + (size_t)x->y[r] * x->W)
-                                                  : static_cast<void*>(x->rx[slot][r]);
-        XN(ncclRecv(to, band_bytes(x, r), ncclUint8, (int)r, comm, s));
-    }
-    XN(ncclGroupEnd());
-    if (x->fmt == TRI_GROUP_FMT_DBP) {  // every remote band in one launch (up to TRI_DBP_MAX_BANDS)
-        const uint8_t* from[TRI_DBP_MAX_BANDS];
-        uint32_t* to[TRI_DBP_MAX_BANDS];
-        uint64_t npx[TRI_DBP_MAX_BANDS];
-        uint32_t k = 0;
+        if (xc->lb) {
+            const int rc = lb_send(xc, src, band_bytes(x, me), x->display, s, x->lb_sent[slot]);
+            if (rc) return rc;
+        } else {
+            XN(ncclSend(src, band_bytes(x, me), ncclUint8, (int)x->display, comm, s));
+        }
+    } else {
+        if (!xc->lb) XN(ncclGroupStart());
         for (uint32_t r = 0; r < N; ++r) {
             if (r == me) continue;
-            from[k] = x->rx[slot][r];
-            to[k] = frame + (size_t)x->y[r] * x->W;
-            npx[k] = band_pixels(x, r);
-            if (++k == TRI_DBP_MAX_BANDS) {
-                XH(tri_launch_dbp_unpack_bands(from, to, npx, k, x->alpha, x->slot_bytes, s));
-                k = 0;
+            void* to = x->fmt == TRI_GROUP_FMT_BGRA32 ? static_cast<void*>(frame + (size_t)x->y[r] * x->W)
+                                                      : static_cast<void*>(x->rx[slot][r]);
+            if (xc->lb) {
+                const int rc = lb_recv(xc, to, band_bytes(x, r), r, s);
+                if (rc) return rc;
+            } else {
+                XN(ncclRecv(to, band_bytes(x, r), ncclUint8, (int)r, comm, s));
             }
         }
-        if (k) XH(tri_launch_dbp_unpack_bands(from, to, npx, k, x->alpha, x->slot_bytes, s));
-    } else if (x->fmt == TRI_GROUP_FMT_BGR24) {
-        for (uint32_t r = 0; r < N; ++r)
-            if (r != me)
-                XH(tri_launch_unpack_bgr24(x->rx[slot][r], frame + (size_t)x->y[r] * x->W, band_pixels(x, r), x->alpha, s));
+        if (!xc->lb) XN(ncclGroupEnd());
+        if (x->fmt == TRI_GROUP_FMT_DBP) {  // every remote band in one launch (up to TRI_DBP_MAX_BANDS)
+            const uint8_t* from[TRI_DBP_MAX_BANDS];
+            uint32_t* to[TRI_DBP_MAX_BANDS];
+            uint64_t npx[TRI_DBP_MAX_BANDS];
+            uint32_t k = 0;
+            for (uint32_t r = 0; r < N; ++r) {
+                if (r == me) continue;
+                from[k] = x->rx[slot][r];
+                to[k] = frame + (size_t)x->y[r] * x->W;
+                npx[k] = band_pixels(x, r);
+                if (++k == TRI_DBP_MAX_BANDS) {
+                    XH(tri_launch_dbp_unpack_bands(from, to, npx, k, x->alpha, x->slot_bytes, s, x->flags));
+                    k = 0;
+                }
+            }
+            if (k) XH(tri_launch_dbp_unpack_bands(from, to, npx, k, x->alpha, x->slot_bytes, s, x->flags));
+        } else if (x->fmt == TRI_GROUP_FMT_BGR24) {
+            for (uint32_t r = 0; r < N; ++r)
+                if (r != me) {
+                    const uint64_t px = band_pixels(x, r);
+                    XH(tri_launch_unpack_bgr24(x->rx[slot][r], frame + (size_t)x->y[r] * x->W, px, x->alpha, s,
+                                               reinterpret_cast<const uint32_t*>(x->rx[slot][r] + bgr24_trailer(px)),
+                                               x->flags));
+                }
+        }
+    }
+    if (shared) {
+        XH(hipEventRecord(xc->after, s));
+        xc->last = s;
+    }
+    return TRI_OK;
+}
+
+int tri_xfer_set_timeout(tri_xfer* x, uint32_t timeout_ms) {
+    if (!x) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_set_timeout: null exchange");
+    x->timeout_ms = timeout_ms;
+    return TRI_OK;
+}
+
+int tri_xfer_wait(tri_xfer* x) {
+    if (!x) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_wait: null exchange");
+    XH(hipSetDevice(x->device));
+    // every slot's stream, polled against the deadline together with the communicators' asynchronous errors: a
+    // transfer whose peer never comes (a dead or diverged rank) must end the caller, not hang the whole job
+    const auto t0 = std::chrono::steady_clock::now();
+    for (hipStream_t st : x->stream) {
+        if (!st) continue;
+        for (;;) {
+            const hipError_t e = hipStreamQuery(st);
+            if (e == hipSuccess) break;
+            if (e != hipErrorNotReady) return xfail(e, "tri_xfer_wait: hipStreamQuery");
+            for (tri_xfer_comm* c : x->xc) {
+                ncclResult_t ae = ncclSuccess;
+                if (c->comm && ncclCommGetAsyncError(c->comm, &ae) == ncclSuccess && ae != ncclSuccess && ae != ncclInProgress) {
+                    abort_comms(x);
+                    return nfail(ae, "tri_xfer_wait: a communicator failed (aborted)");
+                }
+            }
+            const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+            if (x->timeout_ms && ms > (double)x->timeout_ms) {
+                abort_comms(x);
+                return tri_internal_fail(TRI_E_TIMEOUT, "tri_xfer_wait: the exchange did not complete before the "
+                                                        "deadline (communicators aborted)");
+            }
+            // (spinning for the first 2 ms: a timed region's closing wait must not add a sleep's granularity)
+            if (ms < 2.0) std::this_thread::yield();
+            else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        }
     }
     return TRI_OK;
 }
 
 int tri_xfer_synchronize(tri_xfer* x) {
-    if (!x) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_synchronize: null exchange");
-    XH(hipSetDevice(x->device));
-    for (hipStream_t st : x->stream)
-        if (st) XH(hipStreamSynchronize(st));
+    const int rc = tri_xfer_wait(x);
+    if (rc) return rc;
     uint32_t f[2] = {0, 0};
     XH(hipMemcpy(f, x->flags, 8, hipMemcpyDeviceToHost));
     if (f[0] & 1u) return tri_internal_fail(TRI_E_STATE, "tri_xfer: a band's alpha was not the proven value (lossy packed transfer)");
     if (f[0] & 2u) return tri_internal_fail(TRI_E_OVERFLOW, "tri_xfer: a band outgrew the agreed dbp slot size (lossy transfer)");
+    return TRI_OK;
+}
+
+int tri_xfer_comm_count(tri_xfer* x, uint32_t* count) {
+    if (!x || !count) return tri_internal_fail(TRI_E_INVALID, "tri_xfer_comm_count: null argument");
+    *count = (uint32_t)x->xc.size();
     return TRI_OK;
 }
 

@@ -100,6 +100,12 @@ public:
     void SetPresentExtent(uint32_t width, uint32_t height) { m_PresentWidth = width; m_PresentHeight = height; }
     // The last presented image (RGBA8 rows, BGRA reordered) and its size; false before a present.
     bool ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height);
+    // Wait for the frame the last DrawFrame submitted (its viewport passes and present blit), re-rendering a pass
+    // that outgrew the internal queues. DrawFrame itself calls it first, for the previous frame — the reference waits
+    // for the previous frame's timeline value at the start of DrawFrame (Renderer.cpp:752-772) — so the caller's host
+    // work between frames overlaps the GPU. The readers (ReadViewportPixels, ReadPresentPixels, GetViewportTexture)
+    // call it on demand.
+    void FinishFrame();
     uint32_t GetActiveViewportId() const { return m_ActiveViewportId; }
     ViewportInfo GetViewport() const;
     // Vulkan returned a VkDescriptorSet for ImGui (Renderer.h:235); here: an opaque handle, a pointer to
@@ -260,6 +266,14 @@ private:
     // the extent the last present was produced at (SetPresentExtent may change before ReadPresentPixels)
     uint32_t m_PresentedWidth = 0, m_PresentedHeight = 0;
     uint32_t m_RasterFlags = 0;
+    struct PendingFrame {  // what the last DrawFrame submitted and FinishFrame has not waited for yet
+        bool m_Active = false;
+        std::vector<ViewportContext*> m_Targets;
+        ViewportContext* m_Legacy = nullptr;  // the legacy present target among them
+        ViewportContext* m_Blit = nullptr;    // the primary viewport whose present blit was enqueued
+        uint32_t m_BlitWidth = 0, m_BlitHeight = 0;
+    };
+    PendingFrame m_Pending;
 
     glm::vec3 m_AmbientColor{0.03f};
     float m_AmbientIntensity = 1.0f;

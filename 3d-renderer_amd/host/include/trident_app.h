@@ -113,6 +113,8 @@ int trident_app_submit_ai_frame(trident_app* app, const float* pixels, uint32_t 
 int trident_app_read_present(trident_app* app, uint8_t* rgba, uint32_t width, uint32_t height);
 
 int trident_app_draw_frame(trident_app* app);
+/* Renderer::FinishFrame: wait for the frame the last draw_frame submitted (the next draw_frame does it first). */
+int trident_app_finish_frame(trident_app* app);
 /* Renderer::GetViewportTexture: copies the viewport's image handle (TRI_E_STATE before its first frame). */
 int trident_app_viewport_texture(trident_app* app, uint32_t viewport_id, tri_image* out);
 /* Renderer::GetGeometryUploadCount. */

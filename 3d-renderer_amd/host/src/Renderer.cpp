@@ -216,6 +216,7 @@ void Renderer::Init() {
 }
 
 void Renderer::DestroyViewportTargets() {
+    m_Pending = PendingFrame{};  // (its targets go; tri_destroy / tri_group_destroy wait for their streams)
     for (auto& it : m_Viewports) {
         ViewportContext& vc = it.second;
         tri_destroy(vc.m_Ctx);
@@ -994,6 +995,7 @@ bool Renderer::SubmitTarget(ViewportContext& vc, const tri_global_ubo& ubo, cons
 void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     const auto t0 = std::chrono::steady_clock::now();
     if (!m_Initialised || m_Shutdown) return;
+    FinishFrame();  // the previous frame's fence (Renderer.cpp:752-772)
     GatherDraws();
     PrepareBonePaletteBuffer();
     std::vector<tri_draw> draws;
@@ -1039,39 +1041,68 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
             }
         }
     }
-    // Frame fence (Renderer.cpp:744-760). A frame that outgrew the bin/clip queues has grown them
-    // inside tri_synchronize and is re-rendered, so a presented frame is always complete.
-    for (ViewportContext* vc : submitted) {
+    // Primary viewport -> swapchain image, VK_FILTER_LINEAR (Renderer.cpp:5346-5361), stream-ordered behind its pass.
+    m_Pending = PendingFrame{};
+    m_Pending.m_Targets = submitted;
+    m_Pending.m_Legacy = legacy;
+    if (primaryActive && m_PresentWidth && m_PresentHeight) {
+        const Target t{active->second.m_Ctx, active->second.m_Group};
+        if (t.Blit(m_PresentWidth, m_PresentHeight) == TRI_OK) {
+            m_Pending.m_Blit = &active->second;
+            m_Pending.m_BlitWidth = m_PresentWidth;
+            m_Pending.m_BlitHeight = m_PresentHeight;
+        } else {
+            LogError("present blit", tri_last_error());
+        }
+    }
+    m_Pending.m_Active = true;
+    // no wait here: the next DrawFrame (or a reader) fences this frame, as the reference fences the previous
+    // frame's timeline value at the start of DrawFrame (Renderer.cpp:752-772)
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    RecordFrameTiming(ms);
+}
+
+void Renderer::FinishFrame() {  // the frame fence (Renderer.cpp:744-772)
+    if (!m_Pending.m_Active) return;
+    PendingFrame p = std::move(m_Pending);
+    m_Pending = PendingFrame{};
+    // A frame that outgrew the bin/clip queues has grown them inside tri_synchronize and is re-rendered (and its
+    // present blit redone), so a presented frame is always complete.
+    for (ViewportContext* vc : p.m_Targets) {
         const Target t{vc->m_Ctx, vc->m_Group};
         int rc = t.Sync();
+        bool rerendered = false;
         for (int retry = 0; rc == TRI_E_OVERFLOW && retry < 3; ++retry) {
             rc = t.Render();
             if (rc == TRI_OK) rc = t.Sync();
+            rerendered = true;
         }
         if (rc != TRI_OK) LogError("frame fence", tri_last_error());
         if (rc == TRI_OK) vc->m_HasImage = t.Output(&vc->m_Image) == TRI_OK;  // a re-render moves a group's buffer
-        if (vc == legacy && rc == TRI_OK) {
+        if (vc == p.m_Legacy && rc == TRI_OK) {
             m_PresentSource = vc->m_Ctx;
             m_PresentGroup = vc->m_Group;
             m_PresentLegacy = true;
             m_PresentedWidth = (uint32_t)vc->m_Info.Size.x;  // the target PrepareViewport sized
             m_PresentedHeight = (uint32_t)vc->m_Info.Size.y;
         }
+        if (vc == p.m_Blit && rc != TRI_OK) p.m_Blit = nullptr;
+        if (vc == p.m_Blit && rerendered && t.Blit(p.m_BlitWidth, p.m_BlitHeight) != TRI_OK) {
+            LogError("present blit", tri_last_error());
+            p.m_Blit = nullptr;
+        }
     }
-    // Primary viewport -> swapchain image, VK_FILTER_LINEAR (Renderer.cpp:5346-5361).
-    if (primaryActive && m_PresentWidth && m_PresentHeight) {
-        const Target t{active->second.m_Ctx, active->second.m_Group};
-        if (t.Blit(m_PresentWidth, m_PresentHeight) == TRI_OK && t.Sync() == TRI_OK) {
-            m_PresentSource = active->second.m_Ctx;
-            m_PresentGroup = active->second.m_Group;
-            m_PresentedWidth = m_PresentWidth;  // the blit's destination extent
-            m_PresentedHeight = m_PresentHeight;
+    if (p.m_Blit) {
+        const Target t{p.m_Blit->m_Ctx, p.m_Blit->m_Group};
+        if (t.Sync() == TRI_OK) {
+            m_PresentSource = p.m_Blit->m_Ctx;
+            m_PresentGroup = p.m_Blit->m_Group;
+            m_PresentedWidth = p.m_BlitWidth;  // the blit's destination extent
+            m_PresentedHeight = p.m_BlitHeight;
         } else {
             LogError("present blit", tri_last_error());
         }
     }
-    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    RecordFrameTiming(ms);
 }
 
 void Renderer::RecordFrameTiming(double ms) {  // Renderer.cpp:6286-6343
@@ -1102,12 +1133,14 @@ void Renderer::RecordFrameTiming(double ms) {  // Renderer.cpp:6286-6343
 }
 
 void* Renderer::GetViewportTexture(uint32_t viewportId) const {
+    const_cast<Renderer*>(this)->FinishFrame();  // the handle's contents are a completed frame
     auto it = m_Viewports.find(viewportId);
     if (it == m_Viewports.end() || (!it->second.m_Ctx && !it->second.m_Group) || !it->second.m_HasImage) return nullptr;
     return const_cast<tri_image*>(&it->second.m_Image);
 }
 
 bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgba, std::vector<float>* depth) {
+    FinishFrame();
     auto it = m_Viewports.find(viewportId);
     if (it == m_Viewports.end() || (!it->second.m_Ctx && !it->second.m_Group)) return false;
     ViewportContext& vc = it->second;
@@ -1133,6 +1166,7 @@ bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgb
 }
 
 bool Renderer::ReadPresentPixels(std::vector<uint8_t>& rgba, uint32_t& width, uint32_t& height) {
+    FinishFrame();
     if (!m_PresentSource && !m_PresentGroup) return false;
     // sized from the extent the present was produced at, not the current SetPresentExtent (a resize between
     // DrawFrame and this read would otherwise under-size the buffer the readback fills)

@@ -519,6 +519,13 @@ int trident_app_draw_frame(trident_app* app) {
     });
 }
 
+int trident_app_finish_frame(trident_app* app) {
+    return Guard(app, [&] {
+        app->renderer.FinishFrame();
+        return TRI_OK;
+    });
+}
+
 int trident_app_read_pixels(trident_app* app, uint32_t viewport_id, uint8_t* rgba, float* depth) {
     return Guard(app, [&] {
         if (!rgba) return TRI_E_INVALID;

@@ -18,6 +18,7 @@ TRI_E_OOM = -3
 TRI_E_OVERFLOW = -4
 TRI_E_UNSUPPORTED = -5
 TRI_E_STATE = -6
+TRI_E_TIMEOUT = -7
 
 TRI_MAX_POINT_LIGHTS = 8
 TRI_MAX_TEXTURE_SLOTS = 256
@@ -250,7 +251,13 @@ CABI_FUNCTIONS = [
     ("tri_xfer_frame", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
                                  C.c_uint32, C.c_uint32]),
     ("tri_xfer_synchronize", C.c_int, [C.c_void_p]),
+    ("tri_xfer_wait", C.c_int, [C.c_void_p]),
+    ("tri_xfer_set_timeout", C.c_int, [C.c_void_p, C.c_uint32]),
+    ("tri_xfer_comm_count", C.c_int, [C.c_void_p, C.POINTER(C.c_uint32)]),
     ("tri_xfer_info", C.c_int, [C.c_void_p, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64), C.POINTER(C.c_uint32)]),
+    ("tri_xfer_loopback_create", C.c_int, [C.c_uint32, C.POINTER(C.c_void_p)]),
+    ("tri_xfer_loopback_destroy", C.c_int, [C.c_void_p]),
+    ("tri_xfer_comm_create_loopback", C.c_int, [C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(C.c_void_p)]),
     ("tri_dbp_unpack_bands", C.c_int, [C.POINTER(C.c_void_p), C.POINTER(C.c_void_p), C.POINTER(C.c_uint64), C.c_uint32,
                                        C.c_uint32, C.c_uint32, C.c_void_p]),
     ("tri_set_timing", C.c_int, [C.c_void_p, C.c_int]),

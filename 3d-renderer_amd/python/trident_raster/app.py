@@ -51,6 +51,7 @@ _APP_FUNCTIONS = [
     ("trident_app_set_clear_color", C.c_int, [C.c_void_p, _f3]),
     ("trident_app_set_skybox", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("trident_app_draw_frame", C.c_int, [C.c_void_p]),
+    ("trident_app_finish_frame", C.c_int, [C.c_void_p]),
     ("trident_app_read_pixels", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("trident_app_frame_inputs", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(abi.TriGlobalUbo), C.c_void_p, C.c_uint32,
                                            C.POINTER(C.c_uint32)]),
@@ -233,6 +234,10 @@ class TridentApp:
 
     def draw_frame(self):
         _check(self._lib.trident_app_draw_frame(self._h), "draw_frame")
+
+    def finish_frame(self):
+        """Wait for the last draw_frame's frame (Renderer::FinishFrame; the next draw_frame does it first)."""
+        _check(self._lib.trident_app_finish_frame(self._h), "finish_frame")
 
     def read_pixels(self, viewport_id, width, height, depth=True):
         rgba = np.zeros((height, width, 4), np.uint8)

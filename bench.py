@@ -466,11 +466,15 @@ class GatherRing:
 
 _XFER_COMMS = []
 XFER_COMMS = 3  # one RCCL communicator per frame in flight (the most the bench uses), each used on one stream
+XFER_TIMEOUT_MS = 60000  # tri_xfer_set_timeout: a wait that outlasts it aborts the communicators and raises
 
 
 def xfer_comms(lib, world, rank, device_index, dev):
     """The process's RCCL communicators for tri_xfer (the native band exchange), created once: for each, rank 0 draws
-    a unique id, torch.distributed broadcasts its 128 bytes, and every rank joins (collective). Destroyed at exit."""
+    a unique id, torch.distributed broadcasts its 128 bytes, and every rank joins (collective). If a later
+    communicator cannot be created on some rank (the outcome is agreed over ranks after each), the exchange runs on
+    the ones made so far: tri_xfer fences a communicator that several frames in flight share.
+    Destroyed at exit."""
     import atexit
     import ctypes as C
 
@@ -480,7 +484,7 @@ def xfer_comms(lib, world, rank, device_index, dev):
 
     if _XFER_COMMS:
         return _XFER_COMMS
-    for _ in range(XFER_COMMS):
+    for k in range(XFER_COMMS):
         uid = (C.c_uint8 * 128)()
         if rank == 0:
             raster._check(lib.tri_xfer_unique_id(uid))
@@ -488,10 +492,31 @@ def xfer_comms(lib, world, rank, device_index, dev):
         dist.broadcast(t, src=0)
         uid = (C.c_uint8 * 128)(*t.cpu().tolist())
         comm = C.c_void_p()
-        raster._check(lib.tri_xfer_comm_create(uid, world, rank, device_index, C.byref(comm)))
+        rc = lib.tri_xfer_comm_create(uid, world, rank, device_index, C.byref(comm))
+        if rc and k == 0:
+            raster._check(rc)  # no communicator at all: the caller's fallback (torch.distributed) takes over
+        failed = max_over_ranks(1.0 if rc else 0.0, dev, True)
+        if failed:
+            if not rc:
+                lib.tri_xfer_comm_destroy(comm)
+            print(f"bench.py: WARNING: RCCL communicator {k + 1} of {XFER_COMMS} could not be created; the native "
+                  f"exchange shares {k} communicator(s) across its frames in flight", file=sys.stderr, flush=True)
+            break
         _XFER_COMMS.append(comm)
     atexit.register(lambda: [lib.tri_xfer_comm_destroy(c) for c in _XFER_COMMS])
     return _XFER_COMMS
+
+
+def arm_watchdog(seconds, phase):
+    """N > 1: a host-side deadline for one phase of the run. If the phase does not finish in time (a rank stuck in
+    a collective's host call, where no device-side deadline reaches), dump every thread's stack and exit the process
+    non-zero, so torchrun ends the job instead of leaving 8 GPUs waiting. Re-armed at each phase; 0 disarms."""
+    import faulthandler
+
+    faulthandler.cancel_dump_traceback_later()
+    if seconds > 0:
+        print(f"bench.py: phase '{phase}' (watchdog {seconds:.0f} s)", file=sys.stderr, flush=True)
+        faulthandler.dump_traceback_later(seconds, exit=True)
 
 
 class BandRenderer:
@@ -575,7 +600,7 @@ class BandRenderer:
         # torch.distributed's point-to-point calls cost the host ~20 us each (tools/p2p_host_cost.py), which at
         # N = 8 would bind the display rank far below one GPU's frame rate. The GatherRing above stays the
         # exchange for --exchange torch, the all-gather and the gloo tests.
-        self.xfer, self._kx = None, 0
+        self.xfer, self._kx, self.xfer_comms = None, 0, 0
         if native:
             self._attach_xfer(device_index)
         self.frames = 0
@@ -601,6 +626,8 @@ class BandRenderer:
         carr = (C.c_void_p * len(comms))(*[c.value for c in comms])
         self._raster._check(lib.tri_xfer_create(carr, len(comms), C.byref(cfg), C.byref(x)))
         self.xfer = x
+        self._raster._check(lib.tri_xfer_set_timeout(x, XFER_TIMEOUT_MS))
+        self.xfer_comms = len(comms)
         for s, b in enumerate(self.xbufs):
             self._raster._check(lib.tri_xfer_bind_slot(x, s, C.c_void_p(b.data_ptr())))
 
@@ -717,9 +744,14 @@ class BandRenderer:
         with torch.cuda.stream(self.streams[0]):
             self.ring.drain()
 
-    def _sync(self):
+    def _sync(self, check=False):
+        """Device synchronisation; with the native exchange, first its bounded wait (TRI_E_TIMEOUT raises instead of
+        hanging on a transfer whose peer never comes), and with check its status flags (a lossy band raises)."""
         import torch
 
+        if self.xfer is not None:
+            f = self._lib.tri_xfer_synchronize if check else self._lib.tri_xfer_wait
+            self._raster._check(f(self.xfer))
         if self.dev.type == "cuda":
             torch.cuda.synchronize(self.dev)
 
@@ -848,11 +880,11 @@ class BandRenderer:
         self.drain()
         ts = []
         for _ in range(frames):
-            torch.cuda.synchronize(self.dev)
+            self._sync()
             t0 = time.perf_counter()
             self.step()
             self.drain()
-            torch.cuda.synchronize(self.dev)
+            self._sync()
             ts.append((time.perf_counter() - t0) * 1e3)
         ts.sort()
         return ts[len(ts) // 2]
@@ -890,8 +922,7 @@ def measure_fps(br, frames, dist_on):
     import torch
 
     def sync():
-        if br.dev.type == "cuda":
-            torch.cuda.synchronize(br.dev)
+        br._sync()
 
     br.drain()
     sync()
@@ -1004,19 +1035,20 @@ def rebalance_split(make, display_rows, inflight, dist_on, frames=80, rounds=2, 
     return (tuple(sizes) if best[1] > best[0] else display_rows), log
 
 
-def verify_assembly(br, scene, dist_on):
-    """N > 1 parity in the bench itself: one frame through the band exchange, and on the display rank the assembled
-    frame against the same frame rendered whole by one context on that GPU (bit for bit: a band context's pixels are
-    the full frame's). Every rank learns the outcome (a max over ranks). Returns a dict for the
-    bench line's assembly object."""
+def verify_assembly(br, scene, dist_on, frames=1, agree=True):
+    """N > 1 parity in the bench itself: `frames` frames through the band exchange back to back (with several frames
+    in flight every communicator and stream is exercised at once), and on the display rank the last assembled frame
+    against the same frame rendered whole by one context on that GPU (bit for bit: a band context's pixels are the
+    full frame's). With agree, every rank learns the outcome (a max over ranks); without, the
+    caller agrees on "bad" (guarded() does, together with any exception). Returns a dict for the bench line's assembly
+    object."""
     import numpy as np
-    import torch
     from trident_raster import raster, scenes
 
-    br.step()
+    for _ in range(frames):
+        br.step()
     br.drain()
-    torch.cuda.synchronize(br.dev)
-    br.check()
+    br._sync(check=True)  # bounded, and every band lossless (the display sees the senders' status too)
     bad = 0.0
     note = "not the display rank"
     if br.rank == 0:
@@ -1028,8 +1060,30 @@ def verify_assembly(br, scene, dist_on):
         diff = int((got != want).any(-1).sum())
         bad = float(diff)
         note = f"{diff} of {scene.width * scene.height} pixels differ from the one-context frame"
-    bad = max_over_ranks(bad, br.dev, dist_on)
-    return {"bit_exact": bad == 0.0, "detail": note}
+    if agree:
+        bad = max_over_ranks(bad, br.dev, dist_on)
+    return {"bit_exact": bad == 0.0, "detail": note, "bad": bad, "frames": frames}
+
+
+def guarded_call(what, fn, device, dist_on, rank=0, bad=lambda out: 0.0):
+    """Run fn() on every rank; an exception on any rank (a failed or timed-out native exchange: every wait is
+    bounded) or a nonzero bad(out) is agreed over ranks in ONE collective after fn, and every rank then returns
+    (ok, out or the failure detail) together, so the ranks' collective sequences stay aligned. fn's own collectives
+    must not depend on the outcome."""
+    try:
+        out, err = fn(), None
+    except Exception as e:  # noqa: BLE001 - any failure of the native path is reported and replaced
+        out, err = None, f"{what}: {type(e).__name__}: {str(e)[:200]}"
+        print(f"bench.py: rank {rank}: {err}", file=sys.stderr, flush=True)
+    mine = 1e30 if err else float(bad(out))
+    worst = max_over_ranks(mine, device, dist_on)
+    if worst == 0.0:
+        return True, out
+    if err:
+        return False, err
+    if mine and isinstance(out, dict) and "detail" in out:
+        return False, f"{what}: {out['detail']}"
+    return False, f"{what}: failed on another rank ({worst:g})"
 
 
 def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, warm_seconds=0.25):
@@ -1053,7 +1107,7 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, w
     for _ in range(max(warmup, 1)):
         br.step()
     br.drain()
-    torch.cuda.synchronize(br.dev)
+    br._sync(check=True)  # (N > 1: a lossy band fails here, before any frame is counted)
     el = time.perf_counter() - t0
     # every rank runs the same number of frames (each one ends in a collective): the extra frames that
     # fill warm_seconds at the rate just measured, the maximum over ranks
@@ -1066,12 +1120,12 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, w
     batch, prev = max(steps, 20), None
     for _ in range(8):
         br.drain()
-        torch.cuda.synchronize(br.dev)
+        br._sync()
         tb = time.perf_counter()
         for _ in range(batch):
             br.step()
         br.drain()
-        torch.cuda.synchronize(br.dev)
+        br._sync()
         cur = max_over_ranks(time.perf_counter() - tb, br.dev, dist_on)
         extra += batch
         if prev is not None and abs(cur - prev) <= 0.02 * prev:
@@ -1080,7 +1134,7 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, w
     n_warm = max(warmup, 1) + extra
     br.drain()
     br.synchronize()
-    torch.cuda.synchronize(br.dev)
+    br._sync(check=True)
     if dist_on:
         import torch.distributed as dist
 
@@ -1089,7 +1143,7 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, w
     for _ in range(steps):
         br.step()
     br.drain()
-    torch.cuda.synchronize(br.dev)
+    br._sync()  # (the native exchange's bounded wait, then the device; no flag read inside the timed region)
     if dist_on:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -1103,6 +1157,71 @@ def timed_run(br, steps, warmup, dist_on, stage_timing=True, event_frames=256, w
         timing = br.r.timing()
         br.r.set_timing(False)
     return max_over_ranks(dt, br.dev, dist_on), timing, n_warm
+
+
+# Trident-Forge's editor frame: the Scene and Game viewport panels of the reference's own
+# screenshot (Screenshots/Screenshot1.png: 992 x 1078 and 1064 x 1078 inside a 2559 x 1439 window, the extent the
+# swapchain blit fills; tests/test_reference_frame.py crops the same panels)
+FORGE_PANELS = {"viewports": ((2, 1064, 1078), (1, 992, 1078)), "present": (2559, 1439)}
+FORGE_4K = {"viewports": ((1, 3840, 2160),), "present": (3840, 2160)}
+
+
+def forge_frame(layout, frames=200, warm_seconds=0.25):
+    """The frame Forge runs, through the engine API rather than the C-ABI: RenderCommand::DrawFrame on the
+    Trident::Renderer shim (trident_app) with C3's 1M-triangle grid as one mesh entity, C3's sun and four point
+    lights, the editor camera on the Scene viewport and a ready runtime camera on the Game viewport, the cubemap found
+    by Init's discovery, and the present blit of the primary viewport (Renderer.cpp:733-837, :5208-5221, :5346-5361).
+    Every DrawFrame gathers the draws, packs the uniform block per viewport, renders each viewport, blits, and waits
+    for the previous frame first (the reference's fence, :752-772). Returns frames/s (DrawFrames completed per second)
+    and the host cost of one DrawFrame: with the GPU idle (the engine's own work plus the launches) and as the
+    renderer's GetFrameTimingStats record it in the loop (which includes the wait for the previous frame)."""
+    from trident_raster import app, scenes
+
+    s = build_scene("c3")
+    a = app.TridentApp()
+    try:
+        a.set_assets_dir(scenes.ASSETS_DIR)
+        mi = a.append_mesh(s.vertices, s.indices, base_color=(1.0, 1.0, 1.0, 1.0), metallic=0.1, roughness=0.6)
+        a.add_mesh_entity("none", mi)
+        a.add_light("directional", direction=(-0.5, -1.0, -0.3), intensity=3.0)
+        for k, (px, py) in enumerate([(-3.0, 1.5), (3.0, 1.5), (-3.0, -1.5), (3.0, -1.5)]):
+            a.add_light("point", position=(px, py, -2.5), color=(1.0, 0.9 - 0.1 * k, 0.7 + 0.1 * k),
+                        intensity=3.0 + k, range=8.0)
+        a.set_camera("editor", (0.0, 0.0, 0.0), (0.0, 0.0, 0.0), fov=60.0, near=0.1, far=1000.0)
+        a.set_camera("runtime", (0.3, -0.2, 0.5), (4.0, 6.0, 0.0), fov=60.0, near=0.1, far=1000.0)
+        for vid, w, h in layout["viewports"]:  # the last one set is the active (primary) viewport
+            a.set_viewport(vid, w, h)
+        a.set_present_extent(*layout["present"])
+        a.draw_frame()
+        a.finish_frame()
+        t_end = time.perf_counter() + warm_seconds
+        while time.perf_counter() < t_end:
+            a.draw_frame()
+        a.finish_frame()
+        idle = []
+        for _ in range(20):  # DrawFrame's host work with nothing to wait for
+            a.finish_frame()
+            t0 = time.perf_counter()
+            a.draw_frame()
+            idle.append((time.perf_counter() - t0) * 1e3)
+        a.finish_frame()
+        t0 = time.perf_counter()
+        for _ in range(frames):
+            a.draw_frame()
+        a.finish_frame()
+        dt = time.perf_counter() - t0
+        timing = a.frame_timing()
+        idle.sort()
+        px = sum(w * h for _, w, h in layout["viewports"])
+        return {"frames_per_s": frames / dt, "ms_per_frame": dt * 1e3 / frames,
+                "viewports": [[w, h] for _, w, h in layout["viewports"]], "present": list(layout["present"]),
+                "mpix_rendered_per_s": frames / dt * px / 1e6, "frames": frames,
+                "host_ms_per_drawframe_idle_gpu": idle[len(idle) // 2],
+                "drawframe_ms_avg_frame_timing_stats": timing["avg_ms"],
+                "triangles": s.triangles,
+                "path": "RenderCommand::DrawFrame (Trident::Renderer shim, trident_app) -> tri_raster C-ABI"}
+    finally:
+        a.close()
 
 
 def device_copy_gbs(device, nbytes=1 << 29, reps=10):
@@ -1302,6 +1421,9 @@ def main():
                          "'equal', or the display rank's row count")
     ap.add_argument("--inflight-candidates", default="2,3",
                     help="N > 1 with --split auto: the frames-in-flight counts the autotune tries")
+    ap.add_argument("--watchdog-seconds", type=float, default=600.0,
+                    help="N > 1: host-side deadline per phase (exit non-zero with every thread's stack instead of "
+                         "hanging the job); 0 disables")
     ap.add_argument("--no-stage-timing", action="store_true",
                     help="diagnostics: no per-kernel HIP events in the timed loop (roofline fields become null)")
     args = ap.parse_args()
@@ -1329,7 +1451,7 @@ def main():
         return BandRenderer(sc, rank, world, local, assembly=args.assembly, inflight=inflight or inflight_for(sc),
                             display_rows=display_rows, pack=args.pack, exchange=args.exchange)
 
-    def choose_split(sc):
+    def autotuned_split(sc):
         """((display_rows or None, frames in flight), the autotune log) for a config at this world size."""
         if world == 1 or args.assembly != "gather" or args.split == "equal":
             return (None, inflight_for(sc)), None
@@ -1345,6 +1467,46 @@ def main():
             log = {"candidates": log, "rebalance": rlog}
         return (d, k), log
 
+    def fall_back_to_torch(why):
+        print(f"WARNING: native band exchange failed ({why}); using torch.distributed", file=sys.stderr, flush=True)
+        args.exchange = "torch"
+
+    def guarded(what, fn, bad=lambda out: 0.0):
+        return guarded_call(what, fn, torch.device("cuda", local), dist_on, rank, bad)
+
+    def native_check(sc):
+        """Before any autotune: the native exchange on the equal split, 3 frames in flight over 30 frames, bit-exact
+        against the one-GPU frame; (ok, parity dict or failure detail)."""
+        def run():
+            b = make_renderer(sc, None, 3)
+            try:
+                b.warm()
+                return verify_assembly(b, sc, dist_on, frames=30, agree=False)
+            finally:
+                b.close()
+        ok, res = guarded("native exchange check", run, bad=lambda out: out["bad"])
+        if ok:
+            res["bit_exact"] = True
+        return ok, res
+
+    def choose_split(sc):
+        """autotuned_split, with the native exchange verified first and the autotune itself guarded: a failure of
+        either switches the run to the torch.distributed exchange before anything is timed."""
+        if world > 1 and args.assembly == "gather" and args.exchange == "native" and not native_checked:
+            arm_watchdog(args.watchdog_seconds, "native exchange check")
+            ok, res = native_check(sc)
+            native_checked.append(res)
+            if not ok:
+                fall_back_to_torch(res)
+        arm_watchdog(args.watchdog_seconds * 2, f"split autotune ({sc.name})")
+        if args.exchange == "native" and world > 1:
+            ok, res = guarded("split autotune", lambda: autotuned_split(sc))
+            if ok:
+                return res
+            fall_back_to_torch(res)
+        return autotuned_split(sc)
+
+    native_checked = []
     split_log = None
     inflight = inflight_for(scene)
     if args.sim_world and world == 1:
@@ -1361,23 +1523,26 @@ def main():
         br = make_renderer(scene, display_rows, inflight)
     parity = None
     if world > 1 and args.assembly == "gather":
-        # the assembled frame must equal the one-GPU frame; the native exchange falls back to torch.distributed's
-        # if it does not (or fails), and the line says so
-        try:
-            parity = verify_assembly(br, scene, dist_on)
-        except Exception as e:  # noqa: BLE001 - any failure of the native path is reported and replaced
-            parity = {"bit_exact": False, "detail": f"{type(e).__name__}: {str(e)[:200]}"}
-            max_over_ranks(1.0, br.dev, dist_on)  # the other ranks' outcome collective
+        # the assembled frame at the chosen split must equal the one-GPU frame; the native exchange falls back to
+        # torch.distributed's if it does not (or fails), and the line says so
+        arm_watchdog(args.watchdog_seconds, "assembly parity")
+        ok, parity = guarded("assembly parity", lambda: verify_assembly(br, scene, dist_on, frames=10, agree=False),
+                             bad=lambda out: out["bad"])
+        if not ok:
+            parity = {"bit_exact": False, "detail": parity}
+        else:
+            parity["bit_exact"] = True
         if not parity["bit_exact"] and br.xfer is not None:
-            print(f"WARNING: native band exchange failed its parity check ({parity['detail']}); "
-                  "using torch.distributed", file=sys.stderr, flush=True)
+            fall_back_to_torch(parity["detail"])
             br.close()
-            args.exchange = "torch"
             if display_rows == 0 or (isinstance(display_rows, tuple) and display_rows[0] == 0):
                 display_rows = None  # the torch exchange has no assemble-only display: the equal split
             br = make_renderer(scene, display_rows, inflight)
             parity = verify_assembly(br, scene, dist_on)
             parity["native_failed"] = True
+        if native_checked:
+            parity["native_check_before_autotune"] = native_checked[0]
+    arm_watchdog(args.watchdog_seconds if world > 1 else 0, "timed run")
     dt, timing, n_warm = timed_run(br, args.steps, args.warmup, dist_on, not args.no_stage_timing,
                                    warm_seconds=args.warm_seconds)
     fps = args.steps / dt
@@ -1393,6 +1558,7 @@ def main():
         inbound = br.inbound_bytes() if rank == 0 else 0
         assembly = {"render_ms": render_ms, "assembly_ms": asm_ms, "inbound_bytes_per_frame": inbound,
                     "exchange": "native (tri_xfer)" if br.xfer is not None else "torch.distributed",
+                    "rccl_communicators": br.xfer_comms if br.xfer is not None else None,
                     "parity_vs_one_gpu_frame": parity,
                     "band_format": br.codec.mode if br.codec is not None else "bgra32",
                     "dbp_slot_bytes": br.codec.slot if br.codec is not None and br.codec.mode == "dbp" else None,
@@ -1427,6 +1593,7 @@ def main():
         for key in ("c2", "c5", "c3trs"):
             s2 = build_scene(key)
             (d2, k2), log2 = choose_split(s2)
+            arm_watchdog(args.watchdog_seconds if world > 1 else 0, f"secondary {key}")
             br2 = make_renderer(s2, d2, k2)
             # enough frames that the pipeline's fill and drain (about one frame latency, 50 us at C2, 280 us at C5)
             # stay under 1 % of the timed region whatever --steps the headline uses
@@ -1449,7 +1616,13 @@ def main():
             secondary[s2.name] = entry
             br2.close()
             del br2
+    if not args.no_secondary and args.config == "c3" and world == 1:
+        # Forge's editor frame through the engine API: two panels + the present blit, and one 4K
+        # viewport, beside the C-ABI line
+        secondary["forge_editor_frame_c3_panels"] = forge_frame(FORGE_PANELS)
+        secondary["forge_editor_frame_c3_4k"] = forge_frame(FORGE_4K)
 
+    arm_watchdog(0, "")
     copy_gbs = device_copy_gbs(br.dev) if rank == 0 else None
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -1479,6 +1652,9 @@ def main():
                        "split_autotune": split_log},
             "mpix_per_s": fps * W * H / 1e6,
             "latency_ms": latency,
+            # the pipeline's fill and drain: one frame's latency beyond its share of the throughput clock, paid once
+            # per timed region (0.05 ms of a 20-step C3 region is ~2.6 %, of a 200-step one ~0.3 %)
+            "fill_drain_ms": latency - dt / args.steps * 1e3,
             # the contract prices k_raster against HBM; what actually binds it is VALU issue together with the
             # L1 gather path (the VALU floor alone caps this frac near 0.17), see roofline_valu
             "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",

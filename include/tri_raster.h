@@ -38,6 +38,7 @@ extern "C" {
                                 * grown, re-render the frame                                    */
 #define TRI_E_UNSUPPORTED (-5) /* combination outside the path (AI blend + shadow pre-pass)     */
 #define TRI_E_STATE (-6)       /* call order violated (e.g. render before geometry upload)      */
+#define TRI_E_TIMEOUT (-7)     /* a multi-GPU exchange missed its deadline (communicators aborted) */
 
 /* ---- limits mirrored from the reference ----------------------------------------------- */
 #define TRI_MAX_POINT_LIGHTS 8   /* kMaxPointLights, UniformBuffer.h:7                           */
@@ -372,7 +373,9 @@ int tri_xfer_unique_id(uint8_t* id_out);
 int tri_xfer_comm_create(const uint8_t* id, uint32_t world, uint32_t rank, int32_t device, tri_xfer_comm** out);
 int tri_xfer_comm_destroy(tri_xfer_comm* comm);
 /* comms: one communicator per slot in flight (slot s uses comms[s % comm_count]; each created with the same world,
- * rank and device), so that each one's operations stay on one stream (the slot's context stream). */
+ * rank and device), so that each one's operations stay on one stream (the slot's context stream). With fewer
+ * communicators than slots (e.g. a second ncclCommInitRank failed), a communicator shared by several slots has its
+ * operations fenced across their streams by an event (correct, ≈ 2 µs of host time per frame more). */
 int tri_xfer_create(tri_xfer_comm* const* comms, uint32_t comm_count, const tri_xfer_config* config, tri_xfer** out);
 int tri_xfer_destroy(tri_xfer* xfer);
 /* Slot `slot`'s pixel buffer (device, 4-B aligned, caller-owned): this rank's band (a sender) or the whole
@@ -386,12 +389,30 @@ int tri_xfer_bind_slot(tri_xfer* xfer, uint32_t slot, void* bgra8);
  * must make the same sequence of exchanging calls per slot (the transfers match in order per communicator). */
 int tri_xfer_frame(tri_xfer* xfer, uint32_t slot, tri_ctx* ctx, void* depth, const tri_global_ubo* ubo,
                    const float clear_rgba[4], const tri_draw* draws, uint32_t draw_count, uint32_t exchange);
-/* Wait for every slot's stream; TRI_E_STATE if a packed band's alpha differed, TRI_E_OVERFLOW if a band outgrew
- * the agreed dbp slot (both lossy). */
+/* Wait for every slot's stream, at most the exchange's timeout (tri_xfer_set_timeout, default 60000 ms; 0 = none):
+ * TRI_E_TIMEOUT when it expires, TRI_E_HIP when a communicator reports an asynchronous error — both abort the
+ * exchange's communicators (ncclCommAbort; later exchanging frames on them fail with TRI_E_STATE), so the caller can
+ * exit instead of hanging the job. Then TRI_E_STATE if a packed band's alpha differed, TRI_E_OVERFLOW if a band
+ * outgrew the agreed dbp slot (both lossy). On the display rank these report the senders' bands too: the status
+ * travels with each packed band and the decode ORs it in. */
 int tri_xfer_synchronize(tri_xfer* xfer);
+/* The bounded wait alone (TRI_E_TIMEOUT / TRI_E_HIP as above), without reading the status flags. */
+int tri_xfer_wait(tri_xfer* xfer);
+int tri_xfer_set_timeout(tri_xfer* xfer, uint32_t timeout_ms);
+/* The number of communicators the exchange runs on (comm_count at tri_xfer_create). */
+int tri_xfer_comm_count(tri_xfer* xfer, uint32_t* count);
 /* Bytes this rank sends and receives per frame; max_slot_bytes (may be NULL; synchronising): the largest dbp slot
  * this rank's packs needed. */
 int tri_xfer_info(tri_xfer* xfer, uint64_t* sent_bytes, uint64_t* received_bytes, uint32_t* max_slot_bytes);
+/* Loopback transport (tests only; replaces nothing in the reference): `world` tri_xfer exchanges of one process on
+ * one device stand in for `world` ranks (RCCL refuses two ranks on one GPU). tri_xfer_comm_create_loopback is
+ * tri_xfer_comm_create's counterpart: the k-th communicator each rank creates on a hub forms channel k. Sends become
+ * a device copy into the display's receive buffer, ordered by events as ncclSend / ncclRecv order them; every other
+ * step of the exchange runs as on N GPUs. Drive the ranks frame by frame, every sender before the display. */
+typedef struct tri_xfer_loopback tri_xfer_loopback;
+int tri_xfer_loopback_create(uint32_t world, tri_xfer_loopback** out);
+int tri_xfer_loopback_destroy(tri_xfer_loopback* hub);
+int tri_xfer_comm_create_loopback(tri_xfer_loopback* hub, uint32_t rank, int32_t device, tri_xfer_comm** out);
 
 /* ---- measurement -------------------------------------------------------------------------- */
 /* enable = N > 0: HIP events around every stage of every N-th frame (1 = all frames; sampling keeps

@@ -10,8 +10,10 @@ def _zig(d):
     return np.where(d >= 0, 2 * d, -2 * d - 1).astype(np.uint32)
 
 
-def encode(bgra, slot_bytes):
-    """bgra: uint32 [n] (B8G8R8A8 words). Returns (stream uint8 [nslots * slot_bytes], max slot bytes, overflow)."""
+def encode(bgra, slot_bytes, alpha=None):
+    """bgra: uint32 [n] (B8G8R8A8 words). Returns (stream uint8 [nslots * slot_bytes], max slot bytes, overflow).
+    alpha: the promised alpha; a slot holding a pixel whose alpha differs carries 1 in header word 1 (the sender's
+    status, which the display's decode reports)."""
     px = np.asarray(bgra, np.uint32).ravel()
     n = px.size
     nslots = (n + SLOT_PIXELS - 1) // SLOT_PIXELS
@@ -47,12 +49,14 @@ def encode(bgra, slot_bytes):
             hdr[4 + 9 * w + 1: 4 + 9 * w + 9] = widths.view(np.uint32)
         total = 8 * len(planes)
         hdr[0] = total
+        sp = px[s * SLOT_PIXELS:(s + 1) * SLOT_PIXELS]
+        hdr[1] = 1 if alpha is not None and bool(((sp >> 24) != alpha).any()) else 0
         nbytes = HEADER + total
         maxb = max(maxb, nbytes)
         slot = out[s * slot_bytes:(s + 1) * slot_bytes]
         if nbytes > slot_bytes:
             over = True
-            slot[:4] = np.array([total], np.uint32).view(np.uint8)
+            slot[:8] = np.array([total, hdr[1]], np.uint32).view(np.uint8)
             continue
         slot[:HEADER] = hdr.view(np.uint8)
         if planes:

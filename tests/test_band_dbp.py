@@ -96,6 +96,11 @@ def test_gpu_dbp_flags_overflow_and_alpha():
     torch.cuda.synchronize()
     f = flags.cpu().numpy()
     assert f[0] == 3 and f[1] == 12448  # alpha mismatch + overflow; the slots need the maximum
+    # the status travels with the band: slot 1 (pixels 4096..8191) carries the alpha mark in header word 1
+    hdr = stream.cpu().numpy().reshape(2, 4096)[:, :8].copy().view(np.uint32)
+    assert hdr[0, 1] == 0 and hdr[1, 1] == 1, hdr
+    want, _, _ = dbp_ref.encode(px, 4096, alpha=255)
+    assert np.array_equal(want.reshape(2, 4096)[:, :8], stream.cpu().numpy().reshape(2, 4096)[:, :8])
 
 
 @pytest.mark.gpu

@@ -53,3 +53,15 @@ def test_band_renderer_native_exchange_plumbing():
         if br.xfer is not None:
             br.close()
     assert abi.TRI_XFER_ID_BYTES == 128
+
+
+def test_forge_editor_frame_secondary():
+    """bench.forge_frame (the frame Forge runs, through RenderCommand::DrawFrame with its deferred fence): two small
+    panels and the present blit complete and report a rate and a host cost (the shim's pixel parity after the deferred
+    fence is covered by test_host_shim.py / test_present.py, which read through FinishFrame)."""
+    import bench
+
+    layout = {"viewports": ((2, 212, 160), (1, 200, 150)), "present": (320, 240)}
+    r = bench.forge_frame(layout, frames=12, warm_seconds=0.02)
+    assert r["frames_per_s"] > 0 and r["host_ms_per_drawframe_idle_gpu"] > 0
+    assert r["viewports"] == [[212, 160], [200, 150]] and r["triangles"] == 999698

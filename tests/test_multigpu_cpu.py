@@ -330,6 +330,9 @@ class _FakeBand:
     def drain(self):
         pass
 
+    def _sync(self, check=False):
+        pass
+
     def close(self):
         self.closed = True
 
@@ -506,3 +509,49 @@ def test_frame_alpha_proof(hiplib):
     dbp.unpack(st, back)
     assert torch.equal(back, band)
     dbp.check()
+
+
+def _guard_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    sys.path.insert(0, ROOT)
+    import torch
+    import torch.distributed as dist
+
+    import bench
+
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cpu")
+
+    def fails_on_rank1():
+        if rank == 1:
+            raise RuntimeError("tri_xfer_wait: the exchange did not complete before the deadline")
+        return {"bad": 0.0, "detail": "ok"}
+
+    res = [bench.guarded_call("check", fails_on_rank1, dev, True, rank, bad=lambda o: o["bad"])]
+    res.append(bench.guarded_call("check", lambda: {"bad": float(rank == 0) * 7, "detail": "7 pixels differ"}, dev,
+                                  True, rank, bad=lambda o: o["bad"]))
+    res.append(bench.guarded_call("check", lambda: (rank, 1), dev, True, rank))
+    after = bench.max_over_ranks(float(rank + 10), dev, True)  # the collective sequence is still aligned
+    np.save(os.path.join(out_dir, f"guard{rank}.npy"),
+            np.array([r[0] for r in res] + [after], dtype=np.float64))
+    with open(os.path.join(out_dir, f"guard{rank}.txt"), "w") as f:
+        f.write("\n".join(str(r[1]) for r in res))
+    dist.destroy_process_group()
+
+
+def test_guarded_call_agrees_on_a_failure_over_ranks(tmp_path):
+    """bench.guarded_call (the fallback guard of the native exchange, VERDICT r5 #1b): an exception on one rank or a
+    parity miss on the display rank makes every rank return not-ok from the same single collective, and the ranks'
+    collective sequences stay aligned afterwards."""
+    import torch.multiprocessing as mp
+
+    world = 2
+    mp.start_processes(_guard_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        got = np.load(tmp_path / f"guard{r}.npy")
+        assert list(got) == [0.0, 0.0, 1.0, 11.0], (r, got)
+    t0 = (tmp_path / "guard0.txt").read_text().splitlines()
+    t1 = (tmp_path / "guard1.txt").read_text().splitlines()
+    assert "failed on another rank" in t0[0] and "deadline" in t1[0]
+    assert "7 pixels differ" in t0[1]
