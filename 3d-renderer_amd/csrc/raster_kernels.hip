@@ -1020,6 +1020,13 @@ __device__ __forceinline__ void bin_pair_box(const TriDeviceBuffers& b, BinBox& 
                                              const uint32_t (&p)[kSetupGroup], uint32_t nbx, uint32_t* bin_count,
                                              uint32_t* bin_list, uint32_t cap, uint32_t lane, uint32_t& nentries) {
     if (kAblate & 4) return;  // diagnostics: 4 = setup without binning
+#ifdef TRI_SETUP_WAVE_BINNING  // A/B: every round through the per-wave reservations (no LDS grid, no barriers)
+#pragma unroll
+    for (int t = 0; t < kSetupGroup; t += 2)
+        bin_pair<SHADOW_QUEUES>(b, ok[t], ok[t + 1], br[t], br[t + 1], p[t], p[t + 1], nbx, bin_count, bin_list, cap,
+                                lane, nentries);
+    return;
+#endif
     const uint32_t q = round & 1u;
     uint32_t (&box)[2][4] = g.box[SHADOW_QUEUES ? 1 : 0];
     uint32_t m[4] = {~0u, ~0u, ~0u, ~0u};
@@ -1250,7 +1257,7 @@ __device__ __forceinline__ void setup_body(const TriFrameParams& fp, const TriDe
                 }
                 // k_raster's (and k_shadow_raster's) route from the primitive to its vertex slots and draw; a
                 // single-draw frame finds the slots in the index buffer instead (prim_slots)
-                if (!ONE && !fp.one_draw && (ok[t] || needs_clip[t] || sok[t]))
+                if (!ONE && !fp.one_draw && !fp.idx_route && (ok[t] || needs_clip[t] || sok[t]))
                     b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | (needs_clip[t] ? TRI_PRIM_CLIPPED : 0u));
             }
             nsetup += ok[t] ? 1u : 0u;
@@ -1379,6 +1386,16 @@ __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDe
         const u32x3v q = rec96<12>(rec_buf(b.indices + fp.draw0.first_index, 12u, fp.nprims), p, 0u);
         sl[0] = q[0] - fp.draw0.min_index; sl[1] = q[1] - fp.draw0.min_index; sl[2] = q[2] - fp.draw0.min_index;
         d = 0;
+    } else if (fp.idx_route) {  // (uniform) the index triple, and the draw from the frame's primitive bases
+        const u32x3v q = rec96<12>(rec_buf(b.indices + fp.idx_k, 12u, fp.nprims), p, 0u);
+        uint32_t dd = 0, v = fp.vbd[0];
+        for (uint32_t i = 1; i < fp.ndraws; ++i) {  // uniform trip count, scalar operands: a compare, two selects
+            const bool ge = p >= fp.pbase[i];
+            dd = ge ? i : dd;
+            v = ge ? fp.vbd[i] : v;
+        }
+        sl[0] = q[0] + v; sl[1] = q[1] + v; sl[2] = q[2] + v;
+        d = dd;
     } else {
         const uint4 pv = rec128<16>(rec_buf(b.prim_vs, 16u, fp.nprims), p, 0u);
         sl[0] = pv.x; sl[1] = pv.y; sl[2] = pv.z;
@@ -3005,7 +3022,14 @@ template <bool EXACT, int BL, bool ONE>
 #ifndef TRI_RASTER_WAVES_PLAIN_ONE
 #define TRI_RASTER_WAVES_PLAIN_ONE 8
 #endif
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? ((ONE && !EXACT) ? TRI_RASTER_WAVES_PLAIN_ONE : TRI_RASTER_WAVES_PLAIN) : 3))) void k_raster_plain(TRI_KARGS) {
+// TRI_RASTER_ONE_VGPRS (A/B): cap the fast single-draw instantiation's VGPRs below the 64 that 8 waves/SIMD allow,
+// so that a concurrent frame's front-end wave fits the register file beside 8 raster waves instead of displacing one
+#ifdef TRI_RASTER_ONE_VGPRS
+#define TRI_RASTER_PLAIN_VGPR_ATTR __attribute__((amdgpu_num_vgpr(TRI_RASTER_ONE_VGPRS)))
+#else
+#define TRI_RASTER_PLAIN_VGPR_ATTR
+#endif
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? ((ONE && !EXACT) ? TRI_RASTER_WAVES_PLAIN_ONE : TRI_RASTER_WAVES_PLAIN) : 3))) TRI_RASTER_PLAIN_VGPR_ATTR void k_raster_plain(TRI_KARGS) {
     TRI_BIND_ARGS;
     raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }

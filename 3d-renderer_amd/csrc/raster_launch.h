@@ -5,6 +5,11 @@
 #include "raster_common.h"
 
 // k_setup occupancy target (waves per SIMD); with 4 waves per workgroup, also its workgroups per CU
+// TRI_IDX_ROUTE: frames of a few draws over concatenated meshes reach a primitive's vertex slots through the index
+// buffer (TriFrameParams::idx_route) instead of a per-primitive prim_vs record; 0 keeps the records
+#ifndef TRI_IDX_ROUTE
+#define TRI_IDX_ROUTE 1
+#endif
 #ifndef TRI_SETUP_WAVES
 #define TRI_SETUP_WAVES 6
 #endif

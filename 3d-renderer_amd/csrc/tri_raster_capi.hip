@@ -157,6 +157,8 @@ struct tri_ctx {
     bool obj48 = false;        // every active draw may keep object-space varyings (TriFrameParams::obj48)
     bool obj48_xform = false;  // ... and some draw's model matrix is not the identity
     uint32_t vdelta[TRI_OBJ48_DRAWS] = {};  // per draw: base_vertex + min_index - first slot
+    bool idx_route = false;                   // TriFrameParams::idx_route and its tables
+    uint32_t idx_k = 0, pbase[TRI_OBJ48_DRAWS] = {}, vbd[TRI_OBJ48_DRAWS] = {};
 
     // work buffers
     float4* d_clip = nullptr; size_t cap_clip = 0;
@@ -521,6 +523,20 @@ int resolve_draws(tri_ctx* c) {
                            o.tex_offset[0] == 0.0f && o.tex_offset[1] == 0.0f;
         c->obj48 = uv_id && draw_obj_ok(*c->geom, o);
         c->obj48_xform = c->obj48_xform || !identity_model(o.model);
+    }
+    // the index route (TriFrameParams::idx_route): every active draw's index rows start at idx_k + 3 * its first
+    // primitive (one K for all)
+    c->idx_route = n >= 2 && n <= TRI_OBJ48_DRAWS;
+    bool have_k = false;
+    for (uint32_t d = 0; d < n && c->idx_route; ++d) {
+        const TriDrawDev& o = dd[d];
+        c->vbd[d] = (uint32_t)((int64_t)vb[d] - (int64_t)o.min_index);
+        c->pbase[d] = pb[d];
+        if (pb[d + 1] == pb[d]) continue;  // no primitives (inactive or skipped)
+        const int64_t k = (int64_t)o.first_index - 3 * (int64_t)pb[d];
+        if (k < 0 || (have_k && (uint32_t)k != c->idx_k)) c->idx_route = false;
+        c->idx_k = (uint32_t)k;
+        have_k = true;
     }
     c->nslots = (uint32_t)vslots;
     c->nprims = (uint32_t)prims;
@@ -1304,11 +1320,17 @@ int tri_render(tri_ctx* c) {
     // (not with the pre-pass over a transformed draw: the shadow instantiation carries no per-draw transform)
     fp.obj48 = (TRI_OBJ48 && !fp.vary36 && c->obj48 && !(c->shadow.size && c->obj48_xform)) ? 1u : 0u;
     fp.obj48_xform = fp.obj48 && c->obj48_xform ? 1u : 0u;
+    fp.idx_route = (TRI_IDX_ROUTE && c->idx_route) ? 1u : 0u;
+    if (fp.idx_route) {
+        fp.idx_k = c->idx_k;
+        std::memcpy(fp.pbase, c->pbase, sizeof fp.pbase);
+        std::memcpy(fp.vbd, c->vbd, sizeof fp.vbd);
+    }
     if (fp.obj48) std::memcpy(fp.vdelta, c->vdelta, sizeof fp.vdelta);  // (zero otherwise: world-space records
                                                                           // at the slots themselves)
     c->last_path = (fp.obj48 ? TRI_PATH_OBJ48 : 0u) | (fp.shade_solid ? TRI_PATH_ONE_DRAW : 0u) | (fp.vary_obj ? TRI_PATH_VARY_OBJ : 0u) |
                    (fp.obj_xform ? TRI_PATH_OBJ_XFORM : 0u) | (fp.obj_ucol ? TRI_PATH_OBJ_UCOL : 0u) |
-                   (c->shadow.size ? TRI_PATH_SHADOW : 0u);
+                   (c->shadow.size ? TRI_PATH_SHADOW : 0u) | (fp.idx_route ? TRI_PATH_IDX_ROUTE : 0u);
     fp.ovf_rec_cap = c->ovf_rec_cap;
     fp.ovf_vert_cap = c->ovf_vert_cap;
     fp.bin_cap = c->bin_cap;

@@ -150,6 +150,7 @@ class TriFrameStats(C.Structure):
 # tri_frame_stats.path bits (include/tri_raster.h)
 TRI_PATH_ONE_DRAW, TRI_PATH_VARY_OBJ, TRI_PATH_OBJ_XFORM, TRI_PATH_OBJ_UCOL, TRI_PATH_SHADOW = 0x1, 0x2, 0x4, 0x8, 0x10
 TRI_PATH_OBJ48 = 0x20
+TRI_PATH_IDX_ROUTE = 0x40
 
 # the delta bit-plane band format (include/tri_raster.h)
 TRI_DBP_SLOT_PIXELS, TRI_DBP_MIN_SLOT, TRI_DBP_MAX_SLOT, TRI_DBP_MAX_BANDS = 4096, 176, 12448, 16

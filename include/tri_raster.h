@@ -168,6 +168,7 @@ typedef struct tri_frame_stats {
 #define TRI_PATH_OBJ_UCOL   0x8u  /* ... one vertex colour for the whole geometry                           */
 #define TRI_PATH_SHADOW    0x10u  /* the shadow-map pre-pass ran                                            */
 #define TRI_PATH_OBJ48     0x20u  /* object-space varyings outside the single-draw solid instantiation      */
+#define TRI_PATH_IDX_ROUTE 0x40u  /* several draws: vertex slots from the index buffer, no per-primitive record */
 
 /* Shadow-map pre-pass (BASELINE.json config 5). The reference reserves the switch
  * (LightComponent::m_ShadowCaster, Trident/src/ECS/Components/LightComponent.h:33) but renders no shadow

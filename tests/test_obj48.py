@@ -90,3 +90,20 @@ def test_obj48_c5_and_fallbacks(oracle):
     assert not frame_path(t)[0] & abi.TRI_PATH_OBJ48
     p = sc.shadow_scene(oracle)  # the ground quad's non-uniform scale
     assert not frame_path(p)[0] & abi.TRI_PATH_OBJ48
+
+
+def test_idx_route_on_and_off(oracle, flags):
+    """Several draws over concatenated meshes in draw order reach their vertex slots through the index buffer
+    (TRI_PATH_IDX_ROUTE: no per-primitive prim_vs record); the same meshes drawn in the other order (index rows no
+    longer follow the primitive numbers) keep the records. Both frames match the oracle, clipped primitives
+    included."""
+    from trident_raster import abi
+
+    s = sc.near_clip_multi()
+    assert_parity(s, oracle, min_covered=10000, flags=flags)
+    path, clipped = frame_path(s, flags)
+    assert path & abi.TRI_PATH_IDX_ROUTE and clipped > 0, hex(path)
+    s.draws = [s.draws[1], s.draws[0]]  # mesh 1 first: the route's one offset no longer fits
+    s.name += "_swapped"
+    assert_parity(s, oracle, min_covered=10000, flags=flags)
+    assert not frame_path(s, flags)[0] & abi.TRI_PATH_IDX_ROUTE
