@@ -30,6 +30,8 @@
 #include <hip/hip_runtime.h>
 #include <math.h>
 
+#include <type_traits>
+
 namespace {
 
 // Diagnostics builds only (tools/build_variant.sh NAME -DTRI_ABLATE=N): 1 = coverage without shading,
@@ -1301,8 +1303,14 @@ __device__ __forceinline__ void setup_body(const TriFrameParams& fp, const TriDe
     TRI_SSTAMP(3);
 }
 
+// TRI_SETUP_WAVES_ONE: the single-draw instantiation without the pre-pass (C2, C3) within 64 VGPRs, so that each of its
+// waves takes exactly one raster wave's registers from a concurrent frame's k_raster (8 waves x 64 fill a SIMD's
+// register file) instead of 72 — with 3 of its workgroups per CU (TRI_SETUP_WGS_PER_CU_OVERLAP) C3 +0.6 % (round 6 A/B)
+#ifndef TRI_SETUP_WAVES_ONE
+#define TRI_SETUP_WAVES_ONE TRI_SETUP_WAVES
+#endif
 template <bool WITH_SHADOW, bool ONE>
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(TRI_SETUP_WAVES))) void k_setup(TRI_KARGS) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu((ONE && !WITH_SHADOW) ? TRI_SETUP_WAVES_ONE : TRI_SETUP_WAVES))) void k_setup(TRI_KARGS) {
     TRI_BIND_ARGS;
     setup_body<WITH_SHADOW, ONE>(fp, b, blockIdx.x, gridDim.x);
 }
@@ -1445,6 +1453,22 @@ __device__ __forceinline__ void rec_bbox(const TriRec& r, int32_t ox, int32_t oy
 
 __device__ __forceinline__ uint32_t key_low(uint32_t prim_sub) {
     return ((TRI_PRIM_MAX - (prim_sub >> 3)) << 3) | (prim_sub & 7u);
+}
+
+// TRI_QTAB (A/B): in a bin of at most kQtab entries on a frame of at most 2^20 primitives, a key's low
+// word carries the winning entry's queue position as a payload BELOW its primitive order:
+//   low = (kQPrimMax - prim) << 11 | sub << 8 | queue position
+// so the minimum still resolves depth ties by primitive order exactly as key_low does (the position only separates
+// entries of one primitive, which never share a pixel), and the fragment finds the entry's vertex slots in an LDS
+// table the coverage pass filled, instead of gathering its index triple. No hash and no sort. The coverage code takes
+// the record's prim_sub re-encoded so that key_low() of it yields this word (qenc).
+#ifndef TRI_QTAB
+#define TRI_QTAB 0
+#endif
+constexpr uint32_t kQtab = 256, kQPrimMax = (1u << 20) - 1u;
+__device__ __forceinline__ uint32_t qenc(uint32_t prim_sub, uint32_t qpos) {
+    const uint32_t low = ((kQPrimMax - (prim_sub >> 3)) << 11) | ((prim_sub & 7u) << 8) | qpos;
+    return (TRI_PRIM_MAX - (low >> 3)) << 3 | (low & 7u);  // key_low() of this is `low`
 }
 
 // Edge values at pixel (cx0, cy0) of the triangle's clipped bbox, the edge steps and the depth plane.
@@ -2303,18 +2327,25 @@ __device__ __forceinline__ void fetch_attrs(const TriFrameParams& fp, const TriD
 // defers clipped pixels, TRI_CLIP_DEFER), 2 = it always does (the deferred pass).
 template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0, typename Put>
 __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                                  int32_t px, int32_t py, const float* lut, Put&& put) {
+                                                  int32_t px, int32_t py, const float* lut, Put&& put,
+                                                  const uint32_t* qtab = nullptr) {
     constexpr bool kInlineVis = SHADOW;
     const uint32_t low = (uint32_t)key;
-    const uint32_t prim = TRI_PRIM_MAX - (low >> 3);
-    const uint32_t sub = CLIPM == 1 ? 0u : (low & 7u);  // >= 1: sub-triangle `sub` of a clipped primitive
+    // qtab (TRI_QTAB bins, uniform): the key names the primitive above its queue position (qenc)
+    const uint32_t prim = qtab ? kQPrimMax - (low >> 11) : TRI_PRIM_MAX - (low >> 3);
+    const uint32_t sub = CLIPM == 1 ? 0u : (qtab ? (low >> 8) & 7u : low & 7u);  // >= 1: sub-triangle of a clipped primitive
     const FetchBufs fb = fetch_bufs<ONE>(fp, b);
     uint32_t sl[3] = {0, 0, 0}, d = 0;
     TriSnap a0{}, a1{}, a2{};
     uint32_t v0 = 0, v1 = 0, v2 = 0, dl = 0;
     Taps taps;
     if (CLIPM != 2) {
-        prim_slots<ONE>(fp, b, prim, sl, d);
+        if (ONE && TRI_QTAB && qtab) {  // the coverage pass's table: three LDS words, no index gather
+            const uint32_t q = low & 0xFFu;
+            sl[0] = qtab[q]; sl[1] = qtab[kQtab + q]; sl[2] = qtab[2 * kQtab + q];
+        } else {
+            prim_slots<ONE>(fp, b, prim, sl, d);
+        }
         // Every gather that needs only the slots is issued before the first wait: the snapped vertices and
         // the varyings are one round trip after the index fetch (the snaps are loaded for a clipped primitive
         // too, unused: its sub-triangle's record names its slots).
@@ -2388,8 +2419,9 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
 
 template <bool EXACT, bool SHADOW, bool ONE, int CLIPM = 0>
 __device__ __forceinline__ void fetch_fragment(const TriFrameParams& fp, const TriDeviceBuffers& b, uint64_t key,
-                                               int32_t px, int32_t py, const float* lut, Frag& f) {
-    fetch_fragment_to<EXACT, SHADOW, ONE, CLIPM>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; });
+                                               int32_t px, int32_t py, const float* lut, Frag& f,
+                                               const uint32_t* qtab = nullptr) {
+    fetch_fragment_to<EXACT, SHADOW, ONE, CLIPM>(fp, b, key, px, py, lut, [&](int i, float x) { (&f.wx)[i] = x; }, qtab);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -2563,7 +2595,7 @@ __device__ __forceinline__ uint32_t sky_bgra_persp(const TriFrameParams& fp, con
 #endif
 template <int BL>
 constexpr int big_area() { return BL == 4 ? TRI_BIG_AREA16 : TRI_BIG_AREA; }
-constexpr int kBigQueue = 1024;
+constexpr int kBigQueue = TRI_QTAB ? 384 : 1024;  // (TRI_QTAB: its table's LDS comes from here)
 
 // Bijective XCD-aware block -> bin remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): workgroups b, b+8, b+16 ... share an XCD's L2, so give them consecutive bins — each
@@ -2702,6 +2734,9 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ CovEntry cov[kBalanced ? kCovPass : 1];
     __shared__ uint32_t wsum[TRI_BLOCK / 64];
     __shared__ uint32_t nbig, nsky;
+    constexpr bool kQt = TRI_QTAB && ONE && BL == 5;
+    __shared__ uint32_t qtab[kQt ? 3 * kQtab : 1];   // TRI_QTAB: per queue position, the entry's vertex slots
+    __shared__ uint16_t bigqp[kQt ? kBigN : 1];      // ... and the large triangles' queue positions
     const int tid = threadIdx.x;
     TRI_STAMP(0);
     if constexpr (TRI_COV_PRIO && BL == 5) __builtin_amdgcn_s_setprio(1 + TRI_RASTER_PRIO);  // (TRI_COV_PRIO above)
@@ -2734,6 +2769,8 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     const uint32_t cnt = (uint32_t)__builtin_amdgcn_readfirstlane((int)cnt_v);
     const uint32_t* queue = b.bin_list + (size_t)bin * fp.bin_cap;
     uint32_t s0 = 0, s1 = min(cnt, fp.bin_cap);
+    // TRI_QTAB: this bin's keys carry queue positions (uniform: small bins of frames within kQPrimMax primitives)
+    const bool qmode = kQt && cnt <= kQtab && fp.nprims <= kQPrimMax;
     if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
             const TriRec r = load_entry<ONE>(fp, b, queue[0]);
@@ -2811,14 +2848,24 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
   } else {
     auto cover = [&](uint32_t i, int32_t sub, int32_t step, bool first) {
         const uint32_t ri = (TRI_QUEUE_PREFETCH && first) ? pre1 : queue[i];
-        const TriRec r = load_entry<ONE>(fp, b, ri);
+        TriRec r = load_entry<ONE>(fp, b, ri);
+        if (kQt && qmode) {  // the entry's slots (set-up orientation undone) at its queue position; the key's payload
+            if (!(ri & TRI_ENTRY_CLIPPED)) {
+                qtab[i] = r.v[0]; qtab[kQtab + i] = r.v[2]; qtab[2 * kQtab + i] = r.v[1];
+            }
+            r.prim_sub = qenc(r.prim_sub, i);
+        }
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         if (cx0 > cx1 || cy0 > cy1) return;
         if ((cx1 - cx0 + 1) * (cy1 - cy0 + 1) > big_area<BL>()) {
             if (sub != 0) return;  // the first lane of the group hands it over
             const uint32_t q = atomicAdd(&nbig, 1u);
-            if (q < (uint32_t)kBigN) { bigq[q] = ri; return; }
+            if (q < (uint32_t)kBigN) {
+                bigq[q] = ri;
+                if (kQt) bigqp[q] = (uint16_t)i;
+                return;
+            }
             raster_serial<BL>(r, cx0, cx1, cy0, cy1, ox, oy, keys);  // queue full: this lane walks it all
             return;
         }
@@ -2837,7 +2884,8 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     TRI_STAMP(2);
     const uint32_t nb = min(nbig, (uint32_t)kBigN);
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        const TriRec r = load_entry<ONE>(fp, b, bigq[q]);
+        TriRec r = load_entry<ONE>(fp, b, bigq[q]);
+        if (kQt && qmode) r.prim_sub = qenc(r.prim_sub, bigqp[q]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
         EdgeSetup e;
@@ -2889,76 +2937,83 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     constexpr int kWaveQ = BIN * BIN / (TRI_BLOCK / 64);
     __shared__ uint16_t clipq[kDefer ? BIN * BIN : 1];
     uint32_t nclip = 0;  // this wave's deferred pixels (wave-uniform)
-    for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
-        const bool in = lx < bw;
-        const uint64_t key = in ? keys[(ly << BL) + lx] : 0ull;
-        const bool bg = in && key == kBgKey;
-        if constexpr (kDefer) {
-            const bool clipped = in && !bg && ((uint32_t)key & 7u) != 0u;
-            const uint64_t m = __ballot(clipped);
-            if (m) {  // uniform
-                if (clipped) clipq[(tid >> 6) * kWaveQ + nclip + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
-                nclip += (uint32_t)__builtin_popcountll(m);
+    // (TRI_QTAB: the loop compiled twice, for bins with and without the queue-position keys, so that neither
+    // carries the other's registers)
+    auto shade_loop = [&](auto QT) {
+        constexpr bool kq = decltype(QT)::value;
+        for (int ly = tid >> BL; ly < bh; ly += TRI_BLOCK / BIN) {
+            const bool in = lx < bw;
+            const uint64_t key = in ? keys[(ly << BL) + lx] : 0ull;
+            const bool bg = in && key == kBgKey;
+            if constexpr (kDefer) {
+                const bool clipped = in && !bg && (((uint32_t)key >> (kq ? 8 : 0)) & 7u) != 0u;
+                const uint64_t m = __ballot(clipped);
+                if (m) {  // uniform
+                    if (clipped) clipq[(tid >> 6) * kWaveQ + nclip + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
+                    nclip += (uint32_t)__builtin_popcountll(m);
+                }
+                if (clipped) continue;
             }
-            if (clipped) continue;
-        }
-        if (sky_queue) {  // wave-aggregated append (uniform control flow here)
-            const uint64_t m = __ballot(bg);
-            if (m) {
-                const uint32_t lane = lanes_below(~0ull);
-                const uint32_t leader = (uint32_t)__builtin_ctzll(m);
-                uint32_t base = 0;
-                if (lane == leader) base = atomicAdd(&nsky, (uint32_t)__builtin_popcountll(m));
-                base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);  // leader: uniform
-                if (bg) skyq[base + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
+            if (sky_queue) {  // wave-aggregated append (uniform control flow here)
+                const uint64_t m = __ballot(bg);
+                if (m) {
+                    const uint32_t lane = lanes_below(~0ull);
+                    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+                    uint32_t base = 0;
+                    if (lane == leader) base = atomicAdd(&nsky, (uint32_t)__builtin_popcountll(m));
+                    base = (uint32_t)__builtin_amdgcn_readlane((int)base, (int)leader);  // leader: uniform
+                    if (bg) skyq[base + lanes_below(m)] = (uint16_t)((ly << BL) + lx);
+                }
             }
-        }
-#ifdef TRI_PRIM_GROUPS
-        {
-            const bool shade = in && !bg;
-            uint64_t m = __ballot(shade);
-            const uint32_t pid = shade ? ((uint32_t)key >> 3) : 0u;
-            const uint32_t active = (uint32_t)__builtin_popcountll(m);
-            uint32_t groups = 0;
-            while (m) {
-                const uint32_t lp = (uint32_t)__shfl((int)pid, (int)__builtin_ctzll(m));
-                m &= ~__ballot(shade && pid == lp);
-                ++groups;
+    #ifdef TRI_PRIM_GROUPS
+            {
+                const bool shade = in && !bg;
+                uint64_t m = __ballot(shade);
+                const uint32_t pid = shade ? ((uint32_t)key >> 3) : 0u;
+                const uint32_t active = (uint32_t)__builtin_popcountll(m);
+                uint32_t groups = 0;
+                while (m) {
+                    const uint32_t lp = (uint32_t)__shfl((int)pid, (int)__builtin_ctzll(m));
+                    m &= ~__ballot(shade && pid == lp);
+                    ++groups;
+                }
+                if ((uint32_t)(tid & 63) == (uint32_t)__builtin_ctzll(__ballot(true)) && active) {
+                    atomicAdd(&g_tri_groups[0], 1ull);
+                    atomicAdd(&g_tri_groups[1], (unsigned long long)groups);
+                    atomicAdd(&g_tri_groups[2], (unsigned long long)active);
+                }
             }
-            if ((uint32_t)(tid & 63) == (uint32_t)__builtin_ctzll(__ballot(true)) && active) {
-                atomicAdd(&g_tri_groups[0], 1ull);
-                atomicAdd(&g_tri_groups[1], (unsigned long long)groups);
-                atomicAdd(&g_tri_groups[2], (unsigned long long)active);
-            }
-        }
-#endif
-        if (!in) continue;
-        const int32_t px = ox + lx, py = oy + ly;
-        uint32_t out;
-        float z;
-        if (bg) {
-            const size_t o = (size_t)(py - fp.y0) * fp.W + px;
-            if (!sky_queue) b.color[o] = bg_bgra;
-            if (fp.write_depth) b.depth[o] = 1.0f;
-            continue;
-        } else if (kAblate & 1) {  // diagnostics: coverage only
-            z = __uint_as_float((uint32_t)(key >> 32));
-            out = (uint32_t)key;
-        } else {
-            z = __uint_as_float((uint32_t)(key >> 32));
-            Frag f;
-            if (kAblate & 256) {  // diagnostics: 256 = no varyings fetch (a fragment made from the key)
-                const float k0 = __uint_as_float(((uint32_t)key & 0x7FFFFFu) | 0x3F000000u);
-                for (int q = 0; q < 20; ++q) (&f.wx)[q] = k0 + 0.01f * q;
+    #endif
+            if (!in) continue;
+            const int32_t px = ox + lx, py = oy + ly;
+            uint32_t out;
+            float z;
+            if (bg) {
+                const size_t o = (size_t)(py - fp.y0) * fp.W + px;
+                if (!sky_queue) b.color[o] = bg_bgra;
+                if (fp.write_depth) b.depth[o] = 1.0f;
+                continue;
+            } else if (kAblate & 1) {  // diagnostics: coverage only
+                z = __uint_as_float((uint32_t)(key >> 32));
+                out = (uint32_t)key;
             } else {
-                fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f);
+                z = __uint_as_float((uint32_t)(key >> 32));
+                Frag f;
+                if (kAblate & 256) {  // diagnostics: 256 = no varyings fetch (a fragment made from the key)
+                    const float k0 = __uint_as_float(((uint32_t)key & 0x7FFFFFu) | 0x3F000000u);
+                    for (int q = 0; q < 20; ++q) (&f.wx)[q] = k0 + 0.01f * q;
+                } else {
+                    fetch_fragment<EXACT, SHADOW, ONE, kDefer ? 1 : 0>(fp, b, key, px, py, lut, f, kq ? qtab : nullptr);
+                }
+                out = shade_bgra<EXACT, ONE, AI>(fp, b, f, px, py);
             }
-            out = shade_bgra<EXACT, ONE, AI>(fp, b, f, px, py);
+            const size_t o = (size_t)(py - fp.y0) * fp.W + px;
+            b.color[o] = out;
+            if (fp.write_depth) b.depth[o] = z;
         }
-        const size_t o = (size_t)(py - fp.y0) * fp.W + px;
-        b.color[o] = out;
-        if (fp.write_depth) b.depth[o] = z;
-    }
+    };
+    if (kQt && qmode) shade_loop(std::true_type{});
+    else shade_loop(std::false_type{});
     if constexpr (kDefer) {  // this wave's clipped pixels (its own LDS slice: no workgroup barrier)
         __builtin_amdgcn_wave_barrier();
         for (uint32_t i = (uint32_t)(tid & 63); i < nclip; i += 64) {
@@ -2967,7 +3022,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             const uint64_t key = keys[li];
             const int32_t px = ox + qx, py = oy + qy;
             Frag f;
-            fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f);
+            fetch_fragment<EXACT, SHADOW, ONE, 2>(fp, b, key, px, py, lut, f, (kQt && qmode) ? qtab : nullptr);
             const size_t o = (size_t)(py - fp.y0) * fp.W + px;
             b.color[o] = shade_bgra<EXACT, ONE, AI>(fp, b, f, px, py);
             if (fp.write_depth) b.depth[o] = __uint_as_float((uint32_t)(key >> 32));
@@ -3022,17 +3077,24 @@ template <bool EXACT, int BL, bool ONE>
 #ifndef TRI_RASTER_WAVES_PLAIN_ONE
 #define TRI_RASTER_WAVES_PLAIN_ONE 8
 #endif
-// TRI_RASTER_ONE_VGPRS (A/B): cap the fast single-draw instantiation's VGPRs below the 64 that 8 waves/SIMD allow,
-// so that a concurrent frame's front-end wave fits the register file beside 8 raster waves instead of displacing one
-#ifdef TRI_RASTER_ONE_VGPRS
-#define TRI_RASTER_PLAIN_VGPR_ATTR __attribute__((amdgpu_num_vgpr(TRI_RASTER_ONE_VGPRS)))
-#else
-#define TRI_RASTER_PLAIN_VGPR_ATTR
+// TRI_RASTER_ONE_VGPRS: cap the fast single-draw instantiation's VGPRs below the 64 that 8 waves/SIMD allow, so that a
+// concurrent frame's front-end wave (k_setup within 64, TRI_SETUP_WAVES_ONE) fits the register file beside 8 raster
+// waves instead of displacing one. On gfx950's unified register file the attribute's value is doubled: 28 caps at 56
+// VGPRs; 0 = no cap.
+#ifndef TRI_RASTER_ONE_VGPRS
+#define TRI_RASTER_ONE_VGPRS 0
 #endif
-__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? ((ONE && !EXACT) ? TRI_RASTER_WAVES_PLAIN_ONE : TRI_RASTER_WAVES_PLAIN) : 3))) TRI_RASTER_PLAIN_VGPR_ATTR void k_raster_plain(TRI_KARGS) {
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? ((ONE && !EXACT) ? TRI_RASTER_WAVES_PLAIN_ONE : TRI_RASTER_WAVES_PLAIN) : 3))) void k_raster_plain(TRI_KARGS) {
     TRI_BIND_ARGS;
     raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
+#if TRI_RASTER_ONE_VGPRS  // C3's instantiation as an explicit specialization: the cap takes no template-dependent value
+template <>
+__global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) __attribute__((amdgpu_num_vgpr(TRI_RASTER_ONE_VGPRS))) void k_raster_plain<false, 5, true>(TRI_KARGS) {
+    TRI_BIND_ARGS;
+    raster_bin<false, 5, false, true>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
+}
+#endif
 // Frames with Default.frag's AI frame blend (AiBlendConfig.w > 0, an uploaded AI frame; never with the shadow
 // pre-pass, which the reference does not have): the general instantiation plus the blend
 template <bool EXACT, int BL>

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <memory>
 #include <string>
@@ -106,6 +107,14 @@ public:
     // work between frames overlaps the GPU. The readers (ReadViewportPixels, ReadPresentPixels, GetViewportTexture)
     // call it on demand.
     void FinishFrame();
+    // Frames in flight (1..4; default 1, the reference's pacing: DrawFrame waits for the previous frame's timeline
+    // value). With n > 1 every single-device viewport keeps n render targets and frame k renders into target k mod n,
+    // so DrawFrame waits only for frame k - n + 1 and the next frames' vertex and set-up work overlaps this frame's
+    // raster (the C-ABI bench's contexts in flight, through the engine API). GetViewportTexture / ReadViewportPixels
+    // return the latest frame's target. Multi-device viewports (SetDeviceCount > 1) keep 1 (tri_group double-buffers
+    // its own frame). Changing it waits for every frame in flight and rebuilds the targets at the next DrawFrame.
+    void SetFramesInFlight(uint32_t n);
+    uint32_t GetFramesInFlight() const { return m_FramesInFlight; }
     uint32_t GetActiveViewportId() const { return m_ActiveViewportId; }
     ViewportInfo GetViewport() const;
     // Vulkan returned a VkDescriptorSet for ImGui (Renderer.h:235); here: an opaque handle, a pointer to
@@ -266,14 +275,22 @@ private:
     // the extent the last present was produced at (SetPresentExtent may change before ReadPresentPixels)
     uint32_t m_PresentedWidth = 0, m_PresentedHeight = 0;
     uint32_t m_RasterFlags = 0;
-    struct PendingFrame {  // what the last DrawFrame submitted and FinishFrame has not waited for yet
-        bool m_Active = false;
+    struct PendingFrame {  // what a DrawFrame submitted and no fence has waited for yet
         std::vector<ViewportContext*> m_Targets;
         ViewportContext* m_Legacy = nullptr;  // the legacy present target among them
-        ViewportContext* m_Blit = nullptr;    // the primary viewport whose present blit was enqueued
+        ViewportContext* m_Blit = nullptr;    // the primary viewport target whose present blit was enqueued
         uint32_t m_BlitWidth = 0, m_BlitHeight = 0;
     };
-    PendingFrame m_Pending;
+    std::deque<PendingFrame> m_Pending;  // oldest first; at most m_FramesInFlight
+    void FinishOldestFrame();
+    // frames in flight: viewport id -> its targets 1 .. n-1 (target 0 is the m_Viewports entry), and the target of its
+    // latest frame
+    uint32_t m_FramesInFlight = 1;
+    uint64_t m_FrameCount = 0;
+    std::map<uint32_t, std::vector<ViewportContext>> m_RingTargets;
+    std::map<uint32_t, uint32_t> m_LatestTarget;
+    ViewportContext& TargetOf(uint32_t viewportId, ViewportContext& primary, uint32_t index);
+    const ViewportContext* LatestTarget(uint32_t viewportId) const;
 
     glm::vec3 m_AmbientColor{0.03f};
     float m_AmbientIntensity = 1.0f;

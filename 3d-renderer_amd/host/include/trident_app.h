@@ -115,6 +115,8 @@ int trident_app_read_present(trident_app* app, uint8_t* rgba, uint32_t width, ui
 int trident_app_draw_frame(trident_app* app);
 /* Renderer::FinishFrame: wait for the frame the last draw_frame submitted (the next draw_frame does it first). */
 int trident_app_finish_frame(trident_app* app);
+/* Renderer::SetFramesInFlight (1..4; 1 = the reference's pacing). */
+int trident_app_set_frames_in_flight(trident_app* app, uint32_t n);
 /* Renderer::GetViewportTexture: copies the viewport's image handle (TRI_E_STATE before its first frame). */
 int trident_app_viewport_texture(trident_app* app, uint32_t viewport_id, tri_image* out);
 /* Renderer::GetGeometryUploadCount. */

@@ -216,16 +216,20 @@ void Renderer::Init() {
 }
 
 void Renderer::DestroyViewportTargets() {
-    m_Pending = PendingFrame{};  // (its targets go; tri_destroy / tri_group_destroy wait for their streams)
-    for (auto& it : m_Viewports) {
-        ViewportContext& vc = it.second;
+    m_Pending.clear();  // (its targets go; tri_destroy / tri_group_destroy wait for their streams)
+    auto drop = [](ViewportContext& vc) {
         tri_destroy(vc.m_Ctx);
         tri_group_destroy(vc.m_Group);
         vc.m_Ctx = nullptr;
         vc.m_Group = nullptr;
         vc.m_HasImage = false;
         vc.m_Width = vc.m_Height = 0;
-    }
+    };
+    for (auto& it : m_Viewports) drop(it.second);
+    for (auto& it : m_RingTargets)
+        for (ViewportContext& vc : it.second) drop(vc);
+    m_RingTargets.clear();
+    m_LatestTarget.clear();
     tri_destroy(m_LegacyTarget.m_Ctx);
     tri_group_destroy(m_LegacyTarget.m_Group);
     m_LegacyTarget = ViewportContext{};
@@ -246,6 +250,34 @@ void Renderer::Shutdown() {
     m_Viewports.clear();
     if (m_Initialised) m_Shutdown = true;
     m_Initialised = false;
+}
+
+void Renderer::SetFramesInFlight(uint32_t n) {
+    n = std::min<uint32_t>(std::max<uint32_t>(n, 1u), 4u);
+    if (n == m_FramesInFlight) return;
+    FinishFrame();
+    DestroyViewportTargets();  // rebuilt by the next DrawFrame's PrepareViewport
+    m_FramesInFlight = n;
+}
+
+// Target `index` of a viewport (0: its m_Viewports entry; 1 .. n-1: the ring's), carrying the viewport's info.
+Renderer::ViewportContext& Renderer::TargetOf(uint32_t viewportId, ViewportContext& primary, uint32_t index) {
+    if (index == 0) return primary;
+    std::vector<ViewportContext>& ring = m_RingTargets[viewportId];
+    if (ring.size() < m_FramesInFlight - 1) ring.resize(m_FramesInFlight - 1);  // (sized once per SetFramesInFlight)
+    ViewportContext& t = ring[index - 1];
+    t.m_Info = primary.m_Info;
+    return t;
+}
+
+const Renderer::ViewportContext* Renderer::LatestTarget(uint32_t viewportId) const {
+    auto it = m_Viewports.find(viewportId);
+    if (it == m_Viewports.end()) return nullptr;
+    auto li = m_LatestTarget.find(viewportId);
+    if (li == m_LatestTarget.end() || li->second == 0) return &it->second;
+    auto ri = m_RingTargets.find(viewportId);
+    if (ri == m_RingTargets.end() || ri->second.size() < li->second) return &it->second;
+    return &ri->second[li->second - 1];
 }
 
 bool Renderer::SetDeviceCount(uint32_t count, const std::vector<int32_t>& devices) {
@@ -995,7 +1027,11 @@ bool Renderer::SubmitTarget(ViewportContext& vc, const tri_global_ubo& ubo, cons
 void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     const auto t0 = std::chrono::steady_clock::now();
     if (!m_Initialised || m_Shutdown) return;
-    FinishFrame();  // the previous frame's fence (Renderer.cpp:752-772)
+    // the fence (Renderer.cpp:752-772): the reference waits for the previous frame; with n frames in flight, for
+    // frame k - n + 1, whose targets this frame is about to reuse
+    const uint32_t inflight = m_Devices.size() > 1 ? 1u : m_FramesInFlight;
+    while (m_Pending.size() >= inflight) FinishOldestFrame();
+    const uint32_t tix = (uint32_t)(m_FrameCount++ % inflight);
     GatherDraws();
     PrepareBonePaletteBuffer();
     std::vector<tri_draw> draws;
@@ -1006,28 +1042,27 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
     tri_global_ubo lastUbo{};
     // RecordCommandBuffer's per-viewport render passes: the other viewports first, the primary one last
     // (Renderer.cpp:5208-5221), so the uniform block left bound is the primary viewport's
-    auto pass = [&](ViewportContext& vc) {
+    ViewportContext* activeTarget = nullptr;
+    auto pass = [&](uint32_t id, ViewportContext& primary) {
+        ViewportContext& vc = TargetOf(id, primary, tix);  // this frame's target of the viewport
         if (!PrepareViewport(vc)) return;
         tri_global_ubo ubo;
         UpdateUniformBuffer(GetActiveCamera(vc), ubo);
         if (!SubmitTarget(vc, ubo, draws, shadow, shadowOn)) return;
         lastUbo = ubo;
         submitted.push_back(&vc);
+        m_LatestTarget[id] = tix;
+        if (id == m_ActiveViewportId) activeTarget = &vc;
     };
     for (auto& it : m_Viewports)
-        if (it.first != m_ActiveViewportId) pass(it.second);
+        if (it.first != m_ActiveViewportId) pass(it.first, it.second);
     auto active = m_Viewports.find(m_ActiveViewportId);
-    if (active != m_Viewports.end()) pass(active->second);
-    const bool primaryActive = active != m_Viewports.end() &&
-                               std::find(submitted.begin(), submitted.end(), &active->second) != submitted.end();
+    if (active != m_Viewports.end()) pass(active->first, active->second);
+    const bool primaryActive = activeTarget != nullptr;
     // Legacy direct-to-swapchain path (Renderer.cpp:5233, :5498-5590): without a rendered primary viewport
     // the skybox, the meshes and the sprites go straight into the present image at the swapchain extent,
     // cleared to the clear colour, with the uniform block last recorded: the null-camera update
     // (GetActiveCamera()) when no viewport rendered (:5223-5226), else the last viewport pass's.
-    m_PresentSource = nullptr;
-    m_PresentGroup = nullptr;
-    m_PresentLegacy = false;
-    m_PresentedWidth = m_PresentedHeight = 0;
     ViewportContext* legacy = nullptr;
     if (!primaryActive && m_PresentWidth && m_PresentHeight) {
         m_LegacyTarget.m_Info.Size = glm::vec2((float)m_PresentWidth, (float)m_PresentHeight);
@@ -1042,30 +1077,39 @@ void Renderer::DrawFrame() {  // Renderer.cpp:733-837
         }
     }
     // Primary viewport -> swapchain image, VK_FILTER_LINEAR (Renderer.cpp:5346-5361), stream-ordered behind its pass.
-    m_Pending = PendingFrame{};
-    m_Pending.m_Targets = submitted;
-    m_Pending.m_Legacy = legacy;
+    PendingFrame pf;
+    pf.m_Targets = submitted;
+    pf.m_Legacy = legacy;
     if (primaryActive && m_PresentWidth && m_PresentHeight) {
-        const Target t{active->second.m_Ctx, active->second.m_Group};
+        const Target t{activeTarget->m_Ctx, activeTarget->m_Group};
         if (t.Blit(m_PresentWidth, m_PresentHeight) == TRI_OK) {
-            m_Pending.m_Blit = &active->second;
-            m_Pending.m_BlitWidth = m_PresentWidth;
-            m_Pending.m_BlitHeight = m_PresentHeight;
+            pf.m_Blit = activeTarget;
+            pf.m_BlitWidth = m_PresentWidth;
+            pf.m_BlitHeight = m_PresentHeight;
         } else {
             LogError("present blit", tri_last_error());
         }
     }
-    m_Pending.m_Active = true;
+    m_Pending.push_back(std::move(pf));
     // no wait here: the next DrawFrame (or a reader) fences this frame, as the reference fences the previous
     // frame's timeline value at the start of DrawFrame (Renderer.cpp:752-772)
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     RecordFrameTiming(ms);
 }
 
-void Renderer::FinishFrame() {  // the frame fence (Renderer.cpp:744-772)
-    if (!m_Pending.m_Active) return;
-    PendingFrame p = std::move(m_Pending);
-    m_Pending = PendingFrame{};
+void Renderer::FinishFrame() {  // every frame in flight
+    while (!m_Pending.empty()) FinishOldestFrame();
+}
+
+void Renderer::FinishOldestFrame() {  // the frame fence (Renderer.cpp:744-772)
+    if (m_Pending.empty()) return;
+    PendingFrame p = std::move(m_Pending.front());
+    m_Pending.pop_front();
+    // this frame's present replaces the previous one (none if it failed)
+    m_PresentSource = nullptr;
+    m_PresentGroup = nullptr;
+    m_PresentLegacy = false;
+    m_PresentedWidth = m_PresentedHeight = 0;
     // A frame that outgrew the bin/clip queues has grown them inside tri_synchronize and is re-rendered (and its
     // present blit redone), so a presented frame is always complete.
     for (ViewportContext* vc : p.m_Targets) {
@@ -1134,16 +1178,16 @@ void Renderer::RecordFrameTiming(double ms) {  // Renderer.cpp:6286-6343
 
 void* Renderer::GetViewportTexture(uint32_t viewportId) const {
     const_cast<Renderer*>(this)->FinishFrame();  // the handle's contents are a completed frame
-    auto it = m_Viewports.find(viewportId);
-    if (it == m_Viewports.end() || (!it->second.m_Ctx && !it->second.m_Group) || !it->second.m_HasImage) return nullptr;
-    return const_cast<tri_image*>(&it->second.m_Image);
+    const ViewportContext* vc = LatestTarget(viewportId);  // the latest frame's target (frames in flight)
+    if (!vc || (!vc->m_Ctx && !vc->m_Group) || !vc->m_HasImage) return nullptr;
+    return const_cast<tri_image*>(&vc->m_Image);
 }
 
 bool Renderer::ReadViewportPixels(uint32_t viewportId, std::vector<uint8_t>& rgba, std::vector<float>* depth) {
     FinishFrame();
-    auto it = m_Viewports.find(viewportId);
-    if (it == m_Viewports.end() || (!it->second.m_Ctx && !it->second.m_Group)) return false;
-    ViewportContext& vc = it->second;
+    const ViewportContext* latest = LatestTarget(viewportId);  // the latest frame's target (frames in flight)
+    if (!latest || (!latest->m_Ctx && !latest->m_Group)) return false;
+    const ViewportContext& vc = *latest;
     std::vector<uint8_t> bgra((size_t)vc.m_Width * vc.m_Height * 4);
     std::vector<uint32_t> dbits;
     if (depth) dbits.resize((size_t)vc.m_Width * vc.m_Height);

@@ -519,6 +519,14 @@ int trident_app_draw_frame(trident_app* app) {
     });
 }
 
+int trident_app_set_frames_in_flight(trident_app* app, uint32_t n) {
+    return Guard(app, [&] {
+        if (n == 0 || n > 4) return TRI_E_INVALID;
+        app->renderer.SetFramesInFlight(n);
+        return TRI_OK;
+    });
+}
+
 int trident_app_finish_frame(trident_app* app) {
     return Guard(app, [&] {
         app->renderer.FinishFrame();

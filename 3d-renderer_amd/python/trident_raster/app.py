@@ -52,6 +52,7 @@ _APP_FUNCTIONS = [
     ("trident_app_set_skybox", C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32]),
     ("trident_app_draw_frame", C.c_int, [C.c_void_p]),
     ("trident_app_finish_frame", C.c_int, [C.c_void_p]),
+    ("trident_app_set_frames_in_flight", C.c_int, [C.c_void_p, C.c_uint32]),
     ("trident_app_read_pixels", C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]),
     ("trident_app_frame_inputs", C.c_int, [C.c_void_p, C.c_uint32, C.POINTER(abi.TriGlobalUbo), C.c_void_p, C.c_uint32,
                                            C.POINTER(C.c_uint32)]),
@@ -234,6 +235,10 @@ class TridentApp:
 
     def draw_frame(self):
         _check(self._lib.trident_app_draw_frame(self._h), "draw_frame")
+
+    def set_frames_in_flight(self, n):
+        """Renderer::SetFramesInFlight (1 = the reference's pacing: DrawFrame waits for the previous frame)."""
+        _check(self._lib.trident_app_set_frames_in_flight(self._h, n), "set_frames_in_flight")
 
     def finish_frame(self):
         """Wait for the last draw_frame's frame (Renderer::FinishFrame; the next draw_frame does it first)."""

@@ -1166,7 +1166,7 @@ FORGE_PANELS = {"viewports": ((2, 1064, 1078), (1, 992, 1078)), "present": (2559
 FORGE_4K = {"viewports": ((1, 3840, 2160),), "present": (3840, 2160)}
 
 
-def forge_frame(layout, frames=200, warm_seconds=0.25):
+def forge_frame(layout, frames=200, warm_seconds=0.25, frames_in_flight=1):
     """The frame Forge runs, through the engine API rather than the C-ABI: RenderCommand::DrawFrame on the
     Trident::Renderer shim (trident_app) with C3's 1M-triangle grid as one mesh entity, C3's sun and four point
     lights, the editor camera on the Scene viewport and a ready runtime camera on the Game viewport, the cubemap found
@@ -1174,13 +1174,16 @@ def forge_frame(layout, frames=200, warm_seconds=0.25):
     Every DrawFrame gathers the draws, packs the uniform block per viewport, renders each viewport, blits, and waits
     for the previous frame first (the reference's fence, :752-772). Returns frames/s (DrawFrames completed per second)
     and the host cost of one DrawFrame: with the GPU idle (the engine's own work plus the launches) and as the
-    renderer's GetFrameTimingStats record it in the loop (which includes the wait for the previous frame)."""
+    renderer's GetFrameTimingStats record it in the loop (which includes the wait for the previous frame).
+    frames_in_flight: Renderer::SetFramesInFlight — 1 is the reference's pacing; more keep that many targets per
+    viewport so the next frames' front end overlaps this frame's raster, as the C-ABI line's contexts do."""
     from trident_raster import app, scenes
 
     s = build_scene("c3")
     a = app.TridentApp()
     try:
         a.set_assets_dir(scenes.ASSETS_DIR)
+        a.set_frames_in_flight(frames_in_flight)
         mi = a.append_mesh(s.vertices, s.indices, base_color=(1.0, 1.0, 1.0, 1.0), metallic=0.1, roughness=0.6)
         a.add_mesh_entity("none", mi)
         a.add_light("directional", direction=(-0.5, -1.0, -0.3), intensity=3.0)
@@ -1218,7 +1221,7 @@ def forge_frame(layout, frames=200, warm_seconds=0.25):
                 "mpix_rendered_per_s": frames / dt * px / 1e6, "frames": frames,
                 "host_ms_per_drawframe_idle_gpu": idle[len(idle) // 2],
                 "drawframe_ms_avg_frame_timing_stats": timing["avg_ms"],
-                "triangles": s.triangles,
+                "triangles": s.triangles, "frames_in_flight": frames_in_flight,
                 "path": "RenderCommand::DrawFrame (Trident::Renderer shim, trident_app) -> tri_raster C-ABI"}
     finally:
         a.close()
@@ -1621,6 +1624,9 @@ def main():
         # viewport, beside the C-ABI line
         secondary["forge_editor_frame_c3_panels"] = forge_frame(FORGE_PANELS)
         secondary["forge_editor_frame_c3_4k"] = forge_frame(FORGE_4K)
+        # the same frames with three targets per viewport in flight (Renderer::SetFramesInFlight(3))
+        secondary["forge_editor_frame_c3_panels_3inflight"] = forge_frame(FORGE_PANELS, frames_in_flight=3)
+        secondary["forge_editor_frame_c3_4k_3inflight"] = forge_frame(FORGE_4K, frames_in_flight=3)
 
     arm_watchdog(0, "")
     copy_gbs = device_copy_gbs(br.dev) if rank == 0 else None

@@ -356,6 +356,39 @@ def test_gpu_shim_shared_geometry_and_viewport_texture(app_mod, oracle):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("inflight", [2, 3])
+def test_gpu_shim_frames_in_flight(app_mod, oracle, inflight):
+    """Renderer::SetFramesInFlight(n): frame k renders into target k mod n of each viewport and DrawFrame fences only
+    frame k - n + 1; whatever frame is read back (pixels, the viewport texture, the present) is the latest one, equal
+    to the oracle's frame of the latest inputs, in both viewports, while the camera and an entity move every frame."""
+    from trident_raster import raster
+
+    a, e = c1_app(app_mod)
+    a.set_frames_in_flight(inflight)
+    assert a.frame_timing()["samples"] == 0
+    a.set_viewport(2, 200, 160)
+    a.set_viewport(1, W, H)  # the primary viewport
+    a.set_present_extent(320, 240)
+    for frame in range(2 * inflight + 1):
+        a.set_entity_transform(e, rotation=(0.0, 17.0 * frame, 0.0))
+        a.set_camera("editor", (0.1 * frame, 3.0, 8.0))
+        a.draw_frame()
+        if frame % inflight == 1 or frame == 2 * inflight:  # read mid-ring and at the end
+            assert_shim_parity(a, oracle, 1, W, H, min_covered=1000)
+            assert_shim_parity(a, oracle, 2, 200, 160, min_covered=200)
+            img = a.viewport_texture(1)
+            bgra = raster.copy_device_to_host(img.device_ptr, H * img.pitch_bytes, img.device).reshape(H, W, 4)
+            rgba, _ = a.read_pixels(1, W, H)
+            assert np.array_equal(bgra[..., [2, 1, 0, 3]], rgba)
+    one, _ = a.read_pixels(1, W, H, depth=False)
+    a.set_frames_in_flight(1)  # back to the reference's pacing: targets rebuilt, same frame
+    a.draw_frame()
+    again, _ = a.read_pixels(1, W, H, depth=False)
+    assert np.array_equal(one, again)
+    a.close()
+
+
+@pytest.mark.gpu
 def test_gpu_contexts_share_one_geometry(oracle):
     import scene_cases as sc
     from trident_raster import raster
