@@ -267,13 +267,6 @@ struct TriFrameParams {
     // its polygon vertices' records in the same layout.
     uint32_t obj48, obj48_xform;
     uint32_t vdelta[TRI_OBJ48_DRAWS];  // per draw: base_vertex + min_index - first slot (mod 2^32)
-    // idx_route (frames of 2..TRI_OBJ48_DRAWS draws whose index rows follow their primitive numbers: first_index =
-    // idx_k + 3 * first primitive for every active draw, as meshes concatenated in draw order are): a primitive p's
-    // vertex slots are its index triple at idx_k + 3 p plus its draw's slot offset vbd[d] (d: the last draw whose
-    // first primitive pbase[d] <= p), as on single-draw frames, so k_setup writes no 16-B prim_vs record per
-    // primitive and the fragment stage gathers 12 index bytes instead of it (C5: 16 MB of set-up writes per frame)
-    uint32_t idx_route, idx_k;
-    uint32_t pbase[TRI_OBJ48_DRAWS], vbd[TRI_OBJ48_DRAWS];
     // shadow-map pre-pass (tri_set_shadow): s_size x s_size map, 32x32 bins
     // Default.frag's AI frame blend (:182-191): on when AiBlendConfig.w > 0 and clamp(AiBlendConfig.x, 0, 1) > 0 (that
     // clamped weight is ai_wgt); the frame texture is ai_tw x ai_th RGBA8 UNORM (TriDeviceBuffers::ai_frame), sampled at
@@ -287,4 +280,11 @@ struct TriFrameParams {
     float s_bias;  // depth bias of the lookup compare
     float s_slope; // slope-scaled depth bias of the depth pass
     float lvp[16]; // light ortho * light view (affine)
+    // idx_route (frames of 2..TRI_OBJ48_DRAWS draws whose index rows follow their primitive numbers: first_index =
+    // idx_k + 3 * first primitive for every active draw, as meshes concatenated in draw order are): a primitive p's
+    // vertex slots are its index triple at idx_k + 3 p plus its draw's slot offset vbd[d] (d: the last draw whose
+    // first primitive pbase[d] <= p), as on single-draw frames, so k_setup writes no 16-B prim_vs record per
+    // primitive and the fragment stage gathers 12 index bytes instead of it (C5: 16 MB of set-up writes per frame)
+    uint32_t idx_route, idx_k;
+    uint32_t pbase[TRI_OBJ48_DRAWS], vbd[TRI_OBJ48_DRAWS];
 };

@@ -1259,7 +1259,7 @@ __device__ __forceinline__ void setup_body(const TriFrameParams& fp, const TriDe
                 }
                 // k_raster's (and k_shadow_raster's) route from the primitive to its vertex slots and draw; a
                 // single-draw frame finds the slots in the index buffer instead (prim_slots)
-                if (!ONE && !fp.one_draw && !fp.idx_route && (ok[t] || needs_clip[t] || sok[t]))
+                if (!ONE && !fp.one_draw && !(TRI_IDX_ROUTE && fp.idx_route) && (ok[t] || needs_clip[t] || sok[t]))
                     b.prim_vs[p[t]] = make_uint4(sl0[t], sl1[t], sl2[t], (uint32_t)d | (needs_clip[t] ? TRI_PRIM_CLIPPED : 0u));
             }
             nsetup += ok[t] ? 1u : 0u;
@@ -1307,7 +1307,7 @@ __device__ __forceinline__ void setup_body(const TriFrameParams& fp, const TriDe
 // waves takes exactly one raster wave's registers from a concurrent frame's k_raster (8 waves x 64 fill a SIMD's
 // register file) instead of 72 — with 3 of its workgroups per CU (TRI_SETUP_WGS_PER_CU_OVERLAP) C3 +0.6 % (round 6 A/B)
 #ifndef TRI_SETUP_WAVES_ONE
-#define TRI_SETUP_WAVES_ONE TRI_SETUP_WAVES
+#define TRI_SETUP_WAVES_ONE 8
 #endif
 template <bool WITH_SHADOW, bool ONE>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu((ONE && !WITH_SHADOW) ? TRI_SETUP_WAVES_ONE : TRI_SETUP_WAVES))) void k_setup(TRI_KARGS) {
@@ -1387,20 +1387,33 @@ __device__ __forceinline__ TriRec rec_from_snaps(uint32_t p, const uint32_t sl[3
 // index - min_index, as k_setup computed them; k_setup writes no prim_vs then), else its prim_vs record.
 // ONE (k_raster_plain's single-draw, 1x1-texture instantiation): fp.one_draw and fp.shade_solid are known
 // to be set, so the other paths and their uniform flags compile away.
-template <bool ONE = false>
+// IDX: the instantiation may take the index route (not the shadow pre-pass's kernels: the draw search cost the C5
+// fragment stage 4 spilled VGPRs and 1.3 % of C5's frame rate, more than the records' writes it saves; the host
+// keeps idx_route off on shadow frames)
+template <bool ONE = false, bool IDX = true>
 __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t p,
                                            uint32_t sl[3], uint32_t& d) {
     if (ONE || fp.one_draw) {
         const u32x3v q = rec96<12>(rec_buf(b.indices + fp.draw0.first_index, 12u, fp.nprims), p, 0u);
         sl[0] = q[0] - fp.draw0.min_index; sl[1] = q[1] - fp.draw0.min_index; sl[2] = q[2] - fp.draw0.min_index;
         d = 0;
-    } else if (fp.idx_route) {  // (uniform) the index triple, and the draw from the frame's primitive bases
+    } else if (IDX && TRI_IDX_ROUTE && fp.idx_route) {  // (uniform) the index triple, the draw from the primitive bases
         const u32x3v q = rec96<12>(rec_buf(b.indices + fp.idx_k, 12u, fp.nprims), p, 0u);
-        uint32_t dd = 0, v = fp.vbd[0];
-        for (uint32_t i = 1; i < fp.ndraws; ++i) {  // uniform trip count, scalar operands: a compare, two selects
-            const bool ge = p >= fp.pbase[i];
-            dd = ge ? i : dd;
-            v = ge ? fp.vbd[i] : v;
+        // the first active lane's draw by a scalar search; when every lane's primitive lies in it (a wave's pixels
+        // are mostly one draw's) the draw and its slot offset stay scalar, else a compare-and-select per draw
+        const uint32_t p0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)p);
+        uint32_t d0 = 0;
+        while (d0 + 1 < fp.ndraws && p0 >= fp.pbase[d0 + 1]) ++d0;
+        const uint32_t hi = d0 + 1 < fp.ndraws ? fp.pbase[d0 + 1] : ~0u;
+        uint32_t dd = d0, v = fp.vbd[d0];
+        if (__ballot(p < fp.pbase[d0] || p >= hi) != 0ull) {
+            dd = 0;
+            v = fp.vbd[0];
+            for (uint32_t i = 1; i < fp.ndraws; ++i) {  // uniform trip count, scalar operands
+                const bool ge = p >= fp.pbase[i];
+                dd = ge ? i : dd;
+                v = ge ? fp.vbd[i] : v;
+            }
         }
         sl[0] = q[0] + v; sl[1] = q[1] + v; sl[2] = q[2] + v;
         d = dd;
@@ -1412,12 +1425,12 @@ __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDe
 }
 
 // A bin-queue entry -> its triangle.
-template <bool ONE = false>
+template <bool ONE = false, bool IDX = true>
 __device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
     if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
     const FetchBufs fb = fetch_bufs(fp, b);
     uint32_t sl[3], d;
-    prim_slots<ONE>(fp, b, e, sl, d);
+    prim_slots<ONE, IDX>(fp, b, e, sl, d);
     return rec_from_snaps(e, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
 }
 
@@ -1463,7 +1476,7 @@ __device__ __forceinline__ uint32_t key_low(uint32_t prim_sub) {
 // table the coverage pass filled, instead of gathering its index triple. No hash and no sort. The coverage code takes
 // the record's prim_sub re-encoded so that key_low() of it yields this word (qenc).
 #ifndef TRI_QTAB
-#define TRI_QTAB 0
+#define TRI_QTAB 1
 #endif
 constexpr uint32_t kQtab = 256, kQPrimMax = (1u << 20) - 1u;
 __device__ __forceinline__ uint32_t qenc(uint32_t prim_sub, uint32_t qpos) {
@@ -2344,7 +2357,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
             const uint32_t q = low & 0xFFu;
             sl[0] = qtab[q]; sl[1] = qtab[kQtab + q]; sl[2] = qtab[2 * kQtab + q];
         } else {
-            prim_slots<ONE>(fp, b, prim, sl, d);
+            prim_slots<ONE, !SHADOW>(fp, b, prim, sl, d);
         }
         // Every gather that needs only the slots is issued before the first wait: the snapped vertices and
         // the varyings are one round trip after the index fetch (the snaps are loaded for a clipped primitive
@@ -2357,7 +2370,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
         taps = load_taps<ONE, true>(fb, v0 + dl, v1 + dl, v2 + dl);
     } else if (!ONE) {
-        prim_slots<ONE>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
+        prim_slots<ONE, !SHADOW>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
     }
     TriRec rc;
     if (CLIPM == 2 || (CLIPM == 0 && sub)) {  // a clipped primitive's sub-triangle: its own slots and varyings
@@ -2595,7 +2608,7 @@ __device__ __forceinline__ uint32_t sky_bgra_persp(const TriFrameParams& fp, con
 #endif
 template <int BL>
 constexpr int big_area() { return BL == 4 ? TRI_BIG_AREA16 : TRI_BIG_AREA; }
-constexpr int kBigQueue = TRI_QTAB ? 384 : 1024;  // (TRI_QTAB: its table's LDS comes from here)
+constexpr int kBigQueue = 1024;
 
 // Bijective XCD-aware block -> bin remap (cdna_hip_programming.md §5 "XCD swizzle must be
 // bijective"): workgroups b, b+8, b+16 ... share an XCD's L2, so give them consecutive bins — each
@@ -2726,7 +2739,9 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
-    constexpr int kBigN = kBalanced ? kBigQueue / 2 : kBigQueue;
+    constexpr bool kQt = TRI_QTAB && ONE && BL == 5;
+    // (the queue-position table's 3 KB come from the large-triangle queue, so that 8 workgroups still fit the LDS)
+    constexpr int kBigN = kBalanced ? kBigQueue / 2 : (kQt ? 384 : kBigQueue);
     __shared__ uint32_t bigq[kBigN];  // queue entries of the large triangles
     __shared__ float lut[512];
     constexpr int kJobWords = (kBalanced && kCovJobs > BIN * BIN ? kCovJobs : BIN * BIN);
@@ -2734,7 +2749,6 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ CovEntry cov[kBalanced ? kCovPass : 1];
     __shared__ uint32_t wsum[TRI_BLOCK / 64];
     __shared__ uint32_t nbig, nsky;
-    constexpr bool kQt = TRI_QTAB && ONE && BL == 5;
     __shared__ uint32_t qtab[kQt ? 3 * kQtab : 1];   // TRI_QTAB: per queue position, the entry's vertex slots
     __shared__ uint16_t bigqp[kQt ? kBigN : 1];      // ... and the large triangles' queue positions
     const int tid = threadIdx.x;
@@ -2773,7 +2787,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     const bool qmode = kQt && cnt <= kQtab && fp.nprims <= kQPrimMax;
     if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
-            const TriRec r = load_entry<ONE>(fp, b, queue[0]);
+            const TriRec r = load_entry<ONE, !SHADOW>(fp, b, queue[0]);
             const uint64_t key = (0x3F000000ull << 32) | key_low(r.prim_sub);
             for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = key;
         }
@@ -2789,7 +2803,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
         int32_t cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
         if (tid < kCovPass && i < s1) {
             const uint32_t ri = queue[i];
-            r = load_entry<ONE>(fp, b, ri);
+            r = load_entry<ONE, !SHADOW>(fp, b, ri);
             rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
             if (cx0 <= cx1 && cy0 <= cy1) {
                 bool big = false;
@@ -2848,7 +2862,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
   } else {
     auto cover = [&](uint32_t i, int32_t sub, int32_t step, bool first) {
         const uint32_t ri = (TRI_QUEUE_PREFETCH && first) ? pre1 : queue[i];
-        TriRec r = load_entry<ONE>(fp, b, ri);
+        TriRec r = load_entry<ONE, !SHADOW>(fp, b, ri);
         if (kQt && qmode) {  // the entry's slots (set-up orientation undone) at its queue position; the key's payload
             if (!(ri & TRI_ENTRY_CLIPPED)) {
                 qtab[i] = r.v[0]; qtab[kQtab + i] = r.v[2]; qtab[2 * kQtab + i] = r.v[1];
@@ -2884,7 +2898,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     TRI_STAMP(2);
     const uint32_t nb = min(nbig, (uint32_t)kBigN);
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        TriRec r = load_entry<ONE>(fp, b, bigq[q]);
+        TriRec r = load_entry<ONE, !SHADOW>(fp, b, bigq[q]);
         if (kQt && qmode) r.prim_sub = qenc(r.prim_sub, bigqp[q]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
@@ -3082,7 +3096,7 @@ template <bool EXACT, int BL, bool ONE>
 // waves instead of displacing one. On gfx950's unified register file the attribute's value is doubled: 28 caps at 56
 // VGPRs; 0 = no cap.
 #ifndef TRI_RASTER_ONE_VGPRS
-#define TRI_RASTER_ONE_VGPRS 0
+#define TRI_RASTER_ONE_VGPRS 28
 #endif
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <= 5 ? ((ONE && !EXACT) ? TRI_RASTER_WAVES_PLAIN_ONE : TRI_RASTER_WAVES_PLAIN) : 3))) void k_raster_plain(TRI_KARGS) {
     TRI_BIND_ARGS;
@@ -3113,7 +3127,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
 __device__ __forceinline__ TriRec load_shadow_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
     const Rsrc snr = make_rsrc(b.lsnap, 16ull * fp.nslots);
     uint32_t sl[3], d;
-    prim_slots(fp, b, e, sl, d);
+    prim_slots<false, false>(fp, b, e, sl, d);
     const uint4 q0 = ld128(snr, sl[0] * 16u), q1 = ld128(snr, sl[1] * 16u), q2 = ld128(snr, sl[2] * 16u);
     const int32_t X0 = ((int32_t)q0.x << 8) >> 8, X1 = ((int32_t)q1.x << 8) >> 8, X2 = ((int32_t)q2.x << 8) >> 8;
     const int32_t Y0 = (int32_t)q0.y, Y1 = (int32_t)q1.y, Y2 = (int32_t)q2.y;

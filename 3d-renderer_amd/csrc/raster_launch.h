@@ -21,13 +21,15 @@
 // bins cannot use while it waits on its fetch -> atomic -> store chain. Fewer, longer workgroups (more primitives
 // per lane) make the set-up slower alone (C3 27.9 -> 37 us) but the frame rate higher (C3 10.39-10.43k -> 10.55k,
 // C3 under a TRS draw +1 %, C2 unchanged: its set-up is one primitive per lane either way). The shadow set-up bins
-// every primitive twice and keeps the resident round (C5 4.90k -> 4.75k with 2).
+// every primitive twice and keeps the resident round (C5 4.90k -> 4.75k with 2). Round 6: with the single-draw set-up
+// within 64 VGPRs and the raster's C3 instantiation within 56 (raster_kernels.hip: TRI_SETUP_WAVES_ONE,
+// TRI_RASTER_ONE_VGPRS) a set-up wave displaces at most one raster wave, and 3 per CU beat 2 (same-box A/B).
 // k_setup's chunk target for bands (cluster culling): most chunks are culled and exit at once
 #ifndef TRI_SETUP_BAND_CHUNKS
 #define TRI_SETUP_BAND_CHUNKS 4096
 #endif
 #ifndef TRI_SETUP_WGS_PER_CU_OVERLAP
-#define TRI_SETUP_WGS_PER_CU_OVERLAP 2
+#define TRI_SETUP_WGS_PER_CU_OVERLAP 3
 #endif
 
 // Device pointers in the global address space (device compilation only; the host sees plain pointers of the same

@@ -1688,6 +1688,7 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    arm_watchdog(args.watchdog_seconds if world > 1 else 0, "teardown")
     br.close()
     if dist_on:
         import torch.distributed as dist

@@ -14,5 +14,5 @@ for setting in "$@"; do
 import json; d=json.loads(open('$log').read().strip().splitlines()[-1])
 st=lambda x: {k[3:]:round(v*1e3,1) for k,v in x.items() if v}
 print('[${setting:-base}] c3 %.0f'%d['value'], st(d['stage_ms']))
-for k,v in d['secondary'].items(): print('    %s %.0f'%(k[:12], v['frames_per_s']), st(v['stage_ms']))"
+for k,v in d['secondary'].items(): print('    %s %.0f'%(k[:24], v['frames_per_s']), st(v.get('stage_ms', {})))"
 done
