@@ -972,7 +972,10 @@ __device__ __forceinline__ void bin_pair(const TriDeviceBuffers& b, bool ok0, bo
 // out, so the grid is never cleared. A round whose box exceeds kBinGrid cells bins with the per-wave
 // reservations above (a uniform choice: every wave reads the same box). Must be reached by the whole
 // workgroup. Rejected alternative: an LDS hash table keyed by bin (CAS probing): C3 set-up +2 us.
-constexpr uint32_t kBinGrid = 1024;
+#ifndef TRI_BIN_GRID
+#define TRI_BIN_GRID 1024
+#endif
+constexpr uint32_t kBinGrid = TRI_BIN_GRID;
 struct BinBox {
     uint32_t cnt[kBinGrid];
     uint32_t base[kBinGrid];
@@ -2741,7 +2744,10 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
     constexpr bool kQt = TRI_QTAB && ONE && BL == 5;
     // (the queue-position table's 3 KB come from the large-triangle queue, so that 8 workgroups still fit the LDS)
-    constexpr int kBigN = kBalanced ? kBigQueue / 2 : (kQt ? 384 : kBigQueue);
+#ifndef TRI_QTAB_BIGN
+#define TRI_QTAB_BIGN 384
+#endif
+    constexpr int kBigN = kBalanced ? kBigQueue / 2 : (kQt ? TRI_QTAB_BIGN : kBigQueue);
     __shared__ uint32_t bigq[kBigN];  // queue entries of the large triangles
     __shared__ float lut[512];
     constexpr int kJobWords = (kBalanced && kCovJobs > BIN * BIN ? kCovJobs : BIN * BIN);

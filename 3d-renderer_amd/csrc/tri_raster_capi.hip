@@ -147,6 +147,7 @@ struct tri_ctx {
     uint32_t* d_cvis = nullptr; size_t cap_cvis = 0;
     uint32_t ncl_total = 0;
     void* h_stage = nullptr; size_t cap_stage = 0;  // pinned upload staging
+    TriCounters* h_ctr = nullptr;  // pinned: the frame's counters, copied on the stream by tri_synchronize
     hipEvent_t stage_free = nullptr;
     uint32_t ndraws = 0, nslots = 0, nprims = 0;
     bool any_skin = false;
@@ -626,9 +627,10 @@ int collect_timing(tri_ctx* c) {
     return TRI_OK;
 }
 
-int check_overflow(tri_ctx* c) {
+int check_overflow(tri_ctx* c, const TriCounters* pinned = nullptr) {
     TriCounters h;
-    HIP_TRY(hipMemcpy(&h, c->d_ctr, sizeof h, hipMemcpyDeviceToHost));
+    if (pinned) h = *pinned;  // (copied on the context's stream before the wait)
+    else HIP_TRY(hipMemcpy(&h, c->d_ctr, sizeof h, hipMemcpyDeviceToHost));
     if (!h.flags) return TRI_OK;
     // the resets are stream-ordered before the next frame's kernels (the context's stream is non-blocking:
     // work on the null stream is not ordered with it)
@@ -934,6 +936,7 @@ int tri_destroy(tri_ctx* c) {
     f(c->d_color_own); f(c->d_depth_own); f(c->d_present);
     f(c->d_lpos); f(c->d_lsnap); f(c->d_sbin_count); f(c->d_sbin_list); f(c->d_shadow);
     if (c->h_stage) (void)hipHostFree(c->h_stage);
+    if (c->h_ctr) (void)hipHostFree(c->h_ctr);
     f(c->d_args);
     if (c->stage_free) (void)hipEventDestroy(c->stage_free);
     for (auto& v : {std::cref(c->pending), std::cref(c->free_sets)})
@@ -1464,8 +1467,12 @@ int tri_synchronize(tri_ctx* c) {
     if (!c) return fail(TRI_E_INVALID, "tri_synchronize: null context");
     int rc = make_current(c);
     if (rc) return rc;
+    // the counters ride the stream into pinned memory, so one wait covers the frame and its flags (a blocking
+    // hipMemcpy after the wait cost the engine's per-frame fence another round trip)
+    if (!c->h_ctr) HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&c->h_ctr), sizeof(TriCounters), hipHostMallocDefault));
+    HIP_TRY(hipMemcpyAsync(c->h_ctr, c->d_ctr, sizeof(TriCounters), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
-    return check_overflow(c);
+    return check_overflow(c, c->h_ctr);
 }
 
 int tri_readback(tri_ctx* c, uint8_t* bgra, uint32_t* depth) {

@@ -1131,21 +1131,18 @@ void Renderer::FinishOldestFrame() {  // the frame fence (Renderer.cpp:744-772)
             m_PresentedHeight = (uint32_t)vc->m_Info.Size.y;
         }
         if (vc == p.m_Blit && rc != TRI_OK) p.m_Blit = nullptr;
-        if (vc == p.m_Blit && rerendered && t.Blit(p.m_BlitWidth, p.m_BlitHeight) != TRI_OK) {
-            LogError("present blit", tri_last_error());
-            p.m_Blit = nullptr;
+        if (vc == p.m_Blit && rerendered) {  // (the first wait covered the blit behind the pass: same stream)
+            if (t.Blit(p.m_BlitWidth, p.m_BlitHeight) != TRI_OK || t.Sync() != TRI_OK) {
+                LogError("present blit", tri_last_error());
+                p.m_Blit = nullptr;
+            }
         }
     }
     if (p.m_Blit) {
-        const Target t{p.m_Blit->m_Ctx, p.m_Blit->m_Group};
-        if (t.Sync() == TRI_OK) {
-            m_PresentSource = p.m_Blit->m_Ctx;
-            m_PresentGroup = p.m_Blit->m_Group;
-            m_PresentedWidth = p.m_BlitWidth;  // the blit's destination extent
-            m_PresentedHeight = p.m_BlitHeight;
-        } else {
-            LogError("present blit", tri_last_error());
-        }
+        m_PresentSource = p.m_Blit->m_Ctx;
+        m_PresentGroup = p.m_Blit->m_Group;
+        m_PresentedWidth = p.m_BlitWidth;  // the blit's destination extent
+        m_PresentedHeight = p.m_BlitHeight;
     }
 }
 

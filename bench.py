@@ -1501,7 +1501,7 @@ def main():
             native_checked.append(res)
             if not ok:
                 fall_back_to_torch(res)
-        arm_watchdog(args.watchdog_seconds * 2, f"split autotune ({sc.name})")
+        arm_watchdog(args.watchdog_seconds * 2 if world > 1 else 0, f"split autotune ({sc.name})")
         if args.exchange == "native" and world > 1:
             ok, res = guarded("split autotune", lambda: autotuned_split(sc))
             if ok:
