@@ -62,7 +62,7 @@ def test_blit_restatements_agree(oracle, shape):
 
 # ---- GPU ----------------------------------------------------------------------------------------
 @pytest.mark.gpu
-@pytest.mark.parametrize("dw,dh", [(1280, 720), (320, 240), (333, 177), (640, 480)])
+@pytest.mark.parametrize("dw,dh", [(1280, 720), (320, 240), (333, 177), (640, 480), (640, 301), (1001, 480)])
 def test_gpu_blit_matches_oracle(oracle, dw, dh):
     from trident_raster import raster, scenes
 
