@@ -2950,7 +2950,14 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     const bool sky_on = fp.sky_size != 0;
     const bool sky_const = sky_on && !EXACT && fp.sky_mode == TRI_SKY_UNIFORM;
     const bool sky_queue = sky_on && !sky_const;
-    const uint32_t bg_bgra = sky_const ? fp.sky_bgra : fp.clear_bgra;
+    // the background colour stays a scalar to its store (its VGPR copy, hoisted out of the loop, was the shadow
+    // instantiation's one spilled register)
+    const uint32_t bg_sgpr = sky_const ? fp.sky_bgra : fp.clear_bgra;
+    auto bg_bgra = [&]() {
+        uint32_t v = bg_sgpr;
+        asm volatile("" : "+s"(v));
+        return v;
+    };
     // Clipped sub-triangles' pixels (rare: near-plane and guard-band crossings) are shaded after the loop, from
     // a per-wave LDS queue (a wave shades exactly BIN * BIN / 4 pixels, so its slice never overflows): the
     // loop then carries no clipped branch and no register merge at its join.
@@ -3011,7 +3018,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             float z;
             if (bg) {
                 const size_t o = (size_t)(py - fp.y0) * fp.W + px;
-                if (!sky_queue) b.color[o] = bg_bgra;
+                if (!sky_queue) b.color[o] = bg_bgra();
                 if (fp.write_depth) b.depth[o] = 1.0f;
                 continue;
             } else if (kAblate & 1) {  // diagnostics: coverage only

@@ -8,7 +8,7 @@ name=$1; shift
 mkdir -p lib/variants/obj_$name
 for s in raster_kernels raster_plain vertex_stage tri_raster_capi tri_group band_codec tri_xfer; do
   extra=""; [ $s = raster_plain ] && extra="-fno-slp-vectorize -mllvm --amdgpu-sched-strategy=max-ilp"
-  [ $s = vertex_stage ] && extra="${VERTEX_SCHED--mllvm --amdgpu-sched-strategy=max-ilp}"
+  [ $s = vertex_stage ] && extra="${VERTEX_SCHED-}"  # (the Makefile default: the default scheduler)
   /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -ffp-contract=off -Wno-unused-function -mllvm -amdgpu-kernarg-preload-count=2 $extra "$@" \
     -c csrc/$s.hip -o lib/variants/obj_$name/$s.o &
 done
