@@ -493,12 +493,14 @@ def xfer_comms(lib, world, rank, device_index, dev):
         uid = (C.c_uint8 * 128)(*t.cpu().tolist())
         comm = C.c_void_p()
         rc = lib.tri_xfer_comm_create(uid, world, rank, device_index, C.byref(comm))
-        if rc and k == 0:
-            raster._check(rc)  # no communicator at all: the caller's fallback (torch.distributed) takes over
-        failed = max_over_ranks(1.0 if rc else 0.0, dev, True)
+        failed = max_over_ranks(1.0 if rc else 0.0, dev, True)  # agreed first, so that every rank takes one branch
         if failed:
             if not rc:
                 lib.tri_xfer_comm_destroy(comm)
+            if k == 0:  # no communicator at all, on every rank: the caller's fallback (torch.distributed) takes over
+                if rc:
+                    raster._check(rc)  # this rank's own error
+                raise RuntimeError("tri_xfer_comm_create failed on another rank")
             print(f"bench.py: WARNING: RCCL communicator {k + 1} of {XFER_COMMS} could not be created; the native "
                   f"exchange shares {k} communicator(s) across its frames in flight", file=sys.stderr, flush=True)
             break
