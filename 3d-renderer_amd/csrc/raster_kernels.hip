@@ -2191,6 +2191,13 @@ __device__ __forceinline__ float shadow_vis(const TriFrameParams& fp, const uint
 #ifndef TRI_COLOUR_LATE
 #define TRI_COLOUR_LATE 1
 #endif
+// TRI_COLOUR_EARLY_ONE: the single-draw solid instantiation (C3's) issues its colour gathers with the other
+// varyings after all: within its 56-VGPR cap the scheduler keeps them without a spill, and their latency no longer
+// sits between the weights and the shading (C3 10.89k -> 11.03k frames/s, same box; every other instantiation
+// spills with them early, so keeps them late)
+#ifndef TRI_COLOUR_EARLY_ONE
+#define TRI_COLOUR_EARLY_ONE 1
+#endif
 struct Taps {
     V4 a0, a1, a2, b0, b1, b2, c0, c1, c2;
 };
@@ -2205,13 +2212,13 @@ __device__ __forceinline__ V4 ld_vary(const FetchBufs& fb, uint32_t slot, uint32
     const uint4 q = rec128<48>(SRC ? fb.src : fb.vary, slot, j * 16u);
     return V4{__uint_as_float(q.x), __uint_as_float(q.y), __uint_as_float(q.z), __uint_as_float(q.w)};
 }
-template <bool ONE = false, bool SRC = false>
-__device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint32_t v1, uint32_t v2) {
+template <bool ONE = false, bool SRC = false, bool EARLY = !TRI_COLOUR_LATE>
+__device__ __forceinline__ Taps load_taps(const FetchBufs& fb, uint32_t v0, uint32_t v1, uint32_t v2, bool colour = true) {
     Taps t;
     t.a0 = ld_vary<ONE, SRC>(fb, v0, 0); t.a1 = ld_vary<ONE, SRC>(fb, v0, 1);
     t.b0 = ld_vary<ONE, SRC>(fb, v1, 0); t.b1 = ld_vary<ONE, SRC>(fb, v1, 1);
     t.c0 = ld_vary<ONE, SRC>(fb, v2, 0); t.c1 = ld_vary<ONE, SRC>(fb, v2, 1);
-    if (!TRI_COLOUR_LATE) {
+    if (EARLY && colour) {
         t.a2 = ld_vary<ONE, SRC>(fb, v0, 2); t.b2 = ld_vary<ONE, SRC>(fb, v1, 2); t.c2 = ld_vary<ONE, SRC>(fb, v2, 2);
     }
     return t;
@@ -2351,6 +2358,10 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     const uint32_t prim = qtab ? kQPrimMax - (low >> 11) : TRI_PRIM_MAX - (low >> 3);
     const uint32_t sub = CLIPM == 1 ? 0u : (qtab ? (low >> 8) & 7u : low & 7u);  // >= 1: sub-triangle of a clipped primitive
     const FetchBufs fb = fetch_bufs<ONE>(fp, b);
+    constexpr bool kEarly = !TRI_COLOUR_LATE || (TRI_COLOUR_EARLY_ONE && ONE && !EXACT && !SHADOW);
+    // (issued early, the colour gathers are unconditional: on a frame with one vertex colour (obj_ucol) they read the
+    // records' colours beside their positions, unused; a uniform branch around them cost the instantiation 4 spills)
+    const bool vcol = kEarly || !(ONE && TRI_VARY_OBJ && obj_mode(fp) && fp.obj_ucol);
     uint32_t sl[3] = {0, 0, 0}, d = 0;
     TriSnap a0{}, a1{}, a2{};
     uint32_t v0 = 0, v1 = 0, v2 = 0, dl = 0;
@@ -2371,7 +2382,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         if (!ONE) dl = obj_delta(fp, d);  // (0 unless obj48: the host zeroes vdelta)
         // the varyings are gathered before the (rare) clipped branch: its record loads are waited for inside
         // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
-        taps = load_taps<ONE, true>(fb, v0 + dl, v1 + dl, v2 + dl);
+        taps = load_taps<ONE, true, kEarly>(fb, v0 + dl, v1 + dl, v2 + dl, vcol);
     } else if (!ONE) {
         prim_slots<ONE, !SHADOW>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
     }
@@ -2379,7 +2390,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     if (CLIPM == 2 || (CLIPM == 0 && sub)) {  // a clipped primitive's sub-triangle: its own slots and varyings
         rc = load_rec(b.recs, b.clip_slot[prim] + sub - 1u);
         v0 = rc.v[0]; v1 = rc.v[1]; v2 = rc.v[2];
-        taps = load_taps<ONE>(fb, v0, v1, v2);
+        taps = load_taps<ONE, false, kEarly>(fb, v0, v1, v2, vcol);
     }
     const bool from_rec = CLIPM == 2 || (CLIPM == 0 && sub);
     // the three vertices' light-space positions (rejected in round 4: recomputing them from the varyings' world
@@ -2408,7 +2419,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         taps.a2 = V4{w0, w1, w2, 0.0f}; taps.b2 = taps.a2; taps.c2 = taps.a2;
     } else if (ONE && TRI_VARY_OBJ && obj_mode(fp) && fp.obj_ucol) {
         // one colour for every vertex: fetch_attrs takes it from the frame arguments
-    } else if (TRI_COLOUR_LATE) {
+    } else if (!kEarly) {
         if (!from_rec) {  // an unclipped primitive's vertices: fb.src (fb.vary unless ONE or obj48; with CLIPM 0 a
                           // per-lane choice: both masked)
             taps.a2 = ld_vary<ONE, true>(fb, v0, 2); taps.b2 = ld_vary<ONE, true>(fb, v1, 2);
@@ -3116,7 +3127,8 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
     TRI_BIND_ARGS;
     raster_bin<EXACT, BL, false, ONE>(fp, b, xcd_bin(blockIdx.x, fp.nbins));
 }
-#if TRI_RASTER_ONE_VGPRS  // C3's instantiation as an explicit specialization: the cap takes no template-dependent value
+#if TRI_RASTER_ONE_VGPRS && defined(TRI_RASTER_PLAIN_TU)  // C3's instantiation as an explicit specialization: the cap
+                                                        // takes no template-dependent value (raster_plain.hip's)
 template <>
 __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(8))) __attribute__((amdgpu_num_vgpr(TRI_RASTER_ONE_VGPRS))) void k_raster_plain<false, 5, true>(TRI_KARGS) {
     TRI_BIND_ARGS;
