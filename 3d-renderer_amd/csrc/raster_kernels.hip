@@ -1427,14 +1427,20 @@ __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDe
     }
 }
 
-// A bin-queue entry -> its triangle.
+// A bin-queue entry -> its triangle (and the primitive's draw: 0 for a clipped entry, whose record names its slots).
 template <bool ONE = false, bool IDX = true>
-__device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
+__device__ __forceinline__ TriRec load_entry_d(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e, uint32_t& d) {
+    d = 0;
     if (e & TRI_ENTRY_CLIPPED) return load_rec(b.recs, e & ~TRI_ENTRY_CLIPPED);
     const FetchBufs fb = fetch_bufs(fp, b);
-    uint32_t sl[3], d;
+    uint32_t sl[3];
     prim_slots<ONE, IDX>(fp, b, e, sl, d);
     return rec_from_snaps(e, sl, ld_snap(fb, sl[0]), ld_snap(fb, sl[1]), ld_snap(fb, sl[2]));
+}
+template <bool ONE = false, bool IDX = true>
+__device__ __forceinline__ TriRec load_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
+    uint32_t d;
+    return load_entry_d<ONE, IDX>(fp, b, e, d);
 }
 
 // Fragment depth at pixel centre: plane through the snapped vertices, fixed evaluation order.
@@ -1480,6 +1486,11 @@ __device__ __forceinline__ uint32_t key_low(uint32_t prim_sub) {
 // the record's prim_sub re-encoded so that key_low() of it yields this word (qenc).
 #ifndef TRI_QTAB
 #define TRI_QTAB 1
+#endif
+// TRI_QTAB_SHADOW: the shadow instantiation keeps the table too, with each entry's draw as a fourth word (its
+// fragments then gather no 16-B prim_vs record)
+#ifndef TRI_QTAB_SHADOW
+#define TRI_QTAB_SHADOW 1
 #endif
 constexpr uint32_t kQtab = 256, kQPrimMax = (1u << 20) - 1u;
 __device__ __forceinline__ uint32_t qenc(uint32_t prim_sub, uint32_t qpos) {
@@ -2367,9 +2378,10 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
     uint32_t v0 = 0, v1 = 0, v2 = 0, dl = 0;
     Taps taps;
     if (CLIPM != 2) {
-        if (ONE && TRI_QTAB && qtab) {  // the coverage pass's table: three LDS words, no index gather
+        if (TRI_QTAB && qtab) {  // the coverage pass's table: three LDS words (four with the draw), no index gather
             const uint32_t q = low & 0xFFu;
             sl[0] = qtab[q]; sl[1] = qtab[kQtab + q]; sl[2] = qtab[2 * kQtab + q];
+            if (!ONE) d = qtab[3 * kQtab + q];
         } else {
             prim_slots<ONE, !SHADOW>(fp, b, prim, sl, d);
         }
@@ -2753,13 +2765,14 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     constexpr int BIN = 1 << BL;
     __shared__ uint64_t keys[BIN * BIN];
     constexpr bool kBalanced = TRI_COV_BALANCED && BL == 4;
-    constexpr bool kQt = TRI_QTAB && ONE && BL == 5;
+    constexpr bool kQt = TRI_QTAB && BL == 5 && (ONE || (SHADOW && TRI_QTAB_SHADOW));
+    constexpr uint32_t kQw = ONE ? 3u : 4u;  // table words per entry: the slots (and the draw)
     // (the queue-position table's 3 KB come from the large-triangle queue, so that 8 workgroups still fit the LDS;
     // 192 entries rather than 384: a bin with more large triangles walks the rest per lane, C3 +0.3 %, same box)
 #ifndef TRI_QTAB_BIGN
 #define TRI_QTAB_BIGN 192
 #endif
-    constexpr int kBigN = kBalanced ? kBigQueue / 2 : (kQt ? TRI_QTAB_BIGN : kBigQueue);
+    constexpr int kBigN = kBalanced ? kBigQueue / 2 : ((kQt && ONE) ? TRI_QTAB_BIGN : kBigQueue);
     __shared__ uint32_t bigq[kBigN];  // queue entries of the large triangles
     __shared__ float lut[512];
     constexpr int kJobWords = (kBalanced && kCovJobs > BIN * BIN ? kCovJobs : BIN * BIN);
@@ -2767,7 +2780,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     __shared__ CovEntry cov[kBalanced ? kCovPass : 1];
     __shared__ uint32_t wsum[TRI_BLOCK / 64];
     __shared__ uint32_t nbig, nsky;
-    __shared__ uint32_t qtab[kQt ? 3 * kQtab : 1];   // TRI_QTAB: per queue position, the entry's vertex slots
+    __shared__ uint32_t qtab[kQt ? kQw * kQtab : 1];  // TRI_QTAB: per queue position, the entry's vertex slots
     __shared__ uint16_t bigqp[kQt ? kBigN : 1];      // ... and the large triangles' queue positions
     const int tid = threadIdx.x;
     TRI_STAMP(0);
@@ -2880,10 +2893,12 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
   } else {
     auto cover = [&](uint32_t i, int32_t sub, int32_t step, bool first) {
         const uint32_t ri = (TRI_QUEUE_PREFETCH && first) ? pre1 : queue[i];
-        TriRec r = load_entry<ONE, !SHADOW>(fp, b, ri);
+        uint32_t dq;
+        TriRec r = load_entry_d<ONE, !SHADOW>(fp, b, ri, dq);
         if (kQt && qmode) {  // the entry's slots (set-up orientation undone) at its queue position; the key's payload
             if (!(ri & TRI_ENTRY_CLIPPED)) {
                 qtab[i] = r.v[0]; qtab[kQtab + i] = r.v[2]; qtab[2 * kQtab + i] = r.v[1];
+                if (!ONE) qtab[3 * kQtab + i] = dq;
             }
             r.prim_sub = qenc(r.prim_sub, i);
         }
@@ -3024,7 +3039,11 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
             }
     #endif
             if (!in) continue;
-            const int32_t px = ox + lx, py = oy + ly;
+            int32_t px = ox + lx;
+            const int32_t py = oy + ly;
+            // (the shadow instantiation: px re-formed each pixel, so that 256 px + 128, loop-invariant, is not hoisted
+            // into a register held across the loop, the one its table-reading variant had to spill)
+            if constexpr (SHADOW) asm volatile("" : "+v"(px));
             uint32_t out;
             float z;
             if (bg) {
