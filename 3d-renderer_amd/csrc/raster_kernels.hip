@@ -1427,6 +1427,11 @@ __device__ __forceinline__ void prim_slots(const TriFrameParams& fp, const TriDe
     }
 }
 
+// Whether an instantiation carries the index route's draw search (prim_slots' IDX): the shadow instantiations only with
+// TRI_IDX_ROUTE_SHADOW (raster_launch.h; the host enables the route on shadow frames under the same switch)
+template <bool SHADOW>
+constexpr bool kIdxOk = !SHADOW || TRI_IDX_ROUTE_SHADOW;
+
 // A bin-queue entry -> its triangle (and the primitive's draw: 0 for a clipped entry, whose record names its slots).
 template <bool ONE = false, bool IDX = true>
 __device__ __forceinline__ TriRec load_entry_d(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e, uint32_t& d) {
@@ -2383,7 +2388,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
             sl[0] = qtab[q]; sl[1] = qtab[kQtab + q]; sl[2] = qtab[2 * kQtab + q];
             if (!ONE) d = qtab[3 * kQtab + q];
         } else {
-            prim_slots<ONE, !SHADOW>(fp, b, prim, sl, d);
+            prim_slots<ONE, kIdxOk<SHADOW>>(fp, b, prim, sl, d);
         }
         // Every gather that needs only the slots is issued before the first wait: the snapped vertices and
         // the varyings are one round trip after the index fetch (the snaps are loaded for a clipped primitive
@@ -2396,7 +2401,7 @@ __device__ __forceinline__ void fetch_fragment_to(const TriFrameParams& fp, cons
         // it, and a wait at the join would otherwise hold the snaps and varyings in two round trips
         taps = load_taps<ONE, true, kEarly>(fb, v0 + dl, v1 + dl, v2 + dl, vcol);
     } else if (!ONE) {
-        prim_slots<ONE, !SHADOW>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
+        prim_slots<ONE, kIdxOk<SHADOW>>(fp, b, prim, sl, d);  // the draw (its shade record); the slots come from the record
     }
     TriRec rc;
     if (CLIPM == 2 || (CLIPM == 0 && sub)) {  // a clipped primitive's sub-triangle: its own slots and varyings
@@ -2818,7 +2823,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     const bool qmode = kQt && cnt <= kQtab && fp.nprims <= kQPrimMax;
     if (kAblate & 2) {  // diagnostics: no coverage; every pixel shades the bin's first triangle
         if (s1 > s0) {
-            const TriRec r = load_entry<ONE, !SHADOW>(fp, b, queue[0]);
+            const TriRec r = load_entry<ONE, kIdxOk<SHADOW>>(fp, b, queue[0]);
             const uint64_t key = (0x3F000000ull << 32) | key_low(r.prim_sub);
             for (int i = tid; i < BIN * BIN; i += TRI_BLOCK) keys[i] = key;
         }
@@ -2834,7 +2839,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
         int32_t cx0 = 0, cx1 = -1, cy0 = 0, cy1 = -1;
         if (tid < kCovPass && i < s1) {
             const uint32_t ri = queue[i];
-            r = load_entry<ONE, !SHADOW>(fp, b, ri);
+            r = load_entry<ONE, kIdxOk<SHADOW>>(fp, b, ri);
             rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
             if (cx0 <= cx1 && cy0 <= cy1) {
                 bool big = false;
@@ -2894,7 +2899,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     auto cover = [&](uint32_t i, int32_t sub, int32_t step, bool first) {
         const uint32_t ri = (TRI_QUEUE_PREFETCH && first) ? pre1 : queue[i];
         uint32_t dq;
-        TriRec r = load_entry_d<ONE, !SHADOW>(fp, b, ri, dq);
+        TriRec r = load_entry_d<ONE, kIdxOk<SHADOW>>(fp, b, ri, dq);
         if (kQt && qmode) {  // the entry's slots (set-up orientation undone) at its queue position; the key's payload
             if (!(ri & TRI_ENTRY_CLIPPED)) {
                 qtab[i] = r.v[0]; qtab[kQtab + i] = r.v[2]; qtab[2 * kQtab + i] = r.v[1];
@@ -2931,7 +2936,7 @@ __device__ __forceinline__ void raster_bin(const TriFrameParams& fp, const TriDe
     TRI_STAMP(2);
     const uint32_t nb = min(nbig, (uint32_t)kBigN);
     for (uint32_t q = 0; q < nb; ++q) {  // large triangles: all lanes share the pixels
-        TriRec r = load_entry<ONE, !SHADOW>(fp, b, bigq[q]);
+        TriRec r = load_entry<ONE, kIdxOk<SHADOW>>(fp, b, bigq[q]);
         if (kQt && qmode) r.prim_sub = qenc(r.prim_sub, bigqp[q]);
         int32_t cx0, cx1, cy0, cy1;
         rec_bbox(r, ox, oy, bw, bh, cx0, cx1, cy0, cy1);
@@ -3172,7 +3177,7 @@ __global__ __launch_bounds__(TRI_BLOCK) __attribute__((amdgpu_waves_per_eu(BL <=
 __device__ __forceinline__ TriRec load_shadow_entry(const TriFrameParams& fp, const TriDeviceBuffers& b, uint32_t e) {
     const Rsrc snr = make_rsrc(b.lsnap, 16ull * fp.nslots);
     uint32_t sl[3], d;
-    prim_slots<false, false>(fp, b, e, sl, d);
+    prim_slots<false, kIdxOk<true>>(fp, b, e, sl, d);
     const uint4 q0 = ld128(snr, sl[0] * 16u), q1 = ld128(snr, sl[1] * 16u), q2 = ld128(snr, sl[2] * 16u);
     const int32_t X0 = ((int32_t)q0.x << 8) >> 8, X1 = ((int32_t)q1.x << 8) >> 8, X2 = ((int32_t)q2.x << 8) >> 8;
     const int32_t Y0 = (int32_t)q0.y, Y1 = (int32_t)q1.y, Y2 = (int32_t)q2.y;

@@ -10,6 +10,11 @@
 #ifndef TRI_IDX_ROUTE
 #define TRI_IDX_ROUTE 1
 #endif
+// TRI_IDX_ROUTE_SHADOW: the route on frames with the shadow pre-pass too (its fragments read their slots and draw from
+// the queue-position table, so only the coverage pass, the map raster and the table's fallback search the draws)
+#ifndef TRI_IDX_ROUTE_SHADOW
+#define TRI_IDX_ROUTE_SHADOW 0
+#endif
 #ifndef TRI_SETUP_WAVES
 #define TRI_SETUP_WAVES 6
 #endif

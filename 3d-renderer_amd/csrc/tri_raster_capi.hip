@@ -1323,7 +1323,8 @@ int tri_render(tri_ctx* c) {
     // (not with the pre-pass over a transformed draw: the shadow instantiation carries no per-draw transform)
     fp.obj48 = (TRI_OBJ48 && !fp.vary36 && c->obj48 && !(c->shadow.size && c->obj48_xform)) ? 1u : 0u;
     fp.obj48_xform = fp.obj48 && c->obj48_xform ? 1u : 0u;
-    fp.idx_route = (TRI_IDX_ROUTE && c->idx_route && !c->shadow.size) ? 1u : 0u;  // (not with the pre-pass: prim_slots)
+    // (with the pre-pass only under TRI_IDX_ROUTE_SHADOW: the shadow kernels carry the draw search only then)
+    fp.idx_route = (TRI_IDX_ROUTE && c->idx_route && (!c->shadow.size || TRI_IDX_ROUTE_SHADOW)) ? 1u : 0u;
     if (fp.idx_route) {
         fp.idx_k = c->idx_k;
         std::memcpy(fp.pbase, c->pbase, sizeof fp.pbase);
